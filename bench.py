@@ -1,0 +1,203 @@
+"""bench.py — VAMP iterations/s + HBM GB/s on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3] [--no-cpu-baseline]
+
+A "step" is one VAMP iteration (src/vamp.cpp:148-428) of the linear model
+over the whole synthetic problem, with every vector and the fp64 design
+matrix already resident in HBM.  --stop-criteria-thr is 0, so exactly W+K
+iterations run; W are untimed.
+
+Workloads (synthetic, generated on the device):
+  c2 (default)  N=10,000 x Mt=50,000 i.i.d. Gaussian design (BASELINE configs[1]);
+                with --gpus n > 1: weak scaling at constant per-GPU bytes and
+                constant aspect ratio: N = 10,000*sqrt(n), Mt = 50,000*sqrt(n).
+  c3            per-GPU shard of configs[2] (N=100,000 x 62,500 markers per GPU,
+                methylation-like); at n=8 it is N=100,000 x Mt=500,000.
+
+value = n_gpus * iterations/s ("shard-iterations/s": VAMP iterations over one
+GPU's shard; at n=1 exactly iterations/s of the workload).  Multi-GPU: one
+process per GPU (torchrun), RCCL communicator inside libvampomi for the data
+path, torch.distributed (gloo) only for the id broadcast, barriers and the
+max-over-ranks time.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402  (imported before libvampomi: one HIP runtime)
+import torch.distributed as dist  # noqa: E402
+
+import vampomi_amd as va  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def workload(cfg: str, n: int):
+    if cfg == "c3":
+        return {"workload": "c3-shard", "N": 100000, "Mt": 62500 * n, "kind": va.GEN_METH}
+    if n == 1:
+        return {"workload": "c2", "N": 10000, "Mt": 50000, "kind": va.GEN_GAUSS}
+    s = math.sqrt(n)
+    return {"workload": "c2-weak", "N": int(round(10000 * s)), "Mt": int(round(50000 * s)), "kind": va.GEN_GAUSS}
+
+
+def cpu_baseline(d: "va.Data", w: dict, beta: np.ndarray, seed: int, budget_s: float = 20.0) -> dict:
+    """The CPU oracle (C restatement, OpenMP) on a bounded sample of the same workload."""
+    from oracle import pyoracle as O
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    N, Mt = w["N"], w["Mt"]
+    t0 = time.perf_counter()
+    X = O.generate_markers(seed, w["kind"], N, 0, Mt)  # bit-identical to the device shard
+    tgen = time.perf_counter() - t0
+    y = d.get_phen()
+    # one iteration first to size the sample, then a fresh run of k iterations
+    t0 = time.perf_counter()
+    r1 = O.vamp_infere(X, y, Mt, true_signal=beta, max_iter=1, stop_criteria_thr=0.0, keep_hist=False)
+    t1 = time.perf_counter() - t0
+    k = max(1, min(10, int(budget_s / max(t1, 1e-3))))
+    if k > 1:
+        t0 = time.perf_counter()
+        r = O.vamp_infere(X, y, Mt, true_signal=beta, max_iter=k, stop_criteria_thr=0.0, keep_hist=False)
+        tk = time.perf_counter() - t0
+    else:
+        r, tk = r1, t1
+    passes = int(r["a_passes"])
+    return {
+        "value": k / tk,
+        "unit": "VAMP iterations/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"iterations 1-{k} of {w['workload']} (N={N}, Mt={Mt}) on {threads} OpenMP threads; "
+                  f"{passes} A/A^T passes = {passes * 8.0 * N * Mt / tk / 1e9:.1f} GB/s effective; "
+                  f"data generation ({tgen:.1f} s) not timed",
+        "cg_iters": [int(a) for a in r["cg_iters"]],
+        "ons_iters": [int(a) for a in r["ons_iters"]],
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=48)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="c2", choices=["c2", "c3"])
+    ap.add_argument("--seed", type=int, default=20250711)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-timing", action="store_true", help="skip the HIP-event kernel timing")
+    ap.add_argument("--batch-rhs", type=int, default=1)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    n = world
+    if world > 1:
+        dist.init_process_group("gloo")
+    w = workload(args.config, n)
+    N, Mt = w["N"], w["Mt"]
+
+    comm_id = None
+    if world > 1:
+        obj = [va.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        comm_id = obj[0]
+    d = va.Data(N, Mt, rank=rank, nranks=world, comm_id=comm_id, device=local)
+    t0 = time.perf_counter()
+    d.generate(args.seed, w["kind"])
+    beta = d.simulate_phen(args.seed + 1, lam=0.1, h2=0.8)
+    t_setup = time.perf_counter() - t0
+
+    opts = va.VampOptions(max_iter=args.warmup + args.steps, stop_criteria_thr=0.0, batch_rhs=args.batch_rhs)
+    v = va.Vamp(d, opts, true_signal=beta)
+    v.begin()
+    for _ in range(args.warmup):
+        v.step()
+    ref0, exec0 = v.a_passes
+    d.reset_stats()
+    d.set_timing(not args.no_timing)
+
+    def barrier():
+        d.sync()
+        torch.cuda.synchronize() if torch.cuda.is_available() else None
+        if world > 1:
+            dist.barrier()
+
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        v.step()
+    barrier()
+    el = time.perf_counter() - t0
+    st = d.stats()
+    ref1, exec1 = v.a_passes
+    summ = v.summary()
+    v.end()
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+
+    it_s = args.steps / el
+    # dominant kernel: the (class, batch width) with the most device time
+    cands = []
+    for cls, arr in (("ax_partial_kernel", st.ax_k), ("atx_kernel", st.atx_k)):
+        for k in range(4):
+            if arr[k].launches:
+                cands.append((arr[k].ms_total, cls, k + 1, arr[k]))
+    roof = None
+    if cands:
+        ms, cls, K, ks = max(cands, key=lambda c: c[0])
+        avg_ms = ks.ms_total / ks.launches
+        bytes_per = ks.bytes_total / ks.launches
+        achieved = bytes_per / (avg_ms * 1e-3) / 1e9
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "kernel": f"{cls} K={K}", "avg_launch_us": round(avg_ms * 1e3, 2),
+                "bytes_per_launch": bytes_per, "launches": int(ks.launches)}
+    all_ms = st.ax.ms_total + st.atx.ms_total
+    all_bytes = st.ax.bytes_total + st.atx.bytes_total
+    line = {
+        "metric": "VAMP iterations/s (+ achieved HBM GB/s of the A/A^T kernels)",
+        "value": round(n * it_s, 4),
+        "unit": "shard-iterations/s" if n > 1 else "iterations/s",
+        "n_gpus": n, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(el / args.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "f64", "data": "synthetic (index-keyed dyadic generator, generated in HBM)",
+        "config": {"workload": w["workload"], "N": N, "Mt": Mt, "M_per_gpu": d.M,
+                   "design": "gaussian" if w["kind"] == va.GEN_GAUSS else "methylation-like",
+                   "iterations_timed": f"{args.warmup + 1}-{args.warmup + args.steps}",
+                   "parallelism": f"markers sharded over {n} GPU(s), RCCL all-reduce"},
+        "roofline": roof,
+        "hbm_gbs_all_A_kernels": round(all_bytes / (all_ms * 1e-3) / 1e9, 1) if all_ms > 0 else None,
+        "passes_exec_per_step": round((exec1 - exec0) / args.steps, 2),
+        "passes_ref_per_step": round((ref1 - ref0) / args.steps, 2),
+        "a_kernel_frac_of_step": round(all_ms * 1e-3 / el, 3) if el > 0 else None,
+        "cg_iters": summ["cg_iters"][args.warmup:], "ons_iters": summ["ons_iters"][args.warmup:],
+        "setup_s": round(t_setup, 2),
+        "cpu_baseline": None,
+    }
+    if rank == 0 and n == 1 and not args.no_cpu_baseline:
+        try:
+            line["cpu_baseline"] = cpu_baseline(d, w, beta, args.seed)
+        except Exception as e:  # reported, never fatal for the GPU number
+            line["cpu_baseline"] = {"error": repr(e)}
+    d.close()
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

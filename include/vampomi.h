@@ -1,0 +1,204 @@
+/*
+ * vampomi.h — C ABI of the MI355X-native gVAMPomi VAMP engine.
+ *
+ * Plain C, plain pointers and sizes.  One context per process, driving one
+ * gfx950 device and one contiguous marker shard [S, S+M) of the Mt markers
+ * (the reference's MPI rank, src/utilities.cpp:207-239).  Contexts of a job
+ * are joined by an RCCL communicator over xGMI; every entry point marked
+ * COLLECTIVE must be called by all ranks in the same order, exactly like the
+ * reference's MPI_Allreduce-bearing calls.
+ *
+ * Reference seams replaced (paths relative to the reference repository):
+ *   data::data / read_methylation_data / compute_markers_statistics
+ *        src/data.cpp:24-53, 116-153, 233-283 -> vampomi_open + vampomi_load_meth_*
+ *   data::read_phen            src/data.cpp:58-110      -> vampomi_read_phen / vampomi_set_phen
+ *   data::Ax                   src/data.cpp:340-373     -> vampomi_ax      (COLLECTIVE)
+ *   data::ATx / dot_product    src/data.cpp:294-333     -> vampomi_atx
+ *   data::get_mave/get_msig    src/data.hpp:56-57       -> vampomi_get_marker_stats
+ *   data::get_phen             src/data.hpp:48          -> vampomi_get_phen
+ *   vamp::lmmse_mult           src/vamp.cpp:645-662     -> vampomi_lmmse_mult (COLLECTIVE)
+ *   vamp::precondCG_solver     src/vamp.cpp:664-757     -> vampomi_pcg      (COLLECTIVE)
+ *   vamp::g1 / vamp::g1d       src/vamp.cpp:440-492     -> vampomi_denoise  (COLLECTIVE: alpha1 sum)
+ *   vamp::vamp + vamp::infere / infere_linear
+ *        src/vamp.cpp:18-91, 94-107, 110-438            -> vampomi_infere   (COLLECTIVE)
+ *        (or vampomi_vamp_begin / _step / _end, one VAMP iteration per step)
+ *   divide_work                src/utilities.cpp:207-239 -> vampomi_divide_work
+ *
+ * Errors: every call returns a vampomi_status; nothing aborts the process
+ * (the reference calls MPI_Abort / exit / throw).  vampomi_last_error() gives
+ * a message for the calling thread.
+ */
+#ifndef VAMPOMI_H
+#define VAMPOMI_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VAMPOMI_ABI_VERSION 1
+#define VAMPOMI_MAX_L 64          /* mixture components */
+#define VAMPOMI_UNIQUE_ID_BYTES 128
+
+typedef enum {
+    VAMPOMI_OK = 0,
+    VAMPOMI_ERR_ARG = 1,          /* bad argument / shape */
+    VAMPOMI_ERR_HIP = 2,          /* HIP runtime failure */
+    VAMPOMI_ERR_RCCL = 3,         /* RCCL failure */
+    VAMPOMI_ERR_IO = 4,           /* file could not be opened / read / written */
+    VAMPOMI_ERR_NAN_PHEN = 5,     /* "NA" in phenotype file (src/data.cpp:73-74) */
+    VAMPOMI_ERR_STATE = 6,        /* call out of order (e.g. Ax before data load) */
+    VAMPOMI_ERR_OOM = 7,          /* device or host allocation failed */
+    VAMPOMI_ERR_MODEL = 8         /* unsupported --model (src/vamp.cpp:103-104) */
+} vampomi_status;
+
+/* where a caller buffer lives */
+#define VAMPOMI_MEM_HOST 0
+#define VAMPOMI_MEM_DEVICE 1
+
+/* synthetic design kinds for vampomi_generate_meth */
+#define VAMPOMI_GEN_GAUSS 0       /* i.i.d. N(0,1)-like (simulation/data_sim.py:35) */
+#define VAMPOMI_GEN_METH 1        /* methylation-like beta values in [0,1] */
+
+typedef struct vampomi_ctx vampomi_ctx;
+
+typedef struct {
+    int64_t N;                    /* individuals (--N) */
+    int64_t Mt;                   /* total markers (--Mt) */
+    int rank, nranks;             /* this process's shard */
+    int device;                   /* HIP device ordinal; -1: rank % visible devices */
+    const void* comm_id;          /* VAMPOMI_UNIQUE_ID_BYTES from vampomi_comm_unique_id
+                                     on rank 0, broadcast by the caller; NULL if nranks==1 */
+    double alpha_scale;           /* --alpha-scale (src/data.cpp:261-264) */
+} vampomi_shard_desc;
+
+/* ---- job / context ---- */
+int vampomi_abi_version(void);
+const char* vampomi_last_error(void);
+/* src/utilities.cpp:207-239 */
+void vampomi_divide_work(int64_t Mt, int nranks, int rank, int64_t* M, int64_t* S, int64_t* Mm);
+vampomi_status vampomi_comm_unique_id(void* out /* VAMPOMI_UNIQUE_ID_BYTES */);
+vampomi_status vampomi_open(const vampomi_shard_desc* desc, vampomi_ctx** out);
+void vampomi_close(vampomi_ctx* ctx);
+/* M (local markers), S (first global marker), ld (device leading dimension) */
+vampomi_status vampomi_shard_info(const vampomi_ctx* ctx, int64_t* M, int64_t* S, int64_t* ld);
+vampomi_status vampomi_sync(vampomi_ctx* ctx);          /* drain the context's stream */
+vampomi_status vampomi_barrier(vampomi_ctx* ctx);       /* COLLECTIVE: RCCL barrier + drain */
+
+/* ---- data ingest (data::data) ---- */
+/* marker-major fp64 file (README.md:15): this shard's bytes [S*N*8, (S+M)*N*8) */
+vampomi_status vampomi_load_meth_file(vampomi_ctx* ctx, const char* path);
+/* host shard: M columns of N samples, column stride ld_in >= N doubles */
+vampomi_status vampomi_load_meth_host(vampomi_ctx* ctx, const double* X, int64_t ld_in);
+/* synthetic shard generated on the device (bit-identical to the oracle's) */
+vampomi_status vampomi_generate_meth(vampomi_ctx* ctx, uint64_t seed, int kind);
+/* PLINK phenotype, standardize = scale to unit variance, NOT centred */
+vampomi_status vampomi_read_phen(vampomi_ctx* ctx, const char* path, int standardize);
+vampomi_status vampomi_set_phen(vampomi_ctx* ctx, const double* y /* N, host */, int standardize);
+vampomi_status vampomi_get_phen(vampomi_ctx* ctx, double* y /* N, host */);
+/* synthetic phenotype y = sqrt(N)*A*beta + N(0,1-h2) noise, beta spike-and-slab
+ * (lam causal fraction, h2 heritability), then read_phen scaling.  beta_out
+ * (M local, host, may be NULL) receives beta = the true signal. COLLECTIVE */
+vampomi_status vampomi_simulate_phen(vampomi_ctx* ctx, uint64_t seed, double lam, double h2,
+                                     double* beta_out);
+vampomi_status vampomi_get_marker_stats(vampomi_ctx* ctx, double* mave, double* msig);
+/* copy local markers [i0, i0+count) back to the host, count x N doubles
+ * (data::get_meth_data, src/data.hpp:53) */
+vampomi_status vampomi_read_markers(vampomi_ctx* ctx, int64_t i0, int64_t count, double* out);
+
+/* ---- operators ---- */
+/* out (N) = (sum over all ranks of (X_i - mave_i) * msig_i * x_i) / sqrt(N). COLLECTIVE */
+vampomi_status vampomi_ax(vampomi_ctx* ctx, const double* x /* M */, double* out /* N */, int mem);
+/* out (M) = msig_i * sum_j (X_ij - mave_i) * u_j * (1/sqrt(N)) */
+vampomi_status vampomi_atx(vampomi_ctx* ctx, const double* u /* N */, double* out /* M */, int mem);
+/* out = tau * ATx(Ax(v)) + gam2 * v, zero v short-circuits. COLLECTIVE */
+vampomi_status vampomi_lmmse_mult(vampomi_ctx* ctx, const double* v, double tau, double gam2,
+                                  double* out, int mem);
+/* preconditioned CG on (tau*A^T A + gam2*I) mu = v from mu0 (NULL = zeros);
+ * onsager != 0 adds the Onsager stop of src/vamp.cpp:708-726. COLLECTIVE */
+vampomi_status vampomi_pcg(vampomi_ctx* ctx, const double* v, const double* mu0, double tau,
+                           double gam2, int onsager, int max_iter, double tol, double* mu,
+                           int* iters, int mem);
+/* x1 = g1(r1), x1d = g1d(r1) for the mixture (probs, vars) with vars ALREADY
+ * multiplied by N (src/vamp.cpp:87-88); *sum_d = sum over all ranks of x1d.
+ * COLLECTIVE */
+vampomi_status vampomi_denoise(vampomi_ctx* ctx, const double* r1, double gam1, const double* probs,
+                               const double* vars, int L, double* x1, double* x1d, double* sum_d,
+                               int mem);
+
+/* ---- the VAMP linear model (vamp::infere_linear) ---- */
+typedef struct {
+    double gam1, h2;              /* --gam1, --h2 (gamw = 1/(1-h2), src/main_meth.cpp:52) */
+    int max_iter, CG_max_iter;    /* --iterations, --CG-max-iter */
+    double CG_err_tol;            /* --CG-err-tol */
+    int EM_max_iter;              /* --EM-max-iter */
+    double EM_err_thr, rho;       /* --EM-err-thr, --rho */
+    int learn_vars, learn_prior_delay;
+    double stop_criteria_thr, merge_vars_thr;
+    int L;                        /* number of mixture components */
+    double vars[VAMPOMI_MAX_L];   /* as on the command line (NOT multiplied by N) */
+    double probs[VAMPOMI_MAX_L];
+    uint64_t seed;                /* index-keyed Bernoulli probe seed */
+    const char* out_dir;          /* NULL or "" => write no files */
+    const char* out_name;
+    int verbosity;
+    const double* true_signal;    /* local slice (M) or NULL => zeros (host) */
+    const double* x1hat_init;     /* local slice (M) or NULL => zeros (host) */
+    int batch_rhs;                /* 1 (default): share each A/A^T pass between the x2 and
+                                     Onsager CG solves; 0: run them back to back */
+    const char* model;            /* "linear" (NULL == "linear") */
+} vampomi_params;
+
+typedef struct {
+    int iterations_run;
+    /* per-iteration arrays, caller allocated (max_iter entries; may be NULL) */
+    int* cg_iters;                /* k1 */
+    int* ons_iters;               /* k2 */
+    int* L_hist;                  /* mixture components after updatePrior */
+    double* params;               /* 5 per iteration: alpha1 gam1 alpha2 gam2 gamw */
+    double* metrics;              /* 6 per iteration */
+    double* x1_hist;              /* M per iteration: x1_hat/sqrt(N) (== _it_K.bin slice) */
+    double* r1_hist;              /* M per iteration: r1/sqrt(N)     (== _r1_it_K.bin slice) */
+    double* x1_final;             /* M: returned x1_hat_scaled (src/vamp.cpp:437) */
+    double probs_final[VAMPOMI_MAX_L];
+    double vars_final[VAMPOMI_MAX_L];   /* divided by N, as printed/written */
+    int L_final;
+    int64_t a_passes_ref;         /* A/A^T passes the reference would have run */
+    int64_t a_passes_exec;        /* passes actually executed (X streamed from HBM) */
+} vampomi_result;
+
+void vampomi_params_default(vampomi_params* p);   /* src/options.hpp:62-104 defaults */
+vampomi_status vampomi_infere(vampomi_ctx* ctx, const vampomi_params* p, vampomi_result* r);
+/* step-wise form of vampomi_infere: begin, then one VAMP iteration per step
+ * (*stopped = 1 once the stopping rule fired or max_iter was reached), end. */
+vampomi_status vampomi_vamp_begin(vampomi_ctx* ctx, const vampomi_params* p, vampomi_result* r);
+vampomi_status vampomi_vamp_step(vampomi_ctx* ctx, int* stopped);
+vampomi_status vampomi_vamp_end(vampomi_ctx* ctx);
+
+/* ---- measurement ---- */
+typedef struct {
+    int64_t launches;             /* kernel launches of this class */
+    double ms_total;              /* device time between HIP events around them */
+    double bytes_total;           /* algorithmic HBM bytes */
+    double flops_total;
+} vampomi_kernel_stat;
+
+typedef struct {
+    vampomi_kernel_stat ax;       /* A.x partial-sum kernels (all batch widths) */
+    vampomi_kernel_stat atx;      /* A^T.u kernels */
+    vampomi_kernel_stat ax_k[4];  /* per batch width K = 1..4 (index K-1) */
+    vampomi_kernel_stat atx_k[4];
+    int64_t a_passes_exec;
+    int64_t host_syncs;
+} vampomi_stats;
+
+/* enable HIP-event timing of the A/A^T kernels (adds one event pair per launch) */
+vampomi_status vampomi_set_timing(vampomi_ctx* ctx, int on);
+vampomi_status vampomi_get_stats(vampomi_ctx* ctx, vampomi_stats* out);
+vampomi_status vampomi_reset_stats(vampomi_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

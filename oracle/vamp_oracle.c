@@ -1,0 +1,850 @@
+/*
+ * vamp_oracle.c — CPU restatement (C11 + OpenMP) of the gVAMPomi linear VAMP
+ * hot path.  TEST INFRASTRUCTURE ONLY (see vamp_oracle.h header): tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg are the only users.
+ *
+ * PARITY UNPINNED — the reference is unbuildable here (Boost absent) and ships
+ * no fixtures; this file restates it function by function with file:line
+ * citations into /root/reference/src.  Deviations P1/P2: see vamp_oracle.h.
+ *
+ * Determinism: every reduction is blocked with a fixed block size and summed
+ * in block order, so results do not depend on the OpenMP thread count.
+ */
+#define _GNU_SOURCE
+#include "vamp_oracle.h"
+
+#include <errno.h>
+#include <fcntl.h>
+#include <float.h>
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <unistd.h>
+
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+/* ------------------------------------------------------------------------- */
+/* index-keyed generators                                                    */
+/* ------------------------------------------------------------------------- */
+
+uint64_t orc_splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ULL;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
+    return x ^ (x >> 31);
+}
+
+/* replaces std::bernoulli_distribution(0.5)(std::random_device) of
+ * src/vamp.cpp:142,295-296 (P2) */
+int orc_bern_bit(uint64_t seed, int it, int64_t gidx) {
+    uint64_t k = orc_splitmix64(seed ^ 0xB5AD4ECEDA1CE2A9ULL);
+    uint64_t h = orc_splitmix64(k ^ (((uint64_t)(uint32_t)it << 40) ^ (uint64_t)gidx));
+    return (int)(h >> 63);
+}
+
+/* Synthetic i.i.d. design (stands for simulation/data_sim.py:35, which draws
+ * np.random.normal unseeded): Irwin-Hall sum of 12 dyadic 16-bit uniforms,
+ * centred and unit-variance, exactly representable. */
+double orc_gauss_dyadic(uint64_t seed, int64_t i, int64_t j) {
+    uint64_t k = orc_splitmix64(orc_splitmix64(seed ^ 0x4741555353ULL) + (uint64_t)i);
+    uint64_t acc = 0;
+    for (uint64_t t = 0; t < 3; ++t) {
+        uint64_t h = orc_splitmix64(k ^ (((uint64_t)j << 2) | t));
+        acc += (h & 0xFFFFULL) + ((h >> 16) & 0xFFFFULL) + ((h >> 32) & 0xFFFFULL) + (h >> 48);
+    }
+    return (double)(2 * acc + 12) * (1.0 / 131072.0) - 6.0;
+}
+
+/* Methylation-like beta value: per-marker mean in
+ * [51/1024, 972/1024], sd in [10/1024, 137/1024], clamped to [0,1]. */
+double orc_meth_dyadic(uint64_t seed, int64_t i, int64_t j) {
+    uint64_t hm = orc_splitmix64(orc_splitmix64(seed ^ 0x6D657468ULL) + (uint64_t)i);
+    double mu = (double)(51 + (hm & 1023ULL) % 922ULL) * (1.0 / 1024.0);
+    double sd = (double)(10 + ((hm >> 10) & 127ULL)) * (1.0 / 1024.0);
+    double v = mu + sd * orc_gauss_dyadic(seed ^ 0x5A5A5A5AULL, i, j);
+    return v < 0.0 ? 0.0 : (v > 1.0 ? 1.0 : v);
+}
+
+void orc_generate_markers(uint64_t seed, int kind, int64_t N, int64_t ld, int64_t S, int64_t M,
+                          double* X) {
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < M; ++i) {
+        double* col = X + i * ld;
+        for (int64_t j = 0; j < N; ++j)
+            col[j] = kind == 1 ? orc_meth_dyadic(seed, S + i, j) : orc_gauss_dyadic(seed, S + i, j);
+        for (int64_t j = N; j < ld; ++j) col[j] = 0.0;
+    }
+}
+
+/* ------------------------------------------------------------------------- */
+/* reductions: src/utilities.cpp:138-162 inner_prod / l2_norm2 (deterministic)*/
+/* ------------------------------------------------------------------------- */
+
+#define ORC_BLK 2048
+
+double orc_dot(const double* a, const double* b, int64_t n) {
+    int64_t nb = (n + ORC_BLK - 1) / ORC_BLK;
+    if (nb <= 1) {
+        double s = 0.0;
+        for (int64_t i = 0; i < n; ++i) s += a[i] * b[i];
+        return s;
+    }
+    double* part = (double*)malloc(sizeof(double) * (size_t)nb);
+#pragma omp parallel for schedule(static)
+    for (int64_t k = 0; k < nb; ++k) {
+        int64_t lo = k * ORC_BLK, hi = lo + ORC_BLK < n ? lo + ORC_BLK : n;
+        double s = 0.0;
+        for (int64_t i = lo; i < hi; ++i) s += a[i] * b[i];
+        part[k] = s;
+    }
+    double s = 0.0;
+    for (int64_t k = 0; k < nb; ++k) s += part[k];
+    free(part);
+    return s;
+}
+
+typedef struct {
+    const orc_problem* pb;
+} orc_ctx;
+
+static double allreduce1(const orc_problem* pb, double v) {
+    if (pb->allreduce) pb->allreduce(&v, 1, pb->user);
+    return v;
+}
+
+/* inner_prod(u, v, sync) — src/utilities.cpp:138-158 */
+static double inner_prod(const orc_problem* pb, const double* a, const double* b, int64_t n,
+                         int sync) {
+    double s = orc_dot(a, b, n);
+    return sync ? allreduce1(pb, s) : s;
+}
+
+/* ------------------------------------------------------------------------- */
+/* divide_work — src/utilities.cpp:207-239                                    */
+/* ------------------------------------------------------------------------- */
+void orc_divide_work(int64_t Mt, int nranks, int rank, int64_t* M, int64_t* S, int64_t* Mm) {
+    int64_t modu = Mt % nranks, size = Mt / nranks, cum = 0;
+    for (int r = 0; r < nranks; ++r) {
+        int64_t len = r < modu ? size + 1 : size;
+        if (r == rank) {
+            *M = len;
+            *S = cum;
+        }
+        cum += len;
+    }
+    if (Mm) *Mm = modu != 0 ? size + 1 : size;
+}
+
+/* ------------------------------------------------------------------------- */
+/* read_phen — src/data.cpp:58-110                                            */
+/* ------------------------------------------------------------------------- */
+void orc_standardize_phen(double* y, int64_t n) {
+    /* src/data.cpp:97-104: avg from the running sum; scale only, no centring */
+    double sum = 0.0;
+    for (int64_t i = 0; i < n; ++i) sum += y[i];
+    double avg = sum / (double)n;
+    double sqn = 0.0;
+    for (int64_t i = 0; i < n; ++i)
+        if (y[i] != DBL_MAX) sqn += (y[i] - avg) * (y[i] - avg);
+    sqn = sqrt((double)(n - 1) / sqn);
+    for (int64_t i = 0; i < n; ++i) y[i] *= sqn;
+}
+
+int64_t orc_read_phen(const char* path, int standardize, double* y, int64_t cap,
+                      double* intercept, double* scale) {
+    FILE* f = fopen(path, "r");
+    if (!f) return -1;
+    char* line = NULL;
+    size_t lcap = 0;
+    ssize_t len;
+    int64_t n = 0;
+    double sum = 0.0;
+    while ((len = getline(&line, &lcap, f)) != -1) {
+        if (len > 0 && line[len - 1] == '\n') line[--len] = '\0';
+        /* std::regex("\\s+") token split with -1: leading whitespace yields an
+         * empty first token; tokens[2] is the third field counted that way. */
+        char* p = line;
+        int tok = 0;
+        char* t2 = NULL;
+        char* start = p;
+        for (;;) {
+            char* q = start;
+            while (*q && !(*q == ' ' || *q == '\t' || *q == '\r' || *q == '\v' || *q == '\f')) ++q;
+            if (tok == 2) {
+                t2 = start;
+                if (*q) *q = '\0';
+                break;
+            }
+            if (!*q) break;
+            while (*q == ' ' || *q == '\t' || *q == '\r' || *q == '\v' || *q == '\f') ++q;
+            start = q;
+            ++tok;
+            if (!*start) break; /* trailing separator: regex iterator yields no empty suffix */
+        }
+        if (!t2) continue;
+        if (strcmp(t2, "NA") == 0) {
+            free(line);
+            fclose(f);
+            return -2; /* src/data.cpp:73-74 throw "NAN in data!" */
+        }
+        if (n < cap) y[n] = atof(t2);
+        sum += atof(t2);
+        ++n;
+    }
+    free(line);
+    fclose(f);
+    if (intercept) *intercept = 0.0;
+    if (scale) *scale = 1.0;
+    if (standardize && n > 1) {
+        double avg = sum / (double)n;
+        double sqn = 0.0;
+        for (int64_t i = 0; i < n && i < cap; ++i)
+            if (y[i] != DBL_MAX) sqn += (y[i] - avg) * (y[i] - avg);
+        sqn = sqrt((double)(n - 1) / sqn);
+        for (int64_t i = 0; i < n && i < cap; ++i) y[i] *= sqn;
+        if (intercept) *intercept = avg;
+        if (scale) *scale = sqn;
+    }
+    return n;
+}
+
+/* ------------------------------------------------------------------------- */
+/* compute_markers_statistics — src/data.cpp:233-283                          */
+/* ------------------------------------------------------------------------- */
+void orc_marker_stats(const double* X, int64_t N, int64_t ld, int64_t M, int64_t nonas,
+                      double alpha_scale, double* mave, double* msig) {
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < M; ++i) {
+        const double* m = X + i * ld;
+        double suma = 0.0;
+        for (int64_t j = 0; j < N; ++j) suma += m[j];
+        mave[i] = suma / (double)nonas;
+        double sumsqr = 0.0;
+        for (int64_t j = 0; j < N; ++j) {
+            double val = m[j] - mave[i];
+            sumsqr += val * val;
+        }
+        if (sumsqr != 0.0) {
+            if (alpha_scale == 1.0)
+                msig[i] = 1.0 / sqrt(sumsqr / ((double)nonas - 1.0));
+            else
+                msig[i] = 1.0 / pow(sqrt(sumsqr / ((double)nonas - 1.0)), alpha_scale);
+        } else {
+            msig[i] = 1.0;
+        }
+    }
+}
+
+/* ------------------------------------------------------------------------- */
+/* Ax — src/data.cpp:340-373 (same per-element summation order: markers in    */
+/* index order, one running sum per sample)                                   */
+/* ------------------------------------------------------------------------- */
+#define ORC_ROWBLK 2048
+void orc_ax_local(const double* X, int64_t N, int64_t ld, int64_t M, const double* mave,
+                  const double* msig, const double* x, double* out) {
+    int64_t nb = (N + ORC_ROWBLK - 1) / ORC_ROWBLK;
+#pragma omp parallel for schedule(static)
+    for (int64_t b = 0; b < nb; ++b) {
+        int64_t lo = b * ORC_ROWBLK, hi = lo + ORC_ROWBLK < N ? lo + ORC_ROWBLK : N;
+        double acc[ORC_ROWBLK];
+        for (int64_t j = lo; j < hi; ++j) acc[j - lo] = 0.0;
+        for (int64_t i = 0; i < M; ++i) {
+            const double* m = X + i * ld;
+            double ave = mave[i];
+            double sig_phen_i = msig[i] * x[i];
+            for (int64_t j = lo; j < hi; ++j) acc[j - lo] += (m[j] - ave) * sig_phen_i;
+        }
+        for (int64_t j = lo; j < hi; ++j) out[j] = acc[j - lo];
+    }
+}
+
+void orc_ax(const double* X, int64_t N, int64_t ld, int64_t M, const double* mave,
+            const double* msig, const double* x, double* out, orc_allreduce_fn ar, void* user) {
+    orc_ax_local(X, N, ld, M, mave, msig, x, out);
+    if (ar) ar(out, N, user); /* MPI_Allreduce(N) src/data.cpp:367 */
+    double sq = sqrt((double)N);
+    for (int64_t j = 0; j < N; ++j) out[j] /= sq; /* src/data.cpp:369-370 */
+}
+
+/* ATx / dot_product — src/data.cpp:294-333 */
+void orc_atx(const double* X, int64_t N, int64_t ld, int64_t M, const double* mave,
+             const double* msig, const double* u, double* out) {
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < M; ++i) {
+        const double* m = X + i * ld;
+        double mu = mave[i];
+        double dpa = 0.0;
+        for (int64_t j = 0; j < N; ++j) dpa += (m[j] - mu) * u[j];
+        out[i] = msig[i] * dpa;
+    }
+    double scale = 1.0 / sqrt((double)N);
+    for (int64_t i = 0; i < M; ++i) out[i] *= scale;
+}
+
+/* ------------------------------------------------------------------------- */
+/* g1 / g1d — src/vamp.cpp:440-492                                           */
+/* ------------------------------------------------------------------------- */
+/* std::max / std::min semantics (NaN in the first argument propagates) */
+static double smax(double a, double b) { return (a < b) ? b : a; }
+static double smin(double a, double b) { return (b < a) ? b : a; }
+
+static double vmax(const double* v, int L) {
+    double m = v[0];
+    for (int i = 1; i < L; ++i)
+        if (v[i] > m) m = v[i];
+    return m;
+}
+
+double orc_g1(double y, double gam1, const double* probs, const double* vars, int L) {
+    double sigma = 1 / gam1;
+    double eta_max = vmax(vars, L);
+    double pk = 0, pkd = 0;
+    if (sigma < 1e-10 && sigma > -1e-10) return y;
+    for (int i = 0; i < L; ++i) {
+        double expe_sum = -0.5 * (y * y) * (eta_max - vars[i]) / (vars[i] + sigma) / (eta_max + sigma);
+        double z = probs[i] / sqrt(vars[i] + sigma) * exp(expe_sum);
+        pk = pk + z;
+        z = z / (vars[i] + sigma) * y;
+        pkd = pkd - z;
+    }
+    return y + sigma * pkd / pk;
+}
+
+double orc_g1d(double y, double gam1, const double* probs, const double* vars, int L) {
+    double sigma = 1 / gam1;
+    double eta_max = vmax(vars, L);
+    double pk = 0, pkd = 0, pkdd = 0;
+    if (sigma < 1e-10 && sigma > -1e-10) return 1;
+    for (int i = 0; i < L; ++i) {
+        double expe_sum = -0.5 * (y * y) * (eta_max - vars[i]) / (vars[i] + sigma) / (eta_max + sigma);
+        double z = probs[i] / sqrt(vars[i] + sigma) * exp(expe_sum);
+        pk = pk + z;
+        z = z / (vars[i] + sigma) * y;
+        pkd = pkd - z;
+        double z2 = z / (vars[i] + sigma) * y;
+        pkdd = pkdd - probs[i] / pow(vars[i] + sigma, 1.5) * exp(expe_sum) + z2;
+    }
+    double q = pkd / pk;
+    return 1 + sigma * (pkdd / pk - q * q);
+}
+
+/* ------------------------------------------------------------------------- */
+/* output writers                                                            */
+/* ------------------------------------------------------------------------- */
+
+/* mpi_store_vec_to_file — src/utilities.cpp:241-249: CREATE|WRONLY, no
+ * truncation, M doubles at byte offset S*8 */
+int orc_store_vec(const char* path, const double* v, int64_t S, int64_t M) {
+    int fd = open(path, O_CREAT | O_WRONLY, 0666);
+    if (fd < 0) return -1;
+    size_t want = (size_t)M * sizeof(double);
+    ssize_t w = pwrite(fd, v, want, (off_t)S * (off_t)sizeof(double));
+    close(fd);
+    return w == (ssize_t)want ? 0 : -1;
+}
+
+/* setup_io (src/vamp.cpp:854-882) + write_ofile_csv_header
+ * (src/utilities.cpp:388-401): delete, create exclusively, header at 0 */
+int orc_csv_header(const char* path, const char* const* fields, int n) {
+    unlink(path);
+    int fd = open(path, O_CREAT | O_WRONLY | O_EXCL, 0666);
+    if (fd < 0) return -1;
+    size_t tot = 2;
+    for (int i = 0; i < n; ++i) tot += strlen(fields[i]) + 2;
+    char* s = (char*)malloc(tot);
+    s[0] = '\0';
+    for (int i = 0; i < n; ++i) {
+        if (i) strcat(s, ", ");
+        strcat(s, fields[i]);
+    }
+    strcat(s, "\n");
+    ssize_t w = pwrite(fd, s, strlen(s), 0);
+    close(fd);
+    int ok = w == (ssize_t)strlen(s);
+    free(s);
+    return ok ? 0 : -1;
+}
+
+/* write_ofile_csv — src/utilities.cpp:366-385: "%5d" + ", %20.15f"*n + "\n"
+ * written at byte offset it * strlen(row) */
+int orc_csv_row(const char* path, int it, const double* vals, int n) {
+    char buf[50000];
+    int cx = snprintf(buf, sizeof buf, "%5d", it);
+    for (int i = 0; i < n; ++i) cx += snprintf(buf + cx, sizeof buf - (size_t)cx, ", %20.15f", vals[i]);
+    cx += snprintf(buf + cx, sizeof buf - (size_t)cx, "\n");
+    int fd = open(path, O_WRONLY);
+    if (fd < 0) return -1;
+    ssize_t w = pwrite(fd, buf, (size_t)cx, (off_t)it * (off_t)cx);
+    close(fd);
+    return w == cx ? 0 : -1;
+}
+
+/* ------------------------------------------------------------------------- */
+/* the VAMP state                                                            */
+/* ------------------------------------------------------------------------- */
+typedef struct {
+    const orc_problem* pb;
+    int64_t N, M, Mt;
+    int L;
+    double probs[ORC_MAX_L], vars[ORC_MAX_L];
+    double gam1, gam2, gamw;
+    double* r1;
+    double* bern_vec;
+    double* invQ_bern_vec;
+    double* mu_CG_last;
+    double* x2_hat;
+    int64_t passes;
+    int cg_iters_last;
+    /* params */
+    int CG_max_iter, EM_max_iter, learn_vars, verbosity;
+    double CG_err_tol, EM_err_thr, merge_vars_thr;
+} orc_vamp;
+
+static void ax(orc_vamp* s, const double* x, double* out) {
+    const orc_problem* pb = s->pb;
+    orc_ax(pb->X, pb->N, pb->ld, pb->M, pb->mave, pb->msig, x, out, pb->allreduce, pb->user);
+    s->passes++;
+}
+
+static void atx(orc_vamp* s, const double* u, double* out) {
+    const orc_problem* pb = s->pb;
+    orc_atx(pb->X, pb->N, pb->ld, pb->M, pb->mave, pb->msig, u, out);
+    s->passes++;
+}
+
+static int all_zero(const double* v, int64_t n) {
+    for (int64_t i = 0; i < n; ++i)
+        if (v[i] != 0.0) return 0;
+    return 1;
+}
+
+/* lmmse_mult — src/vamp.cpp:645-662: tau*A^T(A v) + gam2*v; local zero check */
+static void lmmse_mult(orc_vamp* s, const double* v, double tau, double* res, double* tmpN) {
+    int64_t M = s->M;
+    if (all_zero(v, M)) {
+        memset(res, 0, sizeof(double) * (size_t)M);
+        return;
+    }
+    ax(s, v, tmpN);
+    atx(s, tmpN, res);
+    for (int64_t i = 0; i < M; ++i) {
+        res[i] *= tau;
+        res[i] += s->gam2 * v[i];
+    }
+}
+
+/* precondCG_solver — src/vamp.cpp:664-757 */
+static void precondCG(orc_vamp* s, const double* v, const double* mu_start, double tau, int denoiser,
+                      double* mu_out) {
+    const orc_problem* pb = s->pb;
+    int64_t M = s->M, N = s->N;
+    double diag = tau * (double)(N - 1) / (double)N + s->gam2; /* :676-677 */
+    double* mu = mu_out;
+    memcpy(mu, mu_start, sizeof(double) * (size_t)M);
+    double* r = (double*)malloc(sizeof(double) * (size_t)M);
+    double* z = (double*)malloc(sizeof(double) * (size_t)M);
+    double* p = (double*)malloc(sizeof(double) * (size_t)M);
+    double* d = (double*)malloc(sizeof(double) * (size_t)M);
+    double* tmpN = (double*)malloc(sizeof(double) * (size_t)N);
+    lmmse_mult(s, mu, tau, r, tmpN);
+    for (int64_t i = 0; i < M; ++i) r[i] = v[i] - r[i];
+    for (int64_t i = 0; i < M; ++i) z[i] = r[i] / diag;
+    memcpy(p, z, sizeof(double) * (size_t)M);
+    double prev_onsager = 0;
+    int it_done = 0;
+    double norm_v = sqrt(inner_prod(pb, v, v, M, 1));
+    for (int i = 0; i < s->CG_max_iter; ++i) {
+        it_done = i + 1;
+        lmmse_mult(s, p, tau, d, tmpN);
+        double rz = inner_prod(pb, r, z, M, 1);
+        double dp = inner_prod(pb, d, p, M, 1);
+        double alpha = rz / dp;
+        for (int64_t j = 0; j < M; ++j) mu[j] += alpha * p[j];
+        if (denoiser == 0) {
+            double onsager = s->gam2 * inner_prod(pb, v, mu, M, 1);
+            double rel_err = onsager != 0 ? fabs((onsager - prev_onsager) / onsager) : 1;
+            if (rel_err < 1e-8) break;
+            prev_onsager = onsager;
+        }
+        double beta = pow(rz, -1); /* :731 */
+        for (int64_t j = 0; j < M; ++j) r[j] -= d[j] * alpha;
+        for (int64_t j = 0; j < M; ++j) z[j] = r[j] / diag;
+        beta *= inner_prod(pb, r, z, M, 1);
+        for (int64_t j = 0; j < M; ++j) p[j] = z[j] + beta * p[j];
+        double rel_err = sqrt(inner_prod(pb, r, r, M, 1)) / norm_v;
+        if (s->verbosity >= 2 && pb->rank == 0)
+            printf("[CG] it = %d: ||r_it|| / ||RHS|| = %g\n", i, rel_err);
+        if (rel_err < s->CG_err_tol) break;
+    }
+    s->cg_iters_last = it_done;
+    if (denoiser == 1) memcpy(s->mu_CG_last, mu, sizeof(double) * (size_t)M);
+    free(r);
+    free(z);
+    free(p);
+    free(d);
+    free(tmpN);
+}
+
+/* updatePrior — src/vamp.cpp:531-643 */
+static void update_prior(orc_vamp* s) {
+    const orc_problem* pb = s->pb;
+    int64_t M = s->M;
+    double noise_var = 1 / s->gam1;
+    double lambda = 1 - s->probs[0];
+    double omegas[ORC_MAX_L];
+    for (int j = 0; j < s->L; ++j) omegas[j] = s->probs[j];
+    for (int j = 1; j < s->L; ++j) omegas[j] /= lambda;
+    const double* r1 = s->r1;
+    for (int it = 0; it < s->EM_max_iter; ++it) {
+        int L = s->L, Lm = L - 1;
+        double max_sigma = vmax(s->vars, L);
+        double probs_prev[ORC_MAX_L], vars_prev[ORC_MAX_L];
+        memcpy(probs_prev, s->probs, sizeof probs_prev);
+        memcpy(vars_prev, s->vars, sizeof vars_prev);
+        double* beta = (double*)malloc(sizeof(double) * (size_t)(M * (Lm > 0 ? Lm : 1)));
+        double* gammas = (double*)malloc(sizeof(double) * (size_t)(M * (Lm > 0 ? Lm : 1)));
+        double* pin = (double*)malloc(sizeof(double) * (size_t)(M > 0 ? M : 1));
+        double v[ORC_MAX_L];
+#pragma omp parallel for schedule(static)
+        for (int64_t i = 0; i < M; ++i) {
+            double* tb = beta + i * Lm;
+            double* tg = gammas + i * Lm;
+            for (int j = 1; j < L; ++j) {
+                double num = lambda * omegas[j] *
+                             exp(-(r1[i] * r1[i]) / 2 * (max_sigma - s->vars[j]) / (s->vars[j] + noise_var) /
+                                 (max_sigma + noise_var)) /
+                             sqrt(s->vars[j] + noise_var) / sqrt(2 * M_PI);
+                double num_gammas = s->gam1 * r1[i] / (1 / s->vars[j] + s->gam1);
+                tb[j - 1] = num;
+                tg[j - 1] = num_gammas;
+            }
+            double sum_of_elems = 0.0; /* std::accumulate, sequential */
+            for (int j = 0; j < Lm; ++j) sum_of_elems += tb[j];
+            for (int j = 0; j < Lm; ++j) tb[j] /= sum_of_elems;
+            pin[i] = 1 / (1 + (1 - lambda) / sqrt(2 * M_PI * noise_var) *
+                                  exp(-(r1[i] * r1[i]) / 2 * max_sigma / noise_var / (noise_var + max_sigma)) /
+                                  sum_of_elems);
+        }
+        for (int j = 1; j < L; ++j) v[j - 1] = 1.0 / (1.0 / s->vars[j] + s->gam1);
+        /* lambda = accumulate(pin) then Allreduce / Mt  (:576-579) */
+        double ones_dummy = 0.0;
+        (void)ones_dummy;
+        double lam_local = 0.0;
+        {
+            /* blocked deterministic sum of pin */
+            double* onesv = (double*)malloc(sizeof(double) * (size_t)(M > 0 ? M : 1));
+            for (int64_t i = 0; i < M; ++i) onesv[i] = 1.0;
+            lam_local = orc_dot(pin, onesv, M);
+            free(onesv);
+        }
+        double lambda_total = allreduce1(pb, lam_local);
+        lambda = lambda_total / (double)s->Mt;
+#pragma omp parallel for schedule(static)
+        for (int64_t i = 0; i < M; ++i)
+            for (int j = 0; j < Lm; ++j) {
+                double g = gammas[i * Lm + j];
+                gammas[i * Lm + j] = beta[i * Lm + j] * (g * g + v[j]);
+            }
+        double sum_of_pin = lambda_total;
+        double* colb = (double*)malloc(sizeof(double) * (size_t)(M > 0 ? M : 1));
+        double* colg = (double*)malloc(sizeof(double) * (size_t)(M > 0 ? M : 1));
+        for (int j = 0; j < Lm; ++j) {
+            for (int64_t i = 0; i < M; ++i) {
+                colb[i] = beta[i * Lm + j];
+                colg[i] = gammas[i * Lm + j];
+            }
+            double res = orc_dot(colb, pin, M);
+            double res_gammas = orc_dot(colg, pin, M);
+            double res_gammas_total = allreduce1(pb, res_gammas);
+            double res_total = allreduce1(pb, res);
+            if (s->learn_vars == 1) s->vars[j + 1] = res_gammas_total / res_total;
+            omegas[j + 1] = res_total / sum_of_pin;
+            s->probs[j + 1] = lambda * omegas[j + 1];
+        }
+        s->probs[0] = 1 - lambda;
+        free(colb);
+        free(colg);
+        free(beta);
+        free(gammas);
+        free(pin);
+        double distance_probs = 0, norm_probs = 0, distance_vars = 0, norm_vars = 0;
+        for (int j = 0; j < L; ++j) {
+            distance_probs += (s->probs[j] - probs_prev[j]) * (s->probs[j] - probs_prev[j]);
+            norm_probs += s->probs[j] * s->probs[j];
+            distance_vars += (s->vars[j] - vars_prev[j]) * (s->vars[j] - vars_prev[j]);
+            norm_vars += s->vars[j] * s->vars[j];
+        }
+        double dist_probs = sqrt(distance_probs / norm_probs);
+        double dist_vars = sqrt(distance_vars / norm_vars);
+        if (dist_probs < s->EM_err_thr && dist_vars < s->EM_err_thr) break;
+    }
+    /* merging close variances (:626-642); abs() on double == fabs */
+    for (int j = 0; j < s->L; ++j) {
+        for (int k = j + 1; k < s->L; ++k) {
+            double denom = s->vars[j] != 0 ? smin(s->vars[j], s->vars[k]) : 1e-7;
+            if (fabs(s->vars[j] - s->vars[k]) / denom < s->merge_vars_thr) {
+                double sum2probs = s->probs[j] + s->probs[k];
+                for (int q = k; q + 1 < s->L; ++q) {
+                    s->vars[q] = s->vars[q + 1];
+                    s->probs[q] = s->probs[q + 1];
+                }
+                s->L--;
+                s->probs[j] = sum2probs;
+                k--;
+            }
+        }
+    }
+}
+
+/* err_measures — src/vamp.cpp:760-852 (scalars only; Axest given) */
+static void err_measures(orc_vamp* s, const double* xhat, const double* ts, const double* Axest,
+                         const double* y, int ind, double* metrics) {
+    const orc_problem* pb = s->pb;
+    int64_t M = s->M, N = s->N;
+    double corr = inner_prod(pb, xhat, ts, M, 1) /
+                  sqrt(inner_prod(pb, xhat, xhat, M, 1) * inner_prod(pb, ts, ts, M, 1));
+    if (ind == 1)
+        metrics[1] = corr;
+    else
+        metrics[3] = corr;
+    double* tempN = (double*)malloc(sizeof(double) * (size_t)N);
+    for (int64_t i = 0; i < N; ++i) tempN[i] = -Axest[i] + y[i];
+    double l2_pred_err = sqrt(inner_prod(pb, tempN, tempN, N, 0) / inner_prod(pb, y, y, N, 0));
+    double R2 = 1 - l2_pred_err * l2_pred_err;
+    double corr_y = inner_prod(pb, Axest, y, N, 1) /
+                    sqrt(inner_prod(pb, Axest, Axest, N, 1) * inner_prod(pb, y, y, N, 1));
+    double corr_y_2 = corr_y * corr_y;
+    free(tempN);
+    if (ind == 1) {
+        metrics[0] = R2;
+        metrics[4] = corr_y_2;
+    } else {
+        metrics[2] = R2;
+        metrics[5] = corr_y_2;
+    }
+}
+
+static void join_path(char* dst, size_t cap, const char* dir, const char* name, const char* suffix) {
+    snprintf(dst, cap, "%s/%s%s", dir, name, suffix);
+}
+
+/* ------------------------------------------------------------------------- */
+/* infere_linear — src/vamp.cpp:110-438 (constructor :18-91)                  */
+/* ------------------------------------------------------------------------- */
+int orc_vamp_infere_linear(const orc_problem* pb, const orc_params* prm, orc_result* res) {
+    int64_t N = pb->N, M = pb->M, Mt = pb->Mt;
+    orc_vamp s;
+    memset(&s, 0, sizeof s);
+    s.pb = pb;
+    s.N = N;
+    s.M = M;
+    s.Mt = Mt;
+    s.L = prm->L;
+    if (s.L < 1 || s.L > ORC_MAX_L) return -1;
+    for (int j = 0; j < s.L; ++j) {
+        s.probs[j] = prm->probs[j];
+        s.vars[j] = prm->vars[j] * (double)N; /* :87-88 */
+    }
+    s.gam1 = prm->gam1;
+    s.gamw = 1.0 / (1.0 - prm->h2);
+    s.gam2 = 0;
+    s.CG_max_iter = prm->CG_max_iter;
+    s.CG_err_tol = prm->CG_err_tol;
+    s.EM_max_iter = prm->EM_max_iter;
+    s.EM_err_thr = prm->EM_err_thr;
+    s.learn_vars = prm->learn_vars;
+    s.merge_vars_thr = prm->merge_vars_thr;
+    s.verbosity = prm->verbosity;
+    int write = prm->out_dir && prm->out_dir[0] && pb->rank >= 0;
+    size_t Mb = sizeof(double) * (size_t)(M > 0 ? M : 1), Nb = sizeof(double) * (size_t)N;
+
+    double sqrtN = sqrt((double)N);
+    double* x1_hat = (double*)calloc(1, Mb);
+    double* x1_hat_prev = (double*)calloc(1, Mb);
+    double* x1_hat_d = (double*)calloc(1, Mb);
+    double* x1_scaled = (double*)calloc(1, Mb);
+    double* r2 = (double*)calloc(1, Mb);
+    double* v = (double*)calloc(1, Mb);
+    double* z1 = (double*)calloc(1, Nb);
+    double* Ax2 = (double*)calloc(1, Nb);
+    double* tmpN = (double*)calloc(1, Nb);
+    double* tmpM = (double*)calloc(1, Mb);
+    double* ts = (double*)calloc(1, Mb);
+    s.r1 = (double*)calloc(1, Mb);
+    s.bern_vec = (double*)calloc(1, Mb);
+    s.invQ_bern_vec = (double*)calloc(1, Mb);
+    s.mu_CG_last = (double*)calloc(1, Mb);
+    s.x2_hat = (double*)calloc(1, Mb);
+    if (pb->true_signal) memcpy(ts, pb->true_signal, sizeof(double) * (size_t)M);
+    /* P1: x1_hat and r1 sized M, then :71-72, :78-79 */
+    for (int64_t i = 0; i < M; ++i) {
+        double init = pb->x1hat_init ? pb->x1hat_init[i] : 0.0;
+        x1_hat[i] = init / sqrt((double)N);
+        s.r1[i] = init / sqrt((double)N);
+    }
+    const double* y = pb->y;
+
+    char p_params[4096], p_metrics[4096], p_prior[4096], pbuf[4096];
+    if (write) {
+        join_path(p_metrics, sizeof p_metrics, prm->out_dir, prm->out_name, "_metrics.csv");
+        join_path(p_params, sizeof p_params, prm->out_dir, prm->out_name, "_params.csv");
+        join_path(p_prior, sizeof p_prior, prm->out_dir, prm->out_name, "_prior.csv");
+        if (pb->rank == 0) {
+            static const char* mh[] = {"iteration",          "R2 denoising",         "x1 correlation denoising",
+                                       "R2 LMMSE",           "x2 correlation LMMSE", "z1 correlation denoising",
+                                       "z2 correlation LMMSE"};
+            static const char* ph[] = {"iteration", "alpha1", "gam1", "alpha2", "gam2", "gamw"};
+            char names[2 + 2 * ORC_MAX_L][16];
+            const char* prh[2 + 2 * ORC_MAX_L];
+            prh[0] = "iteration";
+            prh[1] = "number of components";
+            int np = 2;
+            for (int i = 0; i < s.L; ++i) {
+                snprintf(names[np], 16, "prob%d", i);
+                prh[np] = names[np];
+                ++np;
+            }
+            for (int i = 0; i < s.L; ++i) {
+                snprintf(names[np], 16, "var%d", i);
+                prh[np] = names[np];
+                ++np;
+            }
+            orc_csv_header(p_metrics, mh, 7);
+            orc_csv_header(p_params, ph, 6);
+            orc_csv_header(p_prior, prh, np);
+        }
+    }
+
+    double metrics[6] = {0, 0, 0, 0, 0, 0}, params[5] = {0, 0, 0, 0, 0};
+    double alpha1 = 0, alpha2 = 0, eta1 = 0, eta2 = 0;
+    int it;
+    int iters_run = 0;
+    for (it = 1; it <= prm->max_iter; ++it) {
+        iters_run = it;
+        if (it > prm->learn_prior_delay) update_prior(&s); /* :186-187 */
+        if (res && res->L_hist) res->L_hist[it - 1] = s.L;
+
+        memcpy(x1_hat_prev, x1_hat, Mb); /* :203 */
+        for (int64_t i = 0; i < M; ++i) x1_hat[i] = orc_g1(s.r1[i], s.gam1, s.probs, s.vars, s.L);
+        if (it > 1)
+            for (int64_t i = 0; i < M; ++i) x1_hat[i] = prm->rho * x1_hat[i] + (1 - prm->rho) * x1_hat_prev[i];
+        for (int64_t i = 0; i < M; ++i) x1_hat_d[i] = orc_g1d(s.r1[i], s.gam1, s.probs, s.vars, s.L);
+        {
+            double* onesv = tmpM;
+            for (int64_t i = 0; i < M; ++i) onesv[i] = 1.0;
+            double sum_d = orc_dot(x1_hat_d, onesv, M);
+            alpha1 = allreduce1(pb, sum_d) / (double)Mt; /* :221-223 */
+        }
+        eta1 = s.gam1 / alpha1;
+        ax(&s, x1_hat, z1); /* :232 */
+
+        for (int64_t i = 0; i < M; ++i) x1_scaled[i] = x1_hat[i] / sqrtN;
+        if (res && res->x1_hist) memcpy(res->x1_hist + (int64_t)(it - 1) * M, x1_scaled, Mb);
+        if (res && res->r1_hist)
+            for (int64_t i = 0; i < M; ++i) res->r1_hist[(int64_t)(it - 1) * M + i] = s.r1[i] / sqrtN;
+        if (write) {
+            char suf[64];
+            snprintf(suf, sizeof suf, "_it_%d.bin", it);
+            join_path(pbuf, sizeof pbuf, prm->out_dir, prm->out_name, suf);
+            orc_store_vec(pbuf, x1_scaled, pb->S, M);
+            for (int64_t i = 0; i < M; ++i) tmpM[i] = s.r1[i] / sqrtN;
+            snprintf(suf, sizeof suf, "_r1_it_%d.bin", it);
+            join_path(pbuf, sizeof pbuf, prm->out_dir, prm->out_name, suf);
+            orc_store_vec(pbuf, tmpM, pb->S, M);
+        }
+
+        s.gam2 = eta1 - s.gam1; /* :255-256 */
+        s.gam2 = smin(smax(s.gam2, 1e-11), 1e11);
+        for (int64_t i = 0; i < M; ++i) r2[i] = (eta1 * x1_hat[i] - s.gam1 * s.r1[i]) / s.gam2;
+
+        err_measures(&s, x1_hat, ts, z1, y, 1, metrics); /* :272 */
+        params[0] = alpha1;
+        params[1] = s.gam1;
+
+        /* LMMSE */
+        for (int64_t i = 0; i < M; ++i) /* :295-296 with P2 */
+            s.bern_vec[i] = (2 * orc_bern_bit(prm->seed, it, pb->S + i) - 1) / sqrt((double)Mt);
+        atx(&s, y, v); /* :303 */
+        for (int64_t i = 0; i < M; ++i) v[i] = s.gamw * v[i] + s.gam2 * r2[i];
+        if (it == 1)
+            memset(tmpM, 0, Mb);
+        else
+            memcpy(tmpM, s.mu_CG_last, Mb);
+        precondCG(&s, v, tmpM, s.gamw, 1, s.x2_hat); /* :308-311 */
+        if (res && res->cg_iters) res->cg_iters[it - 1] = s.cg_iters_last;
+
+        /* g2d_onsager :494-501 */
+        memset(tmpM, 0, Mb);
+        precondCG(&s, s.bern_vec, tmpM, s.gamw, 0, s.invQ_bern_vec);
+        if (res && res->ons_iters) res->ons_iters[it - 1] = s.cg_iters_last;
+        alpha2 = s.gam2 * inner_prod(pb, s.bern_vec, s.invQ_bern_vec, M, 1);
+
+        eta2 = s.gam2 / alpha2; /* :341-346 */
+        double gam1_prev = s.gam1;
+        s.gam1 = eta2 - s.gam2;
+        s.gam1 = smin(smax(s.gam1, 1e-11), 1e11);
+        s.gam1 = prm->rho * s.gam1 + (1 - prm->rho) * gam1_prev;
+        for (int64_t i = 0; i < M; ++i) s.r1[i] = (eta2 * s.x2_hat[i] - s.gam2 * r2[i]) / s.gam1;
+
+        /* updateNoisePrec :504-529 */
+        ax(&s, s.x2_hat, Ax2);
+        for (int64_t i = 0; i < N; ++i) tmpN[i] = Ax2[i] - y[i];
+        double temp_norm2 = inner_prod(pb, tmpN, tmpN, N, 0);
+        ax(&s, s.invQ_bern_vec, tmpN);
+        atx(&s, tmpN, tmpM);
+        double trace_corr = inner_prod(pb, s.bern_vec, tmpM, M, 1) * (double)Mt;
+        s.gamw = (double)N / (temp_norm2 + trace_corr);
+
+        /* err_measures(2): Ax(x2_hat) recomputed at :826 — same operator, same
+         * input; counted as a pass, value identical to Ax2 */
+        s.passes++;
+        err_measures(&s, s.x2_hat, ts, Ax2, y, 2, metrics);
+        params[2] = alpha2;
+        params[3] = s.gam2;
+        params[4] = s.gamw;
+        if (res && res->params) memcpy(res->params + (int64_t)(it - 1) * 5, params, sizeof params);
+        if (res && res->metrics) memcpy(res->metrics + (int64_t)(it - 1) * 6, metrics, sizeof metrics);
+        if (write && pb->rank == 0) {
+            orc_csv_row(p_params, it, params, 5);
+            orc_csv_row(p_metrics, it, metrics, 6);
+        }
+        if (prm->verbosity >= 1 && pb->rank == 0)
+            printf("it %d: alpha1 %.6g gam1 %.6g alpha2 %.6g gam2 %.6g gamw %.6g L %d cg %d\n", it, alpha1,
+                   s.gam1, alpha2, s.gam2, s.gamw, s.L, s.cg_iters_last);
+
+        /* stopping criteria :409-423 */
+        for (int64_t i = 0; i < M; ++i) tmpM[i] = x1_hat_prev[i] - x1_hat[i];
+        double NMSE = sqrt(inner_prod(pb, tmpM, tmpM, M, 1) / inner_prod(pb, x1_hat_prev, x1_hat_prev, M, 1));
+        if (it > 1 && NMSE < prm->stop_criteria_thr) break;
+    }
+    if (res) {
+        res->iterations_run = iters_run;
+        if (res->x1_final) memcpy(res->x1_final, x1_scaled, sizeof(double) * (size_t)M);
+        res->L_final = s.L;
+        if (res->probs_final)
+            for (int j = 0; j < s.L; ++j) res->probs_final[j] = s.probs[j];
+        if (res->vars_final)
+            for (int j = 0; j < s.L; ++j) res->vars_final[j] = s.vars[j] / (double)N;
+        res->a_passes = s.passes;
+    }
+    free(x1_hat);
+    free(x1_hat_prev);
+    free(x1_hat_d);
+    free(x1_scaled);
+    free(r2);
+    free(v);
+    free(z1);
+    free(Ax2);
+    free(tmpN);
+    free(tmpM);
+    free(ts);
+    free(s.r1);
+    free(s.bern_vec);
+    free(s.invQ_bern_vec);
+    free(s.mu_CG_last);
+    free(s.x2_hat);
+    return 0;
+}

@@ -1,0 +1,32 @@
+"""Build libvampomi.so + main_meth.exe (hipcc, gfx950) and the CPU oracle.
+
+    python -m vampomi_amd.build [--clean]
+
+Everything is built in-tree (vampomi_amd/lib, vampomi_amd/bin,
+oracle/build) so the artefacts travel with the repository snapshot.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+
+
+def _make(path: str, clean: bool = False) -> None:
+    jobs = str(min(16, os.cpu_count() or 4))
+    if clean:
+        subprocess.run(["make", "-C", path, "clean"], check=True)
+    subprocess.run(["make", "-C", path, "-j", jobs], check=True)
+
+
+def build(clean: bool = False, oracle: bool = True) -> None:
+    _make(os.path.join(HERE, "csrc"), clean)
+    if oracle:
+        _make(os.path.join(ROOT, "oracle"), clean)
+
+
+if __name__ == "__main__":
+    build(clean="--clean" in sys.argv)

@@ -1,0 +1,119 @@
+// hostio.cpp — gVAMPomi file formats (see hostio.h for the reference lines).
+#include "hostio.h"
+
+#include <fcntl.h>
+#include <unistd.h>
+
+#include <cfloat>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+
+namespace vio {
+
+static bool is_ws(char c) { return c == ' ' || c == '\t' || c == '\r' || c == '\n' || c == '\v' || c == '\f'; }
+
+int64_t read_phen(const std::string& path, std::vector<double>& y) {
+    std::ifstream in(path);
+    if (!in.is_open()) return -1;
+    y.clear();
+    std::string line;
+    while (std::getline(in, line)) {
+        // third token of the "\\s+" split with submatch -1: a leading run of
+        // whitespace produces an empty first token.
+        std::vector<std::string> tok;
+        size_t i = 0;
+        const size_t n = line.size();
+        for (;;) {
+            size_t j = i;
+            while (j < n && !is_ws(line[j])) ++j;
+            if (j == n) {  // suffix after the last separator: only if non-empty
+                if (j > i || tok.empty()) tok.push_back(line.substr(i, j - i));
+                break;
+            }
+            tok.push_back(line.substr(i, j - i));  // text before a separator (may be empty)
+            while (j < n && is_ws(line[j])) ++j;
+            i = j;
+            if (i == n) break;
+        }
+        if (tok.size() < 3) continue;
+        if (tok[2] == "NA") return -2;
+        y.push_back(std::atof(tok[2].c_str()));
+    }
+    return (int64_t)y.size();
+}
+
+double standardize_phen(std::vector<double>& y) {
+    double sum = 0.0;
+    for (double v : y) sum += v;
+    const int64_t nonas = (int64_t)y.size();
+    const double avg = sum / double(nonas);
+    double sqn = 0.0;
+    for (size_t i = 0; i < y.size(); ++i)
+        if (y[i] != DBL_MAX) sqn += (y[i] - avg) * (y[i] - avg);
+    sqn = std::sqrt(double(nonas - 1) / sqn);
+    for (size_t i = 0; i < y.size(); ++i) y[i] *= sqn;
+    return sqn;
+}
+
+bool store_vec(const std::string& path, const double* v, int64_t S, int64_t M) {
+    int fd = ::open(path.c_str(), O_CREAT | O_WRONLY, 0666);
+    if (fd < 0) return false;
+    const size_t want = (size_t)M * sizeof(double);
+    size_t done = 0;
+    while (done < want) {
+        ssize_t w = ::pwrite(fd, (const char*)v + done, want - done, (off_t)S * 8 + (off_t)done);
+        if (w <= 0) break;
+        done += (size_t)w;
+    }
+    ::close(fd);
+    return done == want;
+}
+
+bool read_vec(const std::string& path, double* v, int64_t S, int64_t M) {
+    int fd = ::open(path.c_str(), O_RDONLY);
+    if (fd < 0) return false;
+    std::memset(v, 0, (size_t)M * sizeof(double));
+    const size_t want = (size_t)M * sizeof(double);
+    size_t done = 0;
+    while (done < want) {
+        ssize_t r = ::pread(fd, (char*)v + done, want - done, (off_t)S * 8 + (off_t)done);
+        if (r <= 0) break;
+        done += (size_t)r;
+    }
+    ::close(fd);
+    return true;
+}
+
+bool csv_create_with_header(const std::string& path, const std::vector<std::string>& fields) {
+    ::unlink(path.c_str());
+    int fd = ::open(path.c_str(), O_CREAT | O_WRONLY | O_EXCL, 0666);
+    if (fd < 0) return false;
+    std::string s = fields.empty() ? std::string() : fields[0];
+    for (size_t i = 1; i < fields.size(); ++i) s += ", " + fields[i];
+    s += "\n";
+    ssize_t w = ::pwrite(fd, s.data(), s.size(), 0);
+    ::close(fd);
+    return w == (ssize_t)s.size();
+}
+
+std::string csv_format_row(int it, const double* vals, int n) {
+    char buf[50000];
+    int cx = std::snprintf(buf, sizeof buf, "%5d", it);
+    for (int i = 0; i < n; ++i) cx += std::snprintf(buf + cx, sizeof buf - (size_t)cx, ", %20.15f", vals[i]);
+    cx += std::snprintf(buf + cx, sizeof buf - (size_t)cx, "\n");
+    return std::string(buf, (size_t)cx);
+}
+
+bool csv_write_row(const std::string& path, int it, const double* vals, int n) {
+    const std::string row = csv_format_row(it, vals, n);
+    int fd = ::open(path.c_str(), O_WRONLY);
+    if (fd < 0) return false;
+    ssize_t w = ::pwrite(fd, row.data(), row.size(), (off_t)it * (off_t)row.size());
+    ::close(fd);
+    return w == (ssize_t)row.size();
+}
+
+}  // namespace vio

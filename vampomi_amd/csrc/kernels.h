@@ -1,0 +1,134 @@
+// kernels.h — launch wrappers for the gfx950 kernels of the VAMP hot path
+// (internal to libvampomi; the public boundary is include/vampomi.h).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace vk {
+
+constexpr int kMaxRhs = 4;     // right-hand sides sharing one pass over X
+constexpr int kMaxL = 64;      // mixture components (VAMPOMI_MAX_L)
+constexpr int kMaxTerms = 8;   // dot-product terms per reduction launch
+constexpr int kRedBlocks = 256;  // max partial blocks of a reduction
+
+struct CPtrs { const double* p[kMaxRhs]; };
+struct Ptrs { double* p[kMaxRhs]; };
+
+// The device-resident marker shard: M columns (markers) of N samples, column
+// stride ld >= N doubles (ld % 16 == 0, pad rows zero), plus marker stats.
+struct Shard {
+    const double* X;
+    int64_t ld, N, M;
+    const double* mave;
+    const double* msig;
+};
+
+// ---- A.x : two-stage, deterministic --------------------------------------
+// Stage 1 (ax_partial): a workgroup owns a 512-row tile and a chunk of
+// markers, accumulates in registers, writes part[chunk][k][ld].  Stage 2
+// (ax_reduce): sums the chunks in index order.
+struct AxPlan {
+    int tiles;        // ceil(N / 512)
+    int nchunks;      // marker chunks (grid.y)
+    int64_t chunk;    // markers per chunk
+};
+AxPlan ax_plan(int64_t N, int64_t M);
+hipError_t ax_partial(const Shard& s, const AxPlan& pl, int K, CPtrs x, double* part, hipStream_t st);
+// out_k[j] = sum_c part[c][k][j]; if div > 0 then out_k[j] /= div
+hipError_t ax_reduce(const AxPlan& pl, int K, int64_t N, int64_t ld, const double* part, Ptrs out,
+                     double div, hipStream_t st);
+// out_k[j] /= div (after the cross-rank all-reduce)
+hipError_t vec_div(int K, int64_t n, int64_t ld, Ptrs v, double div, hipStream_t st);
+
+// ---- A^T.u : one wave per group of markers --------------------------------
+// mode 0: out_k[i] = (msig_i * dot_k(i)) * scale
+// mode 1 (lmmse_mult): out_k[i] = ((msig_i*dot)*scale)*tau + gam2*p_k[i],
+//   and per-workgroup partials of <out_k, p_k> into dp_part[blk*K + k]
+int atx_blocks(int64_t M);
+hipError_t atx(const Shard& s, int K, CPtrs u, Ptrs out, double scale, int mode, double tau,
+               double gam2, CPtrs p, double* dp_part, hipStream_t st);
+
+// ---- marker statistics (data::compute_markers_statistics) ----------------
+hipError_t marker_stats(const double* X, int64_t ld, int64_t N, int64_t M, double nonas,
+                        double alpha_scale, double* mave, double* msig, hipStream_t st);
+
+// ---- synthetic data --------------------------------------------------------
+hipError_t gen_markers(uint64_t seed, int kind, int64_t N, int64_t ld, int64_t S, int64_t M, double* X,
+                       hipStream_t st);
+// beta_i = gauss(seed) for causal markers (uniform < lam), else 0; causal flag
+// count partials in cnt_part (one per block)
+hipError_t gen_beta(uint64_t seed, double lam, int64_t S, int64_t M, double* beta, double* cnt_part,
+                    int* nblk, hipStream_t st);
+hipError_t scale_vec(int64_t n, double* v, double a, hipStream_t st);
+// y_j = y_j + sqrt1mh2 * gauss(seed, noise stream, j)
+hipError_t add_noise(uint64_t seed, int64_t N, double sd, double* y, hipStream_t st);
+
+// ---- reductions --------------------------------------------------------------
+enum DotOp { DOT = 0, DIFF2 = 1, SUM = 2 };
+struct DotTerm { const double* a; const double* b; int op; };
+struct DotArgs { DotTerm t[kMaxTerms]; int nt; };
+int red_blocks(int64_t n);
+// per-block partials part[blk*nt + q]
+hipError_t dots_partial(const DotArgs& a, int64_t n, double* part, hipStream_t st);
+// out[q] = sum over blocks in index order of part[blk*nq + q]
+hipError_t sum_partials(const double* part, int nblk, int nq, double* out, hipStream_t st);
+
+// ---- denoiser (vamp::g1 / g1d) ---------------------------------------------
+struct Mix {
+    double probs[kMaxL];
+    double vars[kMaxL];
+    int L;
+};
+// x1 = g1(r1) (then rho*x1 + (1-rho)*x1_prev if damp), x1d = g1d(r1),
+// per-block partial sums of x1d in part
+hipError_t denoise(int64_t M, const double* r1, double gam1, const Mix& mix, double* x1,
+                   const double* x1_prev, int damp, double rho, double* x1d, double* part, int* nblk,
+                   hipStream_t st);
+
+// ---- EM prior update (vamp::updatePrior) per-marker sums --------------------
+struct EmArgs {
+    double omegas[kMaxL];
+    double vars[kMaxL];
+    double v[kMaxL];
+    double lambda, noise_var, gam1, max_sigma;
+    int L;
+};
+// part[blk*Q + q], Q = 1 + 2(L-1): q=0 sum pin; q=j (1..L-1) sum beta_j pin;
+// q=L-1+j sum beta_j (g_j^2 + v_j) pin
+hipError_t em_sums(int64_t M, const double* r1, const EmArgs& a, double* part, int* nblk, hipStream_t st);
+
+// ---- elementwise VAMP updates -----------------------------------------------
+// out = (a*x - b*y) / c        (r2 and r1 updates, src/vamp.cpp:259-261, 348-350)
+hipError_t lincomb_div(int64_t n, double a, const double* x, double b, const double* y, double c,
+                       double* out, hipStream_t st);
+// out = a*x + b*y              (v = gamw*ATx(y) + gam2*r2, src/vamp.cpp:305-306)
+hipError_t axpby(int64_t n, double a, const double* x, double b, const double* y, double* out,
+                 hipStream_t st);
+// bern[i] = (2*bit(seed,it,S+i) - 1) / sqrtMt
+hipError_t bernoulli(uint64_t seed, int it, int64_t S, int64_t M, double sqrtMt, double* out,
+                     hipStream_t st);
+// out = x / d
+hipError_t div_scalar(int64_t n, const double* x, double d, double* out, hipStream_t st);
+
+// ---- PCG (vamp::precondCG_solver), K right-hand sides --------------------------
+struct CgVecs {
+    double* mu[kMaxRhs];
+    double* r[kMaxRhs];
+    double* z[kMaxRhs];
+    double* p[kMaxRhs];
+    const double* d[kMaxRhs];   // lmmse_mult(mu0) for init (nullptr: mu0 == 0), A p in the loop
+    const double* v[kMaxRhs];
+};
+// r = v - d (or v), z = r/diag, p = z; partials <r,z>, <v,v> (2K terms)
+hipError_t cg_init(int K, int64_t M, const CgVecs& c, double diag, double* part, int* nblk, hipStream_t st);
+// alpha_k = rz[k] / dp_dev[k]; mu += alpha p; r -= d alpha; z = r/diag;
+// partials <r,z>, <r,r>, <v,mu> (3K terms, ordered k-major)
+struct CgScalars { double rz[kMaxRhs]; };
+hipError_t cg_update(int K, int64_t M, const CgVecs& c, double diag, CgScalars rz, const double* dp_dev,
+                     double* part, int* nblk, hipStream_t st);
+// p = z + beta_k p
+struct CgBeta { double beta[kMaxRhs]; };
+hipError_t cg_pupdate(int K, int64_t M, const CgVecs& c, CgBeta b, hipStream_t st);
+
+}  // namespace vk

@@ -1,0 +1,784 @@
+// kernels.hip — gfx950 (CDNA4) kernels for the gVAMPomi VAMP hot path.
+//
+// The design matrix X is fp64, marker-major (each marker = one column of N
+// samples, contiguous, README.md:15 / src/data.cpp:127-142), resident in HBM
+// with a 128-byte aligned column stride ld.  A.x and A^T.u are HBM-bound
+// GEMVs (0.375 flop/B); they stream X with 16-byte-per-lane nontemporal loads
+// and never use MFMA.  All reductions are two-stage with fixed block counts
+// and fixed summation order, so every result is bitwise reproducible run to
+// run and independent of the rank count's effect on scheduling.
+#include "kernels.h"
+
+#include <hip/hip_runtime.h>
+
+namespace vk {
+
+typedef double v2d __attribute__((ext_vector_type(2)));
+
+static constexpr int kBlock = 256;   // 4 waves of 64
+
+// ---------------------------------------------------------------------------
+// small helpers
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;  // butterfly: every lane holds the same value
+}
+
+// sum over a 256-thread block; every thread gets the result
+__device__ __forceinline__ double block_sum(double v, double* lds4) {
+    v = wave_sum(v);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    __syncthreads();
+    if (lane == 0) lds4[w] = v;
+    __syncthreads();
+    return ((lds4[0] + lds4[1]) + lds4[2]) + lds4[3];
+}
+
+__device__ __forceinline__ v2d ld_stream(const double* p) {
+    return __builtin_nontemporal_load(reinterpret_cast<const v2d*>(p));
+}
+
+__device__ __forceinline__ v2d ld2(const double* p) { return *reinterpret_cast<const v2d*>(p); }
+
+__host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ULL;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
+    return x ^ (x >> 31);
+}
+
+// Irwin-Hall(12) dyadic normal draw; same specification as the oracle's
+// orc_gauss_dyadic (oracle/vamp_oracle.c), exactly representable.
+__device__ __forceinline__ double gauss_dyadic(uint64_t seed, int64_t i, int64_t j) {
+    const uint64_t k = splitmix64(splitmix64(seed ^ 0x4741555353ULL) + (uint64_t)i);
+    uint64_t acc = 0;
+#pragma unroll
+    for (uint64_t t = 0; t < 3; ++t) {
+        const uint64_t h = splitmix64(k ^ (((uint64_t)j << 2) | t));
+        acc += (h & 0xFFFFULL) + ((h >> 16) & 0xFFFFULL) + ((h >> 32) & 0xFFFFULL) + (h >> 48);
+    }
+    return (double)(2 * acc + 12) * (1.0 / 131072.0) - 6.0;
+}
+
+__device__ __forceinline__ double meth_dyadic(uint64_t seed, int64_t i, int64_t j) {
+    const uint64_t hm = splitmix64(splitmix64(seed ^ 0x6D657468ULL) + (uint64_t)i);
+    const double mu = (double)(51 + (hm & 1023ULL) % 922ULL) * (1.0 / 1024.0);
+    const double sd = (double)(10 + ((hm >> 10) & 127ULL)) * (1.0 / 1024.0);
+    const double v = mu + sd * gauss_dyadic(seed ^ 0x5A5A5A5AULL, i, j);
+    return v < 0.0 ? 0.0 : (v > 1.0 ? 1.0 : v);
+}
+
+__device__ __forceinline__ int bern_bit(uint64_t seed, int it, int64_t gidx) {
+    const uint64_t k = splitmix64(seed ^ 0xB5AD4ECEDA1CE2A9ULL);
+    const uint64_t h = splitmix64(k ^ (((uint64_t)(uint32_t)it << 40) ^ (uint64_t)gidx));
+    return (int)(h >> 63);
+}
+
+static inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// ---------------------------------------------------------------------------
+// A.x   (data::Ax, src/data.cpp:340-373)
+// ---------------------------------------------------------------------------
+// Workgroup (tile, chunk): rows [512*tile, 512*tile+512) x markers of the
+// chunk.  Lane owns two adjacent rows (16-byte load); per marker the wave
+// reads 1 KiB contiguous, the workgroup 4 KiB.  Eight markers are loaded
+// before any arithmetic so each lane keeps 8 x 16 B of HBM reads in flight.
+// Per-sample summation order within a chunk is the reference's: markers in
+// index order, acc += (x - mave_i) * (msig_i * x_i).
+template <int K>
+__global__ __launch_bounds__(kBlock) void ax_partial_kernel(const double* __restrict__ X, int64_t ld,
+                                                            int64_t N, int64_t M,
+                                                            const double* __restrict__ mave,
+                                                            const double* __restrict__ msig, CPtrs xs,
+                                                            int64_t chunk, double* __restrict__ part) {
+    const int64_t j = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * 2;
+    const int64_t i0 = (int64_t)blockIdx.y * chunk;
+    const int64_t i1 = (i0 + chunk < M) ? i0 + chunk : M;
+    double a0[K], a1[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) a0[k] = a1[k] = 0.0;
+    if (j < N) {
+        const double* col = X + i0 * ld + j;
+        int64_t i = i0;
+        constexpr int U = 8;
+        for (; i + U <= i1; i += U) {
+            v2d xv[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) xv[u] = ld_stream(col + (int64_t)u * ld);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const double ave = mave[i + u];
+                const double sg = msig[i + u];
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    const double w = sg * xs.p[k][i + u];
+                    a0[k] += (xv[u].x - ave) * w;
+                    a1[k] += (xv[u].y - ave) * w;
+                }
+            }
+            col += (int64_t)U * ld;
+        }
+        for (; i < i1; ++i) {
+            const v2d xv = ld_stream(col);
+            const double ave = mave[i];
+            const double sg = msig[i];
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const double w = sg * xs.p[k][i];
+                a0[k] += (xv.x - ave) * w;
+                a1[k] += (xv.y - ave) * w;
+            }
+            col += ld;
+        }
+        double* dst = part + (int64_t)blockIdx.y * K * ld + j;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            dst[(int64_t)k * ld] = a0[k];
+            if (j + 1 < N) dst[(int64_t)k * ld + 1] = a1[k];
+        }
+    }
+}
+
+AxPlan ax_plan(int64_t N, int64_t M) {
+    AxPlan p;
+    p.tiles = (int)cdiv(N, 512);
+    int64_t target = 2048;  // 8 workgroups per CU on 256 CUs
+    int64_t nch = cdiv(target, p.tiles);
+    int64_t maxch = M / 64 > 0 ? M / 64 : 1;  // at least 64 markers per chunk
+    if (nch > maxch) nch = maxch;
+    if (nch < 1) nch = 1;
+    p.chunk = cdiv(M, nch);
+    if (p.chunk < 1) p.chunk = 1;
+    p.nchunks = (int)cdiv(M, p.chunk);
+    if (p.nchunks < 1) p.nchunks = 1;
+    return p;
+}
+
+hipError_t ax_partial(const Shard& s, const AxPlan& pl, int K, CPtrs x, double* part, hipStream_t st) {
+    dim3 grid(pl.tiles, pl.nchunks), block(kBlock);
+    switch (K) {
+        case 1: hipLaunchKernelGGL(ax_partial_kernel<1>, grid, block, 0, st, s.X, s.ld, s.N, s.M, s.mave, s.msig, x, pl.chunk, part); break;
+        case 2: hipLaunchKernelGGL(ax_partial_kernel<2>, grid, block, 0, st, s.X, s.ld, s.N, s.M, s.mave, s.msig, x, pl.chunk, part); break;
+        case 3: hipLaunchKernelGGL(ax_partial_kernel<3>, grid, block, 0, st, s.X, s.ld, s.N, s.M, s.mave, s.msig, x, pl.chunk, part); break;
+        case 4: hipLaunchKernelGGL(ax_partial_kernel<4>, grid, block, 0, st, s.X, s.ld, s.N, s.M, s.mave, s.msig, x, pl.chunk, part); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(kBlock) void ax_reduce_kernel(int K, int64_t N, int64_t ld, int nchunks,
+                                                           const double* __restrict__ part, Ptrs out,
+                                                           double div) {
+    const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (e >= (int64_t)K * N) return;
+    const int k = (int)(e / N);
+    const int64_t j = e - (int64_t)k * N;
+    const double* p = part + (int64_t)k * ld + j;
+    const int64_t stride = (int64_t)K * ld;
+    double s = 0.0;
+    int c = 0;
+    for (; c + 4 <= nchunks; c += 4) {
+        const double q0 = p[(int64_t)(c + 0) * stride], q1 = p[(int64_t)(c + 1) * stride];
+        const double q2 = p[(int64_t)(c + 2) * stride], q3 = p[(int64_t)(c + 3) * stride];
+        s += q0;
+        s += q1;
+        s += q2;
+        s += q3;
+    }
+    for (; c < nchunks; ++c) s += p[(int64_t)c * stride];
+    if (div > 0.0) s /= div;  // src/data.cpp:369-370: Ax_total[i] /= sqrt(N)
+    out.p[k][j] = s;
+}
+
+hipError_t ax_reduce(const AxPlan& pl, int K, int64_t N, int64_t ld, const double* part, Ptrs out, double div,
+                     hipStream_t st) {
+    const int64_t n = (int64_t)K * N;
+    hipLaunchKernelGGL(ax_reduce_kernel, dim3((unsigned)cdiv(n, kBlock)), dim3(kBlock), 0, st, K, N, ld, pl.nchunks,
+                       part, out, div);
+    return hipGetLastError();
+}
+
+__global__ void vec_div_kernel(int K, int64_t n, Ptrs v, double div) {
+    const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (e >= (int64_t)K * n) return;
+    const int k = (int)(e / n);
+    const int64_t j = e - (int64_t)k * n;
+    v.p[k][j] /= div;
+}
+
+hipError_t vec_div(int K, int64_t n, int64_t /*ld*/, Ptrs v, double div, hipStream_t st) {
+    hipLaunchKernelGGL(vec_div_kernel, dim3((unsigned)cdiv((int64_t)K * n, kBlock)), dim3(kBlock), 0, st, K, n, v,
+                       div);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// A^T.u  (data::ATx + data::dot_product, src/data.cpp:294-333)
+// ---------------------------------------------------------------------------
+// A wave owns G consecutive markers; lanes stride the samples two at a time,
+// so each load instruction reads 1 KiB of one column.  Every u value loaded
+// serves G markers.  The wave's partial dots are reduced with a DPP-style xor
+// butterfly; mode 1 fuses the lmmse_mult epilogue (src/vamp.cpp:656-659) and
+// the <d,p> partial of the next CG step.
+template <int G, int K, int MODE>
+__global__ __launch_bounds__(kBlock) void atx_kernel(const double* __restrict__ X, int64_t ld, int64_t N, int64_t M,
+                                                     const double* __restrict__ mave,
+                                                     const double* __restrict__ msig, CPtrs u, Ptrs out,
+                                                     double scale, double tau, double gam2, CPtrs pv,
+                                                     double* __restrict__ dp_part) {
+    __shared__ double lds[4][K];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t m0 = ((int64_t)blockIdx.x * 4 + wave) * G;
+    double acc[G][K];
+    double mu[G];
+    const double* col[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        const int64_t m = (m0 + g < M) ? m0 + g : M - 1;  // clamp: in-bounds, discarded
+        mu[g] = mave[m];
+        col[g] = X + m * ld;
+#pragma unroll
+        for (int k = 0; k < K; ++k) acc[g][k] = 0.0;
+    }
+    int64_t j = 2 * lane;
+    for (; j + 128 < N; j += 256) {
+        v2d uu0[K], uu1[K], x0[G], x1[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            x0[g] = ld_stream(col[g] + j);
+            x1[g] = ld_stream(col[g] + j + 128);
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            uu0[k] = ld2(u.p[k] + j);
+            uu1[k] = ld2(u.p[k] + j + 128);
+        }
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const double d0 = x0[g].x - mu[g], d1 = x0[g].y - mu[g];
+            const double d2 = x1[g].x - mu[g], d3 = x1[g].y - mu[g];
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                acc[g][k] += d0 * uu0[k].x;
+                acc[g][k] += d1 * uu0[k].y;
+                acc[g][k] += d2 * uu1[k].x;
+                acc[g][k] += d3 * uu1[k].y;
+            }
+        }
+    }
+    for (; j < N; j += 128) {  // tail; j+1 may be the zero pad row (u pad is zero too)
+        v2d uu[K], xx[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) xx[g] = ld_stream(col[g] + j);
+#pragma unroll
+        for (int k = 0; k < K; ++k) uu[k] = ld2(u.p[k] + j);
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const double d0 = xx[g].x - mu[g], d1 = xx[g].y - mu[g];
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                acc[g][k] += d0 * uu[k].x;
+                acc[g][k] += d1 * uu[k].y;
+            }
+        }
+    }
+    double dpw[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) dpw[k] = 0.0;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const double dot = wave_sum(acc[g][k]);
+            const int64_t m = m0 + g;
+            if (m < M) {
+                double val = msig[m] * dot;  // sigma_inv * dpa
+                val *= scale;                // ATx[mloc] *= 1/sqrt(N)
+                if (MODE == 1) {
+                    const double pm = pv.p[k][m];
+                    val *= tau;              // res[i] *= tau
+                    val += gam2 * pm;        // res[i] += gam2 * v[i]
+                    dpw[k] += val * pm;
+                }
+                if (lane == 0) out.p[k][m] = val;
+            }
+        }
+    }
+    if (MODE == 1) {
+        if (lane == 0) {
+#pragma unroll
+            for (int k = 0; k < K; ++k) lds[wave][k] = dpw[k];
+        }
+        __syncthreads();
+        if (threadIdx.x < K) {
+            const int k = threadIdx.x;
+            dp_part[(int64_t)blockIdx.x * K + k] = ((lds[0][k] + lds[1][k]) + lds[2][k]) + lds[3][k];
+        }
+    }
+}
+
+static constexpr int kAtxG = 4;
+int atx_blocks(int64_t M) { return (int)cdiv(M, 4 * kAtxG); }
+
+template <int K, int MODE>
+static void launch_atx(const Shard& s, CPtrs u, Ptrs out, double scale, double tau, double gam2, CPtrs p,
+                       double* dp_part, hipStream_t st) {
+    hipLaunchKernelGGL((atx_kernel<kAtxG, K, MODE>), dim3(atx_blocks(s.M)), dim3(kBlock), 0, st, s.X, s.ld, s.N, s.M,
+                       s.mave, s.msig, u, out, scale, tau, gam2, p, dp_part);
+}
+
+hipError_t atx(const Shard& s, int K, CPtrs u, Ptrs out, double scale, int mode, double tau, double gam2, CPtrs p,
+               double* dp_part, hipStream_t st) {
+    if (mode == 0) {
+        switch (K) {
+            case 1: launch_atx<1, 0>(s, u, out, scale, tau, gam2, p, dp_part, st); break;
+            case 2: launch_atx<2, 0>(s, u, out, scale, tau, gam2, p, dp_part, st); break;
+            case 3: launch_atx<3, 0>(s, u, out, scale, tau, gam2, p, dp_part, st); break;
+            case 4: launch_atx<4, 0>(s, u, out, scale, tau, gam2, p, dp_part, st); break;
+            default: return hipErrorInvalidValue;
+        }
+    } else {
+        switch (K) {
+            case 1: launch_atx<1, 1>(s, u, out, scale, tau, gam2, p, dp_part, st); break;
+            case 2: launch_atx<2, 1>(s, u, out, scale, tau, gam2, p, dp_part, st); break;
+            case 3: launch_atx<3, 1>(s, u, out, scale, tau, gam2, p, dp_part, st); break;
+            case 4: launch_atx<4, 1>(s, u, out, scale, tau, gam2, p, dp_part, st); break;
+            default: return hipErrorInvalidValue;
+        }
+    }
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// marker statistics (src/data.cpp:233-283): one wave per marker, two passes
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void stats_kernel(const double* __restrict__ X, int64_t ld, int64_t N, int64_t M,
+                                                       double nonas, double alpha_scale, double* __restrict__ mave,
+                                                       double* __restrict__ msig) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t m = (int64_t)blockIdx.x * 4 + wave;
+    if (m >= M) return;
+    const double* col = X + m * ld;
+    double s = 0.0;
+    for (int64_t j = 2 * lane; j < N; j += 128) {
+        const v2d x = ld2(col + j);
+        s += x.x;
+        if (j + 1 < N) s += x.y;
+    }
+    s = wave_sum(s);
+    const double mean = s / nonas;
+    double q = 0.0;
+    for (int64_t j = 2 * lane; j < N; j += 128) {
+        const v2d x = ld2(col + j);
+        const double a = x.x - mean;
+        q += a * a;
+        if (j + 1 < N) {
+            const double b = x.y - mean;
+            q += b * b;
+        }
+    }
+    q = wave_sum(q);
+    if (lane == 0) {
+        mave[m] = mean;
+        double sg;
+        if (q != 0.0) {
+            if (alpha_scale == 1.0)
+                sg = 1.0 / sqrt(q / (nonas - 1.0));
+            else
+                sg = 1.0 / pow(sqrt(q / (nonas - 1.0)), alpha_scale);
+        } else {
+            sg = 1.0;
+        }
+        msig[m] = sg;
+    }
+}
+
+hipError_t marker_stats(const double* X, int64_t ld, int64_t N, int64_t M, double nonas, double alpha_scale,
+                        double* mave, double* msig, hipStream_t st) {
+    if (M <= 0) return hipSuccess;
+    hipLaunchKernelGGL(stats_kernel, dim3((unsigned)cdiv(M, 4)), dim3(kBlock), 0, st, X, ld, N, M, nonas, alpha_scale,
+                       mave, msig);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// synthetic data
+// ---------------------------------------------------------------------------
+__global__ void gen_kernel(uint64_t seed, int kind, int64_t N, int64_t ld, int64_t S, int64_t M, double* X) {
+    const int64_t total = M * ld;
+    for (int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x; e < total; e += (int64_t)gridDim.x * kBlock) {
+        const int64_t i = e / ld, j = e - i * ld;
+        double v = 0.0;
+        if (j < N) v = kind == 1 ? meth_dyadic(seed, S + i, j) : gauss_dyadic(seed, S + i, j);
+        X[e] = v;
+    }
+}
+
+hipError_t gen_markers(uint64_t seed, int kind, int64_t N, int64_t ld, int64_t S, int64_t M, double* X,
+                       hipStream_t st) {
+    int64_t blocks = cdiv(M * ld, kBlock);
+    if (blocks > 65536) blocks = 65536;
+    if (blocks < 1) return hipSuccess;
+    hipLaunchKernelGGL(gen_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, st, seed, kind, N, ld, S, M, X);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(kBlock) void gen_beta_kernel(uint64_t seed, double lam, int64_t S, int64_t M,
+                                                          double* beta, double* cnt_part) {
+    __shared__ double lds[4];
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    double c = 0.0;
+    if (i < M) {
+        const uint64_t h = splitmix64(splitmix64(seed ^ 0x63617573ULL) + (uint64_t)(S + i));
+        const double uni = (double)(h >> 11) * (1.0 / 9007199254740992.0);
+        const bool causal = uni < lam;
+        beta[i] = causal ? gauss_dyadic(seed ^ 0x62657461ULL, S + i, 0) : 0.0;
+        c = causal ? 1.0 : 0.0;
+    }
+    c = block_sum(c, lds);
+    if (threadIdx.x == 0) cnt_part[blockIdx.x] = c;
+}
+
+hipError_t gen_beta(uint64_t seed, double lam, int64_t S, int64_t M, double* beta, double* cnt_part, int* nblk,
+                    hipStream_t st) {
+    *nblk = (int)cdiv(M, kBlock);
+    if (*nblk < 1) return hipSuccess;
+    hipLaunchKernelGGL(gen_beta_kernel, dim3(*nblk), dim3(kBlock), 0, st, seed, lam, S, M, beta, cnt_part);
+    return hipGetLastError();
+}
+
+__global__ void scale_kernel(int64_t n, double* v, double a) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) v[i] *= a;
+}
+
+hipError_t scale_vec(int64_t n, double* v, double a, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(scale_kernel, dim3((unsigned)cdiv(n, kBlock)), dim3(kBlock), 0, st, n, v, a);
+    return hipGetLastError();
+}
+
+__global__ void noise_kernel(uint64_t seed, int64_t N, double sd, double* y) {
+    const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (j < N) y[j] = y[j] + sd * gauss_dyadic(seed ^ 0x6E6F697365ULL, -1, j);
+}
+
+hipError_t add_noise(uint64_t seed, int64_t N, double sd, double* y, hipStream_t st) {
+    hipLaunchKernelGGL(noise_kernel, dim3((unsigned)cdiv(N, kBlock)), dim3(kBlock), 0, st, seed, N, sd, y);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// reductions (inner_prod / l2_norm2, src/utilities.cpp:138-162)
+// ---------------------------------------------------------------------------
+int red_blocks(int64_t n) {
+    int64_t b = cdiv(n, 2048);
+    if (b < 1) b = 1;
+    if (b > kRedBlocks) b = kRedBlocks;
+    return (int)b;
+}
+
+__global__ __launch_bounds__(kBlock) void dots_kernel(DotArgs a, int64_t n, double* __restrict__ part) {
+    __shared__ double lds[4];
+    double acc[kMaxTerms];
+#pragma unroll
+    for (int q = 0; q < kMaxTerms; ++q) acc[q] = 0.0;
+    for (int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x; e < n; e += (int64_t)gridDim.x * kBlock) {
+#pragma unroll
+        for (int q = 0; q < kMaxTerms; ++q) {
+            if (q < a.nt) {
+                const DotTerm& t = a.t[q];
+                if (t.op == DOT) {
+                    acc[q] += t.a[e] * t.b[e];
+                } else if (t.op == DIFF2) {
+                    const double d = t.a[e] - t.b[e];
+                    acc[q] += d * d;
+                } else {
+                    acc[q] += t.a[e];
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < kMaxTerms; ++q) {
+        if (q < a.nt) {
+            const double s = block_sum(acc[q], lds);
+            if (threadIdx.x == 0) part[(int64_t)blockIdx.x * a.nt + q] = s;
+        }
+    }
+}
+
+hipError_t dots_partial(const DotArgs& a, int64_t n, double* part, hipStream_t st) {
+    hipLaunchKernelGGL(dots_kernel, dim3(red_blocks(n)), dim3(kBlock), 0, st, a, n, part);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(kBlock) void sum_partials_kernel(const double* __restrict__ part, int nblk, int nq,
+                                                              double* __restrict__ out) {
+    __shared__ double lds[4];
+    for (int q = 0; q < nq; ++q) {
+        double s = 0.0;
+        for (int b = threadIdx.x; b < nblk; b += kBlock) s += part[(int64_t)b * nq + q];
+        s = block_sum(s, lds);
+        if (threadIdx.x == 0) out[q] = s;
+    }
+}
+
+hipError_t sum_partials(const double* part, int nblk, int nq, double* out, hipStream_t st) {
+    hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(kBlock), 0, st, part, nblk, nq, out);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// denoiser: vamp::g1 / vamp::g1d (src/vamp.cpp:440-492)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void g1_g1d(double y, double gam1, const Mix& mix, double eta_max, double* g,
+                                       double* gd) {
+    const double sigma = 1 / gam1;
+    if (sigma < 1e-10 && sigma > -1e-10) {
+        *g = y;
+        *gd = 1;
+        return;
+    }
+    double pk = 0, pkd = 0, pkdd = 0;
+    for (int i = 0; i < mix.L; ++i) {
+        const double vs = mix.vars[i] + sigma;
+        const double expe_sum = -0.5 * (y * y) * (eta_max - mix.vars[i]) / vs / (eta_max + sigma);
+        const double ex = exp(expe_sum);
+        double z = mix.probs[i] / sqrt(vs) * ex;
+        pk = pk + z;
+        z = z / vs * y;
+        pkd = pkd - z;
+        const double z2 = z / vs * y;
+        pkdd = pkdd - mix.probs[i] / pow(vs, 1.5) * ex + z2;
+    }
+    *g = y + sigma * pkd / pk;
+    const double q = pkd / pk;
+    *gd = 1 + sigma * (pkdd / pk - q * q);
+}
+
+__global__ __launch_bounds__(kBlock) void denoise_kernel(int64_t M, const double* __restrict__ r1, double gam1,
+                                                         Mix mix, double eta_max, double* __restrict__ x1,
+                                                         const double* __restrict__ x1_prev, int damp, double rho,
+                                                         double* __restrict__ x1d, double* __restrict__ part) {
+    __shared__ double lds[4];
+    double acc = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < M; i += (int64_t)gridDim.x * kBlock) {
+        double g, gd;
+        g1_g1d(r1[i], gam1, mix, eta_max, &g, &gd);
+        if (damp) g = rho * g + (1 - rho) * x1_prev[i];  // src/vamp.cpp:208-211
+        x1[i] = g;
+        x1d[i] = gd;
+        acc += gd;
+    }
+    acc = block_sum(acc, lds);
+    if (threadIdx.x == 0) part[blockIdx.x] = acc;
+}
+
+hipError_t denoise(int64_t M, const double* r1, double gam1, const Mix& mix, double* x1, const double* x1_prev,
+                   int damp, double rho, double* x1d, double* part, int* nblk, hipStream_t st) {
+    double eta_max = mix.vars[0];
+    for (int i = 1; i < mix.L; ++i)
+        if (mix.vars[i] > eta_max) eta_max = mix.vars[i];
+    *nblk = red_blocks(M);
+    hipLaunchKernelGGL(denoise_kernel, dim3(*nblk), dim3(kBlock), 0, st, M, r1, gam1, mix, eta_max, x1, x1_prev,
+                       damp, rho, x1d, part);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// EM prior update sums (src/vamp.cpp:554-597), one marker per thread
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double em_num(const EmArgs& a, double r, int j) {
+    return a.lambda * a.omegas[j] *
+           exp(-(r * r) / 2 * (a.max_sigma - a.vars[j]) / (a.vars[j] + a.noise_var) / (a.max_sigma + a.noise_var)) /
+           sqrt(a.vars[j] + a.noise_var) / sqrt(2 * M_PI);
+}
+
+__global__ __launch_bounds__(kBlock) void em_kernel(int64_t M, const double* __restrict__ r1, EmArgs a,
+                                                    double* __restrict__ part) {
+    __shared__ double lds[4];
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const bool valid = i < M;
+    const double r = valid ? r1[i] : 0.0;
+    const int L = a.L, Q = 1 + 2 * (L - 1);
+    double sum_of_elems = 0.0;
+    for (int j = 1; j < L; ++j) sum_of_elems += em_num(a, r, j);
+    const double pin = 1 / (1 + (1 - a.lambda) / sqrt(2 * M_PI * a.noise_var) *
+                                    exp(-(r * r) / 2 * a.max_sigma / a.noise_var / (a.noise_var + a.max_sigma)) /
+                                    sum_of_elems);
+    double s = block_sum(valid ? pin : 0.0, lds);
+    if (threadIdx.x == 0) part[(int64_t)blockIdx.x * Q] = s;
+    for (int j = 1; j < L; ++j) {
+        const double beta = em_num(a, r, j) / sum_of_elems;
+        const double g = a.gam1 * r / (1 / a.vars[j] + a.gam1);
+        const double gam = beta * (g * g + a.v[j - 1]);
+        const double sb = block_sum(valid ? beta * pin : 0.0, lds);
+        const double sg = block_sum(valid ? gam * pin : 0.0, lds);
+        if (threadIdx.x == 0) {
+            part[(int64_t)blockIdx.x * Q + j] = sb;
+            part[(int64_t)blockIdx.x * Q + (L - 1) + j] = sg;
+        }
+    }
+}
+
+hipError_t em_sums(int64_t M, const double* r1, const EmArgs& a, double* part, int* nblk, hipStream_t st) {
+    *nblk = (int)cdiv(M, kBlock);
+    if (*nblk < 1) *nblk = 1;
+    hipLaunchKernelGGL(em_kernel, dim3(*nblk), dim3(kBlock), 0, st, M, r1, a, part);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// elementwise
+// ---------------------------------------------------------------------------
+__global__ void lincomb_div_kernel(int64_t n, double a, const double* __restrict__ x, double b,
+                                   const double* __restrict__ y, double c, double* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) out[i] = (a * x[i] - b * y[i]) / c;
+}
+
+hipError_t lincomb_div(int64_t n, double a, const double* x, double b, const double* y, double c, double* out,
+                       hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(lincomb_div_kernel, dim3((unsigned)cdiv(n, kBlock)), dim3(kBlock), 0, st, n, a, x, b, y, c,
+                       out);
+    return hipGetLastError();
+}
+
+__global__ void axpby_kernel(int64_t n, double a, const double* __restrict__ x, double b,
+                             const double* __restrict__ y, double* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) out[i] = a * x[i] + b * y[i];
+}
+
+hipError_t axpby(int64_t n, double a, const double* x, double b, const double* y, double* out, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(axpby_kernel, dim3((unsigned)cdiv(n, kBlock)), dim3(kBlock), 0, st, n, a, x, b, y, out);
+    return hipGetLastError();
+}
+
+__global__ void bern_kernel(uint64_t seed, int it, int64_t S, int64_t M, double sqrtMt, double* out) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < M) out[i] = (double)(2 * bern_bit(seed, it, S + i) - 1) / sqrtMt;
+}
+
+hipError_t bernoulli(uint64_t seed, int it, int64_t S, int64_t M, double sqrtMt, double* out, hipStream_t st) {
+    if (M <= 0) return hipSuccess;
+    hipLaunchKernelGGL(bern_kernel, dim3((unsigned)cdiv(M, kBlock)), dim3(kBlock), 0, st, seed, it, S, M, sqrtMt,
+                       out);
+    return hipGetLastError();
+}
+
+__global__ void div_scalar_kernel(int64_t n, const double* __restrict__ x, double d, double* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) out[i] = x[i] / d;
+}
+
+hipError_t div_scalar(int64_t n, const double* x, double d, double* out, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(div_scalar_kernel, dim3((unsigned)cdiv(n, kBlock)), dim3(kBlock), 0, st, n, x, d, out);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// PCG vector steps (src/vamp.cpp:671-757), K right-hand sides per launch
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void cg_init_kernel(int K, int64_t M, CgVecs c, double diag,
+                                                         double* __restrict__ part) {
+    __shared__ double lds[4];
+    double acc[2 * kMaxRhs];
+#pragma unroll
+    for (int q = 0; q < 2 * kMaxRhs; ++q) acc[q] = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < M; i += (int64_t)gridDim.x * kBlock) {
+#pragma unroll
+        for (int k = 0; k < kMaxRhs; ++k) {
+            if (k < K) {
+                const double vi = c.v[k][i];
+                const double r = c.d[k] ? vi - c.d[k][i] : vi - 0.0;  // r = v - lmmse_mult(mu0)
+                const double z = r / diag;
+                c.r[k][i] = r;
+                c.z[k][i] = z;
+                c.p[k][i] = z;
+                acc[2 * k] += r * z;
+                acc[2 * k + 1] += vi * vi;
+            }
+        }
+    }
+    for (int q = 0; q < 2 * K; ++q) {
+        double v = 0.0;
+#pragma unroll
+        for (int t = 0; t < 2 * kMaxRhs; ++t)
+            if (t == q) v = acc[t];
+        const double s = block_sum(v, lds);
+        if (threadIdx.x == 0) part[(int64_t)blockIdx.x * 2 * K + q] = s;
+    }
+}
+
+hipError_t cg_init(int K, int64_t M, const CgVecs& c, double diag, double* part, int* nblk, hipStream_t st) {
+    *nblk = red_blocks(M);
+    hipLaunchKernelGGL(cg_init_kernel, dim3(*nblk), dim3(kBlock), 0, st, K, M, c, diag, part);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(kBlock) void cg_update_kernel(int K, int64_t M, CgVecs c, double diag, CgScalars rz,
+                                                           const double* __restrict__ dp_dev,
+                                                           double* __restrict__ part) {
+    __shared__ double lds[4];
+    double alpha[kMaxRhs];
+#pragma unroll
+    for (int k = 0; k < kMaxRhs; ++k) alpha[k] = k < K ? rz.rz[k] / dp_dev[k] : 0.0;
+    double acc[3 * kMaxRhs];
+#pragma unroll
+    for (int q = 0; q < 3 * kMaxRhs; ++q) acc[q] = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < M; i += (int64_t)gridDim.x * kBlock) {
+#pragma unroll
+        for (int k = 0; k < kMaxRhs; ++k) {
+            if (k < K) {
+                const double pi = c.p[k][i];
+                const double mu = c.mu[k][i] + alpha[k] * pi;  // mu += alpha * p
+                const double r = c.r[k][i] - c.d[k][i] * alpha[k];  // r -= d * alpha
+                const double z = r / diag;
+                c.mu[k][i] = mu;
+                c.r[k][i] = r;
+                c.z[k][i] = z;
+                acc[3 * k] += r * z;
+                acc[3 * k + 1] += r * r;
+                acc[3 * k + 2] += c.v[k][i] * mu;
+            }
+        }
+    }
+    for (int q = 0; q < 3 * K; ++q) {
+        double v = 0.0;
+#pragma unroll
+        for (int t = 0; t < 3 * kMaxRhs; ++t)
+            if (t == q) v = acc[t];
+        const double s = block_sum(v, lds);
+        if (threadIdx.x == 0) part[(int64_t)blockIdx.x * 3 * K + q] = s;
+    }
+}
+
+hipError_t cg_update(int K, int64_t M, const CgVecs& c, double diag, CgScalars rz, const double* dp_dev, double* part,
+                     int* nblk, hipStream_t st) {
+    *nblk = red_blocks(M);
+    hipLaunchKernelGGL(cg_update_kernel, dim3(*nblk), dim3(kBlock), 0, st, K, M, c, diag, rz, dp_dev, part);
+    return hipGetLastError();
+}
+
+__global__ void cg_pupdate_kernel(int K, int64_t M, CgVecs c, CgBeta b) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= M) return;
+#pragma unroll
+    for (int k = 0; k < kMaxRhs; ++k)
+        if (k < K) c.p[k][i] = c.z[k][i] + b.beta[k] * c.p[k][i];
+}
+
+hipError_t cg_pupdate(int K, int64_t M, const CgVecs& c, CgBeta b, hipStream_t st) {
+    if (M <= 0) return hipSuccess;
+    hipLaunchKernelGGL(cg_pupdate_kernel, dim3((unsigned)cdiv(M, kBlock)), dim3(kBlock), 0, st, K, M, c, b);
+    return hipGetLastError();
+}
+
+}  // namespace vk

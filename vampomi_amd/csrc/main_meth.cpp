@@ -1,0 +1,169 @@
+// main_meth.cpp — drop-in for the reference's main_meth.exe (src/main_meth.cpp)
+// in --run-mode infere, linear model: same flags, same output files.
+//
+// Ranks: the reference is launched with `mpirun -np P`; this binary runs one
+// process per GPU, rank/size from VAMPOMI_RANK/VAMPOMI_NRANKS (or the
+// torchrun variables RANK/WORLD_SIZE, LOCAL_RANK for the device).  The RCCL
+// communicator id is handed from rank 0 to the others through a rendezvous
+// file (VAMPOMI_RDZV, default <out-dir>/.<out-name>.rdzv).
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <iostream>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/vampomi.h"
+#include "hostio.h"
+#include "options.h"
+
+static int env_int(const char* a, const char* b, int dflt) {
+    const char* v = std::getenv(a);
+    if (!v && b) v = std::getenv(b);
+    return v ? std::atoi(v) : dflt;
+}
+
+static bool exchange_id(const std::string& path, int rank, unsigned char* id) {
+    if (rank == 0) {
+        if (vampomi_comm_unique_id(id) != VAMPOMI_OK) return false;
+        const std::string tmp = path + ".tmp";
+        std::ofstream f(tmp, std::ios::binary);
+        f.write((const char*)id, VAMPOMI_UNIQUE_ID_BYTES);
+        f.close();
+        return std::rename(tmp.c_str(), path.c_str()) == 0;
+    }
+    for (int t = 0; t < 6000; ++t) {  // up to 10 minutes
+        std::ifstream f(path, std::ios::binary);
+        if (f.good()) {
+            f.read((char*)id, VAMPOMI_UNIQUE_ID_BYTES);
+            if (f.gcount() == VAMPOMI_UNIQUE_ID_BYTES) return true;
+        }
+        std::this_thread::sleep_for(std::chrono::milliseconds(100));
+    }
+    return false;
+}
+
+static int die(const char* what) {
+    std::cout << "FATAL  : " << what << ": " << vampomi_last_error() << std::endl;
+    return EXIT_FAILURE;
+}
+
+int main(int argc, char** argv) {
+    vopt::Options opt;
+    std::string echo;
+    const int rank = env_int("VAMPOMI_RANK", "RANK", 0);
+    const int nranks = env_int("VAMPOMI_NRANKS", "WORLD_SIZE", 1);
+    if (!vopt::parse(argc, argv, opt, echo)) return EXIT_FAILURE;
+    if (rank == 0) std::cout << echo << std::endl;
+
+    int64_t M = 0, S = 0, Mm = 0;
+    vampomi_divide_work(opt.Mt, nranks, rank, &M, &S, &Mm);
+    std::printf("INFO   : rank %4d has %lld markers over tot Mt = %u, max Mm = %lld, starting at S = %lld\n", rank,
+                (long long)M, opt.Mt, (long long)Mm, (long long)S);
+
+    if (opt.run_mode != "infere") {
+        std::cout << "FATAL  : run mode \"" << opt.run_mode << "\" is not provided by this build (infere only)"
+                  << std::endl;
+        return EXIT_FAILURE;
+    }
+    if (opt.model != "linear") {
+        std::cout << "FATAL  : model \"" << opt.model << "\" is not provided by this build (linear only)" << std::endl;
+        return EXIT_FAILURE;
+    }
+
+    unsigned char id[VAMPOMI_UNIQUE_ID_BYTES] = {0};
+    if (nranks > 1) {
+        const char* rz = std::getenv("VAMPOMI_RDZV");
+        const std::string path = rz ? rz : opt.out_dir + "/." + opt.out_name + ".rdzv";
+        if (!exchange_id(path, rank, id)) return die("communicator rendezvous failed");
+    }
+    vampomi_shard_desc d{};
+    d.N = opt.N;
+    d.Mt = opt.Mt;
+    d.rank = rank;
+    d.nranks = nranks;
+    d.device = env_int("LOCAL_RANK", nullptr, -1);
+    d.comm_id = nranks > 1 ? id : nullptr;
+    d.alpha_scale = opt.alpha_scale;
+    vampomi_ctx* ctx = nullptr;
+    if (vampomi_open(&d, &ctx) != VAMPOMI_OK) return die("cannot open the device context");
+
+    // data::data: phenotype first (standardised for the linear model), then the shard
+    auto t0 = std::chrono::steady_clock::now();
+    if (vampomi_read_phen(ctx, opt.phen_file.c_str(), 1) != VAMPOMI_OK) return die("phenotype");
+    if (rank == 0) std::cout << "meth file name = " << opt.meth_file << std::endl;
+    if (vampomi_load_meth_file(ctx, opt.meth_file.c_str()) != VAMPOMI_OK) return die("methylation data");
+    if (rank == 0)
+        std::cout << "reading methylation data took "
+                  << std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() << " seconds."
+                  << std::endl;
+
+    std::vector<double> ts, init;
+    if (!opt.true_signal_file.empty()) {  // src/main_meth.cpp:69-73
+        ts.assign((size_t)M, 0.0);
+        vio::read_vec(opt.true_signal_file, ts.data(), S, M);
+    }
+    if (!opt.estimate_file.empty()) {  // src/main_meth.cpp:75-80
+        init.assign((size_t)M, 0.0);
+        vio::read_vec(opt.estimate_file, init.data(), S, M);
+    }
+
+    vampomi_params p;
+    vampomi_params_default(&p);
+    p.gam1 = opt.gam1;
+    p.h2 = opt.h2;
+    p.max_iter = (int)opt.iterations;
+    p.CG_max_iter = (int)opt.CG_max_iter;
+    p.CG_err_tol = opt.CG_err_tol;
+    p.EM_max_iter = (int)opt.EM_max_iter;
+    p.EM_err_thr = opt.EM_err_thr;
+    p.rho = opt.rho;
+    p.learn_vars = (int)opt.learn_vars;
+    p.learn_prior_delay = (int)opt.learn_prior_delay;
+    p.stop_criteria_thr = opt.stop_criteria_thr;
+    p.merge_vars_thr = opt.merge_vars_thr;
+    if (opt.vars.size() != opt.probs.size() || opt.vars.empty() || opt.vars.size() > VAMPOMI_MAX_L) {
+        std::cout << "FATAL  : --vars and --probs must have the same number (1.." << VAMPOMI_MAX_L << ") of entries"
+                  << std::endl;
+        return EXIT_FAILURE;
+    }
+    p.L = (int)opt.vars.size();
+    for (int j = 0; j < p.L; ++j) {
+        p.vars[j] = opt.vars[j];
+        p.probs[j] = opt.probs[j];
+    }
+    p.seed = opt.seed;
+    p.out_dir = opt.out_dir.c_str();
+    p.out_name = opt.out_name.c_str();
+    p.verbosity = opt.verbosity;
+    p.true_signal = ts.empty() ? nullptr : ts.data();
+    p.x1hat_init = init.empty() ? nullptr : init.data();
+    p.batch_rhs = opt.batch_rhs;
+    p.model = opt.model.c_str();
+
+    std::vector<int> cg((size_t)p.max_iter), ons((size_t)p.max_iter);
+    vampomi_result r{};
+    r.cg_iters = cg.data();
+    r.ons_iters = ons.data();
+    auto t1 = std::chrono::steady_clock::now();
+    if (vampomi_infere(ctx, &p, &r) != VAMPOMI_OK) return die("inference");
+    const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count();
+    if (rank == 0) {
+        std::cout << "iterations run = " << r.iterations_run << ", total computation time = " << secs
+                  << " s, A-passes executed = " << r.a_passes_exec << " (reference-equivalent " << r.a_passes_ref
+                  << ")" << std::endl;
+        for (int i = 0; i < r.iterations_run; ++i)
+            std::cout << "it " << (i + 1) << ": CG iterations " << cg[i] << ", onsager CG iterations " << ons[i]
+                      << std::endl;
+    }
+    vampomi_barrier(ctx);
+    vampomi_close(ctx);
+    return 0;
+}
