@@ -203,7 +203,7 @@ def test_cli_drop_in_files(tmp_path):
             b = np.fromfile(out_o / (pat % it), dtype="<f8")
             assert a.shape == b.shape == (Mt,)
             assert relerr(a, b) <= 1e-10
-    assert relerr(np.fromfile(out_g / "ex_it_%d.bin" % its, dtype="<f8"), ref["x1_final"]) <= 1e-10
+    assert relerr(np.fromfile(out_g / ("ex_it_%d.bin" % its), dtype="<f8"), ref["x1_final"]) <= 1e-10
 
 
 def test_cli_resume_from_estimate_file(tmp_path):
@@ -261,5 +261,6 @@ def test_c2_shape_properties():
         b = va.Vamp(d, va.VampOptions(max_iter=3, stop_criteria_thr=0.0, batch_rhs=0), true_signal=beta)
         b.infere(keep_hist=True)
         assert np.array_equal(a.x1_hist[:3], b.x1_hist[:3])
-        assert np.all(np.isfinite(a.metrics[:3]))
-        assert a.metrics[2, 3] > 0.3  # x2 correlation with the true signal
+        # x1 = 0 at iteration 1, so its correlations are 0/0 (the reference writes -nan)
+        assert np.isnan(a.metrics[0, 1]) and np.all(np.isfinite(a.metrics[1:3]))
+        assert np.all(a.metrics[1:3, 3] > 0.1)  # x2 correlates with the true signal

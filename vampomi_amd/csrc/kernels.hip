@@ -42,6 +42,21 @@ __device__ __forceinline__ v2d ld_stream(const double* p) {
 
 __device__ __forceinline__ v2d ld2(const double* p) { return *reinterpret_cast<const v2d*>(p); }
 
+// x^1.5, correctly rounded except in hard midpoint cases (glibc's pow is within
+// 0.52 ulp, i.e. the same double in practice).  sqrt is correctly rounded;
+// e = x - s^2 and the product's low part are exact through fma, so
+// t + (t_lo + x*e/(2s)) is x*sqrt(x) to ~2^-105 before the final rounding.
+// g1d's pkdd term needs this: at gam1 = 1e-6 (sigma = 1e6) it feeds a
+// cancellation 1 + sigma*(...) ~ 5e-8 that amplifies one ulp ~1e7-fold.
+__device__ __forceinline__ double pow_1p5(double x) {
+    if (!(x > 0.0) || x == __builtin_huge_val()) return pow(x, 1.5);
+    const double s = sqrt(x);
+    const double e = __builtin_fma(-s, s, x);
+    const double t = x * s;
+    const double t_lo = __builtin_fma(x, s, -t);
+    return t + (t_lo + x * (e / (2.0 * s)));
+}
+
 __host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
     x += 0x9E3779B97F4A7C15ULL;
     x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
@@ -552,7 +567,7 @@ __device__ __forceinline__ void g1_g1d(double y, double gam1, const Mix& mix, do
         z = z / vs * y;
         pkd = pkd - z;
         const double z2 = z / vs * y;
-        pkdd = pkdd - mix.probs[i] / pow(vs, 1.5) * ex + z2;
+        pkdd = pkdd - mix.probs[i] / pow_1p5(vs) * ex + z2;
     }
     *g = y + sigma * pkd / pk;
     const double q = pkd / pk;
