@@ -37,17 +37,9 @@ import torch  # noqa: E402  (imported before libvampomi: one HIP runtime)
 import torch.distributed as dist  # noqa: E402
 
 import vampomi_amd as va  # noqa: E402
+from vampomi_amd.workloads import workload  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-
-
-def workload(cfg: str, n: int):
-    if cfg == "c3":
-        return {"workload": "c3-shard", "N": 100000, "Mt": 62500 * n, "kind": va.GEN_METH}
-    if n == 1:
-        return {"workload": "c2", "N": 10000, "Mt": 50000, "kind": va.GEN_GAUSS}
-    s = math.sqrt(n)
-    return {"workload": "c2-weak", "N": int(round(10000 * s)), "Mt": int(round(50000 * s)), "kind": va.GEN_GAUSS}
 
 
 def cpu_baseline(d: "va.Data", w: dict, beta: np.ndarray, seed: int, budget_s: float = 20.0) -> dict:

@@ -1,0 +1,84 @@
+"""The marker-sharded (N > 1) path with real processes: world_size 2 over
+torch.distributed/gloo on CPU.  Each rank runs the oracle on its divide_work
+shard with every MPI_Allreduce call site mapped to
+dist.all_reduce; the result must reproduce the single-rank run (the
+index-keyed Bernoulli probe makes the algorithm rank-count invariant)."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, out_dir, N, Mt, its):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+
+    from _data import make_problem
+    from oracle import pyoracle as O
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    X, y, beta = make_problem(N, Mt)
+    M, S, _ = O.divide_work(Mt, world, rank)
+
+    def allreduce(a):
+        t = torch.from_numpy(a.copy())
+        dist.all_reduce(t)
+        a[:] = t.numpy()
+
+    r = O.vamp_infere(X[S:S + M], y, Mt, S=S, rank=rank, nranks=world, true_signal=beta[S:S + M],
+                      max_iter=its, stop_criteria_thr=0.0, allreduce=allreduce)
+    np.savez(os.path.join(out_dir, f"r{rank}.npz"), x1=r["x1_final"], cg=r["cg_iters"], ons=r["ons_iters"],
+             params=r["params"], S=S, M=M)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2])
+def test_gloo_sharded_oracle_matches_single_rank(tmp_path, world):
+    import torch.multiprocessing as mp
+
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from _data import make_problem
+    from oracle import pyoracle as O
+
+    N, Mt, its = 500, 1003, 6
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), N, Mt, its), nprocs=world, join=True)
+    X, y, beta = make_problem(N, Mt)
+    one = O.vamp_infere(X, y, Mt, true_signal=beta, max_iter=its, stop_criteria_thr=0.0)
+    parts = [np.load(tmp_path / f"r{r}.npz", allow_pickle=False) for r in range(world)]
+    x = np.concatenate([p["x1"] for p in parts])
+    assert [int(p["S"]) for p in parts] == [0, 502]
+    assert np.linalg.norm(x - one["x1_final"]) / np.linalg.norm(one["x1_final"]) < 1e-12
+    for p in parts:
+        assert p["cg"].tolist() == one["cg_iters"].tolist()
+        assert p["ons"].tolist() == one["ons_iters"].tolist()
+        assert np.allclose(p["params"], one["params"], rtol=1e-11)
+
+
+def test_bench_weak_scaling_workloads_keep_per_gpu_bytes():
+    from vampomi_amd.workloads import workload
+
+    w1 = workload("c2", 1)
+    assert (w1["N"], w1["Mt"]) == (10000, 50000)
+    for n in (2, 4, 8):
+        w = workload("c2", n)
+        per_gpu = w["N"] * w["Mt"] / n
+        assert abs(per_gpu / (10000 * 50000) - 1) < 1e-3
+        assert abs(w["Mt"] / w["N"] - 5) < 1e-3
+    w8 = workload("c3", 8)
+    assert (w8["N"], w8["Mt"]) == (100000, 500000)

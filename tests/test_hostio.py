@@ -1,0 +1,75 @@
+"""The engine's host-side file formats (vampomi_amd/csrc/hostio.cpp) against
+the oracle's restatement of the reference writers/readers, byte for byte."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from oracle import pyoracle as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def harness(tmp_path_factory):
+    exe = tmp_path_factory.mktemp("h") / "harness"
+    subprocess.run(["g++", "-O1", "-std=c++17", "-I", os.path.join(ROOT, "vampomi_amd", "csrc"),
+                    os.path.join(ROOT, "tests", "hostio_harness.cpp"),
+                    os.path.join(ROOT, "vampomi_amd", "csrc", "hostio.cpp"), "-o", str(exe)], check=True)
+    return str(exe)
+
+
+def run(h, *args):
+    return subprocess.run([h, *map(str, args)], capture_output=True, text=True, check=True).stdout
+
+
+def test_csv_bytes_identical_to_oracle_writer(harness, tmp_path):
+    import ctypes as C
+
+    lib = O.load()
+    lib.orc_csv_header.argtypes = [C.c_char_p, C.POINTER(C.c_char_p), C.c_int]
+    lib.orc_csv_row.argtypes = [C.c_char_p, C.c_int, C.c_void_p, C.c_int]
+    hdr = ["iteration", "alpha1", "gam1", "alpha2", "gam2", "gamw"]
+    rows = {1: [0.5, 1e-6, 0.9, 19.77, 2.0], 2: [0.25, 0.786, float("nan"), -1.0, 12345.678901234567],
+            3: [1e5, -3.5, 0.0, 1e-300, 2.5]}  # 1e5 widens the row: later offsets shift (reference quirk)
+    a, b = tmp_path / "engine.csv", tmp_path / "oracle.csv"
+    run(harness, "csv", a, 0, *hdr)
+    arr = (C.c_char_p * 6)(*[s.encode() for s in hdr])
+    lib.orc_csv_header(str(b).encode(), arr, 6)
+    for it, v in rows.items():
+        run(harness, "csv", a, it, *v)
+        vv = np.array(v)
+        lib.orc_csv_row(str(b).encode(), it, vv.ctypes.data_as(C.c_void_p), len(v))
+    ba, bb = a.read_bytes(), b.read_bytes()
+    assert ba == bb
+    assert ba.startswith(b"iteration, alpha1, gam1, alpha2, gam2, gamw\n") and len(ba.split(b"\n")[0]) == 43
+    assert ba[44:116] == b"\0" * 72  # hole between the 44-byte header and row 1 at offset 116
+
+
+def test_bin_offsets_and_no_truncation(harness, tmp_path):
+    p = tmp_path / "x_it_1.bin"
+    run(harness, "bin", p, 3, 1.5, 2.5)  # rank with S = 3
+    run(harness, "bin", p, 0, -1, -2, -3)  # rank 0
+    v = np.fromfile(p, dtype="<f8")
+    assert v.tolist() == [-1, -2, -3, 1.5, 2.5]
+    run(harness, "bin", p, 0, 9)  # shorter rewrite keeps the tail (CREATE|WRONLY, no truncate)
+    assert np.fromfile(p, dtype="<f8").tolist() == [9, -2, -3, 1.5, 2.5]
+
+
+@pytest.mark.parametrize("text", ["0 0 1.25\n1 1 -2.5\n2 2 3.0000000001\n", "0\t0\t1e-3\r\n1 1   7\n",
+                                  " 0 0 5\n1 1 6\n", "a b 1 extra\nc d 2\n"])
+def test_phen_reader_matches_oracle(harness, tmp_path, text):
+    p = tmp_path / "y.phen"
+    p.write_text(text)
+    for std in (0, 1):
+        out = run(harness, "phen", p, std).split()
+        n = len(out)
+        ref = O.read_phen(str(p), n, bool(std))
+        assert np.array_equal(np.array(out, dtype=float), ref)
+
+
+def test_phen_reader_na(harness, tmp_path):
+    p = tmp_path / "na.phen"
+    p.write_text("0 0 1\n1 1 NA\n")
+    assert run(harness, "phen", p, 1).strip() == "ERR -2"

@@ -866,6 +866,7 @@ extern "C" vampomi_status vampomi_open(const vampomi_shard_desc* d, vampomi_ctx*
     if (d->N < 2 || d->Mt < 1 || d->nranks < 1 || d->rank < 0 || d->rank >= d->nranks)
         return fail(VAMPOMI_ERR_ARG, "invalid shard description (N >= 2, Mt >= 1, 0 <= rank < nranks)");
     if (d->nranks > 1 && !d->comm_id) return fail(VAMPOMI_ERR_ARG, "nranks > 1 needs a communicator id");
+    if (d->Mt < d->nranks) return fail(VAMPOMI_ERR_ARG, "every rank needs at least one marker (Mt >= nranks)");
     std::unique_ptr<vampomi_ctx> c(new vampomi_ctx());
     c->rank = d->rank;
     c->nranks = d->nranks;
