@@ -198,6 +198,13 @@ vampomi_status vampomi_set_timing(vampomi_ctx* ctx, int on);
 vampomi_status vampomi_get_stats(vampomi_ctx* ctx, vampomi_stats* out);
 vampomi_status vampomi_reset_stats(vampomi_ctx* ctx);
 
+/* ---- development hooks (kernel tuning; not part of the reference interface) ----
+ * which: 0 = A.x partial-sum kernel, 1 = A^T.u kernel.  Variants index the
+ * tuning tables in vampomi_amd/csrc/kernels.hip; variant 0 is the default. */
+vampomi_status vampomi_dev_set_variant(vampomi_ctx* ctx, int which, int variant);
+/* average device time (HIP events) of `reps` back-to-back launches, K RHS */
+vampomi_status vampomi_dev_time_pass(vampomi_ctx* ctx, int which, int K, int reps, double* avg_ms);
+
 #ifdef __cplusplus
 }
 #endif

@@ -264,3 +264,27 @@ def test_c2_shape_properties():
         # x1 = 0 at iteration 1, so its correlations are 0/0 (the reference writes -nan)
         assert np.isnan(a.metrics[0, 1]) and np.all(np.isfinite(a.metrics[1:3]))
         assert np.all(a.metrics[1:3, 3] > 0.1)  # x2 correlates with the true signal
+
+
+def test_every_kernel_variant_is_correct():
+    """All entries of the A.x / A^T.u tuning tables (tools/kbench.py) agree with the oracle."""
+    import ctypes as C
+    from vampomi_amd import _lib
+
+    N, Mt = 4099, 1031  # ragged in both dimensions
+    X, _, _ = _problem(N, Mt)
+    mave, msig = O.marker_stats(X)
+    rng = np.random.default_rng(3)
+    x, u = rng.normal(size=Mt), rng.normal(size=N)
+    ax_ref, atx_ref = O.ax(X, mave, msig, x), O.atx(X, mave, msig, u)
+    lib = va.load()
+    with va.Data(N, Mt) as d:
+        d.load_meth(X)
+        for which, nvar in ((0, 9), (1, 8)):
+            for v in range(nvar):
+                _lib.check(lib.vampomi_dev_set_variant(d.ctx, which, v))
+                if which == 0:
+                    assert relerr(d.Ax(x), ax_ref) < 1e-13, ("ax", v)
+                else:
+                    assert relerr(d.ATx(u), atx_ref) < 1e-13, ("atx", v)
+            _lib.check(lib.vampomi_dev_set_variant(d.ctx, which, 0))

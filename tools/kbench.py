@@ -1,0 +1,52 @@
+"""Kernel tuning sweep for the A.x / A^T.u passes (run on the GPU box).
+
+    python tools/kbench.py [N] [Mt] [reps]
+
+Prints, per variant and batch width K, the average launch time and the
+algorithmic HBM rate 8*N*M + 8*K*N + 8*(2+K)*M bytes per launch.
+"""
+import ctypes as C
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import numpy as np  # noqa: E402
+
+import vampomi_amd as va  # noqa: E402
+from vampomi_amd import _lib  # noqa: E402
+
+N = int(sys.argv[1]) if len(sys.argv) > 1 else 10000
+Mt = int(sys.argv[2]) if len(sys.argv) > 2 else 50000
+reps = int(sys.argv[3]) if len(sys.argv) > 3 else 20
+lib = va.load()
+d = va.Data(N, Mt)
+d.generate(1, va.GEN_GAUSS)
+rng = np.random.default_rng(0)
+x, u = rng.normal(size=Mt), rng.normal(size=N)
+res = {"N": N, "Mt": Mt, "reps": reps, "ax": {}, "atx": {}}
+ref_ax, ref_atx = None, None
+for which, name, Ks, nvar in ((0, "ax", (1, 2, 3), 9), (1, "atx", (1, 2, 3), 8)):
+    for v in range(nvar):
+        _lib.check(lib.vampomi_dev_set_variant(d.ctx, which, v))
+        # correctness against variant 0 (chunking may differ: 1e-13)
+        if which == 0:
+            out = d.Ax(x)
+            ref_ax = out if v == 0 else ref_ax
+            err = float(np.linalg.norm(out - ref_ax) / np.linalg.norm(ref_ax))
+        else:
+            out = d.ATx(u)
+            ref_atx = out if v == 0 else ref_atx
+            err = float(np.linalg.norm(out - ref_atx) / np.linalg.norm(ref_atx))
+        row = {"relerr_vs_v0": err}
+        for K in Ks:
+            ms = C.c_double()
+            _lib.check(lib.vampomi_dev_time_pass(d.ctx, which, K, 2, C.byref(ms)))  # warm
+            _lib.check(lib.vampomi_dev_time_pass(d.ctx, which, K, reps, C.byref(ms)))
+            b = 8.0 * N * Mt + 8.0 * K * N + 8.0 * (2 + K) * Mt
+            row[f"K{K}"] = {"us": round(ms.value * 1e3, 1), "GBs": round(b / (ms.value * 1e-3) / 1e9, 1)}
+        res[name][v] = row
+        print(name, v, json.dumps(row), flush=True)
+    _lib.check(lib.vampomi_dev_set_variant(d.ctx, which, 0))
+print(json.dumps(res))

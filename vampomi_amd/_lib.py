@@ -124,6 +124,8 @@ SIGNATURES = {
     "vampomi_set_timing": (C.c_int, [_P, C.c_int]),
     "vampomi_get_stats": (C.c_int, [_P, C.POINTER(Stats)]),
     "vampomi_reset_stats": (C.c_int, [_P]),
+    "vampomi_dev_set_variant": (C.c_int, [_P, C.c_int, C.c_int]),
+    "vampomi_dev_time_pass": (C.c_int, [_P, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_double)]),
 }
 
 _lib = None

@@ -891,7 +891,7 @@ extern "C" vampomi_status vampomi_open(const vampomi_shard_desc* d, vampomi_ctx*
     STCHK(dev_alloc(&c->ax_part, (size_t)c->axp.nchunks * vk::kMaxRhs * c->ld));
     c->red_cap = std::max<size_t>({(size_t)vk::kRedBlocks * 3 * vk::kMaxRhs,
                                    (size_t)((Mx + 255) / 256) * (1 + 2 * (vk::kMaxL - 1)),
-                                   (size_t)vk::atx_blocks(Mx) * vk::kMaxRhs, (size_t)4096});
+                                   (size_t)(Mx / 8 + 1) * vk::kMaxRhs, (size_t)4096});  // ATx partials at G >= 2
     STCHK(dev_alloc(&c->red_part, c->red_cap));
     STCHK(dev_alloc(&c->scal, SL_TOTAL));
     HIPCHK(hipHostMalloc((void**)&c->h_scal, SL_TOTAL * sizeof(double), hipHostMallocDefault));
@@ -1301,5 +1301,57 @@ extern "C" vampomi_status vampomi_reset_stats(vampomi_ctx* c) {
     HIPCHK(hipStreamSynchronize(c->st));
     resolve_timing(c);
     c->stats = vampomi_stats{};
+    return VAMPOMI_OK;
+}
+
+// ---------------------------------------------------------------------------
+// development hooks (tools/kbench.py): kernel variant selection and timing
+// ---------------------------------------------------------------------------
+extern "C" vampomi_status vampomi_dev_set_variant(vampomi_ctx* c, int which, int variant) {
+    if (!c) return fail(VAMPOMI_ERR_ARG, "null context");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(c->st));
+    if (which == 0) {
+        if (!vk::set_ax_variant(variant)) return fail(VAMPOMI_ERR_ARG, "no such A.x variant");
+        const vk::AxPlan np = vk::ax_plan(c->N, std::max<int64_t>(c->M, 1));
+        if (np.nchunks > c->axp.nchunks) {
+            dev_free(c->ax_part);
+            STCHK(dev_alloc(&c->ax_part, (size_t)np.nchunks * vk::kMaxRhs * c->ld));
+        }
+        c->axp = np;
+    } else {
+        if (!vk::set_atx_variant(variant)) return fail(VAMPOMI_ERR_ARG, "no such A^T.u variant");
+    }
+    return VAMPOMI_OK;
+}
+
+extern "C" vampomi_status vampomi_dev_time_pass(vampomi_ctx* c, int which, int K, int reps, double* avg_ms) {
+    if (!c || !avg_ms || K < 1 || K > (which == 0 ? 4 : 3) || reps < 1) return fail(VAMPOMI_ERR_ARG, "bad argument");
+    if (!c->have_X) return fail(VAMPOMI_ERR_STATE, "no methylation data loaded");
+    HIPCHK(hipSetDevice(c->device));
+    const int64_t Mx = std::max<int64_t>(c->M, 1);
+    vk::CPtrs in{};
+    vk::Ptrs out{};
+    for (int k = 0; k < K; ++k) {
+        in.p[k] = which == 0 ? c->mbuf + k * Mx : c->nbuf + k * c->ld;
+        out.p[k] = which == 0 ? c->nbuf + k * c->ld : c->mbuf + k * Mx;
+    }
+    hipEvent_t a, b;
+    HIPCHK(hipEventCreate(&a));
+    HIPCHK(hipEventCreate(&b));
+    HIPCHK(hipEventRecord(a, c->st));
+    for (int r = 0; r < reps; ++r) {
+        if (which == 0)
+            HIPCHK(vk::ax_partial(c->shard(), c->axp, K, in, c->ax_part, c->st));
+        else
+            HIPCHK(vk::atx(c->shard(), K, in, out, 1.0 / c->sqrtN, 0, 0.0, 0.0, vk::CPtrs{}, c->red_part, c->st));
+    }
+    HIPCHK(hipEventRecord(b, c->st));
+    HIPCHK(hipEventSynchronize(b));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, a, b));
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    *avg_ms = (double)ms / reps;
     return VAMPOMI_OK;
 }

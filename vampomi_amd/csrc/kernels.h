@@ -25,15 +25,20 @@ struct Shard {
 };
 
 // ---- A.x : two-stage, deterministic --------------------------------------
-// Stage 1 (ax_partial): a workgroup owns a 512-row tile and a chunk of
+// Stage 1 (ax_partial): a workgroup owns a row tile and a chunk of
 // markers, accumulates in registers, writes part[chunk][k][ld].  Stage 2
 // (ax_reduce): sums the chunks in index order.
 struct AxPlan {
-    int tiles;        // ceil(N / 512)
+    int variant;      // row/unroll variant (tuning table in kernels.hip)
+    int tiles;        // ceil(N / rows per tile)
     int nchunks;      // marker chunks (grid.y)
     int64_t chunk;    // markers per chunk
 };
 AxPlan ax_plan(int64_t N, int64_t M);
+int ax_variant_count();
+bool set_ax_variant(int v);   // development hook (tools/kbench.py)
+int atx_variant_count();
+bool set_atx_variant(int v);
 hipError_t ax_partial(const Shard& s, const AxPlan& pl, int K, CPtrs x, double* part, hipStream_t st);
 // out_k[j] = sum_c part[c][k][j]; if div > 0 then out_k[j] /= div
 hipError_t ax_reduce(const AxPlan& pl, int K, int64_t N, int64_t ld, const double* part, Ptrs out,

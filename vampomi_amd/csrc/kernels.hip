@@ -96,32 +96,43 @@ static inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 // ---------------------------------------------------------------------------
 // A.x   (data::Ax, src/data.cpp:340-373)
 // ---------------------------------------------------------------------------
-// Workgroup (tile, chunk): rows [512*tile, 512*tile+512) x markers of the
-// chunk.  Lane owns two adjacent rows (16-byte load); per marker the wave
-// reads 1 KiB contiguous, the workgroup 4 KiB.  Eight markers are loaded
-// before any arithmetic so each lane keeps 8 x 16 B of HBM reads in flight.
-// Per-sample summation order within a chunk is the reference's: markers in
-// index order, acc += (x - mave_i) * (msig_i * x_i).
-template <int K>
+// Workgroup (tile, chunk): a tile of 256*R rows x the markers of one chunk.
+// Wave w owns the contiguous slab of 64*R rows [tile0 + 64*R*w, ...); its lane
+// l owns rows 2l + 128q (q < R/2), i.e. each 16-byte load instruction reads
+// 1 KiB contiguous, and the workgroup streams 2*R KiB of every marker column.
+// U markers are loaded before any arithmetic (U*R/2 16-byte loads in flight
+// per lane).  Per-sample summation order within a chunk is the reference's:
+// markers in index order, acc += (x - mave_i) * (msig_i * x_i).
+template <int K, int R, int U, bool NT>
 __global__ __launch_bounds__(kBlock) void ax_partial_kernel(const double* __restrict__ X, int64_t ld,
                                                             int64_t N, int64_t M,
                                                             const double* __restrict__ mave,
                                                             const double* __restrict__ msig, CPtrs xs,
                                                             int64_t chunk, double* __restrict__ part) {
-    const int64_t j = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * 2;
+    constexpr int P = R / 2;  // 16-byte pieces per lane per marker
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t j0 = (int64_t)blockIdx.x * (kBlock * R) + (int64_t)wave * (64 * R) + 2 * lane;
     const int64_t i0 = (int64_t)blockIdx.y * chunk;
     const int64_t i1 = (i0 + chunk < M) ? i0 + chunk : M;
-    double a0[K], a1[K];
+    bool ok[P];
 #pragma unroll
-    for (int k = 0; k < K; ++k) a0[k] = a1[k] = 0.0;
-    if (j < N) {
-        const double* col = X + i0 * ld + j;
+    for (int q = 0; q < P; ++q) ok[q] = j0 + 128 * q < N;
+    double acc[K][R];
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc[k][r] = 0.0;
+    if (ok[0]) {
+        const double* col = X + i0 * ld + j0;
         int64_t i = i0;
-        constexpr int U = 8;
         for (; i + U <= i1; i += U) {
-            v2d xv[U];
+            v2d xv[U][P];
 #pragma unroll
-            for (int u = 0; u < U; ++u) xv[u] = ld_stream(col + (int64_t)u * ld);
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int q = 0; q < P; ++q)
+                    xv[u][q] = ok[q] ? (NT ? ld_stream(col + (int64_t)u * ld + 128 * q) : ld2(col + (int64_t)u * ld + 128 * q))
+                                     : v2d{0.0, 0.0};
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const double ave = mave[i + u];
@@ -129,36 +140,66 @@ __global__ __launch_bounds__(kBlock) void ax_partial_kernel(const double* __rest
 #pragma unroll
                 for (int k = 0; k < K; ++k) {
                     const double w = sg * xs.p[k][i + u];
-                    a0[k] += (xv[u].x - ave) * w;
-                    a1[k] += (xv[u].y - ave) * w;
+#pragma unroll
+                    for (int q = 0; q < P; ++q) {
+                        acc[k][2 * q] += (xv[u][q].x - ave) * w;
+                        acc[k][2 * q + 1] += (xv[u][q].y - ave) * w;
+                    }
                 }
             }
             col += (int64_t)U * ld;
         }
         for (; i < i1; ++i) {
-            const v2d xv = ld_stream(col);
+            v2d xv[P];
+#pragma unroll
+            for (int q = 0; q < P; ++q)
+                xv[q] = ok[q] ? (NT ? ld_stream(col + 128 * q) : ld2(col + 128 * q)) : v2d{0.0, 0.0};
             const double ave = mave[i];
             const double sg = msig[i];
 #pragma unroll
             for (int k = 0; k < K; ++k) {
                 const double w = sg * xs.p[k][i];
-                a0[k] += (xv.x - ave) * w;
-                a1[k] += (xv.y - ave) * w;
+#pragma unroll
+                for (int q = 0; q < P; ++q) {
+                    acc[k][2 * q] += (xv[q].x - ave) * w;
+                    acc[k][2 * q + 1] += (xv[q].y - ave) * w;
+                }
             }
             col += ld;
         }
-        double* dst = part + (int64_t)blockIdx.y * K * ld + j;
+        double* dst = part + (int64_t)blockIdx.y * K * ld + j0;
 #pragma unroll
-        for (int k = 0; k < K; ++k) {
-            dst[(int64_t)k * ld] = a0[k];
-            if (j + 1 < N) dst[(int64_t)k * ld + 1] = a1[k];
-        }
+        for (int k = 0; k < K; ++k)
+#pragma unroll
+            for (int q = 0; q < P; ++q) {
+                if (ok[q]) {
+                    dst[(int64_t)k * ld + 128 * q] = acc[k][2 * q];
+                    if (j0 + 128 * q + 1 < N) dst[(int64_t)k * ld + 128 * q + 1] = acc[k][2 * q + 1];
+                }
+            }
     }
+}
+
+// tuning table (rows per lane R, markers in flight U, nontemporal loads)
+struct AxVariant { int R, U; bool NT; };
+static constexpr AxVariant kAxVariants[] = {
+    {2, 8, true}, {2, 8, false}, {4, 4, true}, {4, 8, true}, {8, 4, true},
+    {8, 2, true}, {2, 16, true}, {4, 4, false}, {8, 4, false},
+};
+static constexpr int kNumAxVariants = sizeof(kAxVariants) / sizeof(kAxVariants[0]);
+static int g_ax_variant = 0;
+
+int ax_variant_count() { return kNumAxVariants; }
+bool set_ax_variant(int v) {
+    if (v < 0 || v >= kNumAxVariants) return false;
+    g_ax_variant = v;
+    return true;
 }
 
 AxPlan ax_plan(int64_t N, int64_t M) {
     AxPlan p;
-    p.tiles = (int)cdiv(N, 512);
+    p.variant = g_ax_variant;
+    p.tiles = (int)cdiv(N, (int64_t)kBlock * kAxVariants[p.variant].R);
     int64_t target = 2048;  // 8 workgroups per CU on 256 CUs
     int64_t nch = cdiv(target, p.tiles);
     int64_t maxch = M / 64 > 0 ? M / 64 : 1;  // at least 64 markers per chunk
@@ -171,15 +212,38 @@ AxPlan ax_plan(int64_t N, int64_t M) {
     return p;
 }
 
-hipError_t ax_partial(const Shard& s, const AxPlan& pl, int K, CPtrs x, double* part, hipStream_t st) {
-    dim3 grid(pl.tiles, pl.nchunks), block(kBlock);
-    switch (K) {
-        case 1: hipLaunchKernelGGL(ax_partial_kernel<1>, grid, block, 0, st, s.X, s.ld, s.N, s.M, s.mave, s.msig, x, pl.chunk, part); break;
-        case 2: hipLaunchKernelGGL(ax_partial_kernel<2>, grid, block, 0, st, s.X, s.ld, s.N, s.M, s.mave, s.msig, x, pl.chunk, part); break;
-        case 3: hipLaunchKernelGGL(ax_partial_kernel<3>, grid, block, 0, st, s.X, s.ld, s.N, s.M, s.mave, s.msig, x, pl.chunk, part); break;
-        case 4: hipLaunchKernelGGL(ax_partial_kernel<4>, grid, block, 0, st, s.X, s.ld, s.N, s.M, s.mave, s.msig, x, pl.chunk, part); break;
-        default: return hipErrorInvalidValue;
+template <int K, int R, int U, bool NT>
+static void launch_ax(const Shard& s, const AxPlan& pl, CPtrs x, double* part, hipStream_t st) {
+    hipLaunchKernelGGL((ax_partial_kernel<K, R, U, NT>), dim3(pl.tiles, pl.nchunks), dim3(kBlock), 0, st, s.X, s.ld,
+                       s.N, s.M, s.mave, s.msig, x, pl.chunk, part);
+}
+
+template <int K>
+static bool launch_ax_v(int v, const Shard& s, const AxPlan& pl, CPtrs x, double* part, hipStream_t st) {
+    switch (v) {
+        case 0: launch_ax<K, 2, 8, true>(s, pl, x, part, st); return true;
+        case 1: launch_ax<K, 2, 8, false>(s, pl, x, part, st); return true;
+        case 2: launch_ax<K, 4, 4, true>(s, pl, x, part, st); return true;
+        case 3: launch_ax<K, 4, 8, true>(s, pl, x, part, st); return true;
+        case 4: launch_ax<K, 8, 4, true>(s, pl, x, part, st); return true;
+        case 5: launch_ax<K, 8, 2, true>(s, pl, x, part, st); return true;
+        case 6: launch_ax<K, 2, 16, true>(s, pl, x, part, st); return true;
+        case 7: launch_ax<K, 4, 4, false>(s, pl, x, part, st); return true;
+        case 8: launch_ax<K, 8, 4, false>(s, pl, x, part, st); return true;
+        default: return false;
     }
+}
+
+hipError_t ax_partial(const Shard& s, const AxPlan& pl, int K, CPtrs x, double* part, hipStream_t st) {
+    bool ok = false;
+    switch (K) {
+        case 1: ok = launch_ax_v<1>(pl.variant, s, pl, x, part, st); break;
+        case 2: ok = launch_ax_v<2>(pl.variant, s, pl, x, part, st); break;
+        case 3: ok = launch_ax_v<3>(pl.variant, s, pl, x, part, st); break;
+        case 4: ok = launch_ax_v<4>(pl.variant, s, pl, x, part, st); break;
+        default: break;
+    }
+    if (!ok) return hipErrorInvalidValue;
     return hipGetLastError();
 }
 
@@ -233,11 +297,11 @@ hipError_t vec_div(int K, int64_t n, int64_t /*ld*/, Ptrs v, double div, hipStre
 // A^T.u  (data::ATx + data::dot_product, src/data.cpp:294-333)
 // ---------------------------------------------------------------------------
 // A wave owns G consecutive markers; lanes stride the samples two at a time,
-// so each load instruction reads 1 KiB of one column.  Every u value loaded
-// serves G markers.  The wave's partial dots are reduced with a DPP-style xor
-// butterfly; mode 1 fuses the lmmse_mult epilogue (src/vamp.cpp:656-659) and
-// the <d,p> partial of the next CG step.
-template <int G, int K, int MODE>
+// so each load instruction reads 1 KiB of one column, UJ such 128-row steps
+// per loop trip.  Every u value loaded serves G markers.  The wave's partial
+// dots are reduced with an xor butterfly; mode 1 fuses the lmmse_mult
+// epilogue (src/vamp.cpp:656-659) and the <d,p> partial of the next CG step.
+template <int G, int K, int MODE, int UJ, bool NT>
 __global__ __launch_bounds__(kBlock) void atx_kernel(const double* __restrict__ X, int64_t ld, int64_t N, int64_t M,
                                                      const double* __restrict__ mave,
                                                      const double* __restrict__ msig, CPtrs u, Ptrs out,
@@ -258,35 +322,33 @@ __global__ __launch_bounds__(kBlock) void atx_kernel(const double* __restrict__ 
         for (int k = 0; k < K; ++k) acc[g][k] = 0.0;
     }
     int64_t j = 2 * lane;
-    for (; j + 128 < N; j += 256) {
-        v2d uu0[K], uu1[K], x0[G], x1[G];
+    for (; j + 128 * (UJ - 1) < N; j += 128 * UJ) {
+        v2d uu[UJ][K], xx[UJ][G];
+#pragma unroll
+        for (int t = 0; t < UJ; ++t)
+#pragma unroll
+            for (int g = 0; g < G; ++g) xx[t][g] = NT ? ld_stream(col[g] + j + 128 * t) : ld2(col[g] + j + 128 * t);
+#pragma unroll
+        for (int t = 0; t < UJ; ++t)
+#pragma unroll
+            for (int k = 0; k < K; ++k) uu[t][k] = ld2(u.p[k] + j + 128 * t);
 #pragma unroll
         for (int g = 0; g < G; ++g) {
-            x0[g] = ld_stream(col[g] + j);
-            x1[g] = ld_stream(col[g] + j + 128);
-        }
 #pragma unroll
-        for (int k = 0; k < K; ++k) {
-            uu0[k] = ld2(u.p[k] + j);
-            uu1[k] = ld2(u.p[k] + j + 128);
-        }
+            for (int t = 0; t < UJ; ++t) {
+                const double d0 = xx[t][g].x - mu[g], d1 = xx[t][g].y - mu[g];
 #pragma unroll
-        for (int g = 0; g < G; ++g) {
-            const double d0 = x0[g].x - mu[g], d1 = x0[g].y - mu[g];
-            const double d2 = x1[g].x - mu[g], d3 = x1[g].y - mu[g];
-#pragma unroll
-            for (int k = 0; k < K; ++k) {
-                acc[g][k] += d0 * uu0[k].x;
-                acc[g][k] += d1 * uu0[k].y;
-                acc[g][k] += d2 * uu1[k].x;
-                acc[g][k] += d3 * uu1[k].y;
+                for (int k = 0; k < K; ++k) {
+                    acc[g][k] += d0 * uu[t][k].x;
+                    acc[g][k] += d1 * uu[t][k].y;
+                }
             }
         }
     }
     for (; j < N; j += 128) {  // tail; j+1 may be the zero pad row (u pad is zero too)
         v2d uu[K], xx[G];
 #pragma unroll
-        for (int g = 0; g < G; ++g) xx[g] = ld_stream(col[g] + j);
+        for (int g = 0; g < G; ++g) xx[g] = NT ? ld_stream(col[g] + j) : ld2(col[g] + j);
 #pragma unroll
         for (int k = 0; k < K; ++k) uu[k] = ld2(u.p[k] + j);
 #pragma unroll
@@ -334,35 +396,66 @@ __global__ __launch_bounds__(kBlock) void atx_kernel(const double* __restrict__ 
     }
 }
 
-static constexpr int kAtxG = 4;
-int atx_blocks(int64_t M) { return (int)cdiv(M, 4 * kAtxG); }
+// tuning table (markers per wave G, 128-row steps per trip UJ, nontemporal)
+struct AtxVariant { int G, UJ; bool NT; };
+static constexpr AtxVariant kAtxVariants[] = {
+    {4, 2, true}, {4, 2, false}, {2, 2, true}, {8, 2, true}, {4, 4, true}, {4, 1, true}, {8, 1, true}, {2, 4, true},
+};
+static constexpr int kNumAtxVariants = sizeof(kAtxVariants) / sizeof(kAtxVariants[0]);
+static int g_atx_variant = 0;
 
-template <int K, int MODE>
+int atx_variant_count() { return kNumAtxVariants; }
+bool set_atx_variant(int v) {
+    if (v < 0 || v >= kNumAtxVariants) return false;
+    g_atx_variant = v;
+    return true;
+}
+
+int atx_blocks(int64_t M) { return (int)cdiv(M, 4 * kAtxVariants[g_atx_variant].G); }
+
+template <int G, int K, int MODE, int UJ, bool NT>
 static void launch_atx(const Shard& s, CPtrs u, Ptrs out, double scale, double tau, double gam2, CPtrs p,
                        double* dp_part, hipStream_t st) {
-    hipLaunchKernelGGL((atx_kernel<kAtxG, K, MODE>), dim3(atx_blocks(s.M)), dim3(kBlock), 0, st, s.X, s.ld, s.N, s.M,
-                       s.mave, s.msig, u, out, scale, tau, gam2, p, dp_part);
+    hipLaunchKernelGGL((atx_kernel<G, K, MODE, UJ, NT>), dim3((unsigned)cdiv(s.M, 4 * G)), dim3(kBlock), 0, st, s.X,
+                       s.ld, s.N, s.M, s.mave, s.msig, u, out, scale, tau, gam2, p, dp_part);
+}
+
+template <int K, int MODE>
+static bool launch_atx_v(int v, const Shard& s, CPtrs u, Ptrs out, double scale, double tau, double gam2, CPtrs p,
+                         double* dp, hipStream_t st) {
+    switch (v) {
+        case 0: launch_atx<4, K, MODE, 2, true>(s, u, out, scale, tau, gam2, p, dp, st); return true;
+        case 1: launch_atx<4, K, MODE, 2, false>(s, u, out, scale, tau, gam2, p, dp, st); return true;
+        case 2: launch_atx<2, K, MODE, 2, true>(s, u, out, scale, tau, gam2, p, dp, st); return true;
+        case 3: launch_atx<8, K, MODE, 2, true>(s, u, out, scale, tau, gam2, p, dp, st); return true;
+        case 4: launch_atx<4, K, MODE, 4, true>(s, u, out, scale, tau, gam2, p, dp, st); return true;
+        case 5: launch_atx<4, K, MODE, 1, true>(s, u, out, scale, tau, gam2, p, dp, st); return true;
+        case 6: launch_atx<8, K, MODE, 1, true>(s, u, out, scale, tau, gam2, p, dp, st); return true;
+        case 7: launch_atx<2, K, MODE, 4, true>(s, u, out, scale, tau, gam2, p, dp, st); return true;
+        default: return false;
+    }
 }
 
 hipError_t atx(const Shard& s, int K, CPtrs u, Ptrs out, double scale, int mode, double tau, double gam2, CPtrs p,
                double* dp_part, hipStream_t st) {
+    const int v = g_atx_variant;
+    bool ok = false;
     if (mode == 0) {
         switch (K) {
-            case 1: launch_atx<1, 0>(s, u, out, scale, tau, gam2, p, dp_part, st); break;
-            case 2: launch_atx<2, 0>(s, u, out, scale, tau, gam2, p, dp_part, st); break;
-            case 3: launch_atx<3, 0>(s, u, out, scale, tau, gam2, p, dp_part, st); break;
-            case 4: launch_atx<4, 0>(s, u, out, scale, tau, gam2, p, dp_part, st); break;
-            default: return hipErrorInvalidValue;
+            case 1: ok = launch_atx_v<1, 0>(v, s, u, out, scale, tau, gam2, p, dp_part, st); break;
+            case 2: ok = launch_atx_v<2, 0>(v, s, u, out, scale, tau, gam2, p, dp_part, st); break;
+            case 3: ok = launch_atx_v<3, 0>(v, s, u, out, scale, tau, gam2, p, dp_part, st); break;
+            default: break;
         }
     } else {
         switch (K) {
-            case 1: launch_atx<1, 1>(s, u, out, scale, tau, gam2, p, dp_part, st); break;
-            case 2: launch_atx<2, 1>(s, u, out, scale, tau, gam2, p, dp_part, st); break;
-            case 3: launch_atx<3, 1>(s, u, out, scale, tau, gam2, p, dp_part, st); break;
-            case 4: launch_atx<4, 1>(s, u, out, scale, tau, gam2, p, dp_part, st); break;
-            default: return hipErrorInvalidValue;
+            case 1: ok = launch_atx_v<1, 1>(v, s, u, out, scale, tau, gam2, p, dp_part, st); break;
+            case 2: ok = launch_atx_v<2, 1>(v, s, u, out, scale, tau, gam2, p, dp_part, st); break;
+            case 3: ok = launch_atx_v<3, 1>(v, s, u, out, scale, tau, gam2, p, dp_part, st); break;
+            default: break;
         }
     }
+    if (!ok) return hipErrorInvalidValue;
     return hipGetLastError();
 }
 
