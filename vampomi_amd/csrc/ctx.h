@@ -1,0 +1,147 @@
+// ctx.h — libvampomi internals shared by engine.cpp, pcg.cpp and vamp.cpp.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstdint>
+#include <initializer_list>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/vampomi.h"
+#include "kernels.h"
+
+// ---- errors ---------------------------------------------------------------
+vampomi_status fail(vampomi_status s, const std::string& msg);
+
+#define HIPCHK(expr)                                                                                  \
+    do {                                                                                              \
+        hipError_t _e = (expr);                                                                       \
+        if (_e != hipSuccess)                                                                         \
+            return fail(VAMPOMI_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));          \
+    } while (0)
+
+#define NCCLCHK(expr)                                                                                 \
+    do {                                                                                              \
+        ncclResult_t _r = (expr);                                                                     \
+        if (_r != ncclSuccess)                                                                        \
+            return fail(VAMPOMI_ERR_RCCL, std::string(#expr) + ": " + ncclGetErrorString(_r));        \
+    } while (0)
+
+#define STCHK(expr)                                   \
+    do {                                              \
+        vampomi_status _s = (expr);                   \
+        if (_s != VAMPOMI_OK) return _s;              \
+    } while (0)
+
+// ---- the context ------------------------------------------------------------
+struct VampRun;
+
+struct TimedLaunch {
+    hipEvent_t a, b;
+    int cls;  // 0 ax, 1 atx
+    int K;
+    double bytes, flops;
+};
+
+// scalar slots in ctx->scal: <d,p> of the fused lmmse epilogue, then the
+// synced (summed over ranks) and local halves of a DotBatch
+enum : int { SL_DP = 0, SL_SYNC = 16, SL_NSYNC = 256, SL_LOCAL = SL_SYNC + SL_NSYNC, SL_NLOCAL = 128,
+             SL_TOTAL = 512, SL_BARRIER = SL_TOTAL - 1 };
+
+struct vampomi_ctx {
+    int rank = 0, nranks = 1, device = 0;
+    int64_t N = 0, Mt = 0, M = 0, S = 0, Mm = 0, ld = 0;
+    double alpha_scale = 1.0;
+    double sqrtN = 1.0;
+    hipStream_t st = nullptr;
+    ncclComm_t comm = nullptr;
+
+    double* X = nullptr;     // M columns x ld, marker-major, pad rows zero
+    double* mave = nullptr;
+    double* msig = nullptr;
+    double* y = nullptr;     // ld, zero pad
+    std::vector<double> y_host;
+    bool have_X = false, have_y = false;
+
+    vk::AxPlan axp{};
+    double* ax_part = nullptr;  // nchunks x kMaxRhs x ld partial sums of A.x
+    double* red_part = nullptr;  // per-block partials of every reduction
+    size_t red_cap = 0;
+    double* scal = nullptr;     // device scalars (SL_*)
+    double* h_scal = nullptr;   // pinned mirror
+    double* nbuf = nullptr;     // kMaxRhs * ld scratch N-vectors (API calls)
+    double* mbuf = nullptr;     // (2*kMaxRhs) * M scratch M-vectors (API calls)
+
+    bool timing = false;
+    std::vector<TimedLaunch> pending;
+    std::vector<hipEvent_t> ev_pool;
+    vampomi_stats stats{};
+
+    std::unique_ptr<VampRun> run;
+
+    vk::Shard shard() const { return vk::Shard{X, ld, N, M, mave, msig}; }
+    vampomi_ctx();   // defined in vamp.cpp, where VampRun is complete
+    ~vampomi_ctx();
+};
+
+vampomi_status dev_alloc(double** p, size_t n);
+void dev_free(double*& p);
+vampomi_status host_sync(vampomi_ctx* c);
+vampomi_status allreduce_dev(vampomi_ctx* c, double* buf, size_t n);
+void resolve_timing(vampomi_ctx* c);
+void release_ctx_resources(vampomi_ctx* c);
+
+// ---- operators on device buffers ---------------------------------------------
+// out_k = A x_k (K <= 4), outputs at outbase + k*ld (one all-reduce). COLLECTIVE
+vampomi_status ax_dev(vampomi_ctx* c, int K, const double* const* x, double* outbase);
+// out_k = A^T u_k (mode 0) or tau*A^T u_k + gam2*p_k with <out_k,p_k> summed over
+// ranks into scal[SL_DP + k] (mode 1).  u_k: ld-padded N-vectors.
+vampomi_status atx_dev(vampomi_ctx* c, int K, const double* const* u, double* const* out, int mode, double tau,
+                       double gam2, const double* const* p);
+// d_k = tau*A^T A v_k + gam2*v_k (lmmse_mult), <d_k,v_k> in scal[SL_DP+k]. COLLECTIVE
+vampomi_status lmmse_dev(vampomi_ctx* c, int K, const double* const* v, double* const* d, double tau, double gam2,
+                         double* nscratch);
+
+// ---- batched scalar reductions ---------------------------------------------------
+// Every inner_prod / l2_norm2 of the reference (src/utilities.cpp:138-162) is a
+// fixed-order device reduction into a scalar slot.  A DotBatch queues several
+// of them (each with its own sync flag: sync = summed over ranks, the
+// reference's inner_prod(..., 1)) and resolves them with ONE all-reduce, ONE
+// device-to-host copy and ONE host synchronisation.
+class DotBatch {
+   public:
+    explicit DotBatch(vampomi_ctx* c) : c_(c) {}
+    vampomi_status add(std::initializer_list<vk::DotTerm> terms, int64_t n, bool sync, double* out);
+    vampomi_status add_partials(const double* part, int nblk, int nq, bool sync, double* out);
+    vampomi_status flush();
+    bool empty() const { return sinks_.empty(); }
+
+   private:
+    struct Sink {
+        int slot, count;
+        double* out;
+    };
+    vampomi_ctx* c_;
+    int nsync_ = 0, nlocal_ = 0;
+    std::vector<Sink> sinks_;
+};
+
+inline vk::DotTerm T(const double* a, const double* b, int op = vk::DOT) { return vk::DotTerm{a, b, op}; }
+
+// ---- PCG (vamp::precondCG_solver) ----------------------------------------------
+struct CgSystem {
+    const double* v = nullptr;     // right-hand side (device, M)
+    double* mu = nullptr;          // in: start (if mu0_nonzero), out: solution
+    bool mu0_nonzero = false;      // false: start from zeros (lmmse_mult short-circuit)
+    const double* atx0 = nullptr;  // optional: A^T(A mu0) computed earlier (saves the start's passes)
+    bool onsager = false;          // denoiser == 0 in the reference: extra Onsager stop
+    int iters = 0;
+    double *r = nullptr, *z = nullptr, *p = nullptr, *d = nullptr;  // work vectors (device, M)
+};
+// Solves the systems together: every CG step streams X twice for all still
+// active systems; each keeps its own scalars and stopping rule.  `init` (may
+// be null) is flushed together with the initial residual reductions.
+vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double tau, double gam2, int max_iter,
+                       double tol, double* nscratch, int64_t* ref_passes, DotBatch* init);

@@ -50,7 +50,7 @@ hipError_t vec_div(int K, int64_t n, int64_t ld, Ptrs v, double div, hipStream_t
 // mode 0: out_k[i] = (msig_i * dot_k(i)) * scale
 // mode 1 (lmmse_mult): out_k[i] = ((msig_i*dot)*scale)*tau + gam2*p_k[i],
 //   and per-workgroup partials of <out_k, p_k> into dp_part[blk*K + k]
-int atx_blocks(int64_t M);
+int atx_blocks(int64_t M, int K);
 hipError_t atx(const Shard& s, int K, CPtrs u, Ptrs out, double scale, int mode, double tau,
                double gam2, CPtrs p, double* dp_part, hipStream_t st);
 
@@ -124,8 +124,11 @@ struct CgVecs {
     double* p[kMaxRhs];
     const double* d[kMaxRhs];   // lmmse_mult(mu0) for init (nullptr: mu0 == 0), A p in the loop
     const double* v[kMaxRhs];
+    const double* atx0[kMaxRhs];  // init only: A^T(A mu0) computed earlier (then d is ignored)
+    double tau, gam2;             // init only, with atx0
 };
-// r = v - d (or v), z = r/diag, p = z; partials <r,z>, <v,v> (2K terms)
+// r = v - d (or v, or v - (atx0*tau + gam2*mu)), z = r/diag, p = z;
+// partials <r,z>, <v,v> (2K terms)
 hipError_t cg_init(int K, int64_t M, const CgVecs& c, double diag, double* part, int* nblk, hipStream_t st);
 // alpha_k = rz[k] / dp_dev[k]; mu += alpha p; r -= d alpha; z = r/diag;
 // partials <r,z>, <r,r>, <v,mu> (3K terms, ordered k-major)

@@ -187,7 +187,7 @@ static constexpr AxVariant kAxVariants[] = {
     {8, 2, true}, {2, 16, true}, {4, 4, false}, {8, 4, false},
 };
 static constexpr int kNumAxVariants = sizeof(kAxVariants) / sizeof(kAxVariants[0]);
-static int g_ax_variant = 0;
+static int g_ax_variant = 3;  // R=4, U=8, nontemporal: best at every K on MI355X (tools/kbench.py)
 
 int ax_variant_count() { return kNumAxVariants; }
 bool set_ax_variant(int v) {
@@ -402,16 +402,19 @@ static constexpr AtxVariant kAtxVariants[] = {
     {4, 2, true}, {4, 2, false}, {2, 2, true}, {8, 2, true}, {4, 4, true}, {4, 1, true}, {8, 1, true}, {2, 4, true},
 };
 static constexpr int kNumAtxVariants = sizeof(kAtxVariants) / sizeof(kAtxVariants[0]);
-static int g_atx_variant = 0;
+// -1: per-K choice measured on MI355X at C2 (tools/kbench.py, profiles/r01_kbench.json):
+// K=1 -> G=2,UJ=2 (6.86 TB/s); K>=2 -> G=4,UJ=4 (6.70 TB/s at K=2)
+static int g_atx_variant = -1;
+static int atx_variant_for(int K) { return g_atx_variant >= 0 ? g_atx_variant : (K == 1 ? 2 : 4); }
 
 int atx_variant_count() { return kNumAtxVariants; }
 bool set_atx_variant(int v) {
-    if (v < 0 || v >= kNumAtxVariants) return false;
+    if (v < -1 || v >= kNumAtxVariants) return false;
     g_atx_variant = v;
     return true;
 }
 
-int atx_blocks(int64_t M) { return (int)cdiv(M, 4 * kAtxVariants[g_atx_variant].G); }
+int atx_blocks(int64_t M, int K) { return (int)cdiv(M, 4 * kAtxVariants[atx_variant_for(K)].G); }
 
 template <int G, int K, int MODE, int UJ, bool NT>
 static void launch_atx(const Shard& s, CPtrs u, Ptrs out, double scale, double tau, double gam2, CPtrs p,
@@ -438,7 +441,7 @@ static bool launch_atx_v(int v, const Shard& s, CPtrs u, Ptrs out, double scale,
 
 hipError_t atx(const Shard& s, int K, CPtrs u, Ptrs out, double scale, int mode, double tau, double gam2, CPtrs p,
                double* dp_part, hipStream_t st) {
-    const int v = g_atx_variant;
+    const int v = atx_variant_for(K);
     bool ok = false;
     if (mode == 0) {
         switch (K) {
@@ -805,7 +808,15 @@ __global__ __launch_bounds__(kBlock) void cg_init_kernel(int K, int64_t M, CgVec
         for (int k = 0; k < kMaxRhs; ++k) {
             if (k < K) {
                 const double vi = c.v[k][i];
-                const double r = c.d[k] ? vi - c.d[k][i] : vi - 0.0;  // r = v - lmmse_mult(mu0)
+                double r;
+                if (c.atx0[k]) {  // lmmse_mult(mu0) from a precomputed A^T(A mu0): res*=tau; res+=gam2*v
+                    double dv = c.atx0[k][i];
+                    dv *= c.tau;
+                    dv += c.gam2 * c.mu[k][i];
+                    r = vi - dv;
+                } else {
+                    r = c.d[k] ? vi - c.d[k][i] : vi - 0.0;  // r = v - lmmse_mult(mu0)
+                }
                 const double z = r / diag;
                 c.r[k][i] = r;
                 c.z[k][i] = z;

@@ -1,0 +1,516 @@
+// vamp.cpp — the gVAMPomi linear VAMP model on the device
+// (vamp::vamp + vamp::infere_linear, src/vamp.cpp:18-91, 110-438).
+//
+// Every vector of the VAMP state lives in HBM; the host keeps the scalars
+// the algorithm branches on.  Per iteration the work is the reference's, in
+// the reference's arithmetic, with three bandwidth reformulations that leave
+// every value bitwise unchanged (tests/test_gpu_parity.py checks batch_rhs=1
+// against batch_rhs=0 bit for bit):
+//   1. the x2 CG solve and the Onsager CG solve share each pass over X
+//      (pcg.cpp);
+//   2. updateNoisePrec's A.x2 and A.invQ_bern_vec (:508, :518) share one
+//      pass, which also carries the NEXT iteration's z1 = A.x1_hat (:232):
+//      denoising of iteration it+1 (updatePrior, g1, g1d) needs only r1 and
+//      gam1 of iteration it, so it runs before updateNoisePrec of it;
+//   3. updateNoisePrec's A^T pass (:519) also computes A^T(A x2_hat), which
+//      is the next x2 solve's warm-start product lmmse_mult(mu_CG_last)
+//      (:681) up to the tau / gam2 epilogue applied when those are known.
+// err_measures' A.x2_hat (:826) is the product of (2); A^T y (:303) is
+// computed once.  Scalar reductions are batched per dependency level.
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+
+#include "ctx.h"
+#include "hostio.h"
+
+namespace {
+
+struct Mixture {
+    int L = 0;
+    double probs[VAMPOMI_MAX_L] = {};
+    double vars[VAMPOMI_MAX_L] = {};  // multiplied by N (src/vamp.cpp:87-88)
+};
+
+double smax(double a, double b) { return (a < b) ? b : a; }  // std::max
+double smin(double a, double b) { return (b < a) ? b : a; }  // std::min
+
+}  // namespace
+
+struct VampRun {
+    vampomi_params prm{};
+    vampomi_result* res = nullptr;
+    bool write = false;
+    bool fuse = true;  // batch_rhs: share passes + prefetch the next denoising step
+    std::string out_dir, out_name, p_params, p_metrics, p_prior;
+    int it = 0;
+    bool stopped = false;
+    Mixture mix, mix_next;
+    bool have_next = false;  // x1n, alpha1_next, mix_next, z1 (nb3 slot 2), atx0 valid
+    double gam1 = 0, gam2 = 0, gamw = 0;
+    double alpha1 = 0, alpha2 = 0, eta1 = 0, eta2 = 0, alpha1_next = 0;
+    double metrics[6] = {0, 0, 0, 0, 0, 0}, params[5] = {0, 0, 0, 0, 0};
+    // reduction sinks
+    double e1m[3] = {}, e1n[2] = {}, e1s[3] = {}, e2m[3] = {}, e2n[2] = {}, e2s[3] = {};
+    double tn = 0, tc = 0, nm[2] = {}, sum_d = 0, a2 = 0;
+    // device M-vectors
+    double *r1 = nullptr, *x1 = nullptr, *x1p = nullptr, *x1n = nullptr, *x1d = nullptr, *r2 = nullptr;
+    double *x2 = nullptr, *bern = nullptr, *invQ = nullptr, *v = nullptr, *atxy = nullptr, *ts = nullptr;
+    double *tmpM = nullptr, *atx0 = nullptr;
+    double* cgw[8] = {};  // r, z, p, d of the two CG systems
+    // device N-vectors (ld each)
+    double *z1buf = nullptr, *nb3 = nullptr /* A.x2, A.invQ, A.x1_next */, *nsc = nullptr;
+    const double* z1 = nullptr;
+    int64_t passes_ref = 0;
+
+    ~VampRun() {
+        for (double** p : {&r1, &x1, &x1p, &x1n, &x1d, &r2, &x2, &bern, &invQ, &v, &atxy, &ts, &tmpM, &atx0, &z1buf,
+                           &nb3, &nsc})
+            dev_free(*p);
+        for (auto& p : cgw) dev_free(p);
+    }
+};
+
+vampomi_ctx::vampomi_ctx() = default;
+
+vampomi_ctx::~vampomi_ctx() {
+    run.reset();
+    release_ctx_resources(this);
+}
+
+// updatePrior (src/vamp.cpp:531-643) on mixture m, from r1 and gam1
+static vampomi_status update_prior(vampomi_ctx* c, const VampRun& R, Mixture& m, double gam1, const double* r1) {
+    const double noise_var = 1 / gam1;
+    double lambda = 1 - m.probs[0];
+    double omegas[VAMPOMI_MAX_L];
+    for (int j = 0; j < m.L; ++j) omegas[j] = m.probs[j];
+    for (int j = 1; j < m.L; ++j) omegas[j] /= lambda;
+    std::vector<double> sums(2 * VAMPOMI_MAX_L);
+    for (int emit = 0; emit < R.prm.EM_max_iter; ++emit) {
+        const int L = m.L;
+        double max_sigma = m.vars[0];
+        for (int j = 1; j < L; ++j) max_sigma = smax(max_sigma, m.vars[j]);  // std::max_element
+        double probs_prev[VAMPOMI_MAX_L], vars_prev[VAMPOMI_MAX_L];
+        std::memcpy(probs_prev, m.probs, sizeof probs_prev);
+        std::memcpy(vars_prev, m.vars, sizeof vars_prev);
+        vk::EmArgs a{};
+        for (int j = 0; j < L; ++j) {
+            a.omegas[j] = omegas[j];
+            a.vars[j] = m.vars[j];
+        }
+        for (int j = 1; j < L; ++j) a.v[j - 1] = 1.0 / (1.0 / m.vars[j] + gam1);
+        a.lambda = lambda;
+        a.noise_var = noise_var;
+        a.gam1 = gam1;
+        a.max_sigma = max_sigma;
+        a.L = L;
+        const int Q = 1 + 2 * (L - 1);
+        int nb = 0;
+        HIPCHK(vk::em_sums(c->M, r1, a, c->red_part, &nb, c->st));
+        DotBatch b(c);
+        STCHK(b.add_partials(c->red_part, nb, Q, true, sums.data()));  // :578, :596-597
+        STCHK(b.flush());
+        const double lambda_total = sums[0];
+        lambda = lambda_total / (double)c->Mt;
+        const double sum_of_pin = lambda_total;
+        for (int j = 0; j < L - 1; ++j) {
+            const double res_total = sums[1 + j];
+            const double res_gammas_total = sums[L + j];
+            if (R.prm.learn_vars == 1) m.vars[j + 1] = res_gammas_total / res_total;
+            omegas[j + 1] = res_total / sum_of_pin;
+            m.probs[j + 1] = lambda * omegas[j + 1];
+        }
+        m.probs[0] = 1 - lambda;
+        double dprob = 0, nprob = 0, dvar = 0, nvar = 0;
+        for (int j = 0; j < L; ++j) {
+            dprob += (m.probs[j] - probs_prev[j]) * (m.probs[j] - probs_prev[j]);
+            nprob += m.probs[j] * m.probs[j];
+            dvar += (m.vars[j] - vars_prev[j]) * (m.vars[j] - vars_prev[j]);
+            nvar += m.vars[j] * m.vars[j];
+        }
+        const double dist_probs = std::sqrt(dprob / nprob), dist_vars = std::sqrt(dvar / nvar);
+        if (R.prm.verbosity == 1 && c->rank == 0)
+            std::printf("it = %d: dist_probs = %g & dist_vars = %g\n", emit, dist_probs, dist_vars);
+        if (dist_probs < R.prm.EM_err_thr && dist_vars < R.prm.EM_err_thr) break;
+    }
+    // merging close variances (:626-642)
+    for (int j = 0; j < m.L; ++j) {
+        for (int k = j + 1; k < m.L; ++k) {
+            const double denom = m.vars[j] != 0 ? smin(m.vars[j], m.vars[k]) : 1e-7;
+            if (std::fabs(m.vars[j] - m.vars[k]) / denom < R.prm.merge_vars_thr) {
+                const double sum2probs = m.probs[j] + m.probs[k];
+                for (int q = k; q + 1 < m.L; ++q) {
+                    m.vars[q] = m.vars[q + 1];
+                    m.probs[q] = m.probs[q + 1];
+                }
+                m.L--;
+                m.probs[j] = sum2probs;
+                k--;
+            }
+        }
+    }
+    return VAMPOMI_OK;
+}
+
+// x1 = g1(r1) [damped], x1d = g1d(r1); sum of x1d over ranks queued in b
+static vampomi_status denoise_into(vampomi_ctx* c, const Mixture& m, double gam1, const double* r1, double* x1,
+                                   const double* x1_prev, bool damp, double rho, double* x1d, DotBatch& b,
+                                   double* sum_out) {
+    vk::Mix mix{};
+    mix.L = m.L;
+    for (int j = 0; j < m.L; ++j) {
+        mix.probs[j] = m.probs[j];
+        mix.vars[j] = m.vars[j];
+    }
+    int nb = 0;
+    HIPCHK(vk::denoise(c->M, r1, gam1, mix, x1, x1_prev, damp ? 1 : 0, rho, x1d, c->red_part, &nb, c->st));
+    return b.add_partials(c->red_part, nb, 1, true, sum_out);  // :214-222
+}
+
+// err_measures (src/vamp.cpp:760-852): the reductions (queued) ...
+static vampomi_status err_queue(vampomi_ctx* c, VampRun& R, const double* xhat, const double* Axest, DotBatch& b,
+                                double* m3, double* n2, double* s3) {
+    STCHK(b.add({T(xhat, R.ts), T(xhat, xhat), T(R.ts, R.ts)}, c->M, true, m3));
+    STCHK(b.add({T(c->y, Axest, vk::DIFF2), T(c->y, c->y)}, c->N, false, n2));  // l2_norm2(., 0)
+    return b.add({T(Axest, c->y), T(Axest, Axest), T(c->y, c->y)}, c->N, true, s3);
+}
+
+// ... and the scalar formulas once they are back
+static void err_finish(VampRun& R, const double* m3, const double* n2, const double* s3, int ind) {
+    const double corr = m3[0] / std::sqrt(m3[1] * m3[2]);
+    const double l2_pred_err = std::sqrt(n2[0] / n2[1]);
+    const double R2 = 1 - l2_pred_err * l2_pred_err;
+    const double corr_y = s3[0] / std::sqrt(s3[1] * s3[2]);
+    const double corr_y_2 = corr_y * corr_y;
+    if (ind == 1) {
+        R.metrics[1] = corr;
+        R.metrics[0] = R2;
+        R.metrics[4] = corr_y_2;
+    } else {
+        R.metrics[3] = corr;
+        R.metrics[2] = R2;
+        R.metrics[5] = corr_y_2;
+    }
+}
+
+static vampomi_status upload_or_zero(vampomi_ctx* c, double* dst, const double* host, int64_t n) {
+    if (n <= 0) return VAMPOMI_OK;
+    if (host)
+        HIPCHK(hipMemcpyAsync(dst, host, (size_t)n * 8, hipMemcpyHostToDevice, c->st));
+    else
+        HIPCHK(hipMemsetAsync(dst, 0, (size_t)n * 8, c->st));
+    return VAMPOMI_OK;
+}
+
+static vampomi_status vamp_alloc(vampomi_ctx* c, VampRun& R) {
+    const size_t M = (size_t)std::max<int64_t>(c->M, 1), ld = (size_t)c->ld;
+    for (double** p : {&R.r1, &R.x1, &R.x1p, &R.x1n, &R.x1d, &R.r2, &R.x2, &R.bern, &R.invQ, &R.v, &R.atxy, &R.ts,
+                       &R.tmpM, &R.atx0})
+        STCHK(dev_alloc(p, M));
+    for (auto& p : R.cgw) STCHK(dev_alloc(&p, M));
+    STCHK(dev_alloc(&R.z1buf, ld));
+    STCHK(dev_alloc(&R.nb3, 3 * ld));
+    STCHK(dev_alloc(&R.nsc, vk::kMaxRhs * ld));
+    HIPCHK(hipMemsetAsync(R.z1buf, 0, ld * 8, c->st));
+    HIPCHK(hipMemsetAsync(R.nb3, 0, 3 * ld * 8, c->st));
+    HIPCHK(hipMemsetAsync(R.nsc, 0, vk::kMaxRhs * ld * 8, c->st));
+    return VAMPOMI_OK;
+}
+
+extern "C" vampomi_status vampomi_vamp_begin(vampomi_ctx* c, const vampomi_params* p, vampomi_result* r) {
+    if (!c || !p) return fail(VAMPOMI_ERR_ARG, "null argument");
+    if (!c->have_X || !c->have_y) return fail(VAMPOMI_ERR_STATE, "load methylation data and phenotype first");
+    if (p->model && std::strcmp(p->model, "linear") != 0)
+        return fail(VAMPOMI_ERR_MODEL, std::string("model '") + p->model + "' is not supported (linear only)");
+    if (p->L < 1 || p->L > VAMPOMI_MAX_L) return fail(VAMPOMI_ERR_ARG, "number of mixture components out of range");
+    HIPCHK(hipSetDevice(c->device));
+    c->run.reset(new VampRun());
+    VampRun& R = *c->run;
+    R.prm = *p;
+    R.res = r;
+    R.fuse = p->batch_rhs != 0;
+    R.out_dir = p->out_dir ? p->out_dir : "";
+    R.out_name = p->out_name ? p->out_name : "";
+    R.write = !R.out_dir.empty();
+    R.mix.L = p->L;
+    for (int j = 0; j < p->L; ++j) {
+        R.mix.probs[j] = p->probs[j];
+        R.mix.vars[j] = p->vars[j] * (double)c->N;  // src/vamp.cpp:87-88
+    }
+    R.gam1 = p->gam1;
+    R.gamw = 1.0 / (1.0 - p->h2);  // src/main_meth.cpp:52
+    R.gam2 = 0;
+    STCHK(vamp_alloc(c, R));
+    STCHK(upload_or_zero(c, R.ts, p->true_signal, c->M));
+    // P1 (src/vamp.cpp:70-79): x1_hat = r1 = x1hat_init / sqrt(N)
+    std::vector<double> h((size_t)std::max<int64_t>(c->M, 1), 0.0);
+    for (int64_t i = 0; i < c->M; ++i) h[i] = (p->x1hat_init ? p->x1hat_init[i] : 0.0) / std::sqrt((double)c->N);
+    STCHK(upload_or_zero(c, R.x1, h.data(), c->M));
+    STCHK(upload_or_zero(c, R.r1, h.data(), c->M));
+    STCHK(upload_or_zero(c, R.x2, nullptr, c->M));
+    {  // A^T y is the same every iteration (y fixed, src/vamp.cpp:303): one pass
+        const double* u[1] = {c->y};
+        double* o[1] = {R.atxy};
+        STCHK(atx_dev(c, 1, u, o, 0, 0.0, 0.0, nullptr));
+    }
+    if (R.write) {
+        R.p_metrics = R.out_dir + "/" + R.out_name + "_metrics.csv";
+        R.p_params = R.out_dir + "/" + R.out_name + "_params.csv";
+        R.p_prior = R.out_dir + "/" + R.out_name + "_prior.csv";
+        if (c->rank == 0) {  // setup_io + headers (src/vamp.cpp:115-123, 854-882)
+            std::vector<std::string> prior_h{"iteration", "number of components"};
+            for (int i = 0; i < R.mix.L; ++i) prior_h.push_back("prob" + std::to_string(i));
+            for (int i = 0; i < R.mix.L; ++i) prior_h.push_back("var" + std::to_string(i));
+            const bool ok =
+                vio::csv_create_with_header(R.p_metrics, {"iteration", "R2 denoising", "x1 correlation denoising",
+                                                          "R2 LMMSE", "x2 correlation LMMSE", "z1 correlation denoising",
+                                                          "z2 correlation LMMSE"}) &&
+                vio::csv_create_with_header(R.p_params, {"iteration", "alpha1", "gam1", "alpha2", "gam2", "gamw"}) &&
+                vio::csv_create_with_header(R.p_prior, prior_h);
+            if (!ok) return fail(VAMPOMI_ERR_IO, "cannot create output CSV files in " + R.out_dir);
+        }
+    }
+    if (r) {
+        r->iterations_run = 0;
+        r->a_passes_ref = 0;
+        r->a_passes_exec = 0;
+    }
+    HIPCHK(hipStreamSynchronize(c->st));
+    return VAMPOMI_OK;
+}
+
+static vampomi_status write_bins(vampomi_ctx* c, VampRun& R) {
+    const bool hist = R.res && (R.res->x1_hist || R.res->r1_hist);
+    if (!R.write && !hist) return VAMPOMI_OK;
+    const int64_t M = c->M;
+    std::vector<double> hx((size_t)std::max<int64_t>(M, 1)), hr((size_t)std::max<int64_t>(M, 1));
+    HIPCHK(hipMemcpyAsync(hx.data(), R.x1, (size_t)M * 8, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipMemcpyAsync(hr.data(), R.r1, (size_t)M * 8, hipMemcpyDeviceToHost, c->st));
+    STCHK(host_sync(c));
+    const double sqrtN = std::sqrt((double)c->N);
+    for (int64_t i = 0; i < M; ++i) {
+        hx[i] = hx[i] / sqrtN;  // x1_hat_scaled (src/vamp.cpp:237-238)
+        hr[i] = hr[i] / sqrtN;  // r1_scaled (:246-248)
+    }
+    if (R.res && R.res->x1_hist) std::memcpy(R.res->x1_hist + (int64_t)(R.it - 1) * M, hx.data(), (size_t)M * 8);
+    if (R.res && R.res->r1_hist) std::memcpy(R.res->r1_hist + (int64_t)(R.it - 1) * M, hr.data(), (size_t)M * 8);
+    if (R.write) {
+        const std::string base = R.out_dir + "/" + R.out_name;
+        if (!vio::store_vec(base + "_it_" + std::to_string(R.it) + ".bin", hx.data(), c->S, M) ||
+            !vio::store_vec(base + "_r1_it_" + std::to_string(R.it) + ".bin", hr.data(), c->S, M))
+            return fail(VAMPOMI_ERR_IO, "cannot write iteration vectors to " + R.out_dir);
+    }
+    return VAMPOMI_OK;
+}
+
+// one VAMP iteration (src/vamp.cpp:148-428)
+extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
+    if (!c || !c->run) return fail(VAMPOMI_ERR_STATE, "vampomi_vamp_begin not called");
+    VampRun& R = *c->run;
+    if (R.stopped || R.it >= R.prm.max_iter) {
+        R.stopped = true;
+        if (stopped) *stopped = 1;
+        return VAMPOMI_OK;
+    }
+    HIPCHK(hipSetDevice(c->device));
+    const int64_t M = c->M, N = c->N, Mt = c->Mt, ld = c->ld;
+    const int it = ++R.it;
+    vampomi_result* res = R.res;
+
+    // ---------------- denoising (:177-232) ----------------
+    if (!R.have_next) {
+        if (it > R.prm.learn_prior_delay) STCHK(update_prior(c, R, R.mix, R.gam1, R.r1));  // :186-187
+        std::swap(R.x1, R.x1p);  // x1_hat_prev = x1_hat (:203)
+        DotBatch b(c);
+        STCHK(denoise_into(c, R.mix, R.gam1, R.r1, R.x1, R.x1p, it > 1, R.prm.rho, R.x1d, b, &R.sum_d));
+        STCHK(b.flush());
+        R.alpha1 = R.sum_d / (double)Mt;  // :223
+        const double* xs[1] = {R.x1};
+        STCHK(ax_dev(c, 1, xs, R.z1buf));  // z1 = Ax(x1_hat) (:232)
+        R.z1 = R.z1buf;
+    } else {  // prefetched by iteration it-1 (see file comment, item 2)
+        double* old = R.x1p;
+        R.x1p = R.x1;
+        R.x1 = R.x1n;
+        R.x1n = old;
+        R.mix = R.mix_next;
+        R.alpha1 = R.alpha1_next;
+        R.z1 = R.nb3 + 2 * ld;
+    }
+    R.passes_ref += 1;
+    if (res && res->L_hist) res->L_hist[it - 1] = R.mix.L;
+    R.eta1 = R.gam1 / R.alpha1;  // :230
+    STCHK(write_bins(c, R));     // :235-249
+    R.gam2 = smin(smax(R.eta1 - R.gam1, 1e-11), 1e11);  // :255-256
+    HIPCHK(vk::lincomb_div(M, R.eta1, R.x1, R.gam1, R.r1, R.gam2, R.r2, c->st));  // r2 (:259-261)
+    DotBatch e1(c);
+    STCHK(err_queue(c, R, R.x1, R.z1, e1, R.e1m, R.e1n, R.e1s));  // :272, flushed with the CG start
+    R.params[0] = R.alpha1;
+    R.params[1] = R.gam1;
+
+    // ---------------- LMMSE (:289-350) ----------------
+    HIPCHK(vk::bernoulli(R.prm.seed, it, c->S, M, std::sqrt((double)Mt), R.bern, c->st));  // :295-296 (P2)
+    HIPCHK(vk::axpby(M, R.gamw, R.atxy, R.gam2, R.r2, R.v, c->st));  // v = gamw ATx(y) + gam2 r2 (:303-306)
+    R.passes_ref += 1;
+    CgSystem sx{}, so{};
+    sx.v = R.v;
+    sx.mu = R.x2;  // mu_CG_last: warm start, updated in place (:308-311, :753-754)
+    sx.mu0_nonzero = it > 1;
+    sx.atx0 = (it > 1 && R.have_next) ? R.atx0 : nullptr;
+    sx.r = R.cgw[0];
+    sx.z = R.cgw[1];
+    sx.p = R.cgw[2];
+    sx.d = R.cgw[3];
+    so.v = R.bern;
+    so.mu = R.invQ;  // g2d_onsager starts from zeros (:496, :664-669)
+    so.onsager = true;
+    so.r = R.cgw[4];
+    so.z = R.cgw[5];
+    so.p = R.cgw[6];
+    so.d = R.cgw[7];
+    if (it == 1) HIPCHK(hipMemsetAsync(R.x2, 0, (size_t)std::max<int64_t>(M, 1) * 8, c->st));
+    HIPCHK(hipMemsetAsync(R.invQ, 0, (size_t)std::max<int64_t>(M, 1) * 8, c->st));
+    if (R.fuse) {
+        STCHK(pcg_run(c, {&sx, &so}, R.gamw, R.gam2, R.prm.CG_max_iter, R.prm.CG_err_tol, R.nsc, &R.passes_ref, &e1));
+    } else {
+        STCHK(pcg_run(c, {&sx}, R.gamw, R.gam2, R.prm.CG_max_iter, R.prm.CG_err_tol, R.nsc, &R.passes_ref, &e1));
+        STCHK(pcg_run(c, {&so}, R.gamw, R.gam2, R.prm.CG_max_iter, R.prm.CG_err_tol, R.nsc, &R.passes_ref, nullptr));
+    }
+    err_finish(R, R.e1m, R.e1n, R.e1s, 1);
+    if (res && res->cg_iters) res->cg_iters[it - 1] = sx.iters;
+    if (res && res->ons_iters) res->ons_iters[it - 1] = so.iters;
+    {
+        DotBatch b(c);
+        STCHK(b.add({T(R.bern, R.invQ)}, M, true, &R.a2));
+        STCHK(b.flush());
+        R.alpha2 = R.gam2 * R.a2;  // :498
+    }
+    R.eta2 = R.gam2 / R.alpha2;  // :341
+    const double gam1_prev = R.gam1;
+    R.gam1 = smin(smax(R.eta2 - R.gam2, 1e-11), 1e11);
+    R.gam1 = R.prm.rho * R.gam1 + (1 - R.prm.rho) * gam1_prev;  // :346
+    HIPCHK(vk::lincomb_div(M, R.eta2, R.x2, R.gam2, R.r2, R.gam1, R.r1, c->st));  // r1 (:348-350)
+
+    // ---- prefetch: denoising of iteration it+1 (discarded if the stop fires) ----
+    const bool next = R.fuse && it < R.prm.max_iter;
+    DotBatch fin(c);
+    if (next) {
+        R.mix_next = R.mix;
+        if (it + 1 > R.prm.learn_prior_delay) STCHK(update_prior(c, R, R.mix_next, R.gam1, R.r1));
+        STCHK(denoise_into(c, R.mix_next, R.gam1, R.r1, R.x1n, R.x1, true, R.prm.rho, R.x1d, fin, &R.sum_d));
+    }
+
+    // ---- updateNoisePrec (:504-529) + the next z1 in the same pass ----
+    {
+        const double* xs[3] = {R.x2, R.invQ, R.x1n};
+        STCHK(ax_dev(c, next ? 3 : 2, xs, R.nb3));
+        R.passes_ref += 2;
+        STCHK(fin.add({T(R.nb3, c->y, vk::DIFF2)}, N, false, &R.tn));  // l2_norm2(temp, 0)
+        const double* u[2] = {R.nb3 + ld, R.nb3};  // A.invQ (trace), A.x2 (next warm start)
+        double* o[2] = {R.tmpM, R.atx0};
+        STCHK(atx_dev(c, next ? 2 : 1, u, o, 0, 0.0, 0.0, nullptr));
+        R.passes_ref += 1;
+        STCHK(fin.add({T(R.bern, R.tmpM)}, M, true, &R.tc));
+    }
+    STCHK(err_queue(c, R, R.x2, R.nb3, fin, R.e2m, R.e2n, R.e2s));  // :365 (A.x2_hat of :826 == nb3)
+    R.passes_ref += 1;
+    STCHK(fin.add({T(R.x1p, R.x1, vk::DIFF2), T(R.x1p, R.x1p)}, M, true, R.nm));  // NMSE (:409-413)
+    STCHK(fin.flush());
+    const double trace_corr = R.tc * (double)Mt;  // :521
+    if (R.prm.verbosity >= 1 && c->rank == 0)
+        std::printf("l2_norm2(temp) / N = %g\ntrace_correction / N = %g\n", R.tn / (double)N, trace_corr / (double)N);
+    R.gamw = (double)N / (R.tn + trace_corr);  // :528
+    err_finish(R, R.e2m, R.e2n, R.e2s, 2);
+    R.params[2] = R.alpha2;
+    R.params[3] = R.gam2;
+    R.params[4] = R.gamw;
+    if (res && res->params) std::memcpy(res->params + (int64_t)(it - 1) * 5, R.params, sizeof R.params);
+    if (res && res->metrics) std::memcpy(res->metrics + (int64_t)(it - 1) * 6, R.metrics, sizeof R.metrics);
+    if (R.write && c->rank == 0) {  // :388-393
+        if (!vio::csv_write_row(R.p_params, it, R.params, 5) || !vio::csv_write_row(R.p_metrics, it, R.metrics, 6))
+            return fail(VAMPOMI_ERR_IO, "cannot write CSV rows");
+    }
+    if (R.prm.verbosity >= 1 && c->rank == 0)
+        std::printf("it %d: alpha1 %.6g gam1 %.6g alpha2 %.6g gam2 %.6g gamw %.6g L %d cg %d/%d\n", it, R.alpha1,
+                    R.gam1, R.alpha2, R.gam2, R.gamw, R.mix.L, sx.iters, so.iters);
+
+    // stopping criteria (:409-423)
+    const double NMSE = std::sqrt(R.nm[0] / R.nm[1]);
+    if ((it > 1 && NMSE < R.prm.stop_criteria_thr) || it >= R.prm.max_iter) R.stopped = true;
+    R.have_next = next && !R.stopped;
+    if (R.have_next) R.alpha1_next = R.sum_d / (double)Mt;
+    if (res) {
+        res->iterations_run = it;
+        res->a_passes_ref = R.passes_ref;
+        res->a_passes_exec = c->stats.a_passes_exec;
+    }
+    if (c->timing) resolve_timing(c);
+    if (stopped) *stopped = R.stopped ? 1 : 0;
+    return VAMPOMI_OK;
+}
+
+extern "C" vampomi_status vampomi_vamp_end(vampomi_ctx* c) {
+    if (!c || !c->run) return fail(VAMPOMI_ERR_STATE, "vampomi_vamp_begin not called");
+    VampRun& R = *c->run;
+    vampomi_result* res = R.res;
+    if (res) {
+        if (res->x1_final && c->M > 0) {
+            HIPCHK(hipMemcpyAsync(res->x1_final, R.x1, (size_t)c->M * 8, hipMemcpyDeviceToHost, c->st));
+            STCHK(host_sync(c));
+            const double sqrtN = std::sqrt((double)c->N);
+            for (int64_t i = 0; i < c->M; ++i) res->x1_final[i] = res->x1_final[i] / sqrtN;  // :437
+        }
+        res->L_final = R.mix.L;
+        for (int j = 0; j < R.mix.L; ++j) {
+            res->probs_final[j] = R.mix.probs[j];
+            res->vars_final[j] = R.mix.vars[j] / (double)c->N;
+        }
+        res->a_passes_ref = R.passes_ref;
+        res->a_passes_exec = c->stats.a_passes_exec;
+    }
+    if (c->timing) resolve_timing(c);
+    c->run.reset();
+    return VAMPOMI_OK;
+}
+
+extern "C" vampomi_status vampomi_infere(vampomi_ctx* c, const vampomi_params* p, vampomi_result* r) {
+    STCHK(vampomi_vamp_begin(c, p, r));
+    int stopped = 0;
+    while (!stopped) {
+        vampomi_status s = vampomi_vamp_step(c, &stopped);
+        if (s != VAMPOMI_OK) {
+            c->run.reset();
+            return s;
+        }
+    }
+    return vampomi_vamp_end(c);
+}
+
+extern "C" void vampomi_params_default(vampomi_params* p) {
+    // src/options.hpp:62-104 (code defaults, not the README table)
+    std::memset(p, 0, sizeof *p);
+    p->gam1 = 1e-6;
+    p->h2 = 0.5;
+    p->max_iter = 50;
+    p->CG_max_iter = 500;
+    p->CG_err_tol = 1e-5;
+    p->EM_max_iter = 1;
+    p->EM_err_thr = 1e-2;
+    p->rho = 0.5;
+    p->learn_vars = 1;
+    p->learn_prior_delay = 1;
+    p->stop_criteria_thr = 0.01;
+    p->merge_vars_thr = 5e-1;
+    static const double v[10] = {0, 1e-06, 6e-06, 3e-05, 2e-04, 1e-03, 6e-03, 3e-02, 2e-01, 1e+00};
+    static const double q[10] = {9.90000e-01, 5.00000e-03, 2.50000e-03, 1.25000e-03, 6.25000e-04,
+                                 3.12500e-04, 1.56250e-04, 7.81250e-05, 3.90625e-05, 3.90625e-05};
+    p->L = 10;
+    for (int j = 0; j < 10; ++j) {
+        p->vars[j] = v[j];
+        p->probs[j] = q[j];
+    }
+    p->seed = 0x5EED5EEDULL;
+    p->batch_rhs = 1;
+    p->model = "linear";
+}
