@@ -199,7 +199,7 @@ vampomi_status atx_dev(vampomi_ctx* c, int K, const double* const* u, double* co
         t.b = ev_get(c);
         HIPCHK(hipEventRecord(t.a, c->st));
     }
-    HIPCHK(vk::atx(c->shard(), K, us, os, 1.0 / c->sqrtN, mode, tau, gam2, ps, c->red_part, c->st));
+    HIPCHK(vk::atx(c->shard(), K, us, os, 1.0 / c->sqrtN, mode, tau, gam2, ps, nullptr, c->st));
     if (c->timing) {
         HIPCHK(hipEventRecord(t.b, c->st));
         t.cls = 1;
@@ -210,7 +210,14 @@ vampomi_status atx_dev(vampomi_ctx* c, int K, const double* const* u, double* co
     }
     c->stats.a_passes_exec++;
     if (mode == 1) {
-        HIPCHK(vk::sum_partials(c->red_part, vk::atx_blocks(c->M, K), K, c->scal + SL_DP, c->st));
+        // <d_k, p_k> with the fixed-geometry reduction (depends on M only, not on
+        // the A^T kernel variant chosen for this K), so a system's CG iterates are
+        // bitwise the same whether it runs alone or batched with another
+        vk::DotArgs a{};
+        a.nt = K;
+        for (int k = 0; k < K; ++k) a.t[k] = vk::DotTerm{out[k], p[k], vk::DOT};
+        HIPCHK(vk::dots_partial(a, c->M, c->red_part, c->st));
+        HIPCHK(vk::sum_partials(c->red_part, vk::red_blocks(c->M), K, c->scal + SL_DP, c->st));
         STCHK(allreduce_dev(c, c->scal + SL_DP, K));
     }
     return VAMPOMI_OK;

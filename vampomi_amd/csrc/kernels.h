@@ -10,7 +10,7 @@ namespace vk {
 constexpr int kMaxRhs = 4;     // right-hand sides sharing one pass over X
 constexpr int kMaxL = 64;      // mixture components (VAMPOMI_MAX_L)
 constexpr int kMaxTerms = 8;   // dot-product terms per reduction launch
-constexpr int kRedBlocks = 256;  // max partial blocks of a reduction
+constexpr int kRedBlocks = 1024;  // max partial blocks of a reduction
 
 struct CPtrs { const double* p[kMaxRhs]; };
 struct Ptrs { double* p[kMaxRhs]; };
@@ -48,8 +48,8 @@ hipError_t vec_div(int K, int64_t n, int64_t ld, Ptrs v, double div, hipStream_t
 
 // ---- A^T.u : one wave per group of markers --------------------------------
 // mode 0: out_k[i] = (msig_i * dot_k(i)) * scale
-// mode 1 (lmmse_mult): out_k[i] = ((msig_i*dot)*scale)*tau + gam2*p_k[i],
-//   and per-workgroup partials of <out_k, p_k> into dp_part[blk*K + k]
+// mode 1 (lmmse_mult): out_k[i] = ((msig_i*dot)*scale)*tau + gam2*p_k[i]
+// (dp_part is unused; <out_k, p_k> is a separate fixed-geometry reduction)
 int atx_blocks(int64_t M, int K);
 hipError_t atx(const Shard& s, int K, CPtrs u, Ptrs out, double scale, int mode, double tau,
                double gam2, CPtrs p, double* dp_part, hipStream_t st);

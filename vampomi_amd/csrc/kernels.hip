@@ -247,35 +247,53 @@ hipError_t ax_partial(const Shard& s, const AxPlan& pl, int K, CPtrs x, double* 
     return hipGetLastError();
 }
 
-__global__ __launch_bounds__(kBlock) void ax_reduce_kernel(int K, int64_t N, int64_t ld, int nchunks,
-                                                           const double* __restrict__ part, Ptrs out,
-                                                           double div) {
-    const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (e >= (int64_t)K * N) return;
-    const int k = (int)(e / N);
-    const int64_t j = e - (int64_t)k * N;
-    const double* p = part + (int64_t)k * ld + j;
+// Stage 2: out_k[j] = sum over chunks of part[c][k][j].  A 512-thread block
+// covers 64 consecutive samples (one wave per chunk group, coalesced across
+// lanes); group g sums its contiguous chunk range in index order, then the 8
+// group sums are added in group order: a fixed tree, short dependent chains.
+constexpr int kRedGroups = 8;
+__global__ __launch_bounds__(64 * kRedGroups) void ax_reduce_kernel(int K, int64_t N, int64_t ld, int nchunks,
+                                                                    const double* __restrict__ part, Ptrs out,
+                                                                    double div) {
+    __shared__ double lds[kRedGroups][64];
+    const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+    const int64_t e = (int64_t)blockIdx.x * 64 + lane;
+    const bool valid = e < (int64_t)K * N;
+    const int k = valid ? (int)(e / N) : 0;
+    const int64_t j = valid ? e - (int64_t)k * N : 0;
+    const int per = (nchunks + kRedGroups - 1) / kRedGroups;
+    const int c0 = g * per, c1 = (c0 + per < nchunks) ? c0 + per : nchunks;
     const int64_t stride = (int64_t)K * ld;
+    const double* p = part + (int64_t)k * ld + j;
     double s = 0.0;
-    int c = 0;
-    for (; c + 4 <= nchunks; c += 4) {
-        const double q0 = p[(int64_t)(c + 0) * stride], q1 = p[(int64_t)(c + 1) * stride];
-        const double q2 = p[(int64_t)(c + 2) * stride], q3 = p[(int64_t)(c + 3) * stride];
-        s += q0;
-        s += q1;
-        s += q2;
-        s += q3;
+    if (valid) {
+        int c = c0;
+        for (; c + 4 <= c1; c += 4) {
+            const double q0 = p[(int64_t)(c + 0) * stride], q1 = p[(int64_t)(c + 1) * stride];
+            const double q2 = p[(int64_t)(c + 2) * stride], q3 = p[(int64_t)(c + 3) * stride];
+            s += q0;
+            s += q1;
+            s += q2;
+            s += q3;
+        }
+        for (; c < c1; ++c) s += p[(int64_t)c * stride];
     }
-    for (; c < nchunks; ++c) s += p[(int64_t)c * stride];
-    if (div > 0.0) s /= div;  // src/data.cpp:369-370: Ax_total[i] /= sqrt(N)
-    out.p[k][j] = s;
+    lds[g][lane] = s;
+    __syncthreads();
+    if (g == 0 && valid) {
+        double t = lds[0][lane];
+#pragma unroll
+        for (int q = 1; q < kRedGroups; ++q) t += lds[q][lane];
+        if (div > 0.0) t /= div;  // src/data.cpp:369-370: Ax_total[i] /= sqrt(N)
+        out.p[k][j] = t;
+    }
 }
 
 hipError_t ax_reduce(const AxPlan& pl, int K, int64_t N, int64_t ld, const double* part, Ptrs out, double div,
                      hipStream_t st) {
     const int64_t n = (int64_t)K * N;
-    hipLaunchKernelGGL(ax_reduce_kernel, dim3((unsigned)cdiv(n, kBlock)), dim3(kBlock), 0, st, K, N, ld, pl.nchunks,
-                       part, out, div);
+    hipLaunchKernelGGL(ax_reduce_kernel, dim3((unsigned)cdiv(n, 64)), dim3(64 * kRedGroups), 0, st, K, N, ld,
+                       pl.nchunks, part, out, div);
     return hipGetLastError();
 }
 
@@ -300,14 +318,13 @@ hipError_t vec_div(int K, int64_t n, int64_t /*ld*/, Ptrs v, double div, hipStre
 // so each load instruction reads 1 KiB of one column, UJ such 128-row steps
 // per loop trip.  Every u value loaded serves G markers.  The wave's partial
 // dots are reduced with an xor butterfly; mode 1 fuses the lmmse_mult
-// epilogue (src/vamp.cpp:656-659) and the <d,p> partial of the next CG step.
+// epilogue (src/vamp.cpp:656-659).
 template <int G, int K, int MODE, int UJ, bool NT>
 __global__ __launch_bounds__(kBlock) void atx_kernel(const double* __restrict__ X, int64_t ld, int64_t N, int64_t M,
                                                      const double* __restrict__ mave,
                                                      const double* __restrict__ msig, CPtrs u, Ptrs out,
                                                      double scale, double tau, double gam2, CPtrs pv,
-                                                     double* __restrict__ dp_part) {
-    __shared__ double lds[4][K];
+                                                     double* __restrict__ /*unused*/) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t m0 = ((int64_t)blockIdx.x * 4 + wave) * G;
     double acc[G][K];
@@ -361,37 +378,21 @@ __global__ __launch_bounds__(kBlock) void atx_kernel(const double* __restrict__ 
             }
         }
     }
-    double dpw[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) dpw[k] = 0.0;
 #pragma unroll
     for (int g = 0; g < G; ++g) {
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const double dot = wave_sum(acc[g][k]);
             const int64_t m = m0 + g;
-            if (m < M) {
+            if (m < M && lane == 0) {
                 double val = msig[m] * dot;  // sigma_inv * dpa
                 val *= scale;                // ATx[mloc] *= 1/sqrt(N)
                 if (MODE == 1) {
-                    const double pm = pv.p[k][m];
                     val *= tau;              // res[i] *= tau
-                    val += gam2 * pm;        // res[i] += gam2 * v[i]
-                    dpw[k] += val * pm;
+                    val += gam2 * pv.p[k][m];  // res[i] += gam2 * v[i]
                 }
-                if (lane == 0) out.p[k][m] = val;
+                out.p[k][m] = val;
             }
-        }
-    }
-    if (MODE == 1) {
-        if (lane == 0) {
-#pragma unroll
-            for (int k = 0; k < K; ++k) lds[wave][k] = dpw[k];
-        }
-        __syncthreads();
-        if (threadIdx.x < K) {
-            const int k = threadIdx.x;
-            dp_part[(int64_t)blockIdx.x * K + k] = ((lds[0][k] + lds[1][k]) + lds[2][k]) + lds[3][k];
         }
     }
 }
@@ -585,7 +586,7 @@ hipError_t add_noise(uint64_t seed, int64_t N, double sd, double* y, hipStream_t
 // reductions (inner_prod / l2_norm2, src/utilities.cpp:138-162)
 // ---------------------------------------------------------------------------
 int red_blocks(int64_t n) {
-    int64_t b = cdiv(n, 2048);
+    int64_t b = cdiv(n, 512);  // >= 2 elements per thread; enough blocks to fill 256 CUs at M ~ 1e5
     if (b < 1) b = 1;
     if (b > kRedBlocks) b = kRedBlocks;
     return (int)b;
