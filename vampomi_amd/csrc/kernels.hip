@@ -115,8 +115,12 @@ __global__ __launch_bounds__(kBlock) void ax_partial_kernel(const double* __rest
     const int64_t i0 = (int64_t)blockIdx.y * chunk;
     const int64_t i1 = (i0 + chunk < M) ? i0 + chunk : M;
     bool ok[P];
+    int64_t off[P];  // invalid pieces read row 0 of the column (in bounds) and are discarded at the store
 #pragma unroll
-    for (int q = 0; q < P; ++q) ok[q] = j0 + 128 * q < N;
+    for (int q = 0; q < P; ++q) {
+        ok[q] = j0 + 128 * q < N;
+        off[q] = ok[q] ? 128 * q : -j0;
+    }
     double acc[K][R];
 #pragma unroll
     for (int k = 0; k < K; ++k)
@@ -131,8 +135,7 @@ __global__ __launch_bounds__(kBlock) void ax_partial_kernel(const double* __rest
             for (int u = 0; u < U; ++u)
 #pragma unroll
                 for (int q = 0; q < P; ++q)
-                    xv[u][q] = ok[q] ? (NT ? ld_stream(col + (int64_t)u * ld + 128 * q) : ld2(col + (int64_t)u * ld + 128 * q))
-                                     : v2d{0.0, 0.0};
+                    xv[u][q] = NT ? ld_stream(col + (int64_t)u * ld + off[q]) : ld2(col + (int64_t)u * ld + off[q]);
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const double ave = mave[i + u];
@@ -152,8 +155,7 @@ __global__ __launch_bounds__(kBlock) void ax_partial_kernel(const double* __rest
         for (; i < i1; ++i) {
             v2d xv[P];
 #pragma unroll
-            for (int q = 0; q < P; ++q)
-                xv[q] = ok[q] ? (NT ? ld_stream(col + 128 * q) : ld2(col + 128 * q)) : v2d{0.0, 0.0};
+            for (int q = 0; q < P; ++q) xv[q] = NT ? ld_stream(col + off[q]) : ld2(col + off[q]);
             const double ave = mave[i];
             const double sg = msig[i];
 #pragma unroll
@@ -184,10 +186,10 @@ __global__ __launch_bounds__(kBlock) void ax_partial_kernel(const double* __rest
 struct AxVariant { int R, U; bool NT; };
 static constexpr AxVariant kAxVariants[] = {
     {2, 8, true}, {2, 8, false}, {4, 4, true}, {4, 8, true}, {8, 4, true},
-    {8, 2, true}, {2, 16, true}, {4, 4, false}, {8, 4, false},
+    {8, 2, true}, {2, 16, true}, {4, 6, true}, {2, 12, true},
 };
 static constexpr int kNumAxVariants = sizeof(kAxVariants) / sizeof(kAxVariants[0]);
-static int g_ax_variant = 3;  // R=4, U=8, nontemporal: best at every K on MI355X (tools/kbench.py)
+static int g_ax_variant = 0;  // R=2, U=8, nontemporal, one full round of resident workgroups: best at every K (tools/kbench.py)
 
 int ax_variant_count() { return kNumAxVariants; }
 bool set_ax_variant(int v) {
@@ -196,12 +198,42 @@ bool set_ax_variant(int v) {
     return true;
 }
 
+template <int K>
+static const void* ax_fn(int v) {
+    switch (v) {
+        case 0: return (const void*)ax_partial_kernel<K, 2, 8, true>;
+        case 1: return (const void*)ax_partial_kernel<K, 2, 8, false>;
+        case 2: return (const void*)ax_partial_kernel<K, 4, 4, true>;
+        case 3: return (const void*)ax_partial_kernel<K, 4, 8, true>;
+        case 4: return (const void*)ax_partial_kernel<K, 8, 4, true>;
+        case 5: return (const void*)ax_partial_kernel<K, 8, 2, true>;
+        case 6: return (const void*)ax_partial_kernel<K, 2, 16, true>;
+        case 7: return (const void*)ax_partial_kernel<K, 4, 6, true>;
+        default: return (const void*)ax_partial_kernel<K, 2, 12, true>;
+    }
+}
+
+// resident workgroups of the K=2 kernel (the common batch width) on the device
+static int64_t ax_resident_slots(int v) {
+    int dev = 0, cus = 0, per_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+        return 2048;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ax_fn<2>(v), kBlock, 0) != hipSuccess || per_cu <= 0)
+        return 2048;
+    return (int64_t)cus * per_cu;
+}
+
 AxPlan ax_plan(int64_t N, int64_t M) {
     AxPlan p;
     p.variant = g_ax_variant;
     p.tiles = (int)cdiv(N, (int64_t)kBlock * kAxVariants[p.variant].R);
-    int64_t target = 2048;  // 8 workgroups per CU on 256 CUs
-    int64_t nch = cdiv(target, p.tiles);
+    // whole rounds of resident workgroups (no partly filled last round), >= 2048 workgroups;
+    // the plan is the same for every batch width K, so batched and solo passes sum identically
+    const int64_t slots = ax_resident_slots(p.variant);
+    const int64_t rounds = cdiv(2048, slots);
+    int64_t target = rounds * slots;
+    int64_t nch = target / p.tiles > 0 ? target / p.tiles : 1;
     int64_t maxch = M / 64 > 0 ? M / 64 : 1;  // at least 64 markers per chunk
     if (nch > maxch) nch = maxch;
     if (nch < 1) nch = 1;
@@ -228,8 +260,8 @@ static bool launch_ax_v(int v, const Shard& s, const AxPlan& pl, CPtrs x, double
         case 4: launch_ax<K, 8, 4, true>(s, pl, x, part, st); return true;
         case 5: launch_ax<K, 8, 2, true>(s, pl, x, part, st); return true;
         case 6: launch_ax<K, 2, 16, true>(s, pl, x, part, st); return true;
-        case 7: launch_ax<K, 4, 4, false>(s, pl, x, part, st); return true;
-        case 8: launch_ax<K, 8, 4, false>(s, pl, x, part, st); return true;
+        case 7: launch_ax<K, 4, 6, true>(s, pl, x, part, st); return true;
+        case 8: launch_ax<K, 2, 12, true>(s, pl, x, part, st); return true;
         default: return false;
     }
 }
