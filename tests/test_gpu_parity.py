@@ -288,3 +288,31 @@ def test_every_kernel_variant_is_correct():
                 else:
                     assert relerr(d.ATx(u), atx_ref) < 1e-13, ("atx", v)
             _lib.check(lib.vampomi_dev_set_variant(d.ctx, which, 0))
+
+
+def test_rccl_code_path_single_rank(tmp_path):
+    """The multi-rank data path (RCCL communicator, N-vector and scalar
+    all-reduces, division after the reduce) on a 1-rank communicator gives
+    bitwise the same run as the direct path."""
+    import sys
+
+    code = r'''
+import sys, numpy as np
+sys.path[:0] = [%r, %r]
+import vampomi_amd as va
+from _data import make_problem
+X, y, beta = make_problem(800, 1500)
+with va.Data(800, 1500) as d:
+    d.load_meth(X); d.set_phen(y, standardize=False)
+    v = va.Vamp(d, va.VampOptions(max_iter=5, stop_criteria_thr=0.0), true_signal=beta)
+    v.infere(keep_hist=True)
+    np.save(sys.argv[1], v.x1_hist[:5, :1500])
+''' % (os.path.dirname(os.path.dirname(os.path.abspath(__file__))), os.path.dirname(os.path.abspath(__file__)))
+    outs = []
+    for force in ("0", "1"):
+        f = tmp_path / f"x{force}.npy"
+        env = dict(os.environ, VAMPOMI_FORCE_RCCL=force)
+        r = subprocess.run([sys.executable, "-c", code, str(f)], env=env, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        outs.append(np.load(f))
+    assert np.array_equal(outs[0], outs[1])

@@ -57,6 +57,7 @@ struct vampomi_ctx {
     double sqrtN = 1.0;
     hipStream_t st = nullptr;
     ncclComm_t comm = nullptr;
+    bool use_comm = false;  // nranks > 1 (or VAMPOMI_FORCE_RCCL): all-reduces through RCCL
 
     double* X = nullptr;     // M columns x ld, marker-major, pad rows zero
     double* mave = nullptr;

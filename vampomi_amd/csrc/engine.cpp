@@ -100,7 +100,7 @@ vampomi_status host_sync(vampomi_ctx* c) {
 }
 
 vampomi_status allreduce_dev(vampomi_ctx* c, double* buf, size_t n) {
-    if (c->nranks > 1 && n > 0) NCCLCHK(ncclAllReduce(buf, buf, n, ncclDouble, ncclSum, c->comm, c->st));
+    if (c->use_comm && n > 0) NCCLCHK(ncclAllReduce(buf, buf, n, ncclDouble, ncclSum, c->comm, c->st));
     return VAMPOMI_OK;
 }
 
@@ -170,7 +170,7 @@ vampomi_status ax_dev(vampomi_ctx* c, int K, const double* const* x, double* out
         c->pending.push_back(t);
     }
     c->stats.a_passes_exec++;
-    if (c->nranks == 1) {
+    if (!c->use_comm) {
         HIPCHK(vk::ax_reduce(c->axp, K, c->N, c->ld, c->ax_part, os, c->sqrtN, c->st));
     } else {
         HIPCHK(vk::ax_reduce(c->axp, K, c->N, c->ld, c->ax_part, os, 0.0, c->st));
@@ -321,9 +321,17 @@ extern "C" vampomi_status vampomi_open(const vampomi_shard_desc* d, vampomi_ctx*
     STCHK(dev_alloc(&c->nbuf, (size_t)vk::kMaxRhs * c->ld));
     HIPCHK(hipMemsetAsync(c->nbuf, 0, (size_t)vk::kMaxRhs * c->ld * 8, c->st));
     STCHK(dev_alloc(&c->mbuf, (size_t)2 * vk::kMaxRhs * Mx));
-    if (c->nranks > 1) {
+    // VAMPOMI_FORCE_RCCL=1 runs a 1-rank job through the multi-rank code path
+    // (RCCL communicator, all-reduces, post-reduce division) so that path can
+    // be exercised on a single GPU
+    const char* force = std::getenv("VAMPOMI_FORCE_RCCL");
+    c->use_comm = c->nranks > 1 || (force && std::atoi(force) != 0);
+    if (c->use_comm) {
         ncclUniqueId id;
-        std::memcpy(&id, d->comm_id, sizeof id);
+        if (d->comm_id)
+            std::memcpy(&id, d->comm_id, sizeof id);
+        else
+            NCCLCHK(ncclGetUniqueId(&id));
         NCCLCHK(ncclCommInitRank(&c->comm, c->nranks, id, c->rank));
     }
     HIPCHK(hipStreamSynchronize(c->st));
@@ -348,7 +356,7 @@ extern "C" vampomi_status vampomi_sync(vampomi_ctx* c) {
 
 extern "C" vampomi_status vampomi_barrier(vampomi_ctx* c) {
     if (!c) return fail(VAMPOMI_ERR_ARG, "null context");
-    if (c->nranks > 1) STCHK(allreduce_dev(c, c->scal + SL_BARRIER, 1));
+    if (c->use_comm) STCHK(allreduce_dev(c, c->scal + SL_BARRIER, 1));
     HIPCHK(hipStreamSynchronize(c->st));
     return VAMPOMI_OK;
 }

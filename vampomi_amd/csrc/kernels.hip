@@ -103,7 +103,7 @@ static inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 // U markers are loaded before any arithmetic (U*R/2 16-byte loads in flight
 // per lane).  Per-sample summation order within a chunk is the reference's:
 // markers in index order, acc += (x - mave_i) * (msig_i * x_i).
-template <int K, int R, int U, bool NT>
+template <int K, int R, int U, bool NT, bool IL>
 __global__ __launch_bounds__(kBlock) void ax_partial_kernel(const double* __restrict__ X, int64_t ld,
                                                             int64_t N, int64_t M,
                                                             const double* __restrict__ mave,
@@ -112,8 +112,13 @@ __global__ __launch_bounds__(kBlock) void ax_partial_kernel(const double* __rest
     constexpr int P = R / 2;  // 16-byte pieces per lane per marker
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t j0 = (int64_t)blockIdx.x * (kBlock * R) + (int64_t)wave * (64 * R) + 2 * lane;
-    const int64_t i0 = (int64_t)blockIdx.y * chunk;
-    const int64_t i1 = (i0 + chunk < M) ? i0 + chunk : M;
+    // IL: chunk c owns markers c, c+nch, c+2nch, ... (all workgroups stream
+    // through the same narrow window of columns together: TLB/DRAM locality);
+    // otherwise chunk c owns the contiguous range [c*chunk, (c+1)*chunk)
+    const int64_t nch = gridDim.y;
+    const int64_t i0 = IL ? (int64_t)blockIdx.y : (int64_t)blockIdx.y * chunk;
+    const int64_t istep = IL ? nch : 1;
+    const int64_t i1 = IL ? M : ((i0 + chunk < M) ? i0 + chunk : M);
     bool ok[P];
     int64_t off[P];  // invalid pieces read row 0 of the column (in bounds) and are discarded at the store
 #pragma unroll
@@ -128,21 +133,23 @@ __global__ __launch_bounds__(kBlock) void ax_partial_kernel(const double* __rest
         for (int r = 0; r < R; ++r) acc[k][r] = 0.0;
     if (ok[0]) {
         const double* col = X + i0 * ld + j0;
+        const int64_t cstep = istep * ld;
         int64_t i = i0;
-        for (; i + U <= i1; i += U) {
+        for (; i + (U - 1) * istep < i1; i += U * istep) {
             v2d xv[U][P];
 #pragma unroll
             for (int u = 0; u < U; ++u)
 #pragma unroll
                 for (int q = 0; q < P; ++q)
-                    xv[u][q] = NT ? ld_stream(col + (int64_t)u * ld + off[q]) : ld2(col + (int64_t)u * ld + off[q]);
+                    xv[u][q] = NT ? ld_stream(col + (int64_t)u * cstep + off[q]) : ld2(col + (int64_t)u * cstep + off[q]);
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                const double ave = mave[i + u];
-                const double sg = msig[i + u];
+                const int64_t iu = i + u * istep;
+                const double ave = mave[iu];
+                const double sg = msig[iu];
 #pragma unroll
                 for (int k = 0; k < K; ++k) {
-                    const double w = sg * xs.p[k][i + u];
+                    const double w = sg * xs.p[k][iu];
 #pragma unroll
                     for (int q = 0; q < P; ++q) {
                         acc[k][2 * q] += (xv[u][q].x - ave) * w;
@@ -150,9 +157,9 @@ __global__ __launch_bounds__(kBlock) void ax_partial_kernel(const double* __rest
                     }
                 }
             }
-            col += (int64_t)U * ld;
+            col += (int64_t)U * cstep;
         }
-        for (; i < i1; ++i) {
+        for (; i < i1; i += istep) {
             v2d xv[P];
 #pragma unroll
             for (int q = 0; q < P; ++q) xv[q] = NT ? ld_stream(col + off[q]) : ld2(col + off[q]);
@@ -167,7 +174,7 @@ __global__ __launch_bounds__(kBlock) void ax_partial_kernel(const double* __rest
                     acc[k][2 * q + 1] += (xv[q].y - ave) * w;
                 }
             }
-            col += ld;
+            col += cstep;
         }
         double* dst = part + (int64_t)blockIdx.y * K * ld + j0;
 #pragma unroll
@@ -183,10 +190,10 @@ __global__ __launch_bounds__(kBlock) void ax_partial_kernel(const double* __rest
 }
 
 // tuning table (rows per lane R, markers in flight U, nontemporal loads)
-struct AxVariant { int R, U; bool NT; };
+struct AxVariant { int R, U; bool NT, IL; };
 static constexpr AxVariant kAxVariants[] = {
-    {2, 8, true}, {2, 8, false}, {4, 4, true}, {4, 8, true}, {8, 4, true},
-    {8, 2, true}, {2, 16, true}, {4, 6, true}, {2, 12, true},
+    {2, 8, true, false}, {2, 8, false, false}, {4, 4, true, false}, {4, 8, true, false}, {8, 4, true, false},
+    {2, 8, true, true},  {2, 4, true, true},   {4, 4, true, true},  {2, 12, true, true},
 };
 static constexpr int kNumAxVariants = sizeof(kAxVariants) / sizeof(kAxVariants[0]);
 static int g_ax_variant = 0;  // R=2, U=8, nontemporal, one full round of resident workgroups: best at every K (tools/kbench.py)
@@ -201,15 +208,15 @@ bool set_ax_variant(int v) {
 template <int K>
 static const void* ax_fn(int v) {
     switch (v) {
-        case 0: return (const void*)ax_partial_kernel<K, 2, 8, true>;
-        case 1: return (const void*)ax_partial_kernel<K, 2, 8, false>;
-        case 2: return (const void*)ax_partial_kernel<K, 4, 4, true>;
-        case 3: return (const void*)ax_partial_kernel<K, 4, 8, true>;
-        case 4: return (const void*)ax_partial_kernel<K, 8, 4, true>;
-        case 5: return (const void*)ax_partial_kernel<K, 8, 2, true>;
-        case 6: return (const void*)ax_partial_kernel<K, 2, 16, true>;
-        case 7: return (const void*)ax_partial_kernel<K, 4, 6, true>;
-        default: return (const void*)ax_partial_kernel<K, 2, 12, true>;
+        case 0: return (const void*)ax_partial_kernel<K, 2, 8, true, false>;
+        case 1: return (const void*)ax_partial_kernel<K, 2, 8, false, false>;
+        case 2: return (const void*)ax_partial_kernel<K, 4, 4, true, false>;
+        case 3: return (const void*)ax_partial_kernel<K, 4, 8, true, false>;
+        case 4: return (const void*)ax_partial_kernel<K, 8, 4, true, false>;
+        case 5: return (const void*)ax_partial_kernel<K, 2, 8, true, true>;
+        case 6: return (const void*)ax_partial_kernel<K, 2, 4, true, true>;
+        case 7: return (const void*)ax_partial_kernel<K, 4, 4, true, true>;
+        default: return (const void*)ax_partial_kernel<K, 2, 12, true, true>;
     }
 }
 
@@ -244,10 +251,10 @@ AxPlan ax_plan(int64_t N, int64_t M) {
     return p;
 }
 
-template <int K, int R, int U, bool NT>
+template <int K, int R, int U, bool NT, bool IL = false>
 static void launch_ax(const Shard& s, const AxPlan& pl, CPtrs x, double* part, hipStream_t st) {
-    hipLaunchKernelGGL((ax_partial_kernel<K, R, U, NT>), dim3(pl.tiles, pl.nchunks), dim3(kBlock), 0, st, s.X, s.ld,
-                       s.N, s.M, s.mave, s.msig, x, pl.chunk, part);
+    hipLaunchKernelGGL((ax_partial_kernel<K, R, U, NT, IL>), dim3(pl.tiles, pl.nchunks), dim3(kBlock), 0, st, s.X,
+                       s.ld, s.N, s.M, s.mave, s.msig, x, pl.chunk, part);
 }
 
 template <int K>
@@ -258,10 +265,10 @@ static bool launch_ax_v(int v, const Shard& s, const AxPlan& pl, CPtrs x, double
         case 2: launch_ax<K, 4, 4, true>(s, pl, x, part, st); return true;
         case 3: launch_ax<K, 4, 8, true>(s, pl, x, part, st); return true;
         case 4: launch_ax<K, 8, 4, true>(s, pl, x, part, st); return true;
-        case 5: launch_ax<K, 8, 2, true>(s, pl, x, part, st); return true;
-        case 6: launch_ax<K, 2, 16, true>(s, pl, x, part, st); return true;
-        case 7: launch_ax<K, 4, 6, true>(s, pl, x, part, st); return true;
-        case 8: launch_ax<K, 2, 12, true>(s, pl, x, part, st); return true;
+        case 5: launch_ax<K, 2, 8, true, true>(s, pl, x, part, st); return true;
+        case 6: launch_ax<K, 2, 4, true, true>(s, pl, x, part, st); return true;
+        case 7: launch_ax<K, 4, 4, true, true>(s, pl, x, part, st); return true;
+        case 8: launch_ax<K, 2, 12, true, true>(s, pl, x, part, st); return true;
         default: return false;
     }
 }
