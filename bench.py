@@ -40,6 +40,21 @@ import vampomi_amd as va  # noqa: E402
 from vampomi_amd.workloads import workload  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+PMC_FILE = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+
+
+def pmc_traffic(kernel: str):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc
+    summary (tools/pmc.sh: FETCH_SIZE x2 gfx950 correction + WRITE_SIZE)."""
+    try:
+        import json as _j
+
+        for name, d in _j.load(open(PMC_FILE)).items():
+            if kernel in name:
+                return d.get("traffic_bytes_per_launch")
+    except Exception:
+        return None
+    return None
 
 
 def cpu_baseline(d: "va.Data", w: dict, beta: np.ndarray, seed: int, budget_s: float = 20.0) -> dict:
@@ -142,20 +157,25 @@ def main():
     it_s = args.steps / el
     # dominant kernel: the (class, batch width) with the most device time
     cands = []
-    for cls, arr in (("ax_partial_kernel", st.ax_k), ("atx_kernel", st.atx_k)):
+    for which, arr in ((0, st.ax_k), (1, st.atx_k)):
         for k in range(4):
             if arr[k].launches:
-                cands.append((arr[k].ms_total, cls, k + 1, arr[k]))
+                cands.append((arr[k].ms_total, which, k + 1, arr[k]))
     roof = None
     if cands:
-        ms, cls, K, ks = max(cands, key=lambda c: c[0])
+        ms, which, K, ks = max(cands, key=lambda c: c[0])
+        kname = va.kernel_name(which, K, 1)  # A^T.u in the CG carries the lmmse_mult epilogue (mode 1)
         avg_ms = ks.ms_total / ks.launches
         bytes_per = ks.bytes_total / ks.launches
         achieved = bytes_per / (avg_ms * 1e-3) / 1e9
+        traffic = pmc_traffic(kname)
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                "kernel": f"{cls} K={K}", "avg_launch_us": round(avg_ms * 1e3, 2),
-                "bytes_per_launch": bytes_per, "launches": int(ks.launches)}
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": int(traffic) if traffic else None,
+                "traffic_unit": "HBM bytes per launch (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, "
+                                "profiles/r01_pmc_traffic.json)",
+                "algorithmic_bytes_per_launch": int(bytes_per),
+                "kernel": kname, "avg_launch_us": round(avg_ms * 1e3, 2), "launches": int(ks.launches)}
     all_ms = st.ax.ms_total + st.atx.ms_total
     all_bytes = st.ax.bytes_total + st.atx.bytes_total
     line = {

@@ -38,6 +38,13 @@ def divide_work(Mt: int, nranks: int, rank: int):
     return M.value, S.value, Mm.value
 
 
+def kernel_name(which: int, K: int, mode: int = 0) -> str:
+    """rocprofv3 name of the A.x (which=0) / A^T.u (which=1) kernel launched for K RHS."""
+    buf = C.create_string_buffer(256)
+    check(load().vampomi_dev_kernel_name(which, K, mode, buf, 256))
+    return buf.value.decode()
+
+
 def comm_unique_id() -> bytes:
     """RCCL unique id (rank 0 creates it, the caller broadcasts it)."""
     buf = (C.c_ubyte * UNIQUE_ID_BYTES)()

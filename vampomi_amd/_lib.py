@@ -126,6 +126,7 @@ SIGNATURES = {
     "vampomi_reset_stats": (C.c_int, [_P]),
     "vampomi_dev_set_variant": (C.c_int, [_P, C.c_int, C.c_int]),
     "vampomi_dev_time_pass": (C.c_int, [_P, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_double)]),
+    "vampomi_dev_kernel_name": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_char_p, C.c_int]),
 }
 
 _lib = None

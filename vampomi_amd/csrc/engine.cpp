@@ -752,3 +752,10 @@ extern "C" vampomi_status vampomi_dev_time_pass(vampomi_ctx* c, int which, int K
     *avg_ms = (double)ms / reps;
     return VAMPOMI_OK;
 }
+
+extern "C" vampomi_status vampomi_dev_kernel_name(int which, int K, int mode, char* out, int cap) {
+    if (!out || cap < 1) return fail(VAMPOMI_ERR_ARG, "bad buffer");
+    const std::string n = vk::kernel_name(which, K, mode);
+    std::snprintf(out, (size_t)cap, "%s", n.c_str());
+    return VAMPOMI_OK;
+}

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <string>
 
 namespace vk {
 
@@ -51,6 +52,7 @@ hipError_t vec_div(int K, int64_t n, int64_t ld, Ptrs v, double div, hipStream_t
 // mode 1 (lmmse_mult): out_k[i] = ((msig_i*dot)*scale)*tau + gam2*p_k[i]
 // (dp_part is unused; <out_k, p_k> is a separate fixed-geometry reduction)
 int atx_blocks(int64_t M, int K);
+std::string kernel_name(int which, int K, int mode);  // as rocprofv3 prints it
 hipError_t atx(const Shard& s, int K, CPtrs u, Ptrs out, double scale, int mode, double tau,
                double gam2, CPtrs p, double* dp_part, hipStream_t st);
 

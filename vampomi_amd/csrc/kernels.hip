@@ -11,6 +11,9 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
+#include <string>
+
 namespace vk {
 
 typedef double v2d __attribute__((ext_vector_type(2)));
@@ -452,6 +455,20 @@ bool set_atx_variant(int v) {
     if (v < -1 || v >= kNumAtxVariants) return false;
     g_atx_variant = v;
     return true;
+}
+
+// rocprofv3 kernel name of the launch that ax_partial / atx would make now
+std::string kernel_name(int which, int K, int mode) {
+    char b[160];
+    if (which == 0) {
+        const AxVariant& v = kAxVariants[g_ax_variant];
+        std::snprintf(b, sizeof b, "ax_partial_kernel<%d, %d, %d, %s, %s>", K, v.R, v.U, v.NT ? "true" : "false",
+                      v.IL ? "true" : "false");
+    } else {
+        const AtxVariant& v = kAtxVariants[atx_variant_for(K)];
+        std::snprintf(b, sizeof b, "atx_kernel<%d, %d, %d, %d, %s>", v.G, K, mode, v.UJ, v.NT ? "true" : "false");
+    }
+    return b;
 }
 
 int atx_blocks(int64_t M, int K) { return (int)cdiv(M, 4 * kAtxVariants[atx_variant_for(K)].G); }
