@@ -1,8 +1,9 @@
 """bench.py — VAMP iterations/s + HBM GB/s on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3] [--no-cpu-baseline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c4full] [--no-cpu-baseline]
 
 A "step" is one VAMP iteration (src/vamp.cpp:148-428) of the linear model
+(or src/vamp_probit.cpp:68-463 of the probit model for c4)
 over the whole synthetic problem, with every vector and the fp64 design
 matrix already resident in HBM.  --stop-criteria-thr is 0, so exactly W+K
 iterations run; W are untimed.
@@ -13,6 +14,9 @@ Workloads (synthetic, generated on the device):
                 constant aspect ratio: N = 10,000*sqrt(n), Mt = 50,000*sqrt(n).
   c3            per-GPU shard of configs[2] (N=100,000 x 62,500 markers per GPU,
                 methylation-like); at n=8 it is N=100,000 x Mt=500,000.
+  c4            probit model (configs[3], src/vamp_probit.cpp): N=50,000 x 50,000
+                markers per GPU, binary phenotype; at n=4 it is N=50,000 x Mt=200,000.
+  c4full        configs[3] whole on any n (80 GB: fits one MI355X).
 
 value = n_gpus * iterations/s ("shard-iterations/s": VAMP iterations over one
 GPU's shard; at n=1 exactly iterations/s of the workload).  Multi-GPU: one
@@ -40,16 +44,17 @@ import vampomi_amd as va  # noqa: E402
 from vampomi_amd.workloads import workload  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-PMC_FILE = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r01_pmc_traffic_{}.json")
 
 
-def pmc_traffic(kernel: str):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc
-    summary (tools/pmc.sh: FETCH_SIZE x2 gfx950 correction + WRITE_SIZE)."""
+def pmc_traffic(kernel: str, workload: str):
+    """HBM bytes per launch of `kernel` on `workload` from the committed
+    rocprofv3 --pmc summary (tools/pmc.sh: FETCH_SIZE x2 gfx950 correction +
+    WRITE_SIZE); None when that workload was not profiled."""
     try:
         import json as _j
 
-        for name, d in _j.load(open(PMC_FILE)).items():
+        for name, d in _j.load(open(PMC_FILE.format(workload))).items():
             if kernel in name:
                 return d.get("traffic_bytes_per_launch")
     except Exception:
@@ -69,12 +74,14 @@ def cpu_baseline(d: "va.Data", w: dict, beta: np.ndarray, seed: int, budget_s: f
     y = d.get_phen()
     # one iteration first to size the sample, then a fresh run of k iterations
     t0 = time.perf_counter()
-    r1 = O.vamp_infere(X, y, Mt, true_signal=beta, max_iter=1, stop_criteria_thr=0.0, keep_hist=False)
+    model = w.get("model", "linear")
+    r1 = O.vamp_infere(X, y, Mt, true_signal=beta, max_iter=1, stop_criteria_thr=0.0, keep_hist=False, model=model)
     t1 = time.perf_counter() - t0
     k = max(1, min(10, int(budget_s / max(t1, 1e-3))))
     if k > 1:
         t0 = time.perf_counter()
-        r = O.vamp_infere(X, y, Mt, true_signal=beta, max_iter=k, stop_criteria_thr=0.0, keep_hist=False)
+        r = O.vamp_infere(X, y, Mt, true_signal=beta, max_iter=k, stop_criteria_thr=0.0, keep_hist=False,
+                          model=model)
         tk = time.perf_counter() - t0
     else:
         r, tk = r1, t1
@@ -97,7 +104,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=48)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", default="c2", choices=["c2", "c3"])
+    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c4full"])
     ap.add_argument("--seed", type=int, default=20250711)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="skip the HIP-event kernel timing")
@@ -121,15 +128,20 @@ def main():
     d = va.Data(N, Mt, rank=rank, nranks=world, comm_id=comm_id, device=local)
     t0 = time.perf_counter()
     d.generate(args.seed, w["kind"])
-    beta = d.simulate_phen(args.seed + 1, lam=0.1, h2=0.8)
+    model = w.get("model", "linear")
+    if model == "bin_class":
+        beta = d.simulate_phen_binary(args.seed + 1, lam=0.1, h2=0.8)
+    else:
+        beta = d.simulate_phen(args.seed + 1, lam=0.1, h2=0.8)
     t_setup = time.perf_counter() - t0
 
-    opts = va.VampOptions(max_iter=args.warmup + args.steps, stop_criteria_thr=0.0, batch_rhs=args.batch_rhs)
+    opts = va.VampOptions(max_iter=args.warmup + args.steps, stop_criteria_thr=0.0, batch_rhs=args.batch_rhs,
+                          model=model)
     v = va.Vamp(d, opts, true_signal=beta)
     v.begin()
     for _ in range(args.warmup):
         v.step()
-    ref0, exec0 = v.a_passes
+    ref0, _ = v.a_passes
     d.reset_stats()
     d.set_timing(not args.no_timing)
 
@@ -146,7 +158,7 @@ def main():
     barrier()
     el = time.perf_counter() - t0
     st = d.stats()
-    ref1, exec1 = v.a_passes
+    ref1, _ = v.a_passes
     summ = v.summary()
     v.end()
     if world > 1:
@@ -168,12 +180,12 @@ def main():
         avg_ms = ks.ms_total / ks.launches
         bytes_per = ks.bytes_total / ks.launches
         achieved = bytes_per / (avg_ms * 1e-3) / 1e9
-        traffic = pmc_traffic(kname)
+        traffic = pmc_traffic(kname, w["workload"])
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": int(traffic) if traffic else None,
                 "traffic_unit": "HBM bytes per launch (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, "
-                                "profiles/r01_pmc_traffic.json)",
+                                f"profiles/{os.path.basename(PMC_FILE.format(w['workload']))})",
                 "algorithmic_bytes_per_launch": int(bytes_per),
                 "kernel": kname, "avg_launch_us": round(avg_ms * 1e3, 2), "launches": int(ks.launches)}
     all_ms = st.ax.ms_total + st.atx.ms_total
@@ -186,13 +198,13 @@ def main():
         "ms_per_step": round(el / args.steps * 1e3, 3),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "f64", "data": "synthetic (index-keyed dyadic generator, generated in HBM)",
-        "config": {"workload": w["workload"], "N": N, "Mt": Mt, "M_per_gpu": d.M,
+        "config": {"workload": w["workload"], "model": model, "N": N, "Mt": Mt, "M_per_gpu": d.M,
                    "design": "gaussian" if w["kind"] == va.GEN_GAUSS else "methylation-like",
                    "iterations_timed": f"{args.warmup + 1}-{args.warmup + args.steps}",
                    "parallelism": f"markers sharded over {n} GPU(s), RCCL all-reduce"},
         "roofline": roof,
         "hbm_gbs_all_A_kernels": round(all_bytes / (all_ms * 1e-3) / 1e9, 1) if all_ms > 0 else None,
-        "passes_exec_per_step": round((exec1 - exec0) / args.steps, 2),
+        "passes_exec_per_step": round(st.a_passes_exec / args.steps, 2),  # stats reset at the timed region
         "passes_ref_per_step": round((ref1 - ref0) / args.steps, 2),
         "a_kernel_frac_of_step": round(all_ms * 1e-3 / el, 3) if el > 0 else None,
         "cg_iters": summ["cg_iters"][args.warmup:], "ons_iters": summ["ons_iters"][args.warmup:],

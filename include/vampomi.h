@@ -19,8 +19,11 @@
  *   vamp::lmmse_mult           src/vamp.cpp:645-662     -> vampomi_lmmse_mult (COLLECTIVE)
  *   vamp::precondCG_solver     src/vamp.cpp:664-757     -> vampomi_pcg      (COLLECTIVE)
  *   vamp::g1 / vamp::g1d       src/vamp.cpp:440-492     -> vampomi_denoise  (COLLECTIVE: alpha1 sum)
- *   vamp::vamp + vamp::infere / infere_linear
- *        src/vamp.cpp:18-91, 94-107, 110-438            -> vampomi_infere   (COLLECTIVE)
+ *   vamp::g1_bin_class / g1d_bin_class
+ *        src/vamp_probit.cpp:469-488                    -> vampomi_denoise_bin
+ *   vamp::vamp + vamp::infere / infere_linear / infere_bin_class
+ *        src/vamp.cpp:18-91, 94-107, 110-438,
+ *        src/vamp_probit.cpp:19-488                     -> vampomi_infere   (COLLECTIVE)
  *        (or vampomi_vamp_begin / _step / _end, one VAMP iteration per step)
  *   divide_work                src/utilities.cpp:207-239 -> vampomi_divide_work
  *
@@ -37,7 +40,7 @@
 extern "C" {
 #endif
 
-#define VAMPOMI_ABI_VERSION 1
+#define VAMPOMI_ABI_VERSION 2
 #define VAMPOMI_MAX_L 64          /* mixture components */
 #define VAMPOMI_UNIQUE_ID_BYTES 128
 
@@ -102,6 +105,11 @@ vampomi_status vampomi_get_phen(vampomi_ctx* ctx, double* y /* N, host */);
  * (M local, host, may be NULL) receives beta = the true signal. COLLECTIVE */
 vampomi_status vampomi_simulate_phen(vampomi_ctx* ctx, uint64_t seed, double lam, double h2,
                                      double* beta_out);
+/* binary phenotype for the probit model: the liability of vampomi_simulate_phen
+ * thresholded at 0 (y = 1 if > 0 else 0), stored raw (read_phen(false),
+ * src/data.cpp:40-41). COLLECTIVE */
+vampomi_status vampomi_simulate_phen_binary(vampomi_ctx* ctx, uint64_t seed, double lam, double h2,
+                                            double* beta_out);
 vampomi_status vampomi_get_marker_stats(vampomi_ctx* ctx, double* mave, double* msig);
 /* copy local markers [i0, i0+count) back to the host, count x N doubles
  * (data::get_meth_data, src/data.hpp:53) */
@@ -127,7 +135,14 @@ vampomi_status vampomi_denoise(vampomi_ctx* ctx, const double* r1, double gam1, 
                                const double* vars, int L, double* x1, double* x1d, double* sum_d,
                                int mem);
 
-/* ---- the VAMP linear model (vamp::infere_linear) ---- */
+/* probit z-denoiser: z1[i] = g1_bin_class(p1[i], tau1, y[i]) with the context's
+ * phenotype y (raw 0/1), *sum_d = sum_i g1d_bin_class(p1[i], tau1, y[i]) (local:
+ * the N-side is replicated on every rank).  probit_var = 1, no covariates.
+ * src/vamp_probit.cpp:213-233, 469-488; erfcx src/utilities.cpp:293-363 */
+vampomi_status vampomi_denoise_bin(vampomi_ctx* ctx, const double* p1, double tau1, double* z1,
+                                   double* sum_d, int mem);
+
+/* ---- the VAMP linear and probit models (vamp::infere) ---- */
 typedef struct {
     double gam1, h2;              /* --gam1, --h2 (gamw = 1/(1-h2), src/main_meth.cpp:52) */
     int max_iter, CG_max_iter;    /* --iterations, --CG-max-iter */
@@ -147,7 +162,10 @@ typedef struct {
     const double* x1hat_init;     /* local slice (M) or NULL => zeros (host) */
     int batch_rhs;                /* 1 (default): share each A/A^T pass between the x2 and
                                      Onsager CG solves; 0: run them back to back */
-    const char* model;            /* "linear" (NULL == "linear") */
+    const char* model;            /* "linear" (NULL == "linear") or "bin_class" (probit,
+                                     src/vamp_probit.cpp; phenotype must be raw 0/1, i.e. read
+                                     with standardize = 0; h2/gamw unused; seed also keys the
+                                     Gaussian start p1) */
 } vampomi_params;
 
 typedef struct {
@@ -156,16 +174,21 @@ typedef struct {
     int* cg_iters;                /* k1 */
     int* ons_iters;               /* k2 */
     int* L_hist;                  /* mixture components after updatePrior */
-    double* params;               /* 5 per iteration: alpha1 gam1 alpha2 gam2 gamw */
-    double* metrics;              /* 6 per iteration */
+    double* params;               /* per iteration, 5 (linear): alpha1 gam1 alpha2 gam2 gamw;
+                                     8 (bin_class): alpha1 beta1 gam1 tau1 alpha2 beta2 gam2 tau2 */
+    double* metrics;              /* per iteration, 6 (linear); 12 (bin_class): TP TN FP FN
+                                     acc1 x1_corr TP TN FP FN acc2 x2_corr */
     double* x1_hist;              /* M per iteration: x1_hat/sqrt(N) (== _it_K.bin slice) */
     double* r1_hist;              /* M per iteration: r1/sqrt(N)     (== _r1_it_K.bin slice) */
-    double* x1_final;             /* M: returned x1_hat_scaled (src/vamp.cpp:437) */
+    double* x1_final;             /* M: what vamp::infere returns: x1_hat_scaled for linear
+                                     (src/vamp.cpp:437), x1_hat for bin_class (vamp_probit.cpp:465) */
     double probs_final[VAMPOMI_MAX_L];
     double vars_final[VAMPOMI_MAX_L];   /* divided by N, as printed/written */
     int L_final;
     int64_t a_passes_ref;         /* A/A^T passes the reference would have run */
     int64_t a_passes_exec;        /* passes actually executed (X streamed from HBM) */
+    double* prior_hist;           /* bin_class: (1 + 2*VAMPOMI_MAX_L) per iteration: the
+                                     _prior.csv row L, probs[L], vars[L] (vars x N), zero padded */
 } vampomi_result;
 
 void vampomi_params_default(vampomi_params* p);   /* src/options.hpp:62-104 defaults */

@@ -41,7 +41,7 @@ class Result(C.Structure):
                 ("L_hist", C.c_void_p), ("params", C.c_void_p), ("metrics", C.c_void_p),
                 ("x1_hist", C.c_void_p), ("r1_hist", C.c_void_p), ("x1_final", C.c_void_p),
                 ("probs_final", C.c_void_p), ("vars_final", C.c_void_p), ("L_final", C.c_int),
-                ("a_passes", C.c_int64)]
+                ("a_passes", C.c_int64), ("prior_hist", C.c_void_p)]
 
 
 _lib = None
@@ -80,6 +80,15 @@ def load() -> C.CDLL:
         lib.orc_vamp_infere_linear.restype = C.c_int
         lib.orc_vamp_infere_linear.argtypes = [C.POINTER(Problem), C.POINTER(Params), C.POINTER(Result)]
         lib.orc_store_vec.argtypes = [C.c_char_p, p, i64, i64]
+        lib.orc_vamp_infere_probit.restype = C.c_int
+        lib.orc_vamp_infere_probit.argtypes = [C.POINTER(Problem), C.POINTER(Params), C.POINTER(Result)]
+        lib.orc_probit_p1.restype = d
+        lib.orc_probit_p1.argtypes = [C.c_uint64, i64]
+        lib.orc_erfcx.restype = d
+        lib.orc_erfcx.argtypes = [d]
+        for f in (lib.orc_g1_bin, lib.orc_g1d_bin):
+            f.restype = d
+            f.argtypes = [d, d, d]
         _lib = lib
     return _lib
 
@@ -145,6 +154,23 @@ def g1d(y: float, gam1: float, probs, vars_scaled) -> float:
     return load().orc_g1d(y, gam1, _p(pr), _p(va), len(pr))
 
 
+def erfcx(x: float) -> float:
+    return load().orc_erfcx(x)
+
+
+def g1_bin(p: float, tau1: float, y: float) -> float:
+    return load().orc_g1_bin(p, tau1, y)
+
+
+def g1d_bin(p: float, tau1: float, y: float) -> float:
+    return load().orc_g1d_bin(p, tau1, y)
+
+
+def probit_p1(seed: int, N: int) -> np.ndarray:
+    lib = load()
+    return np.array([lib.orc_probit_p1(seed, i) for i in range(N)])
+
+
 def read_phen(path: str, N: int, standardize: bool = True) -> np.ndarray:
     y = np.zeros(N)
     n = load().orc_read_phen(path.encode(), 1 if standardize else 0, _p(y), N, None, None)
@@ -176,8 +202,14 @@ def vamp_infere(X: np.ndarray, y: np.ndarray, Mt: int, S: int = 0, rank: int = 0
                 gam1=1e-6, h2=0.5, max_iter=50, CG_max_iter=500, CG_err_tol=1e-5, EM_max_iter=1, EM_err_thr=1e-2,
                 rho=0.5, learn_vars=1, learn_prior_delay=1, stop_criteria_thr=0.01, merge_vars_thr=0.5,
                 vars: Sequence[float] = DEFAULT_VARS, probs: Sequence[float] = DEFAULT_PROBS,
-                seed=0x5EED5EED, out_dir="", out_name="", verbosity=0, alpha_scale=1.0, keep_hist=True) -> dict:
-    """Run the restated infere_linear on one shard X (M, N) marker-major."""
+                seed=0x5EED5EED, out_dir="", out_name="", verbosity=0, alpha_scale=1.0, keep_hist=True,
+                model="linear") -> dict:
+    """Run the restated infere_linear (model="linear") or infere_bin_class
+    (model="bin_class", y = raw 0/1 phenotype) on one shard X (M, N)."""
+    probit = model == "bin_class"
+    if model not in ("linear", "bin_class"):
+        raise ValueError(model)
+    npar, nmet = (8, 12) if probit else (5, 6)
     lib = load()
     X = np.ascontiguousarray(X, dtype=np.float64)
     M, N = X.shape
@@ -199,22 +231,27 @@ def vamp_infere(X: np.ndarray, y: np.ndarray, Mt: int, S: int = 0, rank: int = 0
     cg = np.zeros(max_iter, dtype=np.int32)
     ons = np.zeros(max_iter, dtype=np.int32)
     Lh = np.zeros(max_iter, dtype=np.int32)
-    params = np.zeros((max_iter, 5))
-    metrics = np.zeros((max_iter, 6))
+    params = np.zeros((max_iter, npar))
+    metrics = np.zeros((max_iter, nmet))
+    prior = np.zeros((max_iter, 1 + 2 * MAX_L)) if probit else None
     x1h = np.zeros((max_iter, max(M, 1))) if keep_hist else None
     r1h = np.zeros((max_iter, max(M, 1))) if keep_hist else None
     x1f = np.zeros(max(M, 1))
     pf, vf = np.zeros(MAX_L), np.zeros(MAX_L)
     res = Result(cg_iters=_p(cg), ons_iters=_p(ons), L_hist=_p(Lh), params=_p(params), metrics=_p(metrics),
-                 x1_hist=_p(x1h), r1_hist=_p(r1h), x1_final=_p(x1f), probs_final=_p(pf), vars_final=_p(vf))
-    rc = lib.orc_vamp_infere_linear(C.byref(pb), C.byref(pr), C.byref(res))
+                 x1_hist=_p(x1h), r1_hist=_p(r1h), x1_final=_p(x1f), probs_final=_p(pf), vars_final=_p(vf),
+                 prior_hist=_p(prior))
+    fn = lib.orc_vamp_infere_probit if probit else lib.orc_vamp_infere_linear
+    rc = fn(C.byref(pb), C.byref(pr), C.byref(res))
     if rc != 0:
-        raise RuntimeError(f"orc_vamp_infere_linear -> {rc}")
+        raise RuntimeError(f"{fn.__name__} -> {rc}")
     n = res.iterations_run
     out = {"iterations": n, "cg_iters": cg[:n].copy(), "ons_iters": ons[:n].copy(), "L": Lh[:n].copy(),
            "params": params[:n].copy(), "metrics": metrics[:n].copy(), "x1_final": x1f[:M].copy(),
            "probs_final": pf[:res.L_final].copy(), "vars_final": vf[:res.L_final].copy(), "a_passes": res.a_passes,
            "mave": mave, "msig": msig}
+    if probit:
+        out["prior"] = prior[:n].copy()
     if keep_hist:
         out["x1_hist"] = x1h[:n, :M].copy()
         out["r1_hist"] = r1h[:n, :M].copy()

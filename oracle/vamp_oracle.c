@@ -848,3 +848,313 @@ int orc_vamp_infere_linear(const orc_problem* pb, const orc_params* prm, orc_res
     free(s.x2_hat);
     return 0;
 }
+
+/* ------------------------------------------------------------------------- */
+/* probit model — src/vamp_probit.cpp                                        */
+/* ------------------------------------------------------------------------- */
+
+int orc_csv_create(const char* path) {
+    unlink(path);
+    int fd = open(path, O_CREAT | O_WRONLY | O_EXCL, 0666);
+    if (fd < 0) return -1;
+    close(fd);
+    return 0;
+}
+
+/* P2 for the Gaussian start p1 = simulate(N, {1}, {1}) (src/vamp_probit.cpp:53):
+ * one N(0,1)-like dyadic draw per sample, keyed on (seed, i) */
+double orc_probit_p1(uint64_t seed, int64_t i) {
+    return orc_gauss_dyadic(seed ^ 0x50524F4249545031ULL, 0, i);
+}
+
+/* erfcx — src/utilities.cpp:293-363.  The reference embeds N. Juffa's
+ * published scaled-complementary-error-function approximation: map
+ * a = |x| to q = (a-4)/(a+4), evaluate a degree-23 polynomial in q with fma
+ * (Horner), divide by (1+2a) with one Newton correction, reflect for x < 0.
+ * Outside [-10, 10] the reference returns +inf (x < -10) and
+ * std::numeric_limits<double>::lowest() (x > 10) — reproduced as is. */
+static const double ORC_ERFCX_POLY[24] = {
+    0x1.edcad78fc8044p-31,  0x1.b1548f14735d1p-30,  -0x1.a1ad2e6c4a7a8p-27, -0x1.1985b48f08574p-26,
+    0x1.c6a8093ac4f83p-24,  0x1.31c2b2b44b731p-24,  -0x1.b87373facb29fp-21, 0x1.3fef1358803b7p-22,
+    0x1.7eec072bb0be3p-18,  -0x1.78a680a741c4ap-17, -0x1.9951f39295cf4p-16, 0x1.3be1255ce180bp-13,
+    -0x1.a1df71176b791p-13, -0x1.8d4aaa0099bc8p-11, 0x1.49c673066c831p-8,   -0x1.0962386ea02b7p-6,
+    0x1.3079edf465cc3p-5,   -0x1.0fb06dfedc4ccp-4,  0x1.7fee004e266dfp-4,   -0x1.9ddb23c3e14d2p-4,
+    0x1.16ecefcfa4865p-4,   0x1.f7f5df66fc349p-7,   -0x1.1df1ad154a27fp-3,  0x1.dd2c8b74febf6p-3};
+
+double orc_erfcx(double x) {
+    if (x < -10.0) return INFINITY;
+    if (x > 10.0) return -DBL_MAX;
+    const double a = fmax(x, 0.0 - x);
+    /* q = (a-4)/(a+4), refined */
+    const double inv = 1.0 / (a + 4.0);
+    double q = (a - 4.0) * inv;
+    const double t0 = fma(q + 1.0, -4.0, a);
+    q = fma(inv, fma(q, -a, t0), q);
+    double p = ORC_ERFCX_POLY[0];
+    for (int k = 1; k < 24; ++k) p = fma(p, q, ORC_ERFCX_POLY[k]);
+    /* (1 + p) / (1 + 2a) with a residual correction */
+    const double h = (1.0 / (a + 0.5)) * 0.5;
+    const double q1 = fma(p, h, h);
+    const double res = (p - q1) + fma(q1 + q1, -a, 1.0);
+    double r = fma(res, h, q1);
+    if (a > DBL_MAX) r = 0.0;
+    if (x < 0.0) { /* erfcx(x) = 2 exp(x^2) - erfcx(|x|) */
+        const double s = x * x;
+        const double lo = fma(x, x, -s);
+        const double e = exp(s);
+        r = fma(e, lo + lo, e - r) + e;
+        if (e > DBL_MAX) r = e;
+    }
+    return r;
+}
+
+/* g1_bin_class / g1d_bin_class — src/vamp_probit.cpp:469-488 with
+ * probit_var = 1 and m_cov = 0 (main_meth reads no covariates) */
+#define ORC_PROBIT_VAR 1.0
+double orc_g1_bin(double p, double tau1, double y) {
+    const double c = (p + 0.0) / sqrt(ORC_PROBIT_VAR + 1.0 / tau1);
+    const double ratio = 2.0 / sqrt(2 * M_PI) / orc_erfcx(-(2 * y - 1) * c / sqrt(2));
+    return p + (2 * y - 1) * ratio / tau1 / sqrt(ORC_PROBIT_VAR + 1.0 / tau1);
+}
+
+double orc_g1d_bin(double p, double tau1, double y) {
+    const double c = (p + 0.0) / sqrt(ORC_PROBIT_VAR + 1.0 / tau1);
+    const double ratio = 2.0 / sqrt(2 * M_PI) / orc_erfcx(-(2 * y - 1) * c / sqrt(2));
+    return 1 - ratio / (1 + tau1 * ORC_PROBIT_VAR) * ((2 * y - 1) * c + ratio);
+}
+
+/* predict_probit(z, 0.5) + confusion_matrix + accuracy —
+ * src/vamp_probit.cpp:619-663, normal_cdf src/utilities.cpp:284-287.
+ * out: TP, TN, FP, FN, acc */
+static void probit_confusion(const double* z, const double* y, int64_t N, double* out) {
+    int64_t TP = 0, TN = 0, FP = 0, FN = 0;
+    for (int64_t i = 0; i < N; ++i) {
+        const double yh = (0.5 * erfc(-z[i] * M_SQRT1_2) >= 0.5) ? 1.0 : 0.0;
+        if (y[i] == 1 && yh == 1)
+            TP++;
+        else if (y[i] == 0 && yh == 0)
+            TN++;
+        else if (y[i] == 1 && yh == 0)
+            FN++;
+        else if (y[i] == 0 && yh == 1)
+            FP++;
+    }
+    out[0] = (double)TP;
+    out[1] = (double)TN;
+    out[2] = (double)FP;
+    out[3] = (double)FN;
+    out[4] = (double)(TP + TN) / (double)(TP + TN + FP + FN);
+}
+
+/* infere_bin_class — src/vamp_probit.cpp:19-467 */
+int orc_vamp_infere_probit(const orc_problem* pb, const orc_params* prm, orc_result* res) {
+    int64_t N = pb->N, M = pb->M, Mt = pb->Mt;
+    orc_vamp s;
+    memset(&s, 0, sizeof s);
+    s.pb = pb;
+    s.N = N;
+    s.M = M;
+    s.Mt = Mt;
+    s.L = prm->L;
+    if (s.L < 1 || s.L > ORC_MAX_L) return -1;
+    for (int j = 0; j < s.L; ++j) {
+        s.probs[j] = prm->probs[j];
+        s.vars[j] = prm->vars[j] * (double)N; /* src/vamp.cpp:87-88 */
+    }
+    s.gam1 = prm->gam1;
+    s.gam2 = 0;
+    s.CG_max_iter = prm->CG_max_iter;
+    s.CG_err_tol = prm->CG_err_tol;
+    s.EM_max_iter = prm->EM_max_iter;
+    s.EM_err_thr = prm->EM_err_thr;
+    s.learn_vars = prm->learn_vars;
+    s.merge_vars_thr = prm->merge_vars_thr;
+    s.verbosity = prm->verbosity;
+    const double gmin = 1e-11, gmax = 1e11; /* src/vamp.hpp:33-34 */
+    int write = prm->out_dir && prm->out_dir[0];
+    size_t Mb = sizeof(double) * (size_t)(M > 0 ? M : 1), Nb = sizeof(double) * (size_t)N;
+    const double sqrtN = sqrt((double)N);
+
+    double* x1_hat = (double*)calloc(1, Mb);
+    double* x1_hat_prev = (double*)calloc(1, Mb);
+    double* x1_scaled = (double*)calloc(1, Mb);
+    double* x2_s = (double*)calloc(1, Mb);
+    double* r2 = (double*)calloc(1, Mb);
+    double* v = (double*)calloc(1, Mb);
+    double* tmpM = (double*)calloc(1, Mb);
+    double* tss = (double*)calloc(1, Mb);
+    double* p1 = (double*)calloc(1, Nb);
+    double* p2 = (double*)calloc(1, Nb);
+    double* z1_hat = (double*)calloc(1, Nb);
+    double* z2_hat = (double*)calloc(1, Nb);
+    double* zacc = (double*)calloc(1, Nb);
+    s.r1 = (double*)calloc(1, Mb);
+    s.bern_vec = (double*)calloc(1, Mb);
+    s.invQ_bern_vec = (double*)calloc(1, Mb);
+    s.mu_CG_last = (double*)calloc(1, Mb);
+    s.x2_hat = (double*)calloc(1, Mb);
+    /* constructor: x1_hat = x1hat_init / sqrt(N) (P1, src/vamp.cpp:71-72) */
+    for (int64_t i = 0; i < M; ++i) x1_hat[i] = (pb->x1hat_init ? pb->x1hat_init[i] : 0.0) / sqrtN;
+    /* :41-44 true_signal_scaled; true_g = Ax(.) (:46) is never read again:
+     * counted as a pass, not computed */
+    for (int64_t i = 0; i < M; ++i) tss[i] = (pb->true_signal ? pb->true_signal[i] : 0.0) * sqrtN;
+    s.passes++;
+    for (int64_t i = 0; i < N; ++i) p1[i] = orc_probit_p1(prm->seed, i); /* :53 (P2) */
+    double tau1 = s.gam1, tau2 = 0;                                        /* :35 */
+    double alpha1 = 0, alpha2 = 0, eta1 = 0, beta1 = 0, beta2 = 0;
+    const double* y = pb->y;
+
+    char p_params[4096], p_metrics[4096], p_prior[4096], pbuf[4096];
+    if (write) {
+        join_path(p_metrics, sizeof p_metrics, prm->out_dir, prm->out_name, "_metrics.csv");
+        join_path(p_params, sizeof p_params, prm->out_dir, prm->out_name, "_params.csv");
+        join_path(p_prior, sizeof p_prior, prm->out_dir, prm->out_name, "_prior.csv");
+        if (pb->rank == 0) {
+            orc_csv_create(p_metrics);
+            orc_csv_create(p_params);
+            orc_csv_create(p_prior);
+        }
+    }
+    double metrics[12] = {0}, params[8] = {0}, prior_row[1 + 2 * ORC_MAX_L];
+    int iters_run = 0;
+    for (int it = 1; it <= prm->max_iter; ++it) {
+        iters_run = it;
+        /* ---- denoising x (:104-198) ---- */
+        memcpy(x1_hat_prev, x1_hat, Mb);
+        const double alpha1_prev = alpha1;
+        for (int64_t i = 0; i < M; ++i) x1_hat[i] = orc_g1(s.r1[i], s.gam1, s.probs, s.vars, s.L);
+        for (int64_t i = 0; i < M; ++i) tmpM[i] = orc_g1d(s.r1[i], s.gam1, s.probs, s.vars, s.L);
+        {
+            double* onesv = v;
+            for (int64_t i = 0; i < M; ++i) onesv[i] = 1.0;
+            alpha1 = allreduce1(pb, orc_dot(tmpM, onesv, M)) / (double)Mt; /* :120-129 */
+        }
+        eta1 = s.gam1 / alpha1;          /* :130 */
+        if (it > 1) update_prior(&s);    /* :139 (after g1 / g1d) */
+        if (res && res->L_hist) res->L_hist[it - 1] = s.L;
+        if (it > 1) {                    /* :160-165 */
+            for (int64_t i = 0; i < M; ++i) x1_hat[i] = prm->rho * x1_hat[i] + (1 - prm->rho) * x1_hat_prev[i];
+            alpha1 = prm->rho * alpha1 + (1 - prm->rho) * alpha1_prev;
+        }
+        for (int64_t i = 0; i < M; ++i) x1_scaled[i] = x1_hat[i] / sqrtN; /* :168-172 */
+        if (res && res->x1_hist) memcpy(res->x1_hist + (int64_t)(it - 1) * M, x1_scaled, Mb);
+        if (res && res->r1_hist)
+            for (int64_t i = 0; i < M; ++i) res->r1_hist[(int64_t)(it - 1) * M + i] = s.r1[i] / sqrtN;
+        if (write) {
+            char suf[64];
+            snprintf(suf, sizeof suf, "_it_%d.bin", it);
+            join_path(pbuf, sizeof pbuf, prm->out_dir, prm->out_name, suf);
+            orc_store_vec(pbuf, x1_scaled, pb->S, M);
+            for (int64_t i = 0; i < M; ++i) tmpM[i] = s.r1[i] / sqrtN;
+            snprintf(suf, sizeof suf, "_r1_it_%d.bin", it);
+            join_path(pbuf, sizeof pbuf, prm->out_dir, prm->out_name, suf);
+            orc_store_vec(pbuf, tmpM, pb->S, M);
+        }
+        const double x1_corr = inner_prod(pb, x1_hat, tss, M, 1) /
+                               sqrt(inner_prod(pb, x1_hat, x1_hat, M, 1) * inner_prod(pb, tss, tss, M, 1)); /* :189 */
+        s.gam2 = smin(smax(eta1 - s.gam1, gmin), gmax); /* :194 */
+        for (int64_t i = 0; i < M; ++i) r2[i] = (eta1 * x1_hat[i] - s.gam1 * s.r1[i]) / s.gam2;
+
+        /* ---- denoising z (:202-253) ---- */
+        for (int64_t i = 0; i < N; ++i) z1_hat[i] = orc_g1_bin(p1[i], tau1, y[i]);
+        {
+            for (int64_t i = 0; i < N; ++i) zacc[i] = orc_g1d_bin(p1[i], tau1, y[i]);
+            double* onesv = p2;
+            for (int64_t i = 0; i < N; ++i) onesv[i] = 1.0;
+            beta1 = orc_dot(zacc, onesv, N); /* local: y and p1 are replicated */
+        }
+        if (beta1 >= N) beta1 = N - 1.0;
+        beta1 /= N;
+        for (int64_t i = 0; i < N; ++i) p2[i] = (z1_hat[i] - beta1 * p1[i]) / (1 - beta1);
+        tau2 = tau1 * (1 - beta1) / beta1;
+        params[0] = alpha1;
+        params[1] = beta1;
+        params[2] = s.gam1;
+        params[3] = tau1;
+        ax(&s, x1_scaled, zacc); /* :271-282 */
+        probit_confusion(zacc, y, N, metrics);
+        metrics[5] = x1_corr;
+
+        /* ---- LMMSE (:297-385) ---- */
+        for (int64_t i = 0; i < M; ++i)
+            s.bern_vec[i] = (2 * orc_bern_bit(prm->seed, it, pb->S + i) - 1) / sqrt((double)Mt);
+        atx(&s, p2, v); /* :300-303 */
+        for (int64_t i = 0; i < M; ++i) v[i] = tau2 * v[i] + s.gam2 * r2[i];
+        memset(tmpM, 0, Mb);
+        precondCG(&s, v, tmpM, tau2, 1, s.x2_hat); /* :307 (zero start) */
+        if (res && res->cg_iters) res->cg_iters[it - 1] = s.cg_iters_last;
+        memset(tmpM, 0, Mb);
+        precondCG(&s, s.bern_vec, tmpM, tau2, 0, s.invQ_bern_vec); /* g2d_onsager(gam2, tau2) :311 */
+        if (res && res->ons_iters) res->ons_iters[it - 1] = s.cg_iters_last;
+        alpha2 = s.gam2 * inner_prod(pb, s.bern_vec, s.invQ_bern_vec, M, 1);
+        for (int64_t i = 0; i < M; ++i) x2_s[i] = s.x2_hat[i] / sqrt((double)N); /* :318-320 */
+        const double x2_corr = inner_prod(pb, s.x2_hat, tss, M, 1) /
+                               sqrt(inner_prod(pb, s.x2_hat, s.x2_hat, M, 1) * inner_prod(pb, tss, tss, M, 1));
+        for (int64_t i = 0; i < M; ++i) s.r1[i] = (s.x2_hat[i] - alpha2 * r2[i]) / (1 - alpha2); /* :337-338 */
+        s.gam1 = smin(smax(s.gam2 * (1 - alpha2) / alpha2, gmin), gmax);                    /* :345-346 */
+        ax(&s, s.x2_hat, z2_hat);                                                                /* :352 */
+        beta2 = (double)Mt / N * (1 - alpha2);                                                   /* :354 */
+        for (int64_t i = 0; i < N; ++i) p1[i] = (z2_hat[i] - beta2 * p2[i]) / (1 - beta2);      /* :367-368 */
+        tau1 = smin(smax(tau2 * (1 - beta2) / beta2, gmin), gmax);                               /* :375-376 */
+        params[4] = alpha2;
+        params[5] = beta2;
+        params[6] = s.gam2;
+        params[7] = tau2;
+        ax(&s, x2_s, zacc); /* :403-415 */
+        probit_confusion(zacc, y, N, metrics + 6);
+        metrics[11] = x2_corr;
+        /* prior row (:423-428): L, probs, vars (still multiplied by N) */
+        int np = 0;
+        prior_row[np++] = (double)s.L;
+        for (int j = 0; j < s.L; ++j) prior_row[np++] = s.probs[j];
+        for (int j = 0; j < s.L; ++j) prior_row[np++] = s.vars[j];
+        if (res && res->params) memcpy(res->params + (int64_t)(it - 1) * 8, params, sizeof params);
+        if (res && res->metrics) memcpy(res->metrics + (int64_t)(it - 1) * 12, metrics, sizeof metrics);
+        if (res && res->prior_hist) {
+            double* dst = res->prior_hist + (int64_t)(it - 1) * (1 + 2 * ORC_MAX_L);
+            memset(dst, 0, sizeof(double) * (1 + 2 * ORC_MAX_L));
+            memcpy(dst, prior_row, sizeof(double) * (size_t)np);
+        }
+        if (write && pb->rank == 0) { /* :430-435 */
+            orc_csv_row(p_params, it, params, 8);
+            orc_csv_row(p_metrics, it, metrics, 12);
+            orc_csv_row(p_prior, it, prior_row, np);
+        }
+        if (prm->verbosity >= 1 && pb->rank == 0)
+            printf("it %d: alpha1 %.6g beta1 %.6g gam1 %.6g tau1 %.6g alpha2 %.6g beta2 %.6g L %d\n", it, alpha1,
+                   beta1, s.gam1, tau1, alpha2, beta2, s.L);
+        /* stopping criteria (:444-458) */
+        for (int64_t i = 0; i < M; ++i) tmpM[i] = x1_hat_prev[i] - x1_hat[i];
+        double NMSE = sqrt(inner_prod(pb, tmpM, tmpM, M, 1) / inner_prod(pb, x1_hat_prev, x1_hat_prev, M, 1));
+        if (it > 1 && NMSE < prm->stop_criteria_thr) break;
+    }
+    if (res) {
+        res->iterations_run = iters_run;
+        if (res->x1_final) memcpy(res->x1_final, x1_hat, sizeof(double) * (size_t)M); /* :465 */
+        res->L_final = s.L;
+        if (res->probs_final)
+            for (int j = 0; j < s.L; ++j) res->probs_final[j] = s.probs[j];
+        if (res->vars_final)
+            for (int j = 0; j < s.L; ++j) res->vars_final[j] = s.vars[j] / (double)N;
+        res->a_passes = s.passes;
+    }
+    free(x1_hat);
+    free(x1_hat_prev);
+    free(x1_scaled);
+    free(x2_s);
+    free(r2);
+    free(v);
+    free(tmpM);
+    free(tss);
+    free(p1);
+    free(p2);
+    free(z1_hat);
+    free(z2_hat);
+    free(zacc);
+    free(s.r1);
+    free(s.bern_vec);
+    free(s.invQ_bern_vec);
+    free(s.mu_CG_last);
+    free(s.x2_hat);
+    return 0;
+}

@@ -122,15 +122,34 @@ typedef struct {
     double* vars_final;         /* ORC_MAX_L (divided by N, as printed) */
     int L_final;
     int64_t a_passes;           /* reference-equivalent A/A^T passes executed */
+    double* prior_hist;         /* probit: 1 + 2*ORC_MAX_L per iteration: L, probs, vars (x N) */
 } orc_result;
 
 /* returns 0 on success */
 int orc_vamp_infere_linear(const orc_problem* pb, const orc_params* prm, orc_result* res);
 
+/* ---- the probit model (src/vamp_probit.cpp:19-467) ----
+ * Same problem/params as the linear run, y = raw 0/1 phenotype
+ * (read_phen(false), src/data.cpp:40-43).  h2 is unused.  Result widths:
+ * params 8 per iteration (alpha1 beta1 gam1 tau1 alpha2 beta2 gam2 tau2),
+ * metrics 12 (TP TN FP FN acc1 x1_corr | TP TN FP FN acc2 x2_corr),
+ * x1_final = x1_hat NOT divided by sqrt(N) (src/vamp_probit.cpp:465).
+ * P2 also covers the Gaussian start p1 (src/vamp_probit.cpp:53, simulate()
+ * with std::random_device): p1[i] = orc_probit_p1(seed, i). */
+int orc_vamp_infere_probit(const orc_problem* pb, const orc_params* prm, orc_result* res);
+double orc_probit_p1(uint64_t seed, int64_t i);
+/* src/utilities.cpp:293-363 (published erfcx, with the reference's clamps) */
+double orc_erfcx(double x);
+/* src/vamp_probit.cpp:469-488, probit_var = 1 (src/vamp.hpp:35), m_cov = 0 */
+double orc_g1_bin(double p, double tau1, double y);
+double orc_g1d_bin(double p, double tau1, double y);
+
 /* ---- output writers (src/utilities.cpp:241-249, 366-401) ---- */
 int orc_store_vec(const char* path, const double* v, int64_t S, int64_t M);
 int orc_csv_header(const char* path, const char* const* fields, int n);
 int orc_csv_row(const char* path, int it, const double* vals, int n);
+/* setup_io without a header (the probit path writes none) */
+int orc_csv_create(const char* path);
 
 #ifdef __cplusplus
 }

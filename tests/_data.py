@@ -3,6 +3,8 @@ the oracle's fixed-order arithmetic, so inputs are bit-identical on every host
 (no BLAS, no numpy RNG)."""
 from __future__ import annotations
 
+import threading
+
 import numpy as np
 
 from oracle import pyoracle as O
@@ -22,3 +24,68 @@ def make_problem(N: int, Mt: int, seed: int = 3, kind: int = 0, lam: float = 0.1
     noise = np.array([lib.orc_gauss_dyadic(seed + 202, -1, j) for j in range(N)])
     y = O.standardize_phen(z + np.sqrt(1 - h2) * noise)
     return X, y, beta
+
+
+class ThreadComm:
+    """In-process SUM all-reduce for P threads acting as ranks (summed in rank order)."""
+
+    def __init__(self, P):
+        self.P = P
+        self.bar = threading.Barrier(P)
+        self.buf = {}
+        self.lock = threading.Lock()
+
+    def make(self, rank):
+        def ar(a):
+            with self.lock:
+                self.buf[rank] = a.copy()
+            self.bar.wait()
+            tot = np.zeros_like(a)
+            for r in range(self.P):
+                tot += self.buf[r]
+            self.bar.wait()
+            a[:] = tot
+        return ar
+
+
+def sharded_oracle(X, y, beta, Mt, P, **kw):
+    """The oracle on P marker shards (divide_work), one thread per rank."""
+    comm = ThreadComm(P)
+    res = [None] * P
+
+    def work(r):
+        M, S, _ = O.divide_work(Mt, P, r)
+        res[r] = O.vamp_infere(X[S:S + M], y, Mt, S=S, rank=r, nranks=P,
+                               true_signal=None if beta is None else beta[S:S + M], allreduce=comm.make(r), **kw)
+
+    th = [threading.Thread(target=work, args=(r,)) for r in range(P)]
+    [t.start() for t in th]
+    [t.join() for t in th]
+    return res
+
+
+def oracle_with_spread(X, y, beta, Mt, ranks=(2, 3, 4), **kw):
+    """The single-rank oracle run plus the reference's own sensitivity to the
+    all-reduce order: per iteration, the largest norm-relative change of
+    x1 / r1 (and element-wise of params) when the same problem runs on 2, 3
+    or 4 ranks.  Returns (ref, spread) with spread["x1"], spread["r1"] of
+    shape (iterations,) and spread["params"] like ref["params"]."""
+    ref = O.vamp_infere(X, y, Mt, true_signal=beta, **kw)
+    kw = {k: v for k, v in kw.items() if k not in ("out_dir", "out_name")}  # files: single-rank run only
+    n = ref["iterations"]
+    sp = {"x1": np.zeros(n), "r1": np.zeros(n), "params": np.zeros_like(ref["params"]),
+          "metrics": np.zeros_like(ref["metrics"])}
+    for P in ranks:
+        res = sharded_oracle(X, y, beta, Mt, P, **kw)
+        assert res[0]["iterations"] == n, "the reference's own iteration count depends on the rank count"
+        for key in ("x1", "r1"):
+            h = np.concatenate([r[f"{key}_hist"] for r in res], axis=1)
+            num = np.linalg.norm(h - ref[f"{key}_hist"], axis=1)
+            den = np.maximum(np.linalg.norm(ref[f"{key}_hist"], axis=1), 1e-300)
+            sp[key] = np.maximum(sp[key], num / den)
+        for key in ("params", "metrics"):
+            a, b = res[0][key], ref[key]
+            with np.errstate(invalid="ignore", divide="ignore"):
+                e = np.where(np.isnan(a) & np.isnan(b), 0.0, np.abs(a - b) / np.maximum(np.abs(b), 1e-300))
+            sp[key] = np.maximum(sp[key], e)
+    return ref, sp

@@ -11,6 +11,8 @@ it reads /root/reference, which does not exist on the GPU box).
    problem (tests/_data.py, N=1000, Mt=2000): per-iteration x1/r1 at selected
    iterations, params, metrics, CG/Onsager/L counts and the three CSV files'
    raw bytes.  They are regression pins for the oracle and GPU references.
+   ``oracle_probit_*``: the same for the probit model (--model bin_class) on
+   the C1 problem's liability thresholded at 0.
 
     python tests/golden/make_golden.py
 """
@@ -47,10 +49,10 @@ def run_data_sim(N=100, M=200, seed=12345):
         sys.argv = argv
 
 
-def oracle_case(name, X, y, Mt, beta, its, thr):
+def oracle_case(name, X, y, Mt, beta, its, thr, model="linear"):
     with tempfile.TemporaryDirectory() as td:
         r = O.vamp_infere(X, y, Mt, true_signal=beta, max_iter=its, stop_criteria_thr=thr, out_dir=td,
-                          out_name="g")
+                          out_name="g", model=model)
         csv = {k: open(os.path.join(td, f"g_{k}.csv"), "rb").read() for k in ("params", "metrics", "prior")}
     keep = [k for k in KEEP_ITS if k <= r["iterations"]] + [r["iterations"]]
     keep = sorted(set(keep))
@@ -60,7 +62,8 @@ def oracle_case(name, X, y, Mt, beta, its, thr):
         params=r["params"], metrics=r["metrics"], keep_its=np.array(keep),
         x1=r["x1_hist"][np.array(keep) - 1], r1=r["r1_hist"][np.array(keep) - 1],
         csv_params=np.frombuffer(csv["params"], dtype=np.uint8), csv_metrics=np.frombuffer(csv["metrics"], np.uint8),
-        csv_prior=np.frombuffer(csv["prior"], dtype=np.uint8), a_passes=r["a_passes"], its=its, thr=thr)
+        csv_prior=np.frombuffer(csv["prior"], dtype=np.uint8), a_passes=r["a_passes"], its=its, thr=thr,
+        model=model, x1_final=r["x1_final"], prior=r.get("prior", np.zeros(0)))
     print(name, r["iterations"], r["cg_iters"].tolist(), r["ons_iters"].tolist())
 
 
@@ -74,6 +77,10 @@ def main():
     X, y, beta = make_problem(1000, 2000)
     oracle_case("c1", X, y, 2000, beta, 30, 0.0)
     oracle_case("c1_stop", X, y, 2000, beta, 50, 0.01)
+    # probit (src/vamp_probit.cpp): the same liability thresholded at 0
+    yb = (y > 0).astype(np.float64)
+    oracle_case("probit_c1", X, yb, 2000, beta, 30, 0.0, model="bin_class")
+    oracle_case("probit_c1_stop", X, yb, 2000, beta, 50, 0.01, model="bin_class")
 
 
 if __name__ == "__main__":

@@ -14,7 +14,7 @@ import numpy as np
 import pytest
 
 from conftest import relerr
-from _data import make_problem
+from _data import make_problem, sharded_oracle
 from oracle import pyoracle as O
 
 
@@ -135,7 +135,7 @@ def test_vamp_oracle_default_stop():
 
 
 def test_vamp_oracle_thread_count_invariant():
-    code = ("import sys; sys.path.insert(0, %r); sys.path.insert(0, %r); from _data import make_problem;"
+    code = ("import sys; sys.path.insert(0, %r); sys.path.insert(0, %r); from _data import make_problem, sharded_oracle;"
             "from oracle import pyoracle as O; X, y, b = make_problem(500, 900);"
             "r = O.vamp_infere(X, y, 900, true_signal=b, max_iter=6, stop_criteria_thr=0.0);"
             "print(r['x1_final'].tobytes().hex()[:64], r['x1_final'].sum().hex())"
@@ -148,49 +148,24 @@ def test_vamp_oracle_thread_count_invariant():
     assert len(outs) == 1, outs
 
 
-class _ThreadComm:
-    """In-process SUM all-reduce for P threads acting as ranks."""
-
-    def __init__(self, P):
-        self.P = P
-        self.bar = threading.Barrier(P)
-        self.buf = {}
-        self.lock = threading.Lock()
-
-    def make(self, rank):
-        def ar(a):
-            with self.lock:
-                self.buf[rank] = a.copy()
-            self.bar.wait()
-            tot = np.zeros_like(a)
-            for r in range(self.P):  # rank order
-                tot += self.buf[r]
-            self.bar.wait()
-            a[:] = tot
-        return ar
-
-
+@pytest.mark.parametrize("model", ["linear", "bin_class"])
 @pytest.mark.parametrize("P", [2, 3])
-def test_vamp_oracle_shard_invariance(P):
+def test_vamp_oracle_shard_invariance(P, model):
     """Marker sharding over P ranks (src/utilities.cpp:207-239) reproduces the
-    single-rank run: the index-keyed Bernoulli makes it rank-count invariant."""
+    single-rank run: the index-keyed Bernoulli makes it rank-count invariant.
+    Linear: to 1e-12.  Probit: the iteration counts exactly, the values to
+    the model's conditioning (alpha2 ~ 1 - 4e-8 at iteration 1 amplifies the
+    all-reduce order by ~1e8)."""
     N, Mt, its = 600, 1100, 8
     X, y, beta = make_problem(N, Mt)
-    one = O.vamp_infere(X, y, Mt, true_signal=beta, max_iter=its, stop_criteria_thr=0.0)
-    comm = _ThreadComm(P)
-    res = [None] * P
-
-    def work(r):
-        M, S, _ = O.divide_work(Mt, P, r)
-        res[r] = O.vamp_infere(X[S:S + M], y, Mt, S=S, rank=r, nranks=P, true_signal=beta[S:S + M],
-                               max_iter=its, stop_criteria_thr=0.0, allreduce=comm.make(r))
-
-    th = [threading.Thread(target=work, args=(r,)) for r in range(P)]
-    [t.start() for t in th]
-    [t.join() for t in th]
+    if model == "bin_class":
+        y = (y > 0).astype(np.float64)
+    one = O.vamp_infere(X, y, Mt, true_signal=beta, max_iter=its, stop_criteria_thr=0.0, model=model)
+    res = sharded_oracle(X, y, beta, Mt, P, max_iter=its, stop_criteria_thr=0.0, model=model)
     x = np.concatenate([r["x1_final"] for r in res])
-    assert relerr(x, one["x1_final"]) < 1e-12
+    assert relerr(x, one["x1_final"]) < (1e-12 if model == "linear" else 1e-6)
     for r in res:
         assert r["cg_iters"].tolist() == one["cg_iters"].tolist()
         assert r["ons_iters"].tolist() == one["ons_iters"].tolist()
-        assert np.allclose(r["params"], one["params"], rtol=1e-11)
+        assert r["L"].tolist() == one["L"].tolist()
+        assert np.allclose(r["params"], one["params"], rtol=1e-11 if model == "linear" else 1e-5)

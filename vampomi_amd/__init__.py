@@ -128,6 +128,12 @@ class Data:
             raise ValueError("phenotype must have N entries")
         check(self._lib.vampomi_set_phen(self.ctx, _dp(y), 1 if standardize else 0))
 
+    def simulate_phen_binary(self, seed: int, lam: float = 0.1, h2: float = 0.8) -> np.ndarray:
+        """Liability of simulate_phen thresholded at 0, stored raw (bin_class); returns beta."""
+        beta = np.zeros(max(self.M, 1))
+        check(self._lib.vampomi_simulate_phen_binary(self.ctx, seed, lam, h2, _dp(beta)))
+        return beta[: self.M]
+
     def simulate_phen(self, seed: int, lam: float = 0.1, h2: float = 0.8) -> np.ndarray:
         beta = np.zeros(max(self.M, 1))
         check(self._lib.vampomi_simulate_phen(self.ctx, seed, lam, h2, _dp(beta)))
@@ -185,6 +191,14 @@ class Data:
         check(self._lib.vampomi_pcg(self.ctx, _dp(v), None if m0 is None else _dp(m0), tau, gam2,
                                     1 if onsager else 0, max_iter, tol, _dp(mu), C.byref(it), MEM_HOST))
         return mu[: self.M], it.value
+
+    def denoise_bin(self, p1: np.ndarray, tau1: float):
+        """g1_bin_class / g1d_bin_class over the phenotype (src/vamp_probit.cpp:469-488): (z1, sum of g1d)."""
+        p1 = np.ascontiguousarray(p1, dtype=np.float64)
+        z = np.zeros(self.N)
+        sd = C.c_double()
+        check(self._lib.vampomi_denoise_bin(self.ctx, _dp(p1), tau1, _dp(z), C.byref(sd), MEM_HOST))
+        return z, sd.value
 
     def denoise(self, r1: np.ndarray, gam1: float, probs: Sequence[float], vars_scaled: Sequence[float]):
         """(g1(r1), g1d(r1), sum of g1d over ranks); vars already multiplied by N."""
@@ -277,8 +291,10 @@ class Vamp:
         self.cg = np.zeros(it, dtype=np.int32)
         self.ons = np.zeros(it, dtype=np.int32)
         self.Lh = np.zeros(it, dtype=np.int32)
-        self.params = np.zeros((it, 5))
-        self.metrics = np.zeros((it, 6))
+        probit = o.model == "bin_class"
+        self.params = np.zeros((it, 8 if probit else 5))
+        self.metrics = np.zeros((it, 12 if probit else 6))
+        self.prior = np.zeros((it, 1 + 2 * MAX_L)) if probit else None
         self.x1_final = np.zeros(max(M, 1))
         r = Result()
         ip = C.POINTER(C.c_int)
@@ -288,6 +304,8 @@ class Vamp:
         r.params = self.params.ctypes.data_as(C.POINTER(C.c_double))
         r.metrics = self.metrics.ctypes.data_as(C.POINTER(C.c_double))
         r.x1_final = self.x1_final.ctypes.data_as(C.POINTER(C.c_double))
+        if self.prior is not None:
+            r.prior_hist = self.prior.ctypes.data_as(C.POINTER(C.c_double))
         if keep_hist:
             self.x1_hist = np.zeros((it, max(M, 1)))
             self.r1_hist = np.zeros((it, max(M, 1)))
@@ -296,7 +314,8 @@ class Vamp:
         self.r = r
 
     def infere(self, keep_hist: bool = False) -> np.ndarray:
-        """Run infere_linear to completion; returns x1_hat / sqrt(N) (local slice)."""
+        """Run vamp::infere to completion; returns what it returns (local slice):
+        x1_hat / sqrt(N) for the linear model, x1_hat for bin_class."""
         self._prepare(keep_hist)
         check(load().vampomi_infere(self.data.ctx, C.byref(self.p), C.byref(self.r)))
         return self.x1_final[: self.data.M].copy()
@@ -336,4 +355,5 @@ class Vamp:
             "metrics": self.metrics[:n].tolist(),
             "a_passes_ref": self.r.a_passes_ref,
             "a_passes_exec": self.r.a_passes_exec,
+            **({"prior": self.prior[:n].tolist()} if self.prior is not None else {}),
         }

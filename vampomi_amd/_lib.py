@@ -74,6 +74,7 @@ class Result(C.Structure):
         ("probs_final", C.c_double * MAX_L), ("vars_final", C.c_double * MAX_L),
         ("L_final", C.c_int),
         ("a_passes_ref", C.c_int64), ("a_passes_exec", C.c_int64),
+        ("prior_hist", C.POINTER(C.c_double)),
     ]
 
 
@@ -108,6 +109,7 @@ SIGNATURES = {
     "vampomi_set_phen": (C.c_int, [_P, _P, C.c_int]),
     "vampomi_get_phen": (C.c_int, [_P, _P]),
     "vampomi_simulate_phen": (C.c_int, [_P, C.c_uint64, C.c_double, C.c_double, _P]),
+    "vampomi_simulate_phen_binary": (C.c_int, [_P, C.c_uint64, C.c_double, C.c_double, _P]),
     "vampomi_get_marker_stats": (C.c_int, [_P, _P, _P]),
     "vampomi_read_markers": (C.c_int, [_P, C.c_int64, C.c_int64, _P]),
     "vampomi_ax": (C.c_int, [_P, _P, _P, C.c_int]),
@@ -115,6 +117,7 @@ SIGNATURES = {
     "vampomi_lmmse_mult": (C.c_int, [_P, _P, C.c_double, C.c_double, _P, C.c_int]),
     "vampomi_pcg": (C.c_int, [_P, _P, _P, C.c_double, C.c_double, C.c_int, C.c_int, C.c_double, _P,
                               C.POINTER(C.c_int), C.c_int]),
+    "vampomi_denoise_bin": (C.c_int, [_P, _P, C.c_double, _P, C.POINTER(C.c_double), C.c_int]),
     "vampomi_denoise": (C.c_int, [_P, _P, C.c_double, _P, _P, C.c_int, _P, _P, C.POINTER(C.c_double), C.c_int]),
     "vampomi_params_default": (None, [C.POINTER(Params)]),
     "vampomi_infere": (C.c_int, [_P, C.POINTER(Params), C.POINTER(Result)]),

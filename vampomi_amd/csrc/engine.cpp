@@ -540,6 +540,13 @@ extern "C" vampomi_status vampomi_simulate_phen(vampomi_ctx* c, uint64_t seed, d
     return upload_phen(c);
 }
 
+extern "C" vampomi_status vampomi_simulate_phen_binary(vampomi_ctx* c, uint64_t seed, double lam, double h2,
+                                                       double* beta_out) {
+    STCHK(vampomi_simulate_phen(c, seed, lam, h2, beta_out));
+    for (double& v : c->y_host) v = v > 0 ? 1.0 : 0.0;  // the scaling is positive: same sign as the liability
+    return upload_phen(c);
+}
+
 // ---------------------------------------------------------------------------
 // operator entry points
 // ---------------------------------------------------------------------------
@@ -672,6 +679,25 @@ extern "C" vampomi_status vampomi_denoise(vampomi_ctx* c, const double* r1, doub
     STCHK(db.flush());
     if (x1) STCHK(stage_out(c, xo, c->M, mem, x1));
     if (x1d) STCHK(stage_out(c, xd, c->M, mem, x1d));
+    if (sum_d) *sum_d = sd;
+    return VAMPOMI_OK;
+}
+
+extern "C" vampomi_status vampomi_denoise_bin(vampomi_ctx* c, const double* p1, double tau1, double* z1,
+                                              double* sum_d, int mem) {
+    if (!c || !p1) return fail(VAMPOMI_ERR_ARG, "null argument");
+    if (!c->have_y) return fail(VAMPOMI_ERR_STATE, "set the phenotype first");
+    HIPCHK(hipSetDevice(c->device));
+    double* pin = c->nbuf;
+    double* zo = c->nbuf + c->ld;
+    STCHK(stage_in(c, p1, c->N, mem, pin));
+    int nb = 0;
+    HIPCHK(vk::probit_denoise(c->N, pin, c->y, tau1, zo, c->red_part, &nb, c->st));
+    double sd = 0.0;
+    DotBatch db(c);
+    STCHK(db.add_partials(c->red_part, nb, 1, false, &sd));
+    STCHK(db.flush());
+    if (z1) STCHK(stage_out(c, zo, c->N, mem, z1));
     if (sum_d) *sum_d = sd;
     return VAMPOMI_OK;
 }

@@ -99,6 +99,14 @@ bool csv_create_with_header(const std::string& path, const std::vector<std::stri
     return w == (ssize_t)s.size();
 }
 
+bool csv_create(const std::string& path) {
+    ::unlink(path.c_str());
+    int fd = ::open(path.c_str(), O_CREAT | O_WRONLY | O_EXCL, 0666);
+    if (fd < 0) return false;
+    ::close(fd);
+    return true;
+}
+
 std::string csv_format_row(int it, const double* vals, int n) {
     char buf[50000];
     int cx = std::snprintf(buf, sizeof buf, "%5d", it);

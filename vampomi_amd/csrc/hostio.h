@@ -23,6 +23,9 @@ bool read_vec(const std::string& path, double* v, int64_t S, int64_t M);
 // setup_io + write_ofile_csv_header (src/vamp.cpp:854-882,
 // src/utilities.cpp:388-401): delete, create exclusively, header at offset 0.
 bool csv_create_with_header(const std::string& path, const std::vector<std::string>& fields);
+// setup_io alone: delete, create exclusively, no header (the probit path
+// writes none, src/vamp_probit.cpp)
+bool csv_create(const std::string& path);
 // write_ofile_csv (src/utilities.cpp:366-385): "%5d" + n x ", %20.15f" + "\n"
 // at byte offset it * strlen(row).
 bool csv_write_row(const std::string& path, int it, const double* vals, int n);

@@ -118,6 +118,18 @@ hipError_t bernoulli(uint64_t seed, int it, int64_t S, int64_t M, double sqrtMt,
 // out = x / d
 hipError_t div_scalar(int64_t n, const double* x, double d, double* out, hipStream_t st);
 
+// ---- probit model (src/vamp_probit.cpp) -------------------------------------
+// z1[i] = g1_bin_class(p1[i], tau1, y[i]); per-block partial sums of
+// g1d_bin_class (src/vamp_probit.cpp:213-233, 469-488; probit_var = 1, m_cov = 0)
+hipError_t probit_denoise(int64_t N, const double* p1, const double* y, double tau1, double* z1, double* part,
+                          int* nblk, hipStream_t st);
+// predict_probit(z_k, 0.5) + confusion_matrix against y (src/vamp_probit.cpp:619-651),
+// nz <= 2 vectors at z + k*ld; part[blk*4*nz + 4k + {TP, TN, FP, FN}]
+hipError_t probit_confusion(int64_t N, int nz, const double* z, int64_t ld, const double* y, double* part,
+                            int* nblk, hipStream_t st);
+// P2 start: p1[i] = gauss(seed ^ salt, 0, i) (replaces simulate(N, {1}, {1}), :53)
+hipError_t probit_p1(uint64_t seed, int64_t N, double* p1, hipStream_t st);
+
 // ---- PCG (vamp::precondCG_solver), K right-hand sides --------------------------
 struct CgVecs {
     double* mu[kMaxRhs];

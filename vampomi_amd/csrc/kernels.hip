@@ -957,4 +957,116 @@ hipError_t cg_pupdate(int K, int64_t M, const CgVecs& c, CgBeta b, hipStream_t s
     return hipGetLastError();
 }
 
+
+// ---------------------------------------------------------------------------
+// probit model: N-side denoiser and accuracy counts (src/vamp_probit.cpp)
+// ---------------------------------------------------------------------------
+// erfcx as the reference evaluates it (src/utilities.cpp:293-363: N. Juffa's
+// published fma approximation, with +inf below -10 and lowest() above 10).
+// Same operations in the same order as the oracle's orc_erfcx; only exp()
+// (OCML vs glibc) may differ in the last bit for x < 0.
+__constant__ double kErfcxPoly[24] = {
+    0x1.edcad78fc8044p-31,  0x1.b1548f14735d1p-30,  -0x1.a1ad2e6c4a7a8p-27, -0x1.1985b48f08574p-26,
+    0x1.c6a8093ac4f83p-24,  0x1.31c2b2b44b731p-24,  -0x1.b87373facb29fp-21, 0x1.3fef1358803b7p-22,
+    0x1.7eec072bb0be3p-18,  -0x1.78a680a741c4ap-17, -0x1.9951f39295cf4p-16, 0x1.3be1255ce180bp-13,
+    -0x1.a1df71176b791p-13, -0x1.8d4aaa0099bc8p-11, 0x1.49c673066c831p-8,   -0x1.0962386ea02b7p-6,
+    0x1.3079edf465cc3p-5,   -0x1.0fb06dfedc4ccp-4,  0x1.7fee004e266dfp-4,   -0x1.9ddb23c3e14d2p-4,
+    0x1.16ecefcfa4865p-4,   0x1.f7f5df66fc349p-7,   -0x1.1df1ad154a27fp-3,  0x1.dd2c8b74febf6p-3};
+
+__device__ __forceinline__ double erfcx_ref(double x) {
+    if (x < -10.0) return __builtin_inf();
+    if (x > 10.0) return -1.7976931348623157e308;
+    const double a = fmax(x, 0.0 - x);
+    const double inv = 1.0 / (a + 4.0);
+    double q = (a - 4.0) * inv;
+    const double t0 = __builtin_fma(q + 1.0, -4.0, a);
+    q = __builtin_fma(inv, __builtin_fma(q, -a, t0), q);
+    double p = kErfcxPoly[0];
+#pragma unroll
+    for (int k = 1; k < 24; ++k) p = __builtin_fma(p, q, kErfcxPoly[k]);
+    const double h = (1.0 / (a + 0.5)) * 0.5;
+    const double q1 = __builtin_fma(p, h, h);
+    const double res = (p - q1) + __builtin_fma(q1 + q1, -a, 1.0);
+    double r = __builtin_fma(res, h, q1);
+    if (a > 1.7976931348623157e308) r = 0.0;
+    if (x < 0.0) {
+        const double s = x * x;
+        const double lo = __builtin_fma(x, x, -s);
+        const double e = exp(s);
+        r = __builtin_fma(e, lo + lo, e - r) + e;
+        if (e > 1.7976931348623157e308) r = e;
+    }
+    return r;
+}
+
+__global__ __launch_bounds__(kBlock) void probit_denoise_kernel(int64_t N, const double* __restrict__ p1,
+                                                                const double* __restrict__ y, double tau1,
+                                                                double* __restrict__ z1, double* __restrict__ part) {
+    __shared__ double lds[4];
+    const double sq = sqrt(1.0 + 1.0 / tau1);           // sqrt(probit_var + 1/tau1)
+    const double k0 = 2.0 / sqrt(2 * M_PI), rt2 = sqrt(2.0);
+    const double den = 1 + tau1 * 1.0;                  // 1 + tau1*probit_var
+    double acc = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < N; i += (int64_t)gridDim.x * kBlock) {
+        const double p = p1[i], s = 2 * y[i] - 1;
+        const double c = (p + 0.0) / sq;
+        const double ratio = k0 / erfcx_ref(-s * c / rt2);
+        z1[i] = p + s * ratio / tau1 / sq;
+        acc += 1 - ratio / den * (s * c + ratio);
+    }
+    acc = block_sum(acc, lds);
+    if (threadIdx.x == 0) part[blockIdx.x] = acc;
+}
+
+hipError_t probit_denoise(int64_t N, const double* p1, const double* y, double tau1, double* z1, double* part,
+                          int* nblk, hipStream_t st) {
+    *nblk = red_blocks(N);
+    hipLaunchKernelGGL(probit_denoise_kernel, dim3(*nblk), dim3(kBlock), 0, st, N, p1, y, tau1, z1, part);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(kBlock) void confusion_kernel(int64_t N, int nz, const double* __restrict__ z,
+                                                           int64_t ld, const double* __restrict__ y,
+                                                           double* __restrict__ part) {
+    __shared__ double lds[4];
+    double cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < N; i += (int64_t)gridDim.x * kBlock) {
+        const double yi = y[i];
+        for (int k = 0; k < nz; ++k) {
+            const double yh = (0.5 * erfc(-z[k * ld + i] * M_SQRT1_2) >= 0.5) ? 1.0 : 0.0;  // normal_cdf >= th
+            if (yi == 1 && yh == 1)
+                cnt[4 * k + 0] += 1;
+            else if (yi == 0 && yh == 0)
+                cnt[4 * k + 1] += 1;
+            else if (yi == 0 && yh == 1)
+                cnt[4 * k + 2] += 1;
+            else if (yi == 1 && yh == 0)
+                cnt[4 * k + 3] += 1;
+        }
+    }
+    for (int q = 0; q < 4 * nz; ++q) {
+        const double s = block_sum(cnt[q], lds);
+        if (threadIdx.x == 0) part[(int64_t)blockIdx.x * 4 * nz + q] = s;
+    }
+}
+
+hipError_t probit_confusion(int64_t N, int nz, const double* z, int64_t ld, const double* y, double* part,
+                            int* nblk, hipStream_t st) {
+    if (nz < 1 || nz > 2) return hipErrorInvalidValue;
+    *nblk = red_blocks(N);
+    hipLaunchKernelGGL(confusion_kernel, dim3(*nblk), dim3(kBlock), 0, st, N, nz, z, ld, y, part);
+    return hipGetLastError();
+}
+
+__global__ void probit_p1_kernel(uint64_t seed, int64_t N, double* p1) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < N) p1[i] = gauss_dyadic(seed ^ 0x50524F4249545031ULL, 0, i);
+}
+
+hipError_t probit_p1(uint64_t seed, int64_t N, double* p1, hipStream_t st) {
+    if (N <= 0) return hipSuccess;
+    hipLaunchKernelGGL(probit_p1_kernel, dim3((unsigned)cdiv(N, kBlock)), dim3(kBlock), 0, st, seed, N, p1);
+    return hipGetLastError();
+}
+
 }  // namespace vk

@@ -1,5 +1,5 @@
 // main_meth.cpp — drop-in for the reference's main_meth.exe (src/main_meth.cpp)
-// in --run-mode infere, linear model: same flags, same output files.
+// in --run-mode infere (--model linear | bin_class): same flags, same output files.
 //
 // Ranks: the reference is launched with `mpirun -np P`; this binary runs one
 // process per GPU, rank/size from VAMPOMI_RANK/VAMPOMI_NRANKS (or the
@@ -73,8 +73,8 @@ int main(int argc, char** argv) {
                   << std::endl;
         return EXIT_FAILURE;
     }
-    if (opt.model != "linear") {
-        std::cout << "FATAL  : model \"" << opt.model << "\" is not provided by this build (linear only)" << std::endl;
+    if (opt.model != "linear" && opt.model != "bin_class") {  // src/vamp.cpp:98-104
+        std::cout << "FATAL  : Invalid model specification! (\"" << opt.model << "\")" << std::endl;
         return EXIT_FAILURE;
     }
 
@@ -95,9 +95,11 @@ int main(int argc, char** argv) {
     vampomi_ctx* ctx = nullptr;
     if (vampomi_open(&d, &ctx) != VAMPOMI_OK) return die("cannot open the device context");
 
-    // data::data: phenotype first (standardised for the linear model), then the shard
+    // data::data: phenotype first (standardised for the linear model, raw 0/1
+    // for bin_class, src/data.cpp:40-43), then the shard
     auto t0 = std::chrono::steady_clock::now();
-    if (vampomi_read_phen(ctx, opt.phen_file.c_str(), 1) != VAMPOMI_OK) return die("phenotype");
+    const int standardize = opt.model == "bin_class" ? 0 : 1;
+    if (vampomi_read_phen(ctx, opt.phen_file.c_str(), standardize) != VAMPOMI_OK) return die("phenotype");
     if (rank == 0) std::cout << "meth file name = " << opt.meth_file << std::endl;
     if (vampomi_load_meth_file(ctx, opt.meth_file.c_str()) != VAMPOMI_OK) return die("methylation data");
     if (rank == 0)

@@ -1,0 +1,65 @@
+// run.h — state of one VAMP run (linear or probit) on the device, shared by
+// vamp.cpp (vamp::infere_linear, begin/step/end) and probit.cpp
+// (vamp::infere_bin_class).  Internal to libvampomi.
+#pragma once
+#include <string>
+#include <vector>
+
+#include "ctx.h"
+
+struct Mixture {
+    int L = 0;
+    double probs[VAMPOMI_MAX_L] = {};
+    double vars[VAMPOMI_MAX_L] = {};  // multiplied by N (src/vamp.cpp:87-88)
+};
+
+inline double smax(double a, double b) { return (a < b) ? b : a; }  // std::max
+inline double smin(double a, double b) { return (b < a) ? b : a; }  // std::min
+
+struct VampRun {
+    vampomi_params prm{};
+    vampomi_result* res = nullptr;
+    bool probit = false;  // model "bin_class"
+    bool write = false;
+    bool fuse = true;  // batch_rhs: share passes + prefetch the next denoising step
+    std::string out_dir, out_name, p_params, p_metrics, p_prior;
+    int it = 0;
+    bool stopped = false;
+    Mixture mix, mix_next;
+    bool have_next = false;  // x1n, alpha1_next, mix_next, z1 (nb3 slot 2), atx0 valid
+    double gam1 = 0, gam2 = 0, gamw = 0;
+    double alpha1 = 0, alpha2 = 0, eta1 = 0, eta2 = 0, alpha1_next = 0;
+    double metrics[12] = {}, params[8] = {};
+    // reduction sinks
+    double e1m[3] = {}, e1n[2] = {}, e1s[3] = {}, e2m[3] = {}, e2n[2] = {}, e2s[3] = {};
+    double tn = 0, tc = 0, nm[2] = {}, sum_d = 0, a2 = 0;
+    // device M-vectors
+    double *r1 = nullptr, *x1 = nullptr, *x1p = nullptr, *x1n = nullptr, *x1d = nullptr, *r2 = nullptr;
+    double *x2 = nullptr, *bern = nullptr, *invQ = nullptr, *v = nullptr, *atxy = nullptr, *ts = nullptr;
+    double *tmpM = nullptr, *atx0 = nullptr;
+    double* cgw[8] = {};  // r, z, p, d of the two CG systems
+    // device N-vectors (ld each)
+    double *z1buf = nullptr, *nb3 = nullptr /* A.x2, A.invQ, A.x1_next */, *nsc = nullptr;
+    const double* z1 = nullptr;
+    int64_t passes_ref = 0;
+    // probit (src/vamp_probit.cpp) state
+    double tau1 = 0, tau2 = 0, beta1 = 0, beta2 = 0;
+    double* p1 = nullptr;   // N
+    double* p2 = nullptr;   // N
+    double* z1h = nullptr;  // N: z1_hat
+    double* x1s = nullptr;  // M: x1_hat / sqrt(N)
+    double* x1sn = nullptr; // M: next iteration's x1_hat / sqrt(N)
+    double* x2s = nullptr;  // M: x2_hat / sqrt(N)
+    double* prior_row = nullptr;  // host staging, unused by the linear model
+
+    ~VampRun();
+};
+
+vampomi_status update_prior(vampomi_ctx* c, const VampRun& R, Mixture& m, double gam1, const double* r1);
+vampomi_status denoise_into(vampomi_ctx* c, const Mixture& m, double gam1, const double* r1, double* x1,
+                            const double* x1_prev, bool damp, double rho, double* x1d, DotBatch& b, double* sum_out);
+vampomi_status upload_or_zero(vampomi_ctx* c, double* dst, const double* host, int64_t n);
+vampomi_status write_bins(vampomi_ctx* c, VampRun& R);
+// probit.cpp
+vampomi_status probit_begin(vampomi_ctx* c, VampRun& R);
+vampomi_status probit_step(vampomi_ctx* c, VampRun& R);

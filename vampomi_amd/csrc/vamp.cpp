@@ -24,53 +24,14 @@
 
 #include "ctx.h"
 #include "hostio.h"
+#include "run.h"
 
-namespace {
-
-struct Mixture {
-    int L = 0;
-    double probs[VAMPOMI_MAX_L] = {};
-    double vars[VAMPOMI_MAX_L] = {};  // multiplied by N (src/vamp.cpp:87-88)
-};
-
-double smax(double a, double b) { return (a < b) ? b : a; }  // std::max
-double smin(double a, double b) { return (b < a) ? b : a; }  // std::min
-
-}  // namespace
-
-struct VampRun {
-    vampomi_params prm{};
-    vampomi_result* res = nullptr;
-    bool write = false;
-    bool fuse = true;  // batch_rhs: share passes + prefetch the next denoising step
-    std::string out_dir, out_name, p_params, p_metrics, p_prior;
-    int it = 0;
-    bool stopped = false;
-    Mixture mix, mix_next;
-    bool have_next = false;  // x1n, alpha1_next, mix_next, z1 (nb3 slot 2), atx0 valid
-    double gam1 = 0, gam2 = 0, gamw = 0;
-    double alpha1 = 0, alpha2 = 0, eta1 = 0, eta2 = 0, alpha1_next = 0;
-    double metrics[6] = {0, 0, 0, 0, 0, 0}, params[5] = {0, 0, 0, 0, 0};
-    // reduction sinks
-    double e1m[3] = {}, e1n[2] = {}, e1s[3] = {}, e2m[3] = {}, e2n[2] = {}, e2s[3] = {};
-    double tn = 0, tc = 0, nm[2] = {}, sum_d = 0, a2 = 0;
-    // device M-vectors
-    double *r1 = nullptr, *x1 = nullptr, *x1p = nullptr, *x1n = nullptr, *x1d = nullptr, *r2 = nullptr;
-    double *x2 = nullptr, *bern = nullptr, *invQ = nullptr, *v = nullptr, *atxy = nullptr, *ts = nullptr;
-    double *tmpM = nullptr, *atx0 = nullptr;
-    double* cgw[8] = {};  // r, z, p, d of the two CG systems
-    // device N-vectors (ld each)
-    double *z1buf = nullptr, *nb3 = nullptr /* A.x2, A.invQ, A.x1_next */, *nsc = nullptr;
-    const double* z1 = nullptr;
-    int64_t passes_ref = 0;
-
-    ~VampRun() {
-        for (double** p : {&r1, &x1, &x1p, &x1n, &x1d, &r2, &x2, &bern, &invQ, &v, &atxy, &ts, &tmpM, &atx0, &z1buf,
-                           &nb3, &nsc})
-            dev_free(*p);
-        for (auto& p : cgw) dev_free(p);
-    }
-};
+VampRun::~VampRun() {
+    for (double** p : {&r1, &x1, &x1p, &x1n, &x1d, &r2, &x2, &bern, &invQ, &v, &atxy, &ts, &tmpM, &atx0, &z1buf,
+                       &nb3, &nsc, &p1, &p2, &z1h, &x1s, &x1sn, &x2s})
+        dev_free(*p);
+    for (auto& p : cgw) dev_free(p);
+}
 
 vampomi_ctx::vampomi_ctx() = default;
 
@@ -80,7 +41,7 @@ vampomi_ctx::~vampomi_ctx() {
 }
 
 // updatePrior (src/vamp.cpp:531-643) on mixture m, from r1 and gam1
-static vampomi_status update_prior(vampomi_ctx* c, const VampRun& R, Mixture& m, double gam1, const double* r1) {
+vampomi_status update_prior(vampomi_ctx* c, const VampRun& R, Mixture& m, double gam1, const double* r1) {
     const double noise_var = 1 / gam1;
     double lambda = 1 - m.probs[0];
     double omegas[VAMPOMI_MAX_L];
@@ -154,7 +115,7 @@ static vampomi_status update_prior(vampomi_ctx* c, const VampRun& R, Mixture& m,
 }
 
 // x1 = g1(r1) [damped], x1d = g1d(r1); sum of x1d over ranks queued in b
-static vampomi_status denoise_into(vampomi_ctx* c, const Mixture& m, double gam1, const double* r1, double* x1,
+vampomi_status denoise_into(vampomi_ctx* c, const Mixture& m, double gam1, const double* r1, double* x1,
                                    const double* x1_prev, bool damp, double rho, double* x1d, DotBatch& b,
                                    double* sum_out) {
     vk::Mix mix{};
@@ -194,7 +155,7 @@ static void err_finish(VampRun& R, const double* m3, const double* n2, const dou
     }
 }
 
-static vampomi_status upload_or_zero(vampomi_ctx* c, double* dst, const double* host, int64_t n) {
+vampomi_status upload_or_zero(vampomi_ctx* c, double* dst, const double* host, int64_t n) {
     if (n <= 0) return VAMPOMI_OK;
     if (host)
         HIPCHK(hipMemcpyAsync(dst, host, (size_t)n * 8, hipMemcpyHostToDevice, c->st));
@@ -221,14 +182,16 @@ static vampomi_status vamp_alloc(vampomi_ctx* c, VampRun& R) {
 extern "C" vampomi_status vampomi_vamp_begin(vampomi_ctx* c, const vampomi_params* p, vampomi_result* r) {
     if (!c || !p) return fail(VAMPOMI_ERR_ARG, "null argument");
     if (!c->have_X || !c->have_y) return fail(VAMPOMI_ERR_STATE, "load methylation data and phenotype first");
-    if (p->model && std::strcmp(p->model, "linear") != 0)
-        return fail(VAMPOMI_ERR_MODEL, std::string("model '") + p->model + "' is not supported (linear only)");
+    const bool probit = p->model && std::strcmp(p->model, "bin_class") == 0;
+    if (p->model && !probit && std::strcmp(p->model, "linear") != 0)  // src/vamp.cpp:98-104
+        return fail(VAMPOMI_ERR_MODEL, std::string("Invalid model specification! ('") + p->model + "')");
     if (p->L < 1 || p->L > VAMPOMI_MAX_L) return fail(VAMPOMI_ERR_ARG, "number of mixture components out of range");
     HIPCHK(hipSetDevice(c->device));
     c->run.reset(new VampRun());
     VampRun& R = *c->run;
     R.prm = *p;
     R.res = r;
+    R.probit = probit;
     R.fuse = p->batch_rhs != 0;
     R.out_dir = p->out_dir ? p->out_dir : "";
     R.out_name = p->out_name ? p->out_name : "";
@@ -249,6 +212,16 @@ extern "C" vampomi_status vampomi_vamp_begin(vampomi_ctx* c, const vampomi_param
     STCHK(upload_or_zero(c, R.x1, h.data(), c->M));
     STCHK(upload_or_zero(c, R.r1, h.data(), c->M));
     STCHK(upload_or_zero(c, R.x2, nullptr, c->M));
+    if (R.probit) {
+        if (r) {
+            r->iterations_run = 0;
+            r->a_passes_ref = 0;
+            r->a_passes_exec = 0;
+        }
+        STCHK(probit_begin(c, R));
+        HIPCHK(hipStreamSynchronize(c->st));
+        return VAMPOMI_OK;
+    }
     {  // A^T y is the same every iteration (y fixed, src/vamp.cpp:303): one pass
         const double* u[1] = {c->y};
         double* o[1] = {R.atxy};
@@ -280,7 +253,7 @@ extern "C" vampomi_status vampomi_vamp_begin(vampomi_ctx* c, const vampomi_param
     return VAMPOMI_OK;
 }
 
-static vampomi_status write_bins(vampomi_ctx* c, VampRun& R) {
+vampomi_status write_bins(vampomi_ctx* c, VampRun& R) {
     const bool hist = R.res && (R.res->x1_hist || R.res->r1_hist);
     if (!R.write && !hist) return VAMPOMI_OK;
     const int64_t M = c->M;
@@ -314,6 +287,12 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
         return VAMPOMI_OK;
     }
     HIPCHK(hipSetDevice(c->device));
+    if (R.probit) {
+        STCHK(probit_step(c, R));
+        if (c->timing) resolve_timing(c);
+        if (stopped) *stopped = R.stopped ? 1 : 0;
+        return VAMPOMI_OK;
+    }
     const int64_t M = c->M, N = c->N, Mt = c->Mt, ld = c->ld;
     const int it = ++R.it;
     vampomi_result* res = R.res;
@@ -425,8 +404,8 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
     R.params[2] = R.alpha2;
     R.params[3] = R.gam2;
     R.params[4] = R.gamw;
-    if (res && res->params) std::memcpy(res->params + (int64_t)(it - 1) * 5, R.params, sizeof R.params);
-    if (res && res->metrics) std::memcpy(res->metrics + (int64_t)(it - 1) * 6, R.metrics, sizeof R.metrics);
+    if (res && res->params) std::memcpy(res->params + (int64_t)(it - 1) * 5, R.params, 5 * sizeof(double));
+    if (res && res->metrics) std::memcpy(res->metrics + (int64_t)(it - 1) * 6, R.metrics, 6 * sizeof(double));
     if (R.write && c->rank == 0) {  // :388-393
         if (!vio::csv_write_row(R.p_params, it, R.params, 5) || !vio::csv_write_row(R.p_metrics, it, R.metrics, 6))
             return fail(VAMPOMI_ERR_IO, "cannot write CSV rows");
@@ -459,7 +438,8 @@ extern "C" vampomi_status vampomi_vamp_end(vampomi_ctx* c) {
             HIPCHK(hipMemcpyAsync(res->x1_final, R.x1, (size_t)c->M * 8, hipMemcpyDeviceToHost, c->st));
             STCHK(host_sync(c));
             const double sqrtN = std::sqrt((double)c->N);
-            for (int64_t i = 0; i < c->M; ++i) res->x1_final[i] = res->x1_final[i] / sqrtN;  // :437
+            if (!R.probit)  // linear returns x1_hat_scaled (:437), probit x1_hat (src/vamp_probit.cpp:465)
+                for (int64_t i = 0; i < c->M; ++i) res->x1_final[i] = res->x1_final[i] / sqrtN;
         }
         res->L_final = R.mix.L;
         for (int j = 0; j < R.mix.L; ++j) {

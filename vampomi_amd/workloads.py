@@ -6,6 +6,11 @@ c2 (default): N=10,000 x Mt=50,000 i.i.d. Gaussian design (configs[1]).  With
     spectrum of A^T A (and with it the CG iteration counts) stays comparable.
 c3: the per-GPU shard of configs[2] (N=100,000, 62,500 methylation-like
     markers per GPU); n=8 is exactly N=100,000 x Mt=500,000.
+c4: probit model (configs[3], --model bin_class): N=50,000 with 50,000
+    Gaussian markers per GPU and a binary phenotype; n=4 is exactly
+    N=50,000 x Mt=200,000.
+c4full: configs[3] whole (N=50,000 x Mt=200,000, 80 GB) on any number of
+    GPUs (strong scaling; it fits one MI355X).
 """
 from __future__ import annotations
 
@@ -16,8 +21,13 @@ GEN_GAUSS, GEN_METH = 0, 1
 
 def workload(cfg: str, n: int) -> dict:
     if cfg == "c3":
-        return {"workload": "c3-shard", "N": 100000, "Mt": 62500 * n, "kind": GEN_METH}
+        return {"workload": "c3-shard", "N": 100000, "Mt": 62500 * n, "kind": GEN_METH, "model": "linear"}
+    if cfg == "c4":
+        return {"workload": "c4-shard", "N": 50000, "Mt": 50000 * n, "kind": GEN_GAUSS, "model": "bin_class"}
+    if cfg == "c4full":
+        return {"workload": "c4", "N": 50000, "Mt": 200000, "kind": GEN_GAUSS, "model": "bin_class"}
     if n == 1:
-        return {"workload": "c2", "N": 10000, "Mt": 50000, "kind": GEN_GAUSS}
+        return {"workload": "c2", "N": 10000, "Mt": 50000, "kind": GEN_GAUSS, "model": "linear"}
     s = math.sqrt(n)
-    return {"workload": "c2-weak", "N": int(round(10000 * s)), "Mt": int(round(50000 * s)), "kind": GEN_GAUSS}
+    return {"workload": "c2-weak", "N": int(round(10000 * s)), "Mt": int(round(50000 * s)), "kind": GEN_GAUSS,
+            "model": "linear"}
