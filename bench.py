@@ -1,6 +1,6 @@
 """bench.py — VAMP iterations/s + HBM GB/s on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c4full] [--no-cpu-baseline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c4full|c5] [--no-cpu-baseline]
 
 A "step" is one VAMP iteration (src/vamp.cpp:148-428) of the linear model
 (or src/vamp_probit.cpp:68-463 of the probit model for c4)
@@ -17,6 +17,10 @@ Workloads (synthetic, generated on the device):
   c4            probit model (configs[3], src/vamp_probit.cpp): N=50,000 x 50,000
                 markers per GPU, binary phenotype; at n=4 it is N=50,000 x Mt=200,000.
   c4full        configs[3] whole on any n (80 GB: fits one MI355X).
+  c5            LOO association test (configs[4]): N=100,000 x 62,500 methylation-
+                like markers per GPU; at n=8 it is N=100,000 x Mt=500,000.  A step
+                is one whole test (A.x of the estimate, then the per-marker pass
+                and the p-values); value = markers tested per second.
 
 value = n_gpus * iterations/s ("shard-iterations/s": VAMP iterations over one
 GPU's shard; at n=1 exactly iterations/s of the workload).  Multi-GPU: one
@@ -100,12 +104,110 @@ def cpu_baseline(d: "va.Data", w: dict, beta: np.ndarray, seed: int, budget_s: f
     }
 
 
+def cpu_baseline_assoc(d: "va.Data", w: dict, est: np.ndarray, seed: int) -> dict:
+    """The oracle's LOO test (OpenMP) on the first Ms markers of the same workload."""
+    from oracle import pyoracle as O
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    N = w["N"]
+    Ms = 8000
+    X = O.generate_markers(seed, w["kind"], N, 0, Ms)
+    y = d.get_phen()
+    t0 = time.perf_counter()
+    O.assoc_loo(X, y, est[:Ms])
+    el = time.perf_counter() - t0
+    return {"value": Ms / el, "unit": "markers/s", "cores": threads, "kind": "port",
+            "sample": f"LOO test of markers 0-{Ms - 1} of {w['workload']} (N={N}, A.x over those markers) on "
+                      f"{threads} OpenMP threads, {el:.1f} s"}
+
+
+def bench_assoc(args, d, w, world, rank, t_start):
+    """--config c5: the LOO association test (src/main_meth.cpp:245-264) on
+    device-resident inputs; a step is one whole test."""
+    import ctypes as C
+
+    N, Mt = w["N"], w["Mt"]
+    beta = d.simulate_phen(args.seed + 1, lam=0.1, h2=0.5)
+    t_setup = time.perf_counter() - t_start
+    est = beta * 0.9 / np.sqrt(N)  # an estimate file's values (x1_hat / sqrt(N))
+    dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+    e_t = torch.from_numpy(est).to(dev)
+    p_t = torch.zeros(max(d.M, 1), dtype=torch.float64, device=dev)
+    lib = va.load()
+
+    def step():
+        va._lib.check(lib.vampomi_assoc_loo(d.ctx, C.c_void_p(e_t.data_ptr()), C.c_void_p(p_t.data_ptr()), None,
+                                            va.MEM_DEVICE))
+
+    for _ in range(args.warmup):
+        step()
+    d.reset_stats()
+    d.set_timing(not args.no_timing)
+
+    def barrier():
+        d.sync()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier()
+    el = time.perf_counter() - t0
+    st = d.stats()
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    roof = None
+    if st.loo.launches:
+        ks = st.loo
+        kname = va.kernel_name(2, 1, 0)
+        avg_ms = ks.ms_total / ks.launches
+        bytes_per = ks.bytes_total / ks.launches
+        achieved = bytes_per / (avg_ms * 1e-3) / 1e9
+        traffic = pmc_traffic(kname, w["workload"])
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": int(traffic) if traffic else None,
+                "traffic_unit": "HBM bytes per launch (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, "
+                                f"profiles/{os.path.basename(PMC_FILE.format(w['workload']))})",
+                "algorithmic_bytes_per_launch": int(bytes_per), "kernel": kname,
+                "avg_launch_us": round(avg_ms * 1e3, 2), "launches": int(ks.launches),
+                "ax_avg_launch_us": round(st.ax.ms_total / max(st.ax.launches, 1) * 1e3, 2)}
+    line = {
+        "metric": "LOO association test: markers tested/s (+ achieved HBM GB/s of the per-marker pass)",
+        "value": round(Mt * args.steps / el, 1),
+        "unit": "markers/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(el / args.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "f64", "data": "synthetic (index-keyed dyadic generator, generated in HBM)",
+        "config": {"workload": w["workload"], "model": "association_test loo", "N": N, "Mt": Mt, "M_per_gpu": d.M,
+                   "design": "methylation-like", "parallelism": f"markers sharded over {world} GPU(s)"},
+        "roofline": roof,
+        "setup_s": round(t_setup, 2),
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            line["cpu_baseline"] = cpu_baseline_assoc(d, w, est, args.seed)
+        except Exception as e:
+            line["cpu_baseline"] = {"error": repr(e)}
+    d.close()
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=48)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c4full"])
+    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c4full", "c5"])
     ap.add_argument("--seed", type=int, default=20250711)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="skip the HIP-event kernel timing")
@@ -130,6 +232,8 @@ def main():
     t0 = time.perf_counter()
     d.generate(args.seed, w["kind"])
     model = w.get("model", "linear")
+    if model == "loo":
+        return bench_assoc(args, d, w, world, rank, t0)
     if model == "bin_class":
         beta = d.simulate_phen_binary(args.seed + 1, lam=0.1, h2=0.8)
     else:

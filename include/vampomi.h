@@ -26,6 +26,8 @@
  *        src/vamp_probit.cpp:19-488                     -> vampomi_infere   (COLLECTIVE)
  *        (or vampomi_vamp_begin / _step / _end, one VAMP iteration per step)
  *   divide_work                src/utilities.cpp:207-239 -> vampomi_divide_work
+ *   association_test loo / se  src/main_meth.cpp:206-264, src/data.cpp:385-417,
+ *                              src/utilities.cpp:269-282 -> vampomi_assoc_loo / _se
  *
  * Errors: every call returns a vampomi_status; nothing aborts the process
  * (the reference calls MPI_Abort / exit / throw).  vampomi_last_error() gives
@@ -199,6 +201,20 @@ vampomi_status vampomi_vamp_begin(vampomi_ctx* ctx, const vampomi_params* p, vam
 vampomi_status vampomi_vamp_step(vampomi_ctx* ctx, int* stopped);
 vampomi_status vampomi_vamp_end(vampomi_ctx* ctx);
 
+/* ---- association tests (--run-mode association_test) ----
+ * loo: src/main_meth.cpp:245-264 + data::pvals_loo src/data.cpp:385-417.
+ * est = this shard's slice of the estimate file as stored (x1_hat/sqrt(N));
+ * the engine multiplies by sqrt(N), forms y_mod = y - Ax(x1_hat) (COLLECTIVE),
+ * then per marker the five sums over y_mark = y_mod + X_j/sqrt(N)*x1_hat_j with
+ * the RAW marker values, and linear_reg1d_pvals (src/utilities.cpp:269-282;
+ * Student-t tail restated, Boost absent).  stats (5*M: sumx sumsqx sumxy sumy
+ * sumsqy per marker) may be NULL.
+ * se: src/main_meth.cpp:218-242, p_j = P(N(r1_j, 1/(gam1 N)) <= 0), 1 - p_j when
+ * r1_j <= 0; rank-local. */
+vampomi_status vampomi_assoc_loo(vampomi_ctx* ctx, const double* est, double* pvals, double* stats,
+                                 int mem);
+vampomi_status vampomi_assoc_se(vampomi_ctx* ctx, const double* r1, double gam1, double* pvals, int mem);
+
 /* ---- measurement ---- */
 typedef struct {
     int64_t launches;             /* kernel launches of this class */
@@ -214,6 +230,7 @@ typedef struct {
     vampomi_kernel_stat atx_k[4];
     int64_t a_passes_exec;
     int64_t host_syncs;
+    vampomi_kernel_stat loo;      /* association-test pass (vampomi_assoc_loo) */
 } vampomi_stats;
 
 /* enable HIP-event timing of the A/A^T kernels (adds one event pair per launch) */
@@ -228,7 +245,8 @@ vampomi_status vampomi_dev_set_variant(vampomi_ctx* ctx, int which, int variant)
 /* average device time (HIP events) of `reps` back-to-back launches, K RHS */
 vampomi_status vampomi_dev_time_pass(vampomi_ctx* ctx, int which, int K, int reps, double* avg_ms);
 /* the kernel (as rocprofv3 names it) that pass `which` with K RHS launches now
- * (mode 1: A^T.u with the lmmse_mult epilogue) */
+ * (mode 1: A^T.u with the lmmse_mult epilogue; which = 2: the association-test
+ * pass of vampomi_assoc_loo) */
 vampomi_status vampomi_dev_kernel_name(int which, int K, int mode, char* out, int cap);
 
 #ifdef __cplusplus

@@ -89,6 +89,14 @@ def load() -> C.CDLL:
         for f in (lib.orc_g1_bin, lib.orc_g1d_bin):
             f.restype = d
             f.argtypes = [d, d, d]
+        lib.orc_t_sf.restype = d
+        lib.orc_t_sf.argtypes = [d, d]
+        lib.orc_lnbeta_half.restype = d
+        lib.orc_lnbeta_half.argtypes = [d]
+        lib.orc_reg1d_pval.restype = d
+        lib.orc_reg1d_pval.argtypes = [d, d, d, d, d, C.c_int]
+        lib.orc_assoc_loo.argtypes = [C.POINTER(Problem), p, p, p]
+        lib.orc_assoc_se.argtypes = [p, i64, d, i64, p]
         _lib = lib
     return _lib
 
@@ -169,6 +177,39 @@ def g1d_bin(p: float, tau1: float, y: float) -> float:
 def probit_p1(seed: int, N: int) -> np.ndarray:
     lib = load()
     return np.array([lib.orc_probit_p1(seed, i) for i in range(N)])
+
+
+def t_sf(t: float, df: float) -> float:
+    return load().orc_t_sf(t, df)
+
+
+def reg1d_pval(sumx, sumsqx, sumxy, sumy, sumsqy, n: int) -> float:
+    return load().orc_reg1d_pval(sumx, sumsqx, sumxy, sumy, sumsqy, n)
+
+
+def assoc_loo(X: np.ndarray, y: np.ndarray, est: np.ndarray, Mt: Optional[int] = None, S: int = 0, rank: int = 0,
+              nranks: int = 1, allreduce: Optional[Callable] = None, alpha_scale: float = 1.0):
+    """--pval-method loo on one shard X (M, N): returns (pvals, stats (M, 5))."""
+    lib = load()
+    X = np.ascontiguousarray(X, dtype=np.float64)
+    M, N = X.shape
+    y = np.ascontiguousarray(y, dtype=np.float64)
+    est = np.ascontiguousarray(est, dtype=np.float64)
+    mave, msig = marker_stats(X, alpha_scale)
+    cb = _make_allreduce(allreduce) if allreduce is not None else ALLREDUCE_FN()
+    pb = Problem(N=N, Mt=Mt or M, M=M, S=S, ld=N, rank=rank, nranks=nranks, X=_p(X), mave=_p(mave), msig=_p(msig),
+                 y=_p(y), true_signal=None, x1hat_init=None, allreduce=cb, user=None)
+    pv = np.zeros(max(M, 1))
+    st = np.zeros((max(M, 1), 5))
+    lib.orc_assoc_loo(C.byref(pb), _p(est), _p(pv), _p(st))
+    return pv[:M], st[:M]
+
+
+def assoc_se(r1: np.ndarray, gam1: float, N: int) -> np.ndarray:
+    r1 = np.ascontiguousarray(r1, dtype=np.float64)
+    out = np.zeros(max(len(r1), 1))
+    load().orc_assoc_se(_p(r1), len(r1), gam1, N, _p(out))
+    return out[:len(r1)]
 
 
 def read_phen(path: str, N: int, standardize: bool = True) -> np.ndarray:

@@ -1158,3 +1158,133 @@ int orc_vamp_infere_probit(const orc_problem* pb, const orc_params* prm, orc_res
     free(s.x2_hat);
     return 0;
 }
+
+/* ------------------------------------------------------------------------- */
+/* association tests — src/main_meth.cpp:206-264, src/data.cpp:385-417,      */
+/* src/utilities.cpp:269-282                                                 */
+/* ------------------------------------------------------------------------- */
+
+/* ln B(a, 1/2).  For a >= 30: ln sqrt(pi) - [lnG(a+1/2) - lnG(a)] with the
+ * asymptotic series of the lgamma difference (error < 2e-16 there); below,
+ * lgamma directly (values small, absolute error ~1e-15). */
+double orc_lnbeta_half(double a) {
+    if (a >= 30.0) {
+        const double i1 = 1.0 / a, i2 = i1 * i1;
+        const double d = 0.5 * log(a) - i1 * (1.0 / 8.0) + i1 * i2 * (1.0 / 192.0) - i1 * i2 * i2 * (1.0 / 640.0) +
+                         i1 * i2 * i2 * i2 * (17.0 / 14336.0);
+        return 0.57236494292470008707 - d; /* ln sqrt(pi) */
+    }
+    return lgamma(a) + lgamma(0.5) - lgamma(a + 0.5);
+}
+
+/* continued fraction of the regularized incomplete beta I_x(a, b)
+ * (modified Lentz, the classic even/odd term pair per step) */
+static double ibeta_cf(double a, double b, double x) {
+    const double tiny = 1e-300, eps = 4e-16;
+    const double qab = a + b, qap = a + 1.0, qam = a - 1.0;
+    double c = 1.0, d = 1.0 - qab * x / qap;
+    if (fabs(d) < tiny) d = tiny;
+    d = 1.0 / d;
+    double h = d;
+    for (int m = 1; m <= 20000; ++m) {
+        const double m2 = 2.0 * m;
+        double aa = m * (b - m) * x / ((qam + m2) * (a + m2));
+        d = 1.0 + aa * d;
+        if (fabs(d) < tiny) d = tiny;
+        c = 1.0 + aa / c;
+        if (fabs(c) < tiny) c = tiny;
+        d = 1.0 / d;
+        h *= d * c;
+        aa = -(a + m) * (qab + m) * x / ((a + m2) * (qap + m2));
+        d = 1.0 + aa * d;
+        if (fabs(d) < tiny) d = tiny;
+        c = 1.0 + aa / c;
+        if (fabs(c) < tiny) c = tiny;
+        d = 1.0 / d;
+        const double del = d * c;
+        h *= del;
+        if (fabs(del - 1.0) < eps) break;
+    }
+    return h;
+}
+
+/* P(T > t) for Student's t with df degrees of freedom, t >= 0:
+ * 0.5 * I_x(df/2, 1/2), x = df / (df + t^2).  Stands for
+ * boost::math::cdf(complement(students_t(df), t)) (Boost is absent here:
+ * pinned against scipy.stats.t.sf in tests/test_oracle_assoc.py). */
+double orc_t_sf(double t, double df) {
+    if (isnan(t) || isnan(df)) return NAN;
+    if (t <= 0.0) return t == 0.0 ? 0.5 : 1.0 - orc_t_sf(-t, df);
+    const double a = 0.5 * df, b = 0.5, tt = t * t;
+    const double lx = -log1p(tt / df);     /* ln x */
+    const double l1x = log(tt / (df + tt)); /* ln (1 - x) */
+    const double x = df / (df + tt);
+    const double front = exp(a * lx + b * l1x - orc_lnbeta_half(a));
+    /* the direct fraction in x for the tail (t >= 3), the fraction of the
+     * complement in 1 - x below: either is accurate to ~2e-12 relative
+     * (worst near t = 3 at large df; mpmath check in DESIGN.md §3) */
+    if (t >= 3.0 && x < (a + 1.0) / (a + b + 2.0)) return 0.5 * (front * ibeta_cf(a, b, x) / a);
+    return 0.5 * (1.0 - front * ibeta_cf(b, a, tt / (df + tt)) / b);
+}
+
+/* linear_reg1d_pvals — src/utilities.cpp:269-282 */
+double orc_reg1d_pval(double sumx, double sumsqx, double sumxy, double sumy, double sumsqy, int n) {
+    const double s2y = (sumsqy - sumy * sumy / n) / (n - 1);
+    const double s2x = (sumsqx - sumx * sumx / n) / (n - 1);
+    const double sxy = (sumxy - sumx * sumy / n) / (n - 1);
+    const double rxy = sxy / sqrt(s2x * s2y);
+    const double t = rxy * sqrt((n - 2) / (1 - rxy * rxy));
+    return 2.0 * orc_t_sf(t > 0 ? t : (0 - t), (double)(n - 2));
+}
+
+/* --pval-method loo — src/main_meth.cpp:245-264 + data::pvals_loo
+ * src/data.cpp:385-417.  est = the --estimate-file slice as stored
+ * (x1_hat / sqrt(N)); X is the RAW marker data (the leave-one-out add-back
+ * uses meth_data, not the standardised column). */
+void orc_assoc_loo(const orc_problem* pb, const double* est, double* pvals, double* stats) {
+    const int64_t N = pb->N, M = pb->M, ld = pb->ld;
+    double* x1 = (double*)malloc(sizeof(double) * (size_t)(M > 0 ? M : 1));
+    double* z1 = (double*)malloc(sizeof(double) * (size_t)N);
+    double* ymod = (double*)malloc(sizeof(double) * (size_t)N);
+    for (int64_t i = 0; i < M; ++i) x1[i] = est[i] * sqrt((double)N); /* :254-255 */
+    orc_ax(pb->X, N, ld, M, pb->mave, pb->msig, x1, z1, pb->allreduce, pb->user); /* :257 */
+    for (int64_t i = 0; i < N; ++i) ymod[i] = pb->y[i] - z1[i];                    /* data.cpp:390-391 */
+#pragma omp parallel for schedule(dynamic, 16)
+    for (int64_t j = 0; j < M; ++j) {
+        const double* meth = pb->X + j * ld;
+        double sumx = 0.0, sumsqx = 0.0, sumxy = 0.0, sumy = 0.0, sumsqy = 0.0;
+        for (int64_t i = 0; i < N; ++i) {
+            const double ym = ymod[i] + meth[i] / sqrt((double)N) * x1[j]; /* :403-404 */
+            sumx += meth[i];
+            sumsqx += meth[i] * meth[i];
+            sumxy += meth[i] * ym;
+            sumy += ym;
+            sumsqy += ym * ym;
+        }
+        if (stats) {
+            double* s = stats + 5 * j;
+            s[0] = sumx;
+            s[1] = sumsqx;
+            s[2] = sumxy;
+            s[3] = sumy;
+            s[4] = sumsqy;
+        }
+        pvals[j] = orc_reg1d_pval(sumx, sumsqx, sumxy, sumy, sumsqy, (int)N);
+    }
+    free(x1);
+    free(z1);
+    free(ymod);
+}
+
+/* --pval-method se — src/main_meth.cpp:218-242: P(N(r1_j, 1/(gam1 N)) <= 0),
+ * flipped for r1_j <= 0.  boost::math::cdf(normal(m, s), x) is
+ * erfc(-((x - m) / s) / sqrt(2)) / 2. */
+void orc_assoc_se(const double* r1, int64_t M, double gam1, int64_t N, double* pvals) {
+    const double sd = sqrt(1.0 / (gam1 * (double)N));
+    for (int64_t j = 0; j < M; ++j) {
+        const double diff = (0.0 - r1[j]) / sd;
+        double p = erfc(-diff / M_SQRT2) / 2;
+        if (r1[j] <= 0.0) p = 1 - p;
+        pvals[j] = p;
+    }
+}

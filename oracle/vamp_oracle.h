@@ -144,6 +144,20 @@ double orc_erfcx(double x);
 double orc_g1_bin(double p, double tau1, double y);
 double orc_g1d_bin(double p, double tau1, double y);
 
+/* ---- association tests (--run-mode association_test) ---- */
+/* linear_reg1d_pvals, src/utilities.cpp:269-282 */
+double orc_reg1d_pval(double sumx, double sumsqx, double sumxy, double sumy, double sumsqy, int n);
+/* Student t upper tail P(T > t) (stands for Boost's complemented cdf) */
+double orc_t_sf(double t, double df);
+double orc_lnbeta_half(double a);
+/* --pval-method loo (src/main_meth.cpp:245-264, src/data.cpp:385-417): est is
+ * the estimate-file slice (x1_hat/sqrt(N)); uses pb->X/mave/msig/y and
+ * pb->allreduce for the Ax.  stats (5 per marker: sumx sumsqx sumxy sumy
+ * sumsqy) may be NULL. */
+void orc_assoc_loo(const orc_problem* pb, const double* est, double* pvals, double* stats);
+/* --pval-method se (src/main_meth.cpp:218-242) */
+void orc_assoc_se(const double* r1, int64_t M, double gam1, int64_t N, double* pvals);
+
 /* ---- output writers (src/utilities.cpp:241-249, 366-401) ---- */
 int orc_store_vec(const char* path, const double* v, int64_t S, int64_t M);
 int orc_csv_header(const char* path, const char* const* fields, int n);

@@ -1,0 +1,127 @@
+"""GPU parity of the association tests (--run-mode association_test,
+src/main_meth.cpp:206-264, src/data.cpp:385-417, src/utilities.cpp:269-282)
+through the C ABI against the oracle.  Bar: the five per-marker sums to
+1e-13 relative, p-values to 1e-10 relative (north_star's floating-point bar),
+SE p-values to 1e-14."""
+import math
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import relerr
+from _data import make_problem
+
+pytestmark = pytest.mark.gpu
+
+va = pytest.importorskip("vampomi_amd")
+from oracle import pyoracle as O  # noqa: E402  (checker)
+
+
+def _estimate(beta, N, scale=0.9, seed=0):
+    rng = np.random.default_rng(seed)
+    return (beta * scale + rng.normal(size=beta.shape) * 1e-3) / np.sqrt(N)  # as an _it_K.bin holds it
+
+
+def _check_loo(p, st, po, sto):
+    for q in range(5):
+        assert relerr(st[:, q], sto[:, q]) < 1e-13, q
+    ok = np.abs(p - po) <= 1e-10 * po + 1e-300
+    assert ok.all(), (p[~ok][:5], po[~ok][:5])
+
+
+@pytest.mark.parametrize("N,Mt,kind", [(1000, 2000, 0), (1000, 2000, 1), (4099, 333, 1), (257, 1031, 0)])
+def test_loo_parity(N, Mt, kind):
+    X, y, beta = make_problem(N, Mt, kind=kind)
+    est = _estimate(beta, N)
+    po, sto = O.assoc_loo(X, y, est)
+    with va.Data(N, Mt) as d:
+        d.load_meth(X)
+        d.set_phen(y, standardize=False)
+        p, st = d.assoc_loo(est)
+    _check_loo(p, st, po, sto)
+    assert np.median(p[beta != 0]) < np.median(p[beta == 0])
+
+
+def test_loo_extreme_p_values():
+    """Strong effects: p-values down to ~1e-300 keep their relative accuracy."""
+    N, Mt = 20000, 64
+    X, y, beta = make_problem(N, Mt, kind=0, lam=0.3, h2=0.95)
+    est = np.zeros(Mt)  # no leave-one-out add-back: plain marginal tests on y
+    po, sto = O.assoc_loo(X, y, est)
+    with va.Data(N, Mt) as d:
+        d.load_meth(X)
+        d.set_phen(y, standardize=False)
+        p, st = d.assoc_loo(est)
+    assert po.min() < 1e-30
+    _check_loo(p, st, po, sto)
+
+
+def test_se_parity():
+    N, Mt = 1000, 2000
+    X, y, beta = make_problem(N, Mt)
+    rng = np.random.default_rng(3)
+    r1 = np.concatenate([rng.normal(size=Mt - 4) * 0.05, [0.0, -0.0, 1e-3, -1e-3]])
+    gam1 = 2.5
+    po = O.assoc_se(r1, gam1, N)
+    with va.Data(N, Mt) as d:
+        d.load_meth(X)
+        p = d.assoc_se(r1, gam1)
+    assert np.allclose(p, po, rtol=1e-14, atol=1e-16)
+
+
+def test_cli_association_files(tmp_path):
+    N, Mt = 600, 1500
+    X, y, beta = make_problem(N, Mt, kind=1)
+    Xp = tmp_path / "ex.bin"
+    X.astype("<f8").tofile(Xp)
+    yp = tmp_path / "ex.phen"
+    yp.write_text("".join("%d %d %0.10f\n" % (i, i, v) for i, v in enumerate(y)))
+    est = _estimate(beta, N)
+    ep = tmp_path / "ex_it_7.bin"
+    est.astype("<f8").tofile(ep)
+    r1 = est * 3
+    rp = tmp_path / "ex_r1_it_7.bin"
+    r1.astype("<f8").tofile(rp)
+    base = [va.CLI_PATH, "--meth-file", str(Xp), "--phen-file", str(yp), "--N", str(N), "--Mt", str(Mt),
+            "--out-dir", str(tmp_path), "--out-name", "as", "--run-mode", "association_test"]
+    r = subprocess.run(base + ["--pval-method", "loo", "--estimate-file", str(ep)], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    got = np.fromfile(tmp_path / "as_it_7_pval_loo.bin", dtype="<f8")
+    yo = O.read_phen(str(yp), N, True)
+    po, _ = O.assoc_loo(X, yo, est)
+    assert got.shape == (Mt,) and np.all(np.abs(got - po) <= 1e-10 * po + 1e-300)
+    r = subprocess.run(base + ["--pval-method", "se", "--r1-file", str(rp), "--gam1", "3.5"], capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    got = np.fromfile(tmp_path / "as_it_7_pval_se.bin", dtype="<f8")
+    assert np.allclose(got, O.assoc_se(r1, 3.5, N), rtol=1e-14, atol=1e-16)
+    r = subprocess.run(base + ["--pval-method", "loo", "--estimate-file", str(tmp_path / "noiter.bin")],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 1 and "cannot parse the iteration" in r.stdout
+
+
+def test_c5_shape_properties():
+    """BASELINE config 5 per-GPU sample dimension (N = 100,000) with a 16k-marker
+    shard: the device sums equal a float64 restatement on sampled markers and
+    the causal markers stand out."""
+    N, Mt = 100000, 16000
+    with va.Data(N, Mt) as d:
+        d.generate(9, va.GEN_METH)
+        beta = d.simulate_phen(10, lam=0.05, h2=0.5)
+        y = d.get_phen()
+        est = _estimate(beta, N)
+        p, st = d.assoc_loo(est)
+        z1 = d.Ax(est * np.sqrt(N))
+        ymod = y - z1
+        for j in (0, 1, 7777, Mt - 1):
+            x = d.get_meth_data(j, 1)[0]
+            ym = ymod + x / np.sqrt(N) * (est[j] * np.sqrt(N))
+            ref = [x.sum(), x @ x, x @ ym, ym.sum(), ym @ ym]
+            assert np.allclose(st[j], ref, rtol=1e-11), j
+            q = O.reg1d_pval(*ref, N)
+            assert abs(p[j] - q) <= 1e-8 * q
+        assert np.all((p >= 0) & (p <= 1))
+        assert np.median(p[beta != 0]) < 1e-3 < np.median(p[beta == 0])

@@ -39,7 +39,8 @@ def divide_work(Mt: int, nranks: int, rank: int):
 
 
 def kernel_name(which: int, K: int, mode: int = 0) -> str:
-    """rocprofv3 name of the A.x (which=0) / A^T.u (which=1) kernel launched for K RHS."""
+    """rocprofv3 name of the A.x (which=0) / A^T.u (which=1) kernel launched for K RHS,
+    or of the association-test pass (which=2)."""
     buf = C.create_string_buffer(256)
     check(load().vampomi_dev_kernel_name(which, K, mode, buf, 256))
     return buf.value.decode()
@@ -191,6 +192,25 @@ class Data:
         check(self._lib.vampomi_pcg(self.ctx, _dp(v), None if m0 is None else _dp(m0), tau, gam2,
                                     1 if onsager else 0, max_iter, tol, _dp(mu), C.byref(it), MEM_HOST))
         return mu[: self.M], it.value
+
+    def assoc_loo(self, est: np.ndarray, mem_device: bool = False):
+        """--pval-method loo (src/main_meth.cpp:245-264, src/data.cpp:385-417).
+        est: this shard's estimate-file slice (x1_hat / sqrt(N)).  COLLECTIVE.
+        Returns (pvals (M), stats (M, 5): sumx sumsqx sumxy sumy sumsqy)."""
+        est = np.ascontiguousarray(est, dtype=np.float64)
+        if est.shape != (self.M,):
+            raise ValueError("estimate slice must have M entries")
+        pv = np.zeros(max(self.M, 1))
+        st = np.zeros((max(self.M, 1), 5))
+        check(self._lib.vampomi_assoc_loo(self.ctx, _dp(est), _dp(pv), _dp(st), MEM_HOST))
+        return pv[: self.M], st[: self.M]
+
+    def assoc_se(self, r1: np.ndarray, gam1: float) -> np.ndarray:
+        """--pval-method se (src/main_meth.cpp:218-242)."""
+        r1 = np.ascontiguousarray(r1, dtype=np.float64)
+        pv = np.zeros(max(self.M, 1))
+        check(self._lib.vampomi_assoc_se(self.ctx, _dp(r1), gam1, _dp(pv), MEM_HOST))
+        return pv[: self.M]
 
     def denoise_bin(self, p1: np.ndarray, tau1: float):
         """g1_bin_class / g1d_bin_class over the phenotype (src/vamp_probit.cpp:469-488): (z1, sum of g1d)."""

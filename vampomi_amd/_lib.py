@@ -85,7 +85,7 @@ class KernelStat(C.Structure):
 
 class Stats(C.Structure):
     _fields_ = [("ax", KernelStat), ("atx", KernelStat), ("ax_k", KernelStat * 4), ("atx_k", KernelStat * 4),
-                ("a_passes_exec", C.c_int64), ("host_syncs", C.c_int64)]
+                ("a_passes_exec", C.c_int64), ("host_syncs", C.c_int64), ("loo", KernelStat)]
 
 
 # exported symbol -> (restype, argtypes); also the list the ABI test checks
@@ -117,6 +117,8 @@ SIGNATURES = {
     "vampomi_lmmse_mult": (C.c_int, [_P, _P, C.c_double, C.c_double, _P, C.c_int]),
     "vampomi_pcg": (C.c_int, [_P, _P, _P, C.c_double, C.c_double, C.c_int, C.c_int, C.c_double, _P,
                               C.POINTER(C.c_int), C.c_int]),
+    "vampomi_assoc_loo": (C.c_int, [_P, _P, _P, _P, C.c_int]),
+    "vampomi_assoc_se": (C.c_int, [_P, _P, C.c_double, _P, C.c_int]),
     "vampomi_denoise_bin": (C.c_int, [_P, _P, C.c_double, _P, C.POINTER(C.c_double), C.c_int]),
     "vampomi_denoise": (C.c_int, [_P, _P, C.c_double, _P, _P, C.c_int, _P, _P, C.POINTER(C.c_double), C.c_int]),
     "vampomi_params_default": (None, [C.POINTER(Params)]),

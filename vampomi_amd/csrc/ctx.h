@@ -40,7 +40,7 @@ struct VampRun;
 
 struct TimedLaunch {
     hipEvent_t a, b;
-    int cls;  // 0 ax, 1 atx
+    int cls;  // 0 ax, 1 atx, 2 loo
     int K;
     double bytes, flops;
 };

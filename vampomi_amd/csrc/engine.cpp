@@ -67,9 +67,10 @@ void resolve_timing(vampomi_ctx* c) {
     for (auto& t : c->pending) {
         float ms = 0.f;
         if (hipEventSynchronize(t.b) == hipSuccess && hipEventElapsedTime(&ms, t.a, t.b) == hipSuccess) {
-            vampomi_kernel_stat* s = t.cls == 0 ? &c->stats.ax : &c->stats.atx;
-            vampomi_kernel_stat* sk = t.cls == 0 ? &c->stats.ax_k[t.K - 1] : &c->stats.atx_k[t.K - 1];
+            vampomi_kernel_stat* s = t.cls == 0 ? &c->stats.ax : t.cls == 1 ? &c->stats.atx : &c->stats.loo;
+            vampomi_kernel_stat* sk = t.cls == 0 ? &c->stats.ax_k[t.K - 1] : t.cls == 1 ? &c->stats.atx_k[t.K - 1] : nullptr;
             for (vampomi_kernel_stat* x : {s, sk}) {
+                if (!x) continue;
                 x->launches += 1;
                 x->ms_total += ms;
                 x->bytes_total += t.bytes;
@@ -702,6 +703,63 @@ extern "C" vampomi_status vampomi_denoise_bin(vampomi_ctx* c, const double* p1, 
     return VAMPOMI_OK;
 }
 
+// --run-mode association_test --pval-method loo (src/main_meth.cpp:245-264,
+// data::pvals_loo src/data.cpp:385-417).  COLLECTIVE (one A.x).
+extern "C" vampomi_status vampomi_assoc_loo(vampomi_ctx* c, const double* est, double* pvals, double* stats,
+                                            int mem) {
+    if (!c || (!est && c->M > 0)) return fail(VAMPOMI_ERR_ARG, "null argument");
+    if (!c->have_X || !c->have_y) return fail(VAMPOMI_ERR_STATE, "load methylation data and phenotype first");
+    HIPCHK(hipSetDevice(c->device));
+    const int64_t M = c->M, N = c->N, Mx = std::max<int64_t>(M, 1), ld = c->ld;
+    double* e = c->mbuf;            // estimate-file values
+    double* x1 = c->mbuf + Mx;      // x1_hat * sqrt(N)
+    double* pv = c->mbuf + 2 * Mx;  // p-values
+    double* st = c->mbuf + 3 * Mx;  // 5 sums per marker (slots 3..7)
+    double* z1 = c->nbuf;
+    double* ymod = c->nbuf + ld;
+    STCHK(stage_in(c, est, M, mem, e));
+    HIPCHK(vk::mul_scalar(M, e, std::sqrt((double)N), x1, c->st));  // :254-255
+    const double* xs[1] = {x1};
+    STCHK(ax_dev(c, 1, xs, z1));                                     // :257
+    HIPCHK(vk::axpby(N, 1.0, c->y, -1.0, z1, ymod, c->st));          // y_mod = y - z1 (data.cpp:390-391)
+    if (ld > N) HIPCHK(hipMemsetAsync(ymod + N, 0, (size_t)(ld - N) * 8, c->st));
+    TimedLaunch t{};
+    if (c->timing) {
+        t.a = ev_get(c);
+        t.b = ev_get(c);
+        HIPCHK(hipEventRecord(t.a, c->st));
+    }
+    HIPCHK(vk::loo_sums(c->shard(), ymod, x1, std::sqrt((double)N), st, c->st));  // data.cpp:393-416
+    if (c->timing) {
+        HIPCHK(hipEventRecord(t.b, c->st));
+        t.cls = 2;
+        t.K = 1;
+        // raw X once, ymod, x1, the five sums; per element 1 div, 2 mul + 1 add
+        // for ym, 5 accumulations (3 of them products)
+        t.bytes = 8.0 * (double)N * (double)M + 8.0 * (double)N + 8.0 * 6.0 * (double)M;
+        t.flops = 11.0 * (double)N * (double)M;
+        c->pending.push_back(t);
+    }
+    c->stats.a_passes_exec++;
+    HIPCHK(vk::loo_pvals(M, st, (int)N, pv, c->st));
+    if (stats) STCHK(stage_out(c, st, 5 * M, mem, stats));
+    if (pvals) STCHK(stage_out(c, pv, M, mem, pvals));
+    HIPCHK(hipStreamSynchronize(c->st));
+    if (c->timing) resolve_timing(c);
+    return VAMPOMI_OK;
+}
+
+// --pval-method se (src/main_meth.cpp:218-242): rank-local
+extern "C" vampomi_status vampomi_assoc_se(vampomi_ctx* c, const double* r1, double gam1, double* pvals, int mem) {
+    if (!c || (!r1 && c->M > 0) || (!pvals && c->M > 0)) return fail(VAMPOMI_ERR_ARG, "null argument");
+    HIPCHK(hipSetDevice(c->device));
+    const int64_t Mx = std::max<int64_t>(c->M, 1);
+    STCHK(stage_in(c, r1, c->M, mem, c->mbuf));
+    HIPCHK(vk::se_pvals(c->M, c->mbuf, gam1, c->N, c->mbuf + Mx, c->st));
+    STCHK(stage_out(c, c->mbuf + Mx, c->M, mem, pvals));
+    return VAMPOMI_OK;
+}
+
 // ---------------------------------------------------------------------------
 // parameters / measurement
 // ---------------------------------------------------------------------------
@@ -781,7 +839,7 @@ extern "C" vampomi_status vampomi_dev_time_pass(vampomi_ctx* c, int which, int K
 
 extern "C" vampomi_status vampomi_dev_kernel_name(int which, int K, int mode, char* out, int cap) {
     if (!out || cap < 1) return fail(VAMPOMI_ERR_ARG, "bad buffer");
-    const std::string n = vk::kernel_name(which, K, mode);
+    const std::string n = which == 2 ? vk::loo_kernel_name() : vk::kernel_name(which, K, mode);
     std::snprintf(out, (size_t)cap, "%s", n.c_str());
     return VAMPOMI_OK;
 }

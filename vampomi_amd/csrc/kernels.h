@@ -130,6 +130,19 @@ hipError_t probit_confusion(int64_t N, int nz, const double* z, int64_t ld, cons
 // P2 start: p1[i] = gauss(seed ^ salt, 0, i) (replaces simulate(N, {1}, {1}), :53)
 hipError_t probit_p1(uint64_t seed, int64_t N, double* p1, hipStream_t st);
 
+// ---- association tests (src/main_meth.cpp:206-264, src/data.cpp:385-417) -------
+// stats[5j + {0..4}] = sum X, sum X^2, sum X*ym, sum ym, sum ym^2 over the
+// samples of marker j (RAW X), ym = ymod + X / sqrtN * x1[j]  (data::pvals_loo)
+hipError_t loo_sums(const Shard& s, const double* ymod, const double* x1, double sqrtN, double* stats,
+                    hipStream_t st);
+std::string loo_kernel_name();
+// pvals[j] = linear_reg1d_pvals(stats[5j..5j+4], n)  (src/utilities.cpp:269-282)
+hipError_t loo_pvals(int64_t M, const double* stats, int n, double* pvals, hipStream_t st);
+// pvals[j] = P(N(r1_j, 1/(gam1 N)) <= 0), flipped for r1_j <= 0 (src/main_meth.cpp:231-236)
+hipError_t se_pvals(int64_t M, const double* r1, double gam1, int64_t N, double* pvals, hipStream_t st);
+// out = x * a
+hipError_t mul_scalar(int64_t n, const double* x, double a, double* out, hipStream_t st);
+
 // ---- PCG (vamp::precondCG_solver), K right-hand sides --------------------------
 struct CgVecs {
     double* mu[kMaxRhs];

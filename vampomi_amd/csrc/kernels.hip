@@ -1069,4 +1069,197 @@ hipError_t probit_p1(uint64_t seed, int64_t N, double* p1, hipStream_t st) {
     return hipGetLastError();
 }
 
+
+// ---------------------------------------------------------------------------
+// association tests: data::pvals_loo (src/data.cpp:385-417) and the SE
+// p-values (src/main_meth.cpp:218-242)
+// ---------------------------------------------------------------------------
+// One pass over the RAW shard: a wave owns G markers, lanes stride the
+// samples (16-B nontemporal loads, 1 KiB per wave per load), every ymod
+// value serves G markers.  Per element exactly the reference's
+// ym = ymod + (X / sqrt(N)) * x1_j (division kept: bitwise per element), then
+// the five sums of linear_reg1d_pvals.  Pad rows are zero in X and ymod and
+// add exact zeros.
+template <int G, int UJ>
+__global__ __launch_bounds__(kBlock) void loo_kernel(const double* __restrict__ X, int64_t ld, int64_t N, int64_t M,
+                                                     const double* __restrict__ ymod, const double* __restrict__ x1,
+                                                     double sqrtN, double* __restrict__ stats) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t m0 = ((int64_t)blockIdx.x * 4 + wave) * G;
+    double acc[G][5];
+    double xj[G];
+    const double* col[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        const int64_t m = (m0 + g < M) ? m0 + g : M - 1;  // clamp: in-bounds, discarded
+        xj[g] = x1[m];
+        col[g] = X + m * ld;
+#pragma unroll
+        for (int q = 0; q < 5; ++q) acc[g][q] = 0.0;
+    }
+    auto add = [&](int g, double m, double y) {
+        const double ym = y + m / sqrtN * xj[g];
+        acc[g][0] += m;
+        acc[g][1] += m * m;
+        acc[g][2] += m * ym;
+        acc[g][3] += ym;
+        acc[g][4] += ym * ym;
+    };
+    int64_t j = 2 * lane;
+    for (; j + 128 * (UJ - 1) < N; j += 128 * UJ) {
+        v2d yy[UJ], xx[UJ][G];
+#pragma unroll
+        for (int t = 0; t < UJ; ++t)
+#pragma unroll
+            for (int g = 0; g < G; ++g) xx[t][g] = ld_stream(col[g] + j + 128 * t);
+#pragma unroll
+        for (int t = 0; t < UJ; ++t) yy[t] = ld2(ymod + j + 128 * t);
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int t = 0; t < UJ; ++t) {
+                add(g, xx[t][g].x, yy[t].x);
+                add(g, xx[t][g].y, yy[t].y);
+            }
+    }
+    for (; j < N; j += 128) {
+        v2d xx[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) xx[g] = ld_stream(col[g] + j);
+        const v2d yy = ld2(ymod + j);
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            add(g, xx[g].x, yy.x);
+            add(g, xx[g].y, yy.y);
+        }
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int q = 0; q < 5; ++q) {
+            const double s = wave_sum(acc[g][q]);
+            if (lane == 0 && m0 + g < M) stats[5 * (m0 + g) + q] = s;
+        }
+}
+
+static constexpr int kLooG = 4, kLooUJ = 2;
+
+std::string loo_kernel_name() {
+    char b[64];
+    std::snprintf(b, sizeof b, "loo_kernel<%d, %d>", kLooG, kLooUJ);
+    return b;
+}
+
+hipError_t loo_sums(const Shard& s, const double* ymod, const double* x1, double sqrtN, double* stats,
+                    hipStream_t st) {
+    if (s.M <= 0) return hipSuccess;
+    hipLaunchKernelGGL((loo_kernel<kLooG, kLooUJ>), dim3((unsigned)cdiv(s.M, 4 * kLooG)), dim3(kBlock), 0, st, s.X,
+                       s.ld, s.N, s.M, ymod, x1, sqrtN, stats);
+    return hipGetLastError();
+}
+
+// ln B(a, 1/2) and the Student-t upper tail: the same operations as the
+// oracle's orc_lnbeta_half / ibeta_cf / orc_t_sf (oracle/vamp_oracle.c),
+// standing for Boost's complemented students_t cdf (src/utilities.cpp:278-279)
+__device__ double lnbeta_half(double a) {
+    if (a >= 30.0) {
+        const double i1 = 1.0 / a, i2 = i1 * i1;
+        const double d = 0.5 * log(a) - i1 * (1.0 / 8.0) + i1 * i2 * (1.0 / 192.0) - i1 * i2 * i2 * (1.0 / 640.0) +
+                         i1 * i2 * i2 * i2 * (17.0 / 14336.0);
+        return 0.57236494292470008707 - d;
+    }
+    return lgamma(a) + lgamma(0.5) - lgamma(a + 0.5);
+}
+
+__device__ double ibeta_cf(double a, double b, double x) {
+    const double tiny = 1e-300, eps = 4e-16;
+    const double qab = a + b, qap = a + 1.0, qam = a - 1.0;
+    double c = 1.0, d = 1.0 - qab * x / qap;
+    if (fabs(d) < tiny) d = tiny;
+    d = 1.0 / d;
+    double h = d;
+    for (int m = 1; m <= 20000; ++m) {
+        const double m2 = 2.0 * m;
+        double aa = m * (b - m) * x / ((qam + m2) * (a + m2));
+        d = 1.0 + aa * d;
+        if (fabs(d) < tiny) d = tiny;
+        c = 1.0 + aa / c;
+        if (fabs(c) < tiny) c = tiny;
+        d = 1.0 / d;
+        h *= d * c;
+        aa = -(a + m) * (qab + m) * x / ((a + m2) * (qap + m2));
+        d = 1.0 + aa * d;
+        if (fabs(d) < tiny) d = tiny;
+        c = 1.0 + aa / c;
+        if (fabs(c) < tiny) c = tiny;
+        d = 1.0 / d;
+        const double del = d * c;
+        h *= del;
+        if (fabs(del - 1.0) < eps) break;
+    }
+    return h;
+}
+
+__device__ double t_sf_pos(double t, double df) {  // t > 0
+    const double a = 0.5 * df, b = 0.5, tt = t * t;
+    const double lx = -log1p(tt / df);
+    const double l1x = log(tt / (df + tt));
+    const double x = df / (df + tt);
+    const double front = exp(a * lx + b * l1x - lnbeta_half(a));
+    if (t >= 3.0 && x < (a + 1.0) / (a + b + 2.0)) return 0.5 * (front * ibeta_cf(a, b, x) / a);
+    return 0.5 * (1.0 - front * ibeta_cf(b, a, tt / (df + tt)) / b);
+}
+
+__device__ double t_sf(double t, double df) {
+    if (isnan(t) || isnan(df)) return __builtin_nan("");
+    if (t == 0.0) return 0.5;
+    return t > 0.0 ? t_sf_pos(t, df) : 1.0 - t_sf_pos(-t, df);
+}
+
+__global__ void loo_pval_kernel(int64_t M, const double* __restrict__ stats, int n, double* __restrict__ pvals) {
+    const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (j >= M) return;
+    const double* s = stats + 5 * j;
+    const double sumx = s[0], sumsqx = s[1], sumxy = s[2], sumy = s[3], sumsqy = s[4];
+    const double s2y = (sumsqy - sumy * sumy / n) / (n - 1);
+    const double s2x = (sumsqx - sumx * sumx / n) / (n - 1);
+    const double sxy = (sumxy - sumx * sumy / n) / (n - 1);
+    const double rxy = sxy / sqrt(s2x * s2y);
+    const double t = rxy * sqrt((n - 2) / (1 - rxy * rxy));
+    pvals[j] = 2.0 * t_sf(t > 0 ? t : (0 - t), (double)(n - 2));
+}
+
+hipError_t loo_pvals(int64_t M, const double* stats, int n, double* pvals, hipStream_t st) {
+    if (M <= 0) return hipSuccess;
+    hipLaunchKernelGGL(loo_pval_kernel, dim3((unsigned)cdiv(M, kBlock)), dim3(kBlock), 0, st, M, stats, n, pvals);
+    return hipGetLastError();
+}
+
+__global__ void se_pval_kernel(int64_t M, const double* __restrict__ r1, double sd, double* __restrict__ pvals) {
+    const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (j >= M) return;
+    const double diff = (0.0 - r1[j]) / sd;  // boost normal cdf at 0: erfc(-diff / sqrt(2)) / 2
+    double p = erfc(-diff / M_SQRT2) / 2;
+    if (r1[j] <= 0.0) p = 1 - p;
+    pvals[j] = p;
+}
+
+hipError_t se_pvals(int64_t M, const double* r1, double gam1, int64_t N, double* pvals, hipStream_t st) {
+    if (M <= 0) return hipSuccess;
+    const double sd = sqrt(1.0 / (gam1 * (double)N));
+    hipLaunchKernelGGL(se_pval_kernel, dim3((unsigned)cdiv(M, kBlock)), dim3(kBlock), 0, st, M, r1, sd, pvals);
+    return hipGetLastError();
+}
+
+__global__ void mul_scalar_kernel(int64_t n, const double* __restrict__ x, double a, double* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) out[i] = x[i] * a;
+}
+
+hipError_t mul_scalar(int64_t n, const double* x, double a, double* out, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(mul_scalar_kernel, dim3((unsigned)cdiv(n, kBlock)), dim3(kBlock), 0, st, n, x, a, out);
+    return hipGetLastError();
+}
+
 }  // namespace vk

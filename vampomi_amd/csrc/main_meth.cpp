@@ -1,5 +1,6 @@
 // main_meth.cpp — drop-in for the reference's main_meth.exe (src/main_meth.cpp)
-// in --run-mode infere (--model linear | bin_class): same flags, same output files.
+// in --run-mode infere (--model linear | bin_class) and association_test
+// (--pval-method loo | se): same flags, same output files.
 //
 // Ranks: the reference is launched with `mpirun -np P`; this binary runs one
 // process per GPU, rank/size from VAMPOMI_RANK/VAMPOMI_NRANKS (or the
@@ -55,6 +56,54 @@ static int die(const char* what) {
     return EXIT_FAILURE;
 }
 
+// the iteration number of an estimate / r1 file name: the text between the
+// last "it_" and the last ".bin" (src/main_meth.cpp:223-226, :249-252)
+static bool iteration_of(const std::string& name, std::string& it_str) {
+    const size_t pos1 = name.rfind("it_") + 3, pos2 = name.rfind(".bin");
+    try {
+        it_str = name.substr(pos1, pos2 - pos1);
+        (void)std::stoi(it_str);
+    } catch (...) {
+        return false;
+    }
+    return true;
+}
+
+// --run-mode association_test (src/main_meth.cpp:206-264)
+static int association_test(vampomi_ctx* ctx, const vopt::Options& opt, int rank, int64_t M, int64_t S) {
+    std::vector<double> in((size_t)std::max<int64_t>(M, 1)), pvals((size_t)std::max<int64_t>(M, 1));
+    std::string it_str, out;
+    if (opt.pval_method == "se") {
+        if (!iteration_of(opt.r1_file, it_str)) {
+            std::cout << "FATAL  : cannot parse the iteration from --r1-file \"" << opt.r1_file << "\"" << std::endl;
+            return EXIT_FAILURE;
+        }
+        if (rank == 0) std::cout << opt.r1_file << std::endl;
+        vio::read_vec(opt.r1_file, in.data(), S, M);
+        if (vampomi_assoc_se(ctx, in.data(), opt.gam1, pvals.data(), VAMPOMI_MEM_HOST) != VAMPOMI_OK)
+            return die("association test (se)");
+        out = opt.out_dir + "/" + opt.out_name + "_it_" + it_str + "_pval_se.bin";
+    } else if (opt.pval_method == "loo") {
+        if (!iteration_of(opt.estimate_file, it_str)) {
+            std::cout << "FATAL  : cannot parse the iteration from --estimate-file \"" << opt.estimate_file << "\""
+                      << std::endl;
+            return EXIT_FAILURE;
+        }
+        vio::read_vec(opt.estimate_file, in.data(), S, M);
+        if (vampomi_assoc_loo(ctx, in.data(), pvals.data(), nullptr, VAMPOMI_MEM_HOST) != VAMPOMI_OK)
+            return die("association test (loo)");
+        out = opt.out_dir + "/" + opt.out_name + "_it_" + it_str + "_pval_loo.bin";
+    } else {
+        return 0;  // the reference computes nothing for another --pval-method
+    }
+    if (rank == 0) std::cout << "Storing p-values to file " + out << std::endl;
+    if (!vio::store_vec(out, pvals.data(), S, M)) {
+        std::cout << "FATAL  : cannot write " << out << std::endl;
+        return EXIT_FAILURE;
+    }
+    return 0;
+}
+
 int main(int argc, char** argv) {
     vopt::Options opt;
     std::string echo;
@@ -68,9 +117,9 @@ int main(int argc, char** argv) {
     std::printf("INFO   : rank %4d has %lld markers over tot Mt = %u, max Mm = %lld, starting at S = %lld\n", rank,
                 (long long)M, opt.Mt, (long long)Mm, (long long)S);
 
-    if (opt.run_mode != "infere") {
-        std::cout << "FATAL  : run mode \"" << opt.run_mode << "\" is not provided by this build (infere only)"
-                  << std::endl;
+    if (opt.run_mode != "infere" && opt.run_mode != "association_test") {
+        std::cout << "FATAL  : run mode \"" << opt.run_mode
+                  << "\" is not provided by this build (infere, association_test)" << std::endl;
         return EXIT_FAILURE;
     }
     if (opt.model != "linear" && opt.model != "bin_class") {  // src/vamp.cpp:98-104
@@ -106,6 +155,13 @@ int main(int argc, char** argv) {
         std::cout << "reading methylation data took "
                   << std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() << " seconds."
                   << std::endl;
+
+    if (opt.run_mode == "association_test") {
+        const int rc = association_test(ctx, opt, rank, M, S);
+        vampomi_barrier(ctx);
+        vampomi_close(ctx);
+        return rc;
+    }
 
     std::vector<double> ts, init;
     if (!opt.true_signal_file.empty()) {  // src/main_meth.cpp:69-73

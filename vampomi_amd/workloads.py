@@ -11,6 +11,9 @@ c4: probit model (configs[3], --model bin_class): N=50,000 with 50,000
     N=50,000 x Mt=200,000.
 c4full: configs[3] whole (N=50,000 x Mt=200,000, 80 GB) on any number of
     GPUs (strong scaling; it fits one MI355X).
+c5: LOO association test (configs[4], --run-mode association_test
+    --pval-method loo): N=100,000 with 62,500 methylation-like markers per
+    GPU; n=8 is exactly N=100,000 x Mt=500,000.
 """
 from __future__ import annotations
 
@@ -24,6 +27,8 @@ def workload(cfg: str, n: int) -> dict:
         return {"workload": "c3-shard", "N": 100000, "Mt": 62500 * n, "kind": GEN_METH, "model": "linear"}
     if cfg == "c4":
         return {"workload": "c4-shard", "N": 50000, "Mt": 50000 * n, "kind": GEN_GAUSS, "model": "bin_class"}
+    if cfg == "c5":
+        return {"workload": "c5-shard", "N": 100000, "Mt": 62500 * n, "kind": GEN_METH, "model": "loo"}
     if cfg == "c4full":
         return {"workload": "c4", "N": 50000, "Mt": 200000, "kind": GEN_GAUSS, "model": "bin_class"}
     if n == 1:
