@@ -239,7 +239,8 @@ vampomi_status vampomi_get_stats(vampomi_ctx* ctx, vampomi_stats* out);
 vampomi_status vampomi_reset_stats(vampomi_ctx* ctx);
 
 /* ---- development hooks (kernel tuning; not part of the reference interface) ----
- * which: 0 = A.x partial-sum kernel, 1 = A^T.u kernel.  Variants index the
+ * which: 0 = A.x partial-sum kernel, 1 = A^T.u kernel, 2 = association-test pass
+ * (K = 1).  Variants index the
  * tuning tables in vampomi_amd/csrc/kernels.hip; variant 0 is the default. */
 vampomi_status vampomi_dev_set_variant(vampomi_ctx* ctx, int which, int variant);
 /* average device time (HIP events) of `reps` back-to-back launches, K RHS */

@@ -73,3 +73,13 @@ def test_phen_reader_na(harness, tmp_path):
     p = tmp_path / "na.phen"
     p.write_text("0 0 1\n1 1 NA\n")
     assert run(harness, "phen", p, 1).strip() == "ERR -2"
+
+
+def test_fma_corrected_division_is_the_ieee_quotient(tmp_path):
+    """loo_kernel divides X by sqrt(N) with a reciprocal and one fma correction
+    (Markstein); it must be bit-identical to IEEE division for every N."""
+    exe = tmp_path / "fastdiv"
+    subprocess.run(["gcc", "-O2", "-ffp-contract=off", os.path.join(ROOT, "tests", "fastdiv_check.c"),
+                    "-o", str(exe), "-lm"], check=True)
+    bad, tot = map(int, run(str(exe), 400000).split())
+    assert tot > 5_000_000 and bad == 0

@@ -1,6 +1,6 @@
 """Kernel tuning sweep for the A.x / A^T.u passes (run on the GPU box).
 
-    python tools/kbench.py [N] [Mt] [reps]
+    python tools/kbench.py [N] [Mt] [reps] [which: ax,atx,loo]
 
 Prints, per variant and batch width K, the average launch time and the
 algorithmic HBM rate 8*N*M + 8*K*N + 8*(2+K)*M bytes per launch.
@@ -25,9 +25,12 @@ d = va.Data(N, Mt)
 d.generate(1, va.GEN_GAUSS)
 rng = np.random.default_rng(0)
 x, u = rng.normal(size=Mt), rng.normal(size=N)
-res = {"N": N, "Mt": Mt, "reps": reps, "ax": {}, "atx": {}}
+only = sys.argv[4].split(",") if len(sys.argv) > 4 else ["ax", "atx", "loo"]
+res = {"N": N, "Mt": Mt, "reps": reps, "ax": {}, "atx": {}, "loo": {}}
 ref_ax, ref_atx = None, None
 for which, name, Ks, nvar in ((0, "ax", (1, 2, 3), 9), (1, "atx", (1, 2), 8)):
+    if name not in only:
+        continue
     for v in range(nvar):
         _lib.check(lib.vampomi_dev_set_variant(d.ctx, which, v))
         # correctness against variant 0 (chunking may differ: 1e-13)
@@ -49,4 +52,21 @@ for which, name, Ks, nvar in ((0, "ax", (1, 2, 3), 9), (1, "atx", (1, 2), 8)):
         res[name][v] = row
         print(name, v, json.dumps(row), flush=True)
     _lib.check(lib.vampomi_dev_set_variant(d.ctx, which, 0))
+if "loo" in only:
+    d.set_phen(rng.normal(size=N), standardize=False)
+    est = rng.normal(size=Mt) * 1e-3
+    ref = None
+    for v in range(8):
+        _lib.check(lib.vampomi_dev_set_variant(d.ctx, 2, v))
+        p, st = d.assoc_loo(est)
+        ref = st if ref is None else ref
+        ms = C.c_double()
+        _lib.check(lib.vampomi_dev_time_pass(d.ctx, 2, 1, 2, C.byref(ms)))
+        _lib.check(lib.vampomi_dev_time_pass(d.ctx, 2, 1, reps, C.byref(ms)))
+        b = 8.0 * N * Mt + 8.0 * N + 48.0 * Mt
+        row = {"kernel": va.kernel_name(2, 1, 0), "bitwise_eq_v0": bool(np.array_equal(st, ref)),
+               "us": round(ms.value * 1e3, 1), "GBs": round(b / (ms.value * 1e-3) / 1e9, 1)}
+        res["loo"][v] = row
+        print("loo", v, json.dumps(row), flush=True)
+    _lib.check(lib.vampomi_dev_set_variant(d.ctx, 2, 0))
 print(json.dumps(res))

@@ -23,7 +23,7 @@ for counter in ("FETCH_SIZE", "WRITE_SIZE"):
                 continue
             acc[r["Kernel_Name"]].append(float(r["Counter_Value"]))
     for k, v in acc.items():
-        if "ax_partial" in k or "atx_kernel" in k:
+        if "ax_partial" in k or "atx_kernel" in k or "loo_kernel" in k:
             d = out.setdefault(k, {})
             d[counter + "_KB_avg"] = sum(v) / len(v)
             d["dispatches"] = len(v)

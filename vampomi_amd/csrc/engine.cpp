@@ -800,14 +800,17 @@ extern "C" vampomi_status vampomi_dev_set_variant(vampomi_ctx* c, int which, int
             STCHK(dev_alloc(&c->ax_part, (size_t)np.nchunks * vk::kMaxRhs * c->ld));
         }
         c->axp = np;
-    } else {
+    } else if (which == 1) {
         if (!vk::set_atx_variant(variant)) return fail(VAMPOMI_ERR_ARG, "no such A^T.u variant");
+    } else {
+        if (!vk::set_loo_variant(variant)) return fail(VAMPOMI_ERR_ARG, "no such association-pass variant");
     }
     return VAMPOMI_OK;
 }
 
 extern "C" vampomi_status vampomi_dev_time_pass(vampomi_ctx* c, int which, int K, int reps, double* avg_ms) {
-    if (!c || !avg_ms || K < 1 || K > (which == 0 ? 4 : 3) || reps < 1) return fail(VAMPOMI_ERR_ARG, "bad argument");
+    if (!c || !avg_ms || K < 1 || K > (which == 0 ? 4 : which == 1 ? 3 : 1) || reps < 1)
+        return fail(VAMPOMI_ERR_ARG, "bad argument");
     if (!c->have_X) return fail(VAMPOMI_ERR_STATE, "no methylation data loaded");
     HIPCHK(hipSetDevice(c->device));
     const int64_t Mx = std::max<int64_t>(c->M, 1);
@@ -824,8 +827,10 @@ extern "C" vampomi_status vampomi_dev_time_pass(vampomi_ctx* c, int which, int K
     for (int r = 0; r < reps; ++r) {
         if (which == 0)
             HIPCHK(vk::ax_partial(c->shard(), c->axp, K, in, c->ax_part, c->st));
-        else
+        else if (which == 1)
             HIPCHK(vk::atx(c->shard(), K, in, out, 1.0 / c->sqrtN, 0, 0.0, 0.0, vk::CPtrs{}, c->red_part, c->st));
+        else  // association pass: ymod = nbuf slot 0, x1 = mbuf slot 0, sums in mbuf slots 3..7
+            HIPCHK(vk::loo_sums(c->shard(), c->nbuf, c->mbuf, c->sqrtN, c->mbuf + 3 * Mx, c->st));
     }
     HIPCHK(hipEventRecord(b, c->st));
     HIPCHK(hipEventSynchronize(b));

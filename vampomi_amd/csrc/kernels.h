@@ -136,6 +136,8 @@ hipError_t probit_p1(uint64_t seed, int64_t N, double* p1, hipStream_t st);
 hipError_t loo_sums(const Shard& s, const double* ymod, const double* x1, double sqrtN, double* stats,
                     hipStream_t st);
 std::string loo_kernel_name();
+int loo_variant_count();
+bool set_loo_variant(int v);  // development hook (tools/kbench.py)
 // pvals[j] = linear_reg1d_pvals(stats[5j..5j+4], n)  (src/utilities.cpp:269-282)
 hipError_t loo_pvals(int64_t M, const double* stats, int n, double* pvals, hipStream_t st);
 // pvals[j] = P(N(r1_j, 1/(gam1 N)) <= 0), flipped for r1_j <= 0 (src/main_meth.cpp:231-236)

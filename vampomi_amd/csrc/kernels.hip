@@ -1077,15 +1077,26 @@ hipError_t probit_p1(uint64_t seed, int64_t N, double* p1, hipStream_t st) {
 // One pass over the RAW shard: a wave owns G markers, lanes stride the
 // samples (16-B nontemporal loads, 1 KiB per wave per load), every ymod
 // value serves G markers.  Per element exactly the reference's
-// ym = ymod + (X / sqrt(N)) * x1_j (division kept: bitwise per element), then
-// the five sums of linear_reg1d_pvals.  Pad rows are zero in X and ymod and
-// add exact zeros.
-template <int G, int UJ>
+// ym = ymod + (X / sqrt(N)) * x1_j, then the five sums of linear_reg1d_pvals.
+// Pad rows are zero in X and ymod and add exact zeros.
+//
+// X / sqrt(N) is the correctly rounded quotient either way: FASTDIV computes
+// q0 = X*r (r = RN(1/sqrt(N))), the exact residual e = fma(-q0, sqrt(N), X)
+// and q = fma(e, r, q0), which is RN(X/sqrt(N)) whenever r is the rounded
+// reciprocal and q0 is within one ulp (Markstein's theorem; checked
+// bit for bit against IEEE division in tests/test_hostio.py and on the
+// device in tests/test_gpu_assoc.py) — 3 instructions instead of the ~10 of
+// the IEEE division sequence, which made the pass ALU-bound.  Only the sign
+// of a zero quotient can differ, which no sum can see.  Every lane adds its
+// samples in increasing order whatever G / UJ are, so all variants give
+// bitwise identical sums.
+template <int G, int UJ, bool FASTDIV>
 __global__ __launch_bounds__(kBlock) void loo_kernel(const double* __restrict__ X, int64_t ld, int64_t N, int64_t M,
                                                      const double* __restrict__ ymod, const double* __restrict__ x1,
                                                      double sqrtN, double* __restrict__ stats) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t m0 = ((int64_t)blockIdx.x * 4 + wave) * G;
+    const double rinv = 1.0 / sqrtN;
     double acc[G][5];
     double xj[G];
     const double* col[G];
@@ -1098,7 +1109,14 @@ __global__ __launch_bounds__(kBlock) void loo_kernel(const double* __restrict__ 
         for (int q = 0; q < 5; ++q) acc[g][q] = 0.0;
     }
     auto add = [&](int g, double m, double y) {
-        const double ym = y + m / sqrtN * xj[g];
+        double q;
+        if (FASTDIV) {
+            const double q0 = m * rinv;
+            q = __builtin_fma(__builtin_fma(-q0, sqrtN, m), rinv, q0);
+        } else {
+            q = m / sqrtN;
+        }
+        const double ym = y + q * xj[g];
         acc[g][0] += m;
         acc[g][1] += m * m;
         acc[g][2] += m * ym;
@@ -1142,19 +1160,50 @@ __global__ __launch_bounds__(kBlock) void loo_kernel(const double* __restrict__ 
         }
 }
 
-static constexpr int kLooG = 4, kLooUJ = 2;
+struct LooVariant { int G, UJ; bool FD; };
+static constexpr LooVariant kLooVariants[] = {
+    {4, 2, true}, {4, 2, false}, {2, 2, true}, {8, 1, true}, {4, 1, true}, {4, 4, true}, {2, 4, true}, {8, 2, true},
+};
+static constexpr int kNumLooVariants = sizeof(kLooVariants) / sizeof(kLooVariants[0]);
+// default: G=2, UJ=2, fma-corrected division: 6.80 TB/s at the c5 shard (N=100,000 x 62,500) on
+// MI355X vs 5.63 TB/s with the IEEE division sequence (tools/kbench.py, profiles/r01_kbench_loo.json)
+static int g_loo_variant = 2;
+
+int loo_variant_count() { return kNumLooVariants; }
+bool set_loo_variant(int v) {
+    if (v < 0 || v >= kNumLooVariants) return false;
+    g_loo_variant = v;
+    return true;
+}
 
 std::string loo_kernel_name() {
+    const LooVariant& v = kLooVariants[g_loo_variant];
     char b[64];
-    std::snprintf(b, sizeof b, "loo_kernel<%d, %d>", kLooG, kLooUJ);
+    std::snprintf(b, sizeof b, "loo_kernel<%d, %d, %s>", v.G, v.UJ, v.FD ? "true" : "false");
     return b;
+}
+
+template <int G, int UJ, bool FD>
+static void launch_loo(const Shard& s, const double* ymod, const double* x1, double sqrtN, double* stats,
+                       hipStream_t st) {
+    hipLaunchKernelGGL((loo_kernel<G, UJ, FD>), dim3((unsigned)cdiv(s.M, 4 * G)), dim3(kBlock), 0, st, s.X, s.ld,
+                       s.N, s.M, ymod, x1, sqrtN, stats);
 }
 
 hipError_t loo_sums(const Shard& s, const double* ymod, const double* x1, double sqrtN, double* stats,
                     hipStream_t st) {
     if (s.M <= 0) return hipSuccess;
-    hipLaunchKernelGGL((loo_kernel<kLooG, kLooUJ>), dim3((unsigned)cdiv(s.M, 4 * kLooG)), dim3(kBlock), 0, st, s.X,
-                       s.ld, s.N, s.M, ymod, x1, sqrtN, stats);
+    switch (g_loo_variant) {
+        case 0: launch_loo<4, 2, true>(s, ymod, x1, sqrtN, stats, st); break;
+        case 1: launch_loo<4, 2, false>(s, ymod, x1, sqrtN, stats, st); break;
+        case 2: launch_loo<2, 2, true>(s, ymod, x1, sqrtN, stats, st); break;
+        case 3: launch_loo<8, 1, true>(s, ymod, x1, sqrtN, stats, st); break;
+        case 4: launch_loo<4, 1, true>(s, ymod, x1, sqrtN, stats, st); break;
+        case 5: launch_loo<4, 4, true>(s, ymod, x1, sqrtN, stats, st); break;
+        case 6: launch_loo<2, 4, true>(s, ymod, x1, sqrtN, stats, st); break;
+        case 7: launch_loo<8, 2, true>(s, ymod, x1, sqrtN, stats, st); break;
+        default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 
