@@ -26,6 +26,7 @@
  *        src/vamp_probit.cpp:19-488                     -> vampomi_infere   (COLLECTIVE)
  *        (or vampomi_vamp_begin / _step / _end, one VAMP iteration per step)
  *   divide_work                src/utilities.cpp:207-239 -> vampomi_divide_work
+ *   run mode test              src/main_meth.cpp:112-205 -> vampomi_test_metrics (COLLECTIVE)
  *   association_test loo / se  src/main_meth.cpp:206-264, src/data.cpp:385-417,
  *                              src/utilities.cpp:269-282 -> vampomi_assoc_loo / _se
  *
@@ -214,6 +215,13 @@ vampomi_status vampomi_vamp_end(vampomi_ctx* ctx);
 vampomi_status vampomi_assoc_loo(vampomi_ctx* ctx, const double* est, double* pvals, double* stats,
                                  int mem);
 vampomi_status vampomi_assoc_se(vampomi_ctx* ctx, const double* r1, double gam1, double* pvals, int mem);
+
+/* ---- --run-mode test (src/main_meth.cpp:112-205) ----
+ * On a context holding the TEST data set (N = N_test, its own marker
+ * statistics, phenotype read like the training one): x = est*sqrt(N_test),
+ * z = A x (COLLECTIVE); *r2 = 1 - |y - z|^2 / (calc_stdev(y)^2 * N_test),
+ * *corr2 = (<z,y> / sqrt(|z|^2 |y|^2))^2 — one row of _test.csv. */
+vampomi_status vampomi_test_metrics(vampomi_ctx* ctx, const double* est, double* r2, double* corr2, int mem);
 
 /* ---- measurement ---- */
 typedef struct {

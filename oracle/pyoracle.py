@@ -97,6 +97,7 @@ def load() -> C.CDLL:
         lib.orc_reg1d_pval.argtypes = [d, d, d, d, d, C.c_int]
         lib.orc_assoc_loo.argtypes = [C.POINTER(Problem), p, p, p]
         lib.orc_assoc_se.argtypes = [p, i64, d, i64, p]
+        lib.orc_test_metrics.argtypes = [C.POINTER(Problem), p, p]
         _lib = lib
     return _lib
 
@@ -203,6 +204,24 @@ def assoc_loo(X: np.ndarray, y: np.ndarray, est: np.ndarray, Mt: Optional[int] =
     st = np.zeros((max(M, 1), 5))
     lib.orc_assoc_loo(C.byref(pb), _p(est), _p(pv), _p(st))
     return pv[:M], st[:M]
+
+
+def test_metrics(X: np.ndarray, y: np.ndarray, est: np.ndarray, alpha_scale: float = 1.0):
+    """--run-mode test row for one estimate (one shard, X (M, N_test)): (R2 test, corr^2)."""
+    lib = load()
+    X = np.ascontiguousarray(X, dtype=np.float64)
+    M, N = X.shape
+    y = np.ascontiguousarray(y, dtype=np.float64)
+    est = np.ascontiguousarray(est, dtype=np.float64)
+    mave, msig = marker_stats(X, alpha_scale)
+    pb = Problem(N=N, Mt=M, M=M, S=0, ld=N, rank=0, nranks=1, X=_p(X), mave=_p(mave), msig=_p(msig), y=_p(y),
+                 true_signal=None, x1hat_init=None, allreduce=ALLREDUCE_FN(), user=None)
+    out = np.zeros(2)
+    lib.orc_test_metrics(C.byref(pb), _p(est), _p(out))
+    return float(out[0]), float(out[1])
+
+
+test_metrics.__test__ = False  # not a pytest test
 
 
 def assoc_se(r1: np.ndarray, gam1: float, N: int) -> np.ndarray:

@@ -1288,3 +1288,35 @@ void orc_assoc_se(const double* r1, int64_t M, double gam1, int64_t N, double* p
         pvals[j] = p;
     }
 }
+
+/* ------------------------------------------------------------------------- */
+/* --run-mode test — src/main_meth.cpp:112-205, calc_stdev                   */
+/* src/utilities.cpp:183-205                                                  */
+/* ------------------------------------------------------------------------- */
+/* one estimate file's row of _test.csv: est = this shard's slice as stored
+ * (x1_hat/sqrt(N)); pb describes the TEST data set (N = N_test).
+ * out[0] = R2 test, out[1] = squared correlation of A.x with y. */
+void orc_test_metrics(const orc_problem* pb, const double* est, double* out) {
+    const int64_t N = pb->N, M = pb->M;
+    double* x = (double*)malloc(sizeof(double) * (size_t)(M > 0 ? M : 1));
+    double* z = (double*)malloc(sizeof(double) * (size_t)N);
+    double* d = (double*)malloc(sizeof(double) * (size_t)N);
+    for (int64_t i = 0; i < M; ++i) x[i] = est[i] * sqrt((double)N); /* :172-174 */
+    orc_ax(pb->X, N, pb->ld, M, pb->mave, pb->msig, x, z, pb->allreduce, pb->user); /* :177 */
+    const double* y = pb->y;
+    for (int64_t i = 0; i < N; ++i) d[i] = y[i] - z[i];
+    const double l2 = orc_dot(d, d, N); /* :180-183 */
+    /* calc_stdev(y_test) (sync = 0) */
+    for (int64_t i = 0; i < N; ++i) d[i] = 1.0;
+    const double sum = orc_dot(y, d, N), sq_sum = orc_dot(y, y, N);
+    const double mean = sum / (double)N;
+    const double stdev = sqrt((sq_sum - (double)N * mean * mean) / (double)(N - 1));
+    out[0] = 1 - l2 / (stdev * stdev * (double)N); /* :187 */
+    /* inner_prod(., 1) multiplies each replicated sum by the rank count, which
+     * cancels in the ratio: computed unsynced */
+    const double corr = orc_dot(z, y, N) / sqrt(orc_dot(z, z, N) * orc_dot(y, y, N)); /* :190 */
+    out[1] = corr * corr;
+    free(x);
+    free(z);
+    free(d);
+}

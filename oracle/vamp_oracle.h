@@ -158,6 +158,11 @@ void orc_assoc_loo(const orc_problem* pb, const double* est, double* pvals, doub
 /* --pval-method se (src/main_meth.cpp:218-242) */
 void orc_assoc_se(const double* r1, int64_t M, double gam1, int64_t N, double* pvals);
 
+/* ---- --run-mode test (src/main_meth.cpp:112-205) ----
+ * pb = the TEST data set; est = estimate-file slice (x1_hat/sqrt(N));
+ * out[0] = R2 test, out[1] = z correlation test (squared) */
+void orc_test_metrics(const orc_problem* pb, const double* est, double* out);
+
 /* ---- output writers (src/utilities.cpp:241-249, 366-401) ---- */
 int orc_store_vec(const char* path, const double* v, int64_t S, int64_t M);
 int orc_csv_header(const char* path, const char* const* fields, int n);

@@ -35,7 +35,12 @@ def test_meth_file_required():
 
 def test_echo_and_unsupported_mode():
     r = cli("--meth-file", "m.bin", "--N", "10", "--Mt", "20", "--vars", "0,0.001", "--probs", "0.5,0.5",
-            "--run-mode", "test")
+            "--run-mode", "predict")
     assert "ardyh command line options:" in r.stdout and "--vars 0,0.001" in r.stdout
     assert "INFO   : rank    0 has 20 markers over tot Mt = 20" in r.stdout
-    assert r.returncode == 1 and 'run mode "test"' in r.stdout
+    assert r.returncode == 1 and 'run mode "predict"' in r.stdout
+
+
+def test_unknown_model_is_fatal():
+    r = cli("--meth-file", "m.bin", "--N", "10", "--Mt", "20", "--model", "poisson")
+    assert r.returncode == 1 and "Invalid model specification" in r.stdout

@@ -193,6 +193,18 @@ class Data:
                                     1 if onsager else 0, max_iter, tol, _dp(mu), C.byref(it), MEM_HOST))
         return mu[: self.M], it.value
 
+    def test_metrics(self, est: np.ndarray):
+        """--run-mode test row (src/main_meth.cpp:165-199) for one estimate slice
+        (x1_hat / sqrt(N)) on this (test) data set: (R2 test, squared z correlation)."""
+        est = np.ascontiguousarray(est, dtype=np.float64)
+        if est.shape != (self.M,):
+            raise ValueError("estimate slice must have M entries")
+        r2, c2 = C.c_double(), C.c_double()
+        check(self._lib.vampomi_test_metrics(self.ctx, _dp(est), C.byref(r2), C.byref(c2), MEM_HOST))
+        return r2.value, c2.value
+
+    test_metrics.__test__ = False
+
     def assoc_loo(self, est: np.ndarray, mem_device: bool = False):
         """--pval-method loo (src/main_meth.cpp:245-264, src/data.cpp:385-417).
         est: this shard's estimate-file slice (x1_hat / sqrt(N)).  COLLECTIVE.

@@ -117,6 +117,7 @@ SIGNATURES = {
     "vampomi_lmmse_mult": (C.c_int, [_P, _P, C.c_double, C.c_double, _P, C.c_int]),
     "vampomi_pcg": (C.c_int, [_P, _P, _P, C.c_double, C.c_double, C.c_int, C.c_int, C.c_double, _P,
                               C.POINTER(C.c_int), C.c_int]),
+    "vampomi_test_metrics": (C.c_int, [_P, _P, C.POINTER(C.c_double), C.POINTER(C.c_double), C.c_int]),
     "vampomi_assoc_loo": (C.c_int, [_P, _P, _P, _P, C.c_int]),
     "vampomi_assoc_se": (C.c_int, [_P, _P, C.c_double, _P, C.c_int]),
     "vampomi_denoise_bin": (C.c_int, [_P, _P, C.c_double, _P, C.POINTER(C.c_double), C.c_int]),

@@ -749,6 +749,32 @@ extern "C" vampomi_status vampomi_assoc_loo(vampomi_ctx* c, const double* est, d
     return VAMPOMI_OK;
 }
 
+// --run-mode test (src/main_meth.cpp:165-199): one estimate's R2 test and
+// squared correlation on the context's (test) data set.  COLLECTIVE (one A.x).
+extern "C" vampomi_status vampomi_test_metrics(vampomi_ctx* c, const double* est, double* r2, double* corr2,
+                                               int mem) {
+    if (!c || (!est && c->M > 0)) return fail(VAMPOMI_ERR_ARG, "null argument");
+    if (!c->have_X || !c->have_y) return fail(VAMPOMI_ERR_STATE, "load methylation data and phenotype first");
+    HIPCHK(hipSetDevice(c->device));
+    const int64_t M = c->M, N = c->N, Mx = std::max<int64_t>(M, 1);
+    STCHK(stage_in(c, est, M, mem, c->mbuf));
+    HIPCHK(vk::mul_scalar(M, c->mbuf, std::sqrt((double)N), c->mbuf + Mx, c->st));  // :172-174
+    const double* xs[1] = {c->mbuf + Mx};
+    double* z = c->nbuf;
+    STCHK(ax_dev(c, 1, xs, z));  // :177
+    double s[5] = {};
+    DotBatch b(c);  // the N-side is replicated: local sums (inner_prod(., 1)'s rank factor cancels)
+    STCHK(b.add({T(c->y, z, vk::DIFF2), T(c->y, nullptr, vk::SUM), T(c->y, c->y), T(z, c->y), T(z, z)}, N, false, s));
+    STCHK(b.flush());
+    const double mean = s[1] / (double)N;                                                  // calc_stdev
+    const double stdev = std::sqrt((s[2] - (double)N * mean * mean) / (double)(N - 1));  // utilities.cpp:202
+    if (r2) *r2 = 1 - s[0] / (stdev * stdev * (double)N);                                  // :187
+    const double corr = s[3] / std::sqrt(s[4] * s[2]);                                     // :190
+    if (corr2) *corr2 = corr * corr;
+    if (c->timing) resolve_timing(c);
+    return VAMPOMI_OK;
+}
+
 // --pval-method se (src/main_meth.cpp:218-242): rank-local
 extern "C" vampomi_status vampomi_assoc_se(vampomi_ctx* c, const double* r1, double gam1, double* pvals, int mem) {
     if (!c || (!r1 && c->M > 0) || (!pvals && c->M > 0)) return fail(VAMPOMI_ERR_ARG, "null argument");

@@ -99,6 +99,19 @@ bool csv_create_with_header(const std::string& path, const std::vector<std::stri
     return w == (ssize_t)s.size();
 }
 
+bool read_text_vec(const std::string& path, double* v, int64_t S, int64_t M) {
+    std::ifstream f(path);
+    if (!f) return false;
+    double value;
+    int64_t it = 0;
+    while (f >> value) {
+        if (it >= S + M) break;
+        if (it >= S) v[it - S] = value;
+        ++it;
+    }
+    return true;
+}
+
 bool csv_create(const std::string& path) {
     ::unlink(path.c_str());
     int fd = ::open(path.c_str(), O_CREAT | O_WRONLY | O_EXCL, 0666);

@@ -20,6 +20,10 @@ bool store_vec(const std::string& path, const double* v, int64_t S, int64_t M);
 // missing bytes (short file) read as 0.
 bool read_vec(const std::string& path, double* v, int64_t S, int64_t M);
 
+// read_vec_from_file (src/utilities.cpp:104-122): whitespace-separated text,
+// values with index [S, S+M); missing ones stay as they are (callers zero).
+bool read_text_vec(const std::string& path, double* v, int64_t S, int64_t M);
+
 // setup_io + write_ofile_csv_header (src/vamp.cpp:854-882,
 // src/utilities.cpp:388-401): delete, create exclusively, header at offset 0.
 bool csv_create_with_header(const std::string& path, const std::vector<std::string>& fields);

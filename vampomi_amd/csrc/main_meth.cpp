@@ -1,6 +1,6 @@
 // main_meth.cpp — drop-in for the reference's main_meth.exe (src/main_meth.cpp)
-// in --run-mode infere (--model linear | bin_class) and association_test
-// (--pval-method loo | se): same flags, same output files.
+// in --run-mode infere (--model linear | bin_class), test and
+// association_test (--pval-method loo | se): same flags, same output files.
 //
 // Ranks: the reference is launched with `mpirun -np P`; this binary runs one
 // process per GPU, rank/size from VAMPOMI_RANK/VAMPOMI_NRANKS (or the
@@ -104,6 +104,49 @@ static int association_test(vampomi_ctx* ctx, const vopt::Options& opt, int rank
     return 0;
 }
 
+// --run-mode test (src/main_meth.cpp:112-205): R2 and squared correlation of
+// A.x_est on the test set for the estimate files of iterations
+// --test-iter-range, one _test.csv row each.
+static int test_run(vampomi_ctx* ctx, const vopt::Options& opt, int rank, int64_t M, int64_t S) {
+    const std::string csv = opt.out_dir + "/" + opt.out_name + "_test.csv";
+    if (rank == 0 && !vio::csv_create_with_header(csv, {"iteration", "R2 test", "z correlation test"})) {
+        std::cout << "FATAL  : cannot create " << csv << std::endl;
+        return EXIT_FAILURE;
+    }
+    // file names: <prefix>it_<it>.<ext>, prefix up to the last "it", ext after
+    // the FIRST '.' of the given name (:152-168)
+    const std::string& est = opt.estimate_file;
+    const size_t pos_dot = est.find('.');
+    const std::string ext = pos_dot == std::string::npos ? std::string() : est.substr(pos_dot + 1);
+    const size_t pos_it = est.rfind("it");
+    if (rank == 0) std::cout << "est_file_name = " << est << std::endl;
+    const int min_it = opt.test_iter_range.size() > 0 ? opt.test_iter_range[0] : 1;
+    const int max_it = opt.test_iter_range.size() > 1 ? opt.test_iter_range[1] : min_it;
+    if (rank == 0) std::cout << "iter range = [" << min_it << ", " << max_it << "]" << std::endl;
+    std::vector<double> x((size_t)std::max<int64_t>(M, 1));
+    for (int it = min_it; it <= max_it; ++it) {
+        const std::string name = est.substr(0, pos_it) + "it_" + std::to_string(it) + "." + ext;
+        std::fill(x.begin(), x.end(), 0.0);
+        const bool ok = ext == "bin" ? vio::read_vec(name, x.data(), S, M) : vio::read_text_vec(name, x.data(), S, M);
+        if (!ok) {
+            std::cout << "FATAL  : cannot read estimate file " << name << std::endl;
+            return EXIT_FAILURE;
+        }
+        double row[2];
+        if (vampomi_test_metrics(ctx, x.data(), &row[0], &row[1], VAMPOMI_MEM_HOST) != VAMPOMI_OK)
+            return die("test metrics");
+        if (rank == 0) {
+            std::cout << row[0] << ", ";
+            if (!vio::csv_write_row(csv, it, row, 2)) {
+                std::cout << "FATAL  : cannot write " << csv << std::endl;
+                return EXIT_FAILURE;
+            }
+        }
+    }
+    if (rank == 0) std::cout << std::endl;
+    return 0;
+}
+
 int main(int argc, char** argv) {
     vopt::Options opt;
     std::string echo;
@@ -117,9 +160,9 @@ int main(int argc, char** argv) {
     std::printf("INFO   : rank %4d has %lld markers over tot Mt = %u, max Mm = %lld, starting at S = %lld\n", rank,
                 (long long)M, opt.Mt, (long long)Mm, (long long)S);
 
-    if (opt.run_mode != "infere" && opt.run_mode != "association_test") {
+    if (opt.run_mode != "infere" && opt.run_mode != "association_test" && opt.run_mode != "test") {
         std::cout << "FATAL  : run mode \"" << opt.run_mode
-                  << "\" is not provided by this build (infere, association_test)" << std::endl;
+                  << "\" is not provided by this build (infere, test, association_test)" << std::endl;
         return EXIT_FAILURE;
     }
     if (opt.model != "linear" && opt.model != "bin_class") {  // src/vamp.cpp:98-104
@@ -133,8 +176,9 @@ int main(int argc, char** argv) {
         const std::string path = rz ? rz : opt.out_dir + "/." + opt.out_name + ".rdzv";
         if (!exchange_id(path, rank, id)) return die("communicator rendezvous failed");
     }
+    const bool test_mode = opt.run_mode == "test";  // the context holds the TEST data set (:128)
     vampomi_shard_desc d{};
-    d.N = opt.N;
+    d.N = test_mode ? opt.N_test : opt.N;
     d.Mt = opt.Mt;
     d.rank = rank;
     d.nranks = nranks;
@@ -148,16 +192,18 @@ int main(int argc, char** argv) {
     // for bin_class, src/data.cpp:40-43), then the shard
     auto t0 = std::chrono::steady_clock::now();
     const int standardize = opt.model == "bin_class" ? 0 : 1;
-    if (vampomi_read_phen(ctx, opt.phen_file.c_str(), standardize) != VAMPOMI_OK) return die("phenotype");
-    if (rank == 0) std::cout << "meth file name = " << opt.meth_file << std::endl;
-    if (vampomi_load_meth_file(ctx, opt.meth_file.c_str()) != VAMPOMI_OK) return die("methylation data");
+    const std::string& phen = test_mode ? opt.phen_file_test : opt.phen_file;
+    const std::string& meth = test_mode ? opt.meth_file_test : opt.meth_file;
+    if (vampomi_read_phen(ctx, phen.c_str(), standardize) != VAMPOMI_OK) return die("phenotype");
+    if (rank == 0) std::cout << "meth file name = " << meth << std::endl;
+    if (vampomi_load_meth_file(ctx, meth.c_str()) != VAMPOMI_OK) return die("methylation data");
     if (rank == 0)
         std::cout << "reading methylation data took "
                   << std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() << " seconds."
                   << std::endl;
 
-    if (opt.run_mode == "association_test") {
-        const int rc = association_test(ctx, opt, rank, M, S);
+    if (opt.run_mode == "association_test" || test_mode) {
+        const int rc = test_mode ? test_run(ctx, opt, rank, M, S) : association_test(ctx, opt, rank, M, S);
         vampomi_barrier(ctx);
         vampomi_close(ctx);
         return rc;
