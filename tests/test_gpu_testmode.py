@@ -34,8 +34,7 @@ def test_test_metrics_parity(N, Mt, kind):
 def test_cli_test_mode(tmp_path):
     N, Mt, Nt, its = 500, 800, 300, 4
     X, y, beta = make_problem(N, Mt, seed=3)
-    Xt, yt, _ = make_problem(Nt, Mt, seed=3)  # same markers' effects, fresh samples would need a new
-    Xt = O.generate_markers(77, 0, Nt, 0, Mt)  # generator stream: a held-out design
+    Xt = O.generate_markers(77, 0, Nt, 0, Mt)  # held-out samples: another generator stream, same effects
     mave, msig = O.marker_stats(Xt)
     yt = O.standardize_phen(O.ax(Xt, mave, msig, beta * np.sqrt(Nt)) + 0.3 * np.sin(np.arange(Nt)))
     for name, A, v in (("train", X, y), ("test", Xt, yt)):
