@@ -11,6 +11,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cfloat>
 #include <cmath>
 #include <cstdio>
@@ -18,6 +19,7 @@
 #include <cstring>
 #include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include <fcntl.h>
@@ -390,8 +392,39 @@ extern "C" vampomi_status vampomi_load_meth_host(vampomi_ctx* c, const double* X
     return finish_X(c);
 }
 
+// [off, off + want) of fd into dst, split over nt reader threads (page cache
+// and NVMe both need several requests in flight to stream at full rate)
+static bool pread_parallel(int fd, char* dst, size_t want, off_t off, int nt) {
+    if (nt <= 1 || want < ((size_t)8 << 20)) nt = 1;
+    const size_t per = ((want + nt - 1) / nt + 4095) & ~(size_t)4095;
+    std::atomic<bool> ok{true};
+    auto work = [&](size_t lo, size_t hi) {
+        size_t got = 0;
+        while (lo + got < hi) {
+            const ssize_t r = ::pread(fd, dst + lo + got, hi - lo - got, off + (off_t)(lo + got));
+            if (r <= 0) {
+                ok = false;
+                return;
+            }
+            got += (size_t)r;
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t) {
+        const size_t lo = (size_t)t * per;
+        if (lo < want) th.emplace_back(work, lo, std::min(want, lo + per));
+    }
+    work(0, std::min(want, per));
+    for (auto& x : th) x.join();
+    return ok;
+}
+
 // read_methylation_data (src/data.cpp:116-153): this rank's M*N doubles at byte
-// offset S*N*8, streamed through a pinned staging buffer (64-bit offsets).
+// offset S*N*8 (64-bit offsets: the reference's int i*N overflows past 2^31
+// elements), streamed through three pinned 256 MB staging buffers: the
+// parallel read of chunk k+1 overlaps the host-to-device copy of chunk k,
+// which lands directly in the ld-padded column layout.  Marker statistics
+// follow on the device (finish_X).
 extern "C" vampomi_status vampomi_load_meth_file(vampomi_ctx* c, const char* path) {
     if (!c || !path) return fail(VAMPOMI_ERR_ARG, "null argument");
     HIPCHK(hipSetDevice(c->device));
@@ -399,11 +432,16 @@ extern "C" vampomi_status vampomi_load_meth_file(vampomi_ctx* c, const char* pat
     if (fd < 0) return fail(VAMPOMI_ERR_IO, std::string("cannot open methylation file ") + path);
     STCHK(ensure_X(c));
     const size_t colb = (size_t)c->N * 8;
-    const size_t chunk_cols = std::max<size_t>(1, ((size_t)64 << 20) / colb);
-    double* pin[2] = {nullptr, nullptr};
-    hipEvent_t done[2];
-    for (int b = 0; b < 2; ++b) {
+    const size_t chunk_cols = std::max<size_t>(1, ((size_t)256 << 20) / colb);
+    const char* env = std::getenv("VAMPOMI_IO_THREADS");
+    const int nt = env ? std::max(1, std::atoi(env)) : (int)std::min(8u, std::max(1u, std::thread::hardware_concurrency()));
+    constexpr int NB = 3;
+    double* pin[NB] = {};
+    hipEvent_t done[NB];
+    bool used[NB] = {};
+    for (int b = 0; b < NB; ++b) {
         if (hipHostMalloc((void**)&pin[b], chunk_cols * colb, hipHostMallocDefault) != hipSuccess) {
+            for (int k = 0; k < b; ++k) (void)hipHostFree(pin[k]);
             ::close(fd);
             return fail(VAMPOMI_ERR_OOM, "pinned staging buffer");
         }
@@ -412,19 +450,12 @@ extern "C" vampomi_status vampomi_load_meth_file(vampomi_ctx* c, const char* pat
     vampomi_status st = VAMPOMI_OK;
     int64_t i0 = 0;
     int b = 0;
-    bool used[2] = {false, false};
     while (i0 < c->M && st == VAMPOMI_OK) {
         const int64_t nc = std::min<int64_t>((int64_t)chunk_cols, c->M - i0);
         if (used[b]) (void)hipEventSynchronize(done[b]);
         const size_t want = (size_t)nc * colb;
         const off_t off = (off_t)(c->S + i0) * (off_t)colb;
-        size_t got = 0;
-        while (got < want) {
-            ssize_t r = ::pread(fd, (char*)pin[b] + got, want - got, off + (off_t)got);
-            if (r <= 0) break;
-            got += (size_t)r;
-        }
-        if (got != want) {
+        if (!pread_parallel(fd, (char*)pin[b], want, off, nt)) {
             st = fail(VAMPOMI_ERR_IO, std::string("short read from methylation file ") + path);
             break;
         }
@@ -436,10 +467,10 @@ extern "C" vampomi_status vampomi_load_meth_file(vampomi_ctx* c, const char* pat
         }
         used[b] = true;
         i0 += nc;
-        b ^= 1;
+        b = (b + 1) % NB;
     }
     (void)hipStreamSynchronize(c->st);
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < NB; ++k) {
         (void)hipHostFree(pin[k]);
         (void)hipEventDestroy(done[k]);
     }
