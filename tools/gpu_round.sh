@@ -31,4 +31,5 @@ step pmc_c4 500 bash tools/pmc.sh c4
 step bench_c5 400 python bench.py --config c5 --steps 10 --warmup 2
 step rocprof_c5 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_c5" -o run --output-format csv -- python bench.py --config c5 --steps 6 --warmup 2 --no-cpu-baseline
 step pmc_c5 500 bash tools/pmc.sh c5
+step ingest 600 python tools/ingest_bench.py 100000 25000
 echo "done"
