@@ -30,6 +30,11 @@
  *   association_test loo / se  src/main_meth.cpp:206-264, src/data.cpp:385-417,
  *                              src/utilities.cpp:269-282 -> vampomi_assoc_loo / _se
  *
+ * Testing aid: with VAMPOMI_COMM=loopback in the environment, the contexts
+ * of a multi-rank job are driven by threads of ONE process (any device, the
+ * same one allowed) and all-reduces become an in-process rendezvous that sums
+ * in rank order; comm_id is then any 128 bytes shared by the ranks.
+ *
  * Errors: every call returns a vampomi_status; nothing aborts the process
  * (the reference calls MPI_Abort / exit / throw).  vampomi_last_error() gives
  * a message for the calling thread.

@@ -1,0 +1,142 @@
+"""The multi-rank (marker-sharded) engine on the GPU: P ranks as threads of
+this process, each with its own context on device 0, joined by the
+test-only loopback communicator (VAMPOMI_COMM=loopback: an in-process
+rendezvous summing in rank order).  Every multi-rank code path of the engine
+runs — divide_work shards with S > 0, per-rank A.x partials + all-reduce +
+division, synced and local reductions, the EM / Onsager / noise-precision
+all-reduces, file offsets — except RCCL itself, which
+tests/test_gpu_parity.py::test_rccl_code_path_single_rank covers.  Results
+must match the single-rank GPU run (linear) or the oracle's bars (probit,
+association tests)."""
+import os
+import threading
+
+import numpy as np
+import pytest
+
+from conftest import relerr
+from _data import make_problem, oracle_with_spread
+
+pytestmark = pytest.mark.gpu
+
+va = pytest.importorskip("vampomi_amd")
+from oracle import pyoracle as O  # noqa: E402  (checker)
+
+
+def run_ranks(monkeypatch, P, N, Mt, fn, timeout=600):
+    """fn(rank, data) on P threads, one context each; returns the results by rank."""
+    monkeypatch.setenv("VAMPOMI_COMM", "loopback")
+    cid = os.urandom(va.UNIQUE_ID_BYTES)
+    res, errs = [None] * P, []
+
+    def work(r):
+        try:
+            with va.Data(N, Mt, rank=r, nranks=P, comm_id=cid, device=0) as d:
+                res[r] = fn(r, d)
+        except BaseException as e:  # noqa: BLE001 - reported below
+            errs.append((r, e))
+
+    th = [threading.Thread(target=work, args=(r,), daemon=True) for r in range(P)]
+    [t.start() for t in th]
+    [t.join(timeout) for t in th]
+    assert not any(t.is_alive() for t in th), "a rank is stuck in a collective"
+    assert not errs, errs
+    return res
+
+
+def _vamp(d, X, y, beta, model="linear", **kw):
+    d.load_meth(X[d.S:d.S + d.M])
+    d.set_phen(y, standardize=False)
+    v = va.Vamp(d, va.VampOptions(model=model, **kw), true_signal=beta[d.S:d.S + d.M])
+    x1 = v.infere(keep_hist=True)
+    s = v.summary()
+    n = s["iterations"]
+    s["x1_hist"], s["r1_hist"], s["x1_final"] = v.x1_hist[:n, :d.M].copy(), v.r1_hist[:n, :d.M].copy(), x1
+    s["S"], s["M"] = d.S, d.M
+    return s
+
+
+def _cat(parts, key):
+    return np.concatenate([p[key] for p in parts], axis=-1)
+
+
+@pytest.mark.parametrize("P", [2, 3])
+def test_sharded_operators(monkeypatch, P):
+    N, Mt = 1001, 2003
+    X, y, _ = make_problem(N, Mt)
+    mave, msig = O.marker_stats(X)
+    rng = np.random.default_rng(8)
+    x, u = rng.normal(size=Mt), rng.normal(size=N)
+
+    def fn(r, d):
+        d.load_meth(X[d.S:d.S + d.M])
+        return d.S, d.M, d.Ax(x[d.S:d.S + d.M]), d.ATx(u), d.get_mave(), d.get_msig()
+
+    res = run_ranks(monkeypatch, P, N, Mt, fn)
+    assert [r[0] for r in res] == [O.divide_work(Mt, P, k)[1] for k in range(P)]
+    for r in res:  # A.x is all-reduced: every rank holds the whole product
+        assert relerr(r[2], O.ax(X, mave, msig, x)) < 1e-13
+    assert relerr(np.concatenate([r[3] for r in res]), O.atx(X, mave, msig, u)) < 1e-13
+    assert relerr(np.concatenate([r[4] for r in res]), mave) < 1e-14
+    assert relerr(np.concatenate([r[5] for r in res]), msig) < 1e-14
+
+
+@pytest.mark.parametrize("P", [2, 3])
+def test_sharded_linear_vamp_matches_single_rank(monkeypatch, P):
+    N, Mt, its = 1000, 2000, 12
+    X, y, beta = make_problem(N, Mt)
+    kw = dict(max_iter=its, stop_criteria_thr=0.0)
+    with va.Data(N, Mt) as d:
+        one = _vamp(d, X, y, beta, **kw)
+    parts = run_ranks(monkeypatch, P, N, Mt, lambda r, d: _vamp(d, X, y, beta, **kw))
+    for p in parts:
+        assert p["cg_iters"] == one["cg_iters"] and p["ons_iters"] == one["ons_iters"] and p["L"] == one["L"]
+        assert np.allclose(p["params"], one["params"], rtol=1e-11)
+        assert np.allclose(p["metrics"], one["metrics"], rtol=1e-11, equal_nan=True)
+    for k in range(its):
+        assert relerr(_cat(parts, "x1_hist")[k], one["x1_hist"][k]) < 1e-12, k
+        assert relerr(_cat(parts, "r1_hist")[k], one["r1_hist"][k]) < 1e-12, k
+    ref = O.vamp_infere(X, y, Mt, true_signal=beta, **kw)
+    assert relerr(_cat(parts, "x1_final"), ref["x1_final"]) < 1e-10
+    assert parts[0]["cg_iters"] == ref["cg_iters"].tolist()
+
+
+def test_sharded_probit(monkeypatch):
+    N, Mt, its = 1000, 2000, 12
+    X, y, beta = make_problem(N, Mt)
+    yb = (y > 0).astype(np.float64)
+    kw = dict(max_iter=its, stop_criteria_thr=0.0, model="bin_class")
+    ref, spread = oracle_with_spread(X, yb, beta, Mt, **kw)
+    parts = run_ranks(monkeypatch, 2, N, Mt, lambda r, d: _vamp(d, X, yb, beta, **kw))
+    for p in parts:
+        assert p["cg_iters"] == ref["cg_iters"].tolist() and p["ons_iters"] == ref["ons_iters"].tolist()
+        m = np.array(p["metrics"])
+        for o in (0, 6):
+            assert np.array_equal(m[:, o:o + 4], ref["metrics"][:, o:o + 4])
+    for k in range(its):
+        assert relerr(_cat(parts, "x1_hist")[k], ref["x1_hist"][k]) <= max(1e-10, 10 * spread["x1"][k]), k
+
+
+def test_sharded_association_and_test_mode(monkeypatch):
+    N, Mt = 900, 1501
+    X, y, beta = make_problem(N, Mt, kind=1)
+    est = beta * 0.9
+
+    def fn(r, d):
+        d.load_meth(X[d.S:d.S + d.M])
+        d.set_phen(y, standardize=False)
+        p, st = d.assoc_loo(est[d.S:d.S + d.M])
+        return p, st, d.test_metrics(est[d.S:d.S + d.M]), d.assoc_se(est[d.S:d.S + d.M], 2.0)
+
+    res = run_ranks(monkeypatch, 3, N, Mt, fn)
+    po, sto = O.assoc_loo(X, y, est)
+    st = np.concatenate([r[1] for r in res])
+    p = np.concatenate([r[0] for r in res])
+    for q in range(5):
+        assert relerr(st[:, q], sto[:, q]) < 1e-13
+    pf = np.array([O.reg1d_pval(*s, N) for s in st])
+    assert np.all(np.abs(p - pf) <= 1e-12 * pf + 1e-300)
+    ro, co = O.test_metrics(X, y, est)
+    for r in res:
+        assert abs(r[2][0] - ro) <= 1e-12 * abs(ro) and abs(r[2][1] - co) <= 1e-12 * abs(co)
+    assert np.allclose(np.concatenate([r[3] for r in res]), O.assoc_se(est, 2.0, N), rtol=1e-14, atol=1e-16)

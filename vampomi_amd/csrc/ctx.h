@@ -37,6 +37,7 @@ vampomi_status fail(vampomi_status s, const std::string& msg);
 
 // ---- the context ------------------------------------------------------------
 struct VampRun;
+struct LoopbackComm;  // engine.cpp: test-only in-process communicator
 
 struct TimedLaunch {
     hipEvent_t a, b;
@@ -58,6 +59,7 @@ struct vampomi_ctx {
     hipStream_t st = nullptr;
     ncclComm_t comm = nullptr;
     bool use_comm = false;  // nranks > 1 (or VAMPOMI_FORCE_RCCL): all-reduces through RCCL
+    std::shared_ptr<LoopbackComm> loopback;  // VAMPOMI_COMM=loopback: ranks are threads of one process
 
     double* X = nullptr;     // M columns x ld, marker-major, pad rows zero
     double* mave = nullptr;

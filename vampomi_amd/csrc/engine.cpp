@@ -13,6 +13,9 @@
 #include <algorithm>
 #include <atomic>
 #include <cfloat>
+#include <condition_variable>
+#include <map>
+#include <mutex>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -102,8 +105,69 @@ vampomi_status host_sync(vampomi_ctx* c) {
     return VAMPOMI_OK;
 }
 
+// ---------------------------------------------------------------------------
+// test-only loopback communicator (VAMPOMI_COMM=loopback): the ranks of a job
+// are contexts driven by threads of ONE process, possibly on one GPU, and an
+// all-reduce is a host rendezvous that sums the ranks' buffers in rank order.
+// It exercises every multi-rank code path of the engine (divide_work shards,
+// per-rank partials, each all-reduce site, the post-reduce division) where
+// only one GPU is available; jobs across GPUs use RCCL.
+// ---------------------------------------------------------------------------
+struct LoopbackComm {
+    std::mutex mu;
+    std::condition_variable cv;
+    int P = 0, arrived = 0;
+    uint64_t gen = 0;
+    std::vector<std::vector<double>> in;
+    std::vector<double> out;
+};
+
+static std::mutex g_loopback_mu;
+static std::map<std::string, std::weak_ptr<LoopbackComm>> g_loopback;
+
+static std::shared_ptr<LoopbackComm> loopback_join(const void* id, int P) {
+    const std::string key((const char*)id, VAMPOMI_UNIQUE_ID_BYTES);
+    std::lock_guard<std::mutex> g(g_loopback_mu);
+    std::shared_ptr<LoopbackComm> lb = g_loopback[key].lock();
+    if (!lb) {
+        lb = std::make_shared<LoopbackComm>();
+        lb->P = P;
+        lb->in.resize((size_t)P);
+        g_loopback[key] = lb;
+    }
+    return lb;
+}
+
+static vampomi_status loopback_allreduce(vampomi_ctx* c, double* buf, size_t n) {
+    LoopbackComm& lb = *c->loopback;
+    std::vector<double> mine(n);
+    HIPCHK(hipMemcpyAsync(mine.data(), buf, n * 8, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    {
+        std::unique_lock<std::mutex> g(lb.mu);
+        const uint64_t my_gen = lb.gen;
+        lb.in[(size_t)c->rank] = std::move(mine);
+        if (++lb.arrived == lb.P) {
+            lb.out.assign(n, 0.0);
+            for (int r = 0; r < lb.P; ++r)
+                for (size_t i = 0; i < n; ++i) lb.out[i] += lb.in[(size_t)r][i];
+            lb.arrived = 0;
+            ++lb.gen;
+            lb.cv.notify_all();
+        } else {
+            lb.cv.wait(g, [&] { return lb.gen != my_gen; });
+        }
+        mine = lb.out;  // lb.out is only rewritten once every rank has arrived again
+    }
+    HIPCHK(hipMemcpyAsync(buf, mine.data(), n * 8, hipMemcpyHostToDevice, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    return VAMPOMI_OK;
+}
+
 vampomi_status allreduce_dev(vampomi_ctx* c, double* buf, size_t n) {
-    if (c->use_comm && n > 0) NCCLCHK(ncclAllReduce(buf, buf, n, ncclDouble, ncclSum, c->comm, c->st));
+    if (!c->use_comm || n == 0) return VAMPOMI_OK;
+    if (c->loopback) return loopback_allreduce(c, buf, n);
+    NCCLCHK(ncclAllReduce(buf, buf, n, ncclDouble, ncclSum, c->comm, c->st));
     return VAMPOMI_OK;
 }
 
@@ -329,7 +393,11 @@ extern "C" vampomi_status vampomi_open(const vampomi_shard_desc* d, vampomi_ctx*
     // be exercised on a single GPU
     const char* force = std::getenv("VAMPOMI_FORCE_RCCL");
     c->use_comm = c->nranks > 1 || (force && std::atoi(force) != 0);
-    if (c->use_comm) {
+    const char* mode = std::getenv("VAMPOMI_COMM");
+    if (c->use_comm && mode && std::strcmp(mode, "loopback") == 0) {
+        if (!d->comm_id) return fail(VAMPOMI_ERR_ARG, "the loopback communicator needs a communicator id");
+        c->loopback = loopback_join(d->comm_id, c->nranks);
+    } else if (c->use_comm) {
         ncclUniqueId id;
         if (d->comm_id)
             std::memcpy(&id, d->comm_id, sizeof id);
