@@ -73,7 +73,9 @@ struct vampomi_ctx {
     double* red_part = nullptr;  // per-block partials of every reduction
     size_t red_cap = 0;
     double* scal = nullptr;     // device scalars (SL_*)
-    double* h_scal = nullptr;   // pinned mirror
+    double* h_scal = nullptr;   // pinned host mirror, mapped and coherent: one-rank reductions land here directly
+    double* d_hscal = nullptr;  // its device-side address
+    unsigned* ticket = nullptr; // arrival counter of the fused reductions (zero between launches)
     double* nbuf = nullptr;     // kMaxRhs * ld scratch N-vectors (API calls)
     double* mbuf = nullptr;     // (2*kMaxRhs) * M scratch M-vectors (API calls)
 
@@ -117,7 +119,9 @@ class DotBatch {
    public:
     explicit DotBatch(vampomi_ctx* c) : c_(c) {}
     vampomi_status add(std::initializer_list<vk::DotTerm> terms, int64_t n, bool sync, double* out);
-    vampomi_status add_partials(const double* part, int nblk, int nq, bool sync, double* out);
+    // reserves nq result slots for a fused reduction kernel: *ro says where the
+    // kernel writes; the values reach out[0..nq) at flush()
+    vampomi_status sink(int nq, bool sync, double* out, vk::RedOut* ro);
     vampomi_status flush();
     bool empty() const { return sinks_.empty(); }
 

@@ -171,11 +171,13 @@ vampomi_status allreduce_dev(vampomi_ctx* c, double* buf, size_t n) {
     return VAMPOMI_OK;
 }
 
-vampomi_status DotBatch::add_partials(const double* part, int nblk, int nq, bool sync, double* out) {
+vampomi_status DotBatch::sink(int nq, bool sync, double* out, vk::RedOut* ro) {
     int& used = sync ? nsync_ : nlocal_;
     const int base = sync ? SL_SYNC : SL_LOCAL, cap = sync ? SL_NSYNC : SL_NLOCAL;
     if (used + nq > cap) return fail(VAMPOMI_ERR_STATE, "DotBatch overflow");
-    HIPCHK(vk::sum_partials(part, nblk, nq, c_->scal + base + used, c_->st));
+    ro->part = c_->red_part;
+    ro->out = (c_->use_comm ? c_->scal : c_->d_hscal) + base + used;
+    ro->ticket = c_->ticket;
     sinks_.push_back(Sink{base + used, nq, out});
     used += nq;
     return VAMPOMI_OK;
@@ -187,19 +189,23 @@ vampomi_status DotBatch::add(std::initializer_list<vk::DotTerm> terms, int64_t n
     if (a.nt < 1 || a.nt > vk::kMaxTerms) return fail(VAMPOMI_ERR_ARG, "DotBatch: 1..8 terms");
     int q = 0;
     for (const auto& t : terms) a.t[q++] = t;
-    HIPCHK(vk::dots_partial(a, n, c_->red_part, c_->st));
-    return add_partials(c_->red_part, vk::red_blocks(n), a.nt, sync, out);
+    vk::RedOut ro{};
+    STCHK(sink(a.nt, sync, out, &ro));
+    HIPCHK(vk::dots(a, n, ro, c_->st));
+    return VAMPOMI_OK;
 }
 
 vampomi_status DotBatch::flush() {
     if (sinks_.empty()) return VAMPOMI_OK;
-    if (nsync_ > 0) STCHK(allreduce_dev(c_, c_->scal + SL_SYNC, (size_t)nsync_));
-    if (nsync_ > 0)
-        HIPCHK(hipMemcpyAsync(c_->h_scal + SL_SYNC, c_->scal + SL_SYNC, sizeof(double) * nsync_, hipMemcpyDeviceToHost,
-                              c_->st));
-    if (nlocal_ > 0)
-        HIPCHK(hipMemcpyAsync(c_->h_scal + SL_LOCAL, c_->scal + SL_LOCAL, sizeof(double) * nlocal_,
-                              hipMemcpyDeviceToHost, c_->st));
+    if (c_->use_comm) {  // slots in device memory: all-reduce the synced ones, then one copy each
+        if (nsync_ > 0) STCHK(allreduce_dev(c_, c_->scal + SL_SYNC, (size_t)nsync_));
+        if (nsync_ > 0)
+            HIPCHK(hipMemcpyAsync(c_->h_scal + SL_SYNC, c_->scal + SL_SYNC, sizeof(double) * nsync_,
+                                  hipMemcpyDeviceToHost, c_->st));
+        if (nlocal_ > 0)
+            HIPCHK(hipMemcpyAsync(c_->h_scal + SL_LOCAL, c_->scal + SL_LOCAL, sizeof(double) * nlocal_,
+                                  hipMemcpyDeviceToHost, c_->st));
+    }
     STCHK(host_sync(c_));
     for (const Sink& k : sinks_)
         for (int i = 0; i < k.count; ++i) k.out[i] = c_->h_scal[k.slot + i];
@@ -283,8 +289,7 @@ vampomi_status atx_dev(vampomi_ctx* c, int K, const double* const* u, double* co
         vk::DotArgs a{};
         a.nt = K;
         for (int k = 0; k < K; ++k) a.t[k] = vk::DotTerm{out[k], p[k], vk::DOT};
-        HIPCHK(vk::dots_partial(a, c->M, c->red_part, c->st));
-        HIPCHK(vk::sum_partials(c->red_part, vk::red_blocks(c->M), K, c->scal + SL_DP, c->st));
+        HIPCHK(vk::dots(a, c->M, vk::RedOut{c->red_part, c->scal + SL_DP, c->ticket}, c->st));
         STCHK(allreduce_dev(c, c->scal + SL_DP, K));
     }
     return VAMPOMI_OK;
@@ -342,6 +347,8 @@ void release_ctx_resources(vampomi_ctx* c) {
         dev_free(*p);
     if (c->h_scal) (void)hipHostFree(c->h_scal);
     c->h_scal = nullptr;
+    if (c->ticket) (void)hipFree(c->ticket);
+    c->ticket = nullptr;
     if (c->comm) (void)ncclCommDestroy(c->comm);
     c->comm = nullptr;
     if (c->st) (void)hipStreamDestroy(c->st);
@@ -384,7 +391,10 @@ extern "C" vampomi_status vampomi_open(const vampomi_shard_desc* d, vampomi_ctx*
                                    (size_t)(Mx / 8 + 1) * vk::kMaxRhs, (size_t)4096});  // ATx partials at G >= 2
     STCHK(dev_alloc(&c->red_part, c->red_cap));
     STCHK(dev_alloc(&c->scal, SL_TOTAL));
-    HIPCHK(hipHostMalloc((void**)&c->h_scal, SL_TOTAL * sizeof(double), hipHostMallocDefault));
+    HIPCHK(hipHostMalloc((void**)&c->h_scal, SL_TOTAL * sizeof(double), hipHostMallocMapped | hipHostMallocCoherent));
+    HIPCHK(hipHostGetDevicePointer((void**)&c->d_hscal, c->h_scal, 0));
+    HIPCHK(hipMalloc((void**)&c->ticket, 64 * sizeof(unsigned)));
+    HIPCHK(hipMemsetAsync(c->ticket, 0, 64 * sizeof(unsigned), c->st));
     STCHK(dev_alloc(&c->nbuf, (size_t)vk::kMaxRhs * c->ld));
     HIPCHK(hipMemsetAsync(c->nbuf, 0, (size_t)vk::kMaxRhs * c->ld * 8, c->st));
     STCHK(dev_alloc(&c->mbuf, (size_t)2 * vk::kMaxRhs * Mx));
@@ -616,12 +626,12 @@ extern "C" vampomi_status vampomi_simulate_phen(vampomi_ctx* c, uint64_t seed, d
     if (!c || !c->have_X) return fail(VAMPOMI_ERR_STATE, "load methylation data first");
     HIPCHK(hipSetDevice(c->device));
     double* beta = c->mbuf;
-    int nb = 0;
     const int64_t M = c->M;
     double cm = 0.0;
-    HIPCHK(vk::gen_beta(seed, lam, c->S, M, beta, c->red_part, &nb, c->st));
     DotBatch db(c);
-    STCHK(db.add_partials(c->red_part, nb, 1, true, &cm));  // CM summed over ranks
+    vk::RedOut ro{};
+    STCHK(db.sink(1, true, &cm, &ro));  // CM summed over ranks
+    HIPCHK(vk::gen_beta(seed, lam, c->S, M, beta, ro, c->st));
     STCHK(db.flush());
     if (cm > 0) HIPCHK(vk::scale_vec(M, beta, std::sqrt(h2 / cm), c->st));  // sigma2 = h2 / CM (data_sim.py:39)
     if (beta_out && M > 0) {
@@ -771,11 +781,11 @@ extern "C" vampomi_status vampomi_denoise(vampomi_ctx* c, const double* r1, doub
         mix.probs[j] = probs[j];
         mix.vars[j] = vars[j];
     }
-    int nb = 0;
-    HIPCHK(vk::denoise(c->M, rin, gam1, mix, xo, rin, 0, 1.0, xd, c->red_part, &nb, c->st));
     double sd = 0.0;
     DotBatch db(c);
-    STCHK(db.add_partials(c->red_part, nb, 1, true, &sd));
+    vk::RedOut ro{};
+    STCHK(db.sink(1, true, &sd, &ro));
+    HIPCHK(vk::denoise(c->M, rin, gam1, mix, xo, rin, 0, 1.0, xd, ro, c->st));
     STCHK(db.flush());
     if (x1) STCHK(stage_out(c, xo, c->M, mem, x1));
     if (x1d) STCHK(stage_out(c, xd, c->M, mem, x1d));
@@ -791,11 +801,11 @@ extern "C" vampomi_status vampomi_denoise_bin(vampomi_ctx* c, const double* p1, 
     double* pin = c->nbuf;
     double* zo = c->nbuf + c->ld;
     STCHK(stage_in(c, p1, c->N, mem, pin));
-    int nb = 0;
-    HIPCHK(vk::probit_denoise(c->N, pin, c->y, tau1, zo, c->red_part, &nb, c->st));
     double sd = 0.0;
     DotBatch db(c);
-    STCHK(db.add_partials(c->red_part, nb, 1, false, &sd));
+    vk::RedOut ro{};
+    STCHK(db.sink(1, false, &sd, &ro));
+    HIPCHK(vk::probit_denoise(c->N, pin, c->y, tau1, zo, ro, c->st));
     STCHK(db.flush());
     if (z1) STCHK(stage_out(c, zo, c->N, mem, z1));
     if (sum_d) *sum_d = sd;

@@ -14,6 +14,10 @@ constexpr int kMaxTerms = 8;   // dot-product terms per reduction launch
 constexpr int kRedBlocks = 1024;  // max partial blocks of a reduction
 
 struct CPtrs { const double* p[kMaxRhs]; };
+// Destination of a fused two-stage reduction (see red_finish in kernels.hip):
+// per-block partials in part, the final sums in out[0..nq) (device memory or
+// mapped host memory), ticket a zeroed device counter the kernel re-arms.
+struct RedOut { double* part; double* out; unsigned* ticket; };
 struct Ptrs { double* p[kMaxRhs]; };
 
 // The device-resident marker shard: M columns (markers) of N samples, column
@@ -63,10 +67,9 @@ hipError_t marker_stats(const double* X, int64_t ld, int64_t N, int64_t M, doubl
 // ---- synthetic data --------------------------------------------------------
 hipError_t gen_markers(uint64_t seed, int kind, int64_t N, int64_t ld, int64_t S, int64_t M, double* X,
                        hipStream_t st);
-// beta_i = gauss(seed) for causal markers (uniform < lam), else 0; causal flag
-// count partials in cnt_part (one per block)
-hipError_t gen_beta(uint64_t seed, double lam, int64_t S, int64_t M, double* beta, double* cnt_part,
-                    int* nblk, hipStream_t st);
+// beta_i = gauss(seed) for causal markers (uniform < lam), else 0; the count
+// of causal markers in ro.out[0]
+hipError_t gen_beta(uint64_t seed, double lam, int64_t S, int64_t M, double* beta, const RedOut& ro, hipStream_t st);
 hipError_t scale_vec(int64_t n, double* v, double a, hipStream_t st);
 // y_j = y_j + sqrt1mh2 * gauss(seed, noise stream, j)
 hipError_t add_noise(uint64_t seed, int64_t N, double sd, double* y, hipStream_t st);
@@ -76,10 +79,9 @@ enum DotOp { DOT = 0, DIFF2 = 1, SUM = 2 };
 struct DotTerm { const double* a; const double* b; int op; };
 struct DotArgs { DotTerm t[kMaxTerms]; int nt; };
 int red_blocks(int64_t n);
-// per-block partials part[blk*nt + q]
-hipError_t dots_partial(const DotArgs& a, int64_t n, double* part, hipStream_t st);
-// out[q] = sum over blocks in index order of part[blk*nq + q]
-hipError_t sum_partials(const double* part, int nblk, int nq, double* out, hipStream_t st);
+// ro.out[q] = term q summed over [0, n): per-block partials, then the blocks'
+// sums in block order (fixed geometry: depends on n only)
+hipError_t dots(const DotArgs& a, int64_t n, const RedOut& ro, hipStream_t st);
 
 // ---- denoiser (vamp::g1 / g1d) ---------------------------------------------
 struct Mix {
@@ -88,10 +90,9 @@ struct Mix {
     int L;
 };
 // x1 = g1(r1) (then rho*x1 + (1-rho)*x1_prev if damp), x1d = g1d(r1),
-// per-block partial sums of x1d in part
+// sum of x1d in ro.out[0]
 hipError_t denoise(int64_t M, const double* r1, double gam1, const Mix& mix, double* x1,
-                   const double* x1_prev, int damp, double rho, double* x1d, double* part, int* nblk,
-                   hipStream_t st);
+                   const double* x1_prev, int damp, double rho, double* x1d, const RedOut& ro, hipStream_t st);
 
 // ---- EM prior update (vamp::updatePrior) per-marker sums --------------------
 struct EmArgs {
@@ -101,9 +102,9 @@ struct EmArgs {
     double lambda, noise_var, gam1, max_sigma;
     int L;
 };
-// part[blk*Q + q], Q = 1 + 2(L-1): q=0 sum pin; q=j (1..L-1) sum beta_j pin;
+// ro.out[q], Q = 1 + 2(L-1): q=0 sum pin; q=j (1..L-1) sum beta_j pin;
 // q=L-1+j sum beta_j (g_j^2 + v_j) pin
-hipError_t em_sums(int64_t M, const double* r1, const EmArgs& a, double* part, int* nblk, hipStream_t st);
+hipError_t em_sums(int64_t M, const double* r1, const EmArgs& a, const RedOut& ro, hipStream_t st);
 
 // ---- elementwise VAMP updates -----------------------------------------------
 // out = (a*x - b*y) / c        (r2 and r1 updates, src/vamp.cpp:259-261, 348-350)
@@ -119,14 +120,14 @@ hipError_t bernoulli(uint64_t seed, int it, int64_t S, int64_t M, double sqrtMt,
 hipError_t div_scalar(int64_t n, const double* x, double d, double* out, hipStream_t st);
 
 // ---- probit model (src/vamp_probit.cpp) -------------------------------------
-// z1[i] = g1_bin_class(p1[i], tau1, y[i]); per-block partial sums of
-// g1d_bin_class (src/vamp_probit.cpp:213-233, 469-488; probit_var = 1, m_cov = 0)
-hipError_t probit_denoise(int64_t N, const double* p1, const double* y, double tau1, double* z1, double* part,
-                          int* nblk, hipStream_t st);
+// z1[i] = g1_bin_class(p1[i], tau1, y[i]); the sum of g1d_bin_class in ro.out[0]
+// (src/vamp_probit.cpp:213-233, 469-488; probit_var = 1, m_cov = 0)
+hipError_t probit_denoise(int64_t N, const double* p1, const double* y, double tau1, double* z1, const RedOut& ro,
+                          hipStream_t st);
 // predict_probit(z_k, 0.5) + confusion_matrix against y (src/vamp_probit.cpp:619-651),
-// nz <= 2 vectors at z + k*ld; part[blk*4*nz + 4k + {TP, TN, FP, FN}]
-hipError_t probit_confusion(int64_t N, int nz, const double* z, int64_t ld, const double* y, double* part,
-                            int* nblk, hipStream_t st);
+// nz <= 2 vectors at z + k*ld; ro.out[4k + {TP, TN, FP, FN}]
+hipError_t probit_confusion(int64_t N, int nz, const double* z, int64_t ld, const double* y, const RedOut& ro,
+                            hipStream_t st);
 // P2 start: p1[i] = gauss(seed ^ salt, 0, i) (replaces simulate(N, {1}, {1}), :53)
 hipError_t probit_p1(uint64_t seed, int64_t N, double* p1, hipStream_t st);
 
@@ -157,13 +158,13 @@ struct CgVecs {
     double tau, gam2;             // init only, with atx0
 };
 // r = v - d (or v, or v - (atx0*tau + gam2*mu)), z = r/diag, p = z;
-// partials <r,z>, <v,v> (2K terms)
-hipError_t cg_init(int K, int64_t M, const CgVecs& c, double diag, double* part, int* nblk, hipStream_t st);
+// <r,z>, <v,v> per system in ro.out (2K values)
+hipError_t cg_init(int K, int64_t M, const CgVecs& c, double diag, const RedOut& ro, hipStream_t st);
 // alpha_k = rz[k] / dp_dev[k]; mu += alpha p; r -= d alpha; z = r/diag;
-// partials <r,z>, <r,r>, <v,mu> (3K terms, ordered k-major)
+// <r,z>, <r,r>, <v,mu> in ro.out (3K values, ordered k-major)
 struct CgScalars { double rz[kMaxRhs]; };
 hipError_t cg_update(int K, int64_t M, const CgVecs& c, double diag, CgScalars rz, const double* dp_dev,
-                     double* part, int* nblk, hipStream_t st);
+                     const RedOut& ro, hipStream_t st);
 // p = z + beta_k p
 struct CgBeta { double beta[kMaxRhs]; };
 hipError_t cg_pupdate(int K, int64_t M, const CgVecs& c, CgBeta b, hipStream_t st);

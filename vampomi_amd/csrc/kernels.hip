@@ -39,6 +39,31 @@ __device__ __forceinline__ double block_sum(double v, double* lds4) {
     return ((lds4[0] + lds4[1]) + lds4[2]) + lds4[3];
 }
 
+// Fused finish of a two-stage reduction.  Every block has stored its per-block
+// partials part[blk*nq + q]; the LAST block to arrive (device-scope ticket)
+// sums them in block order, exactly as a separate one-block sum kernel would
+// (so results are bitwise those of the two-launch form), writes out[0..nq)
+// (device memory or mapped host memory) and re-arms the ticket.  Release:
+// fence before the ticket; acquire: fence after it, then agent-scope loads.
+__device__ void red_finish(const RedOut& ro, int nq, double* lds4) {
+    __shared__ int is_last;
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) is_last = atomicAdd(ro.ticket, 1u) == gridDim.x - 1;
+    __syncthreads();
+    if (!is_last) return;
+    __threadfence();
+    const int nblk = (int)gridDim.x;
+    for (int q = 0; q < nq; ++q) {
+        double s = 0.0;
+        for (int b = threadIdx.x; b < nblk; b += kBlock)
+            s += __hip_atomic_load(ro.part + (int64_t)b * nq + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s = block_sum(s, lds4);
+        if (threadIdx.x == 0) ro.out[q] = s;
+    }
+    if (threadIdx.x == 0) __hip_atomic_store(ro.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __device__ __forceinline__ v2d ld_stream(const double* p) {
     return __builtin_nontemporal_load(reinterpret_cast<const v2d*>(p));
 }
@@ -594,7 +619,7 @@ hipError_t gen_markers(uint64_t seed, int kind, int64_t N, int64_t ld, int64_t S
 }
 
 __global__ __launch_bounds__(kBlock) void gen_beta_kernel(uint64_t seed, double lam, int64_t S, int64_t M,
-                                                          double* beta, double* cnt_part) {
+                                                          double* beta, RedOut ro) {
     __shared__ double lds[4];
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     double c = 0.0;
@@ -606,14 +631,13 @@ __global__ __launch_bounds__(kBlock) void gen_beta_kernel(uint64_t seed, double 
         c = causal ? 1.0 : 0.0;
     }
     c = block_sum(c, lds);
-    if (threadIdx.x == 0) cnt_part[blockIdx.x] = c;
+    if (threadIdx.x == 0) ro.part[blockIdx.x] = c;
+    red_finish(ro, 1, lds);
 }
 
-hipError_t gen_beta(uint64_t seed, double lam, int64_t S, int64_t M, double* beta, double* cnt_part, int* nblk,
-                    hipStream_t st) {
-    *nblk = (int)cdiv(M, kBlock);
-    if (*nblk < 1) return hipSuccess;
-    hipLaunchKernelGGL(gen_beta_kernel, dim3(*nblk), dim3(kBlock), 0, st, seed, lam, S, M, beta, cnt_part);
+hipError_t gen_beta(uint64_t seed, double lam, int64_t S, int64_t M, double* beta, const RedOut& ro, hipStream_t st) {
+    const int nblk = (int)std::max<int64_t>(1, cdiv(M, kBlock));
+    hipLaunchKernelGGL(gen_beta_kernel, dim3(nblk), dim3(kBlock), 0, st, seed, lam, S, M, beta, ro);
     return hipGetLastError();
 }
 
@@ -648,7 +672,7 @@ int red_blocks(int64_t n) {
     return (int)b;
 }
 
-__global__ __launch_bounds__(kBlock) void dots_kernel(DotArgs a, int64_t n, double* __restrict__ part) {
+__global__ __launch_bounds__(kBlock) void dots_kernel(DotArgs a, int64_t n, RedOut ro) {
     __shared__ double lds[4];
     double acc[kMaxTerms];
 #pragma unroll
@@ -673,29 +697,14 @@ __global__ __launch_bounds__(kBlock) void dots_kernel(DotArgs a, int64_t n, doub
     for (int q = 0; q < kMaxTerms; ++q) {
         if (q < a.nt) {
             const double s = block_sum(acc[q], lds);
-            if (threadIdx.x == 0) part[(int64_t)blockIdx.x * a.nt + q] = s;
+            if (threadIdx.x == 0) ro.part[(int64_t)blockIdx.x * a.nt + q] = s;
         }
     }
+    red_finish(ro, a.nt, lds);
 }
 
-hipError_t dots_partial(const DotArgs& a, int64_t n, double* part, hipStream_t st) {
-    hipLaunchKernelGGL(dots_kernel, dim3(red_blocks(n)), dim3(kBlock), 0, st, a, n, part);
-    return hipGetLastError();
-}
-
-__global__ __launch_bounds__(kBlock) void sum_partials_kernel(const double* __restrict__ part, int nblk, int nq,
-                                                              double* __restrict__ out) {
-    __shared__ double lds[4];
-    for (int q = 0; q < nq; ++q) {
-        double s = 0.0;
-        for (int b = threadIdx.x; b < nblk; b += kBlock) s += part[(int64_t)b * nq + q];
-        s = block_sum(s, lds);
-        if (threadIdx.x == 0) out[q] = s;
-    }
-}
-
-hipError_t sum_partials(const double* part, int nblk, int nq, double* out, hipStream_t st) {
-    hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(kBlock), 0, st, part, nblk, nq, out);
+hipError_t dots(const DotArgs& a, int64_t n, const RedOut& ro, hipStream_t st) {
+    hipLaunchKernelGGL(dots_kernel, dim3(red_blocks(n)), dim3(kBlock), 0, st, a, n, ro);
     return hipGetLastError();
 }
 
@@ -730,7 +739,7 @@ __device__ __forceinline__ void g1_g1d(double y, double gam1, const Mix& mix, do
 __global__ __launch_bounds__(kBlock) void denoise_kernel(int64_t M, const double* __restrict__ r1, double gam1,
                                                          Mix mix, double eta_max, double* __restrict__ x1,
                                                          const double* __restrict__ x1_prev, int damp, double rho,
-                                                         double* __restrict__ x1d, double* __restrict__ part) {
+                                                         double* __restrict__ x1d, RedOut ro) {
     __shared__ double lds[4];
     double acc = 0.0;
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < M; i += (int64_t)gridDim.x * kBlock) {
@@ -742,17 +751,17 @@ __global__ __launch_bounds__(kBlock) void denoise_kernel(int64_t M, const double
         acc += gd;
     }
     acc = block_sum(acc, lds);
-    if (threadIdx.x == 0) part[blockIdx.x] = acc;
+    if (threadIdx.x == 0) ro.part[blockIdx.x] = acc;
+    red_finish(ro, 1, lds);
 }
 
 hipError_t denoise(int64_t M, const double* r1, double gam1, const Mix& mix, double* x1, const double* x1_prev,
-                   int damp, double rho, double* x1d, double* part, int* nblk, hipStream_t st) {
+                   int damp, double rho, double* x1d, const RedOut& ro, hipStream_t st) {
     double eta_max = mix.vars[0];
     for (int i = 1; i < mix.L; ++i)
         if (mix.vars[i] > eta_max) eta_max = mix.vars[i];
-    *nblk = red_blocks(M);
-    hipLaunchKernelGGL(denoise_kernel, dim3(*nblk), dim3(kBlock), 0, st, M, r1, gam1, mix, eta_max, x1, x1_prev,
-                       damp, rho, x1d, part);
+    hipLaunchKernelGGL(denoise_kernel, dim3(red_blocks(M)), dim3(kBlock), 0, st, M, r1, gam1, mix, eta_max, x1,
+                       x1_prev, damp, rho, x1d, ro);
     return hipGetLastError();
 }
 
@@ -765,8 +774,7 @@ __device__ __forceinline__ double em_num(const EmArgs& a, double r, int j) {
            sqrt(a.vars[j] + a.noise_var) / sqrt(2 * M_PI);
 }
 
-__global__ __launch_bounds__(kBlock) void em_kernel(int64_t M, const double* __restrict__ r1, EmArgs a,
-                                                    double* __restrict__ part) {
+__global__ __launch_bounds__(kBlock) void em_kernel(int64_t M, const double* __restrict__ r1, EmArgs a, RedOut ro) {
     __shared__ double lds[4];
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     const bool valid = i < M;
@@ -778,7 +786,7 @@ __global__ __launch_bounds__(kBlock) void em_kernel(int64_t M, const double* __r
                                     exp(-(r * r) / 2 * a.max_sigma / a.noise_var / (a.noise_var + a.max_sigma)) /
                                     sum_of_elems);
     double s = block_sum(valid ? pin : 0.0, lds);
-    if (threadIdx.x == 0) part[(int64_t)blockIdx.x * Q] = s;
+    if (threadIdx.x == 0) ro.part[(int64_t)blockIdx.x * Q] = s;
     for (int j = 1; j < L; ++j) {
         const double beta = em_num(a, r, j) / sum_of_elems;
         const double g = a.gam1 * r / (1 / a.vars[j] + a.gam1);
@@ -786,16 +794,16 @@ __global__ __launch_bounds__(kBlock) void em_kernel(int64_t M, const double* __r
         const double sb = block_sum(valid ? beta * pin : 0.0, lds);
         const double sg = block_sum(valid ? gam * pin : 0.0, lds);
         if (threadIdx.x == 0) {
-            part[(int64_t)blockIdx.x * Q + j] = sb;
-            part[(int64_t)blockIdx.x * Q + (L - 1) + j] = sg;
+            ro.part[(int64_t)blockIdx.x * Q + j] = sb;
+            ro.part[(int64_t)blockIdx.x * Q + (L - 1) + j] = sg;
         }
     }
+    red_finish(ro, Q, lds);
 }
 
-hipError_t em_sums(int64_t M, const double* r1, const EmArgs& a, double* part, int* nblk, hipStream_t st) {
-    *nblk = (int)cdiv(M, kBlock);
-    if (*nblk < 1) *nblk = 1;
-    hipLaunchKernelGGL(em_kernel, dim3(*nblk), dim3(kBlock), 0, st, M, r1, a, part);
+hipError_t em_sums(int64_t M, const double* r1, const EmArgs& a, const RedOut& ro, hipStream_t st) {
+    const int nblk = (int)std::max<int64_t>(1, cdiv(M, kBlock));
+    hipLaunchKernelGGL(em_kernel, dim3(nblk), dim3(kBlock), 0, st, M, r1, a, ro);
     return hipGetLastError();
 }
 
@@ -854,8 +862,7 @@ hipError_t div_scalar(int64_t n, const double* x, double d, double* out, hipStre
 // ---------------------------------------------------------------------------
 // PCG vector steps (src/vamp.cpp:671-757), K right-hand sides per launch
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void cg_init_kernel(int K, int64_t M, CgVecs c, double diag,
-                                                         double* __restrict__ part) {
+__global__ __launch_bounds__(kBlock) void cg_init_kernel(int K, int64_t M, CgVecs c, double diag, RedOut ro) {
     __shared__ double lds[4];
     double acc[2 * kMaxRhs];
 #pragma unroll
@@ -889,19 +896,18 @@ __global__ __launch_bounds__(kBlock) void cg_init_kernel(int K, int64_t M, CgVec
         for (int t = 0; t < 2 * kMaxRhs; ++t)
             if (t == q) v = acc[t];
         const double s = block_sum(v, lds);
-        if (threadIdx.x == 0) part[(int64_t)blockIdx.x * 2 * K + q] = s;
+        if (threadIdx.x == 0) ro.part[(int64_t)blockIdx.x * 2 * K + q] = s;
     }
+    red_finish(ro, 2 * K, lds);
 }
 
-hipError_t cg_init(int K, int64_t M, const CgVecs& c, double diag, double* part, int* nblk, hipStream_t st) {
-    *nblk = red_blocks(M);
-    hipLaunchKernelGGL(cg_init_kernel, dim3(*nblk), dim3(kBlock), 0, st, K, M, c, diag, part);
+hipError_t cg_init(int K, int64_t M, const CgVecs& c, double diag, const RedOut& ro, hipStream_t st) {
+    hipLaunchKernelGGL(cg_init_kernel, dim3(red_blocks(M)), dim3(kBlock), 0, st, K, M, c, diag, ro);
     return hipGetLastError();
 }
 
 __global__ __launch_bounds__(kBlock) void cg_update_kernel(int K, int64_t M, CgVecs c, double diag, CgScalars rz,
-                                                           const double* __restrict__ dp_dev,
-                                                           double* __restrict__ part) {
+                                                           const double* __restrict__ dp_dev, RedOut ro) {
     __shared__ double lds[4];
     double alpha[kMaxRhs];
 #pragma unroll
@@ -932,14 +938,14 @@ __global__ __launch_bounds__(kBlock) void cg_update_kernel(int K, int64_t M, CgV
         for (int t = 0; t < 3 * kMaxRhs; ++t)
             if (t == q) v = acc[t];
         const double s = block_sum(v, lds);
-        if (threadIdx.x == 0) part[(int64_t)blockIdx.x * 3 * K + q] = s;
+        if (threadIdx.x == 0) ro.part[(int64_t)blockIdx.x * 3 * K + q] = s;
     }
+    red_finish(ro, 3 * K, lds);
 }
 
-hipError_t cg_update(int K, int64_t M, const CgVecs& c, double diag, CgScalars rz, const double* dp_dev, double* part,
-                     int* nblk, hipStream_t st) {
-    *nblk = red_blocks(M);
-    hipLaunchKernelGGL(cg_update_kernel, dim3(*nblk), dim3(kBlock), 0, st, K, M, c, diag, rz, dp_dev, part);
+hipError_t cg_update(int K, int64_t M, const CgVecs& c, double diag, CgScalars rz, const double* dp_dev,
+                     const RedOut& ro, hipStream_t st) {
+    hipLaunchKernelGGL(cg_update_kernel, dim3(red_blocks(M)), dim3(kBlock), 0, st, K, M, c, diag, rz, dp_dev, ro);
     return hipGetLastError();
 }
 
@@ -1001,7 +1007,7 @@ __device__ __forceinline__ double erfcx_ref(double x) {
 
 __global__ __launch_bounds__(kBlock) void probit_denoise_kernel(int64_t N, const double* __restrict__ p1,
                                                                 const double* __restrict__ y, double tau1,
-                                                                double* __restrict__ z1, double* __restrict__ part) {
+                                                                double* __restrict__ z1, RedOut ro) {
     __shared__ double lds[4];
     const double sq = sqrt(1.0 + 1.0 / tau1);           // sqrt(probit_var + 1/tau1)
     const double k0 = 2.0 / sqrt(2 * M_PI), rt2 = sqrt(2.0);
@@ -1015,19 +1021,19 @@ __global__ __launch_bounds__(kBlock) void probit_denoise_kernel(int64_t N, const
         acc += 1 - ratio / den * (s * c + ratio);
     }
     acc = block_sum(acc, lds);
-    if (threadIdx.x == 0) part[blockIdx.x] = acc;
+    if (threadIdx.x == 0) ro.part[blockIdx.x] = acc;
+    red_finish(ro, 1, lds);
 }
 
-hipError_t probit_denoise(int64_t N, const double* p1, const double* y, double tau1, double* z1, double* part,
-                          int* nblk, hipStream_t st) {
-    *nblk = red_blocks(N);
-    hipLaunchKernelGGL(probit_denoise_kernel, dim3(*nblk), dim3(kBlock), 0, st, N, p1, y, tau1, z1, part);
+hipError_t probit_denoise(int64_t N, const double* p1, const double* y, double tau1, double* z1, const RedOut& ro,
+                          hipStream_t st) {
+    hipLaunchKernelGGL(probit_denoise_kernel, dim3(red_blocks(N)), dim3(kBlock), 0, st, N, p1, y, tau1, z1, ro);
     return hipGetLastError();
 }
 
 __global__ __launch_bounds__(kBlock) void confusion_kernel(int64_t N, int nz, const double* __restrict__ z,
                                                            int64_t ld, const double* __restrict__ y,
-                                                           double* __restrict__ part) {
+                                                           RedOut ro) {
     __shared__ double lds[4];
     double cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < N; i += (int64_t)gridDim.x * kBlock) {
@@ -1046,15 +1052,15 @@ __global__ __launch_bounds__(kBlock) void confusion_kernel(int64_t N, int nz, co
     }
     for (int q = 0; q < 4 * nz; ++q) {
         const double s = block_sum(cnt[q], lds);
-        if (threadIdx.x == 0) part[(int64_t)blockIdx.x * 4 * nz + q] = s;
+        if (threadIdx.x == 0) ro.part[(int64_t)blockIdx.x * 4 * nz + q] = s;
     }
+    red_finish(ro, 4 * nz, lds);
 }
 
-hipError_t probit_confusion(int64_t N, int nz, const double* z, int64_t ld, const double* y, double* part,
-                            int* nblk, hipStream_t st) {
+hipError_t probit_confusion(int64_t N, int nz, const double* z, int64_t ld, const double* y, const RedOut& ro,
+                            hipStream_t st) {
     if (nz < 1 || nz > 2) return hipErrorInvalidValue;
-    *nblk = red_blocks(N);
-    hipLaunchKernelGGL(confusion_kernel, dim3(*nblk), dim3(kBlock), 0, st, N, nz, z, ld, y, part);
+    hipLaunchKernelGGL(confusion_kernel, dim3(red_blocks(N)), dim3(kBlock), 0, st, N, nz, z, ld, y, ro);
     return hipGetLastError();
 }
 

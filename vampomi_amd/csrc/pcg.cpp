@@ -48,12 +48,12 @@ vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double
         cv.atx0[k] = s->mu0_nonzero ? s->atx0 : nullptr;
         cv.d[k] = (s->mu0_nonzero && !s->atx0) ? s->d : nullptr;
     }
-    int nb = 0;
-    HIPCHK(vk::cg_init(K, M, cv, diag, c->red_part, &nb, c->st));
     std::vector<double> rzvv(2 * K);
     DotBatch local(c);
     DotBatch& b0 = init ? *init : local;
-    STCHK(b0.add_partials(c->red_part, nb, 2 * K, true, rzvv.data()));
+    vk::RedOut ro{};
+    STCHK(b0.sink(2 * K, true, rzvv.data(), &ro));
+    HIPCHK(vk::cg_init(K, M, cv, diag, ro, c->st));
     STCHK(b0.flush());
     std::vector<double> rz(K), vv(K), prev_ons(K, 0.0);
     std::vector<int> active;
@@ -85,9 +85,10 @@ vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double
         // d = lmmse_mult(p)   (:700); <d,p> lands in scal[SL_DP + a]
         STCHK(lmmse_dev(c, Ka, pp, dd, tau, gam2, nscratch));
         if (ref_passes) *ref_passes += 2 * (int64_t)Ka;
-        HIPCHK(vk::cg_update(Ka, M, cu, diag, rzs, c->scal + SL_DP, c->red_part, &nb, c->st));
         DotBatch b(c);
-        STCHK(b.add_partials(c->red_part, nb, 3 * Ka, true, red.data()));
+        vk::RedOut rou{};
+        STCHK(b.sink(3 * Ka, true, red.data(), &rou));
+        HIPCHK(vk::cg_update(Ka, M, cu, diag, rzs, c->scal + SL_DP, rou, c->st));
         STCHK(b.flush());
         std::vector<int> still;
         vk::CgVecs pv{};

@@ -105,11 +105,11 @@ vampomi_status probit_step(vampomi_ctx* c, VampRun& R) {
     double bsum = 0, cnt1[4] = {}, xc1[3] = {};
     {
         DotBatch b(c);
-        int nb = 0;
-        HIPCHK(vk::probit_denoise(N, R.p1, c->y, R.tau1, R.z1h, c->red_part, &nb, c->st));
-        STCHK(b.add_partials(c->red_part, nb, 1, false, &bsum));  // y, p1 replicated: local sum
-        HIPCHK(vk::probit_confusion(N, 1, zx1, ld, c->y, c->red_part, &nb, c->st));
-        STCHK(b.add_partials(c->red_part, nb, 4, false, cnt1));
+        vk::RedOut ro{};
+        STCHK(b.sink(1, false, &bsum, &ro));  // y, p1 replicated: local sum
+        HIPCHK(vk::probit_denoise(N, R.p1, c->y, R.tau1, R.z1h, ro, c->st));
+        STCHK(b.sink(4, false, cnt1, &ro));
+        HIPCHK(vk::probit_confusion(N, 1, zx1, ld, c->y, ro, c->st));
         STCHK(b.add({T(R.x1, R.ts), T(R.x1, R.x1), T(R.ts, R.ts)}, M, true, xc1));
         STCHK(b.flush());
     }
@@ -191,9 +191,9 @@ vampomi_status probit_step(vampomi_ctx* c, VampRun& R) {
     R.tau1 = clip(R.tau2 * (1 - R.beta2) / R.beta2);                                      // :374-376
     double cnt2[4] = {};
     {
-        int nb = 0;
-        HIPCHK(vk::probit_confusion(N, 1, R.nb3 + ld, ld, c->y, c->red_part, &nb, c->st));  // :403-408
-        STCHK(fin.add_partials(c->red_part, nb, 4, false, cnt2));
+        vk::RedOut ro{};
+        STCHK(fin.sink(4, false, cnt2, &ro));
+        HIPCHK(vk::probit_confusion(N, 1, R.nb3 + ld, ld, c->y, ro, c->st));  // :403-408
     }
     STCHK(fin.add({T(R.x1p, R.x1, vk::DIFF2), T(R.x1p, R.x1p)}, M, true, R.nm));  // NMSE (:444-448)
     STCHK(fin.flush());

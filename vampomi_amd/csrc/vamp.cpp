@@ -67,10 +67,10 @@ vampomi_status update_prior(vampomi_ctx* c, const VampRun& R, Mixture& m, double
         a.max_sigma = max_sigma;
         a.L = L;
         const int Q = 1 + 2 * (L - 1);
-        int nb = 0;
-        HIPCHK(vk::em_sums(c->M, r1, a, c->red_part, &nb, c->st));
         DotBatch b(c);
-        STCHK(b.add_partials(c->red_part, nb, Q, true, sums.data()));  // :578, :596-597
+        vk::RedOut ro{};
+        STCHK(b.sink(Q, true, sums.data(), &ro));  // :578, :596-597
+        HIPCHK(vk::em_sums(c->M, r1, a, ro, c->st));
         STCHK(b.flush());
         const double lambda_total = sums[0];
         lambda = lambda_total / (double)c->Mt;
@@ -124,9 +124,10 @@ vampomi_status denoise_into(vampomi_ctx* c, const Mixture& m, double gam1, const
         mix.probs[j] = m.probs[j];
         mix.vars[j] = m.vars[j];
     }
-    int nb = 0;
-    HIPCHK(vk::denoise(c->M, r1, gam1, mix, x1, x1_prev, damp ? 1 : 0, rho, x1d, c->red_part, &nb, c->st));
-    return b.add_partials(c->red_part, nb, 1, true, sum_out);  // :214-222
+    vk::RedOut ro{};
+    STCHK(b.sink(1, true, sum_out, &ro));  // :214-222
+    HIPCHK(vk::denoise(c->M, r1, gam1, mix, x1, x1_prev, damp ? 1 : 0, rho, x1d, ro, c->st));
+    return VAMPOMI_OK;
 }
 
 // err_measures (src/vamp.cpp:760-852): the reductions (queued) ...
