@@ -76,6 +76,9 @@ struct vampomi_ctx {
     double* h_scal = nullptr;   // pinned host mirror, mapped and coherent: one-rank reductions land here directly
     double* d_hscal = nullptr;  // its device-side address
     unsigned* ticket = nullptr; // arrival counter of the fused reductions (zero between launches)
+    unsigned long long* h_flag = nullptr;  // mapped host word the stream stores sync sequence numbers into
+    unsigned long long* d_flag = nullptr;
+    unsigned long long sync_seq = 0;
     double* nbuf = nullptr;     // kMaxRhs * ld scratch N-vectors (API calls)
     double* mbuf = nullptr;     // (2*kMaxRhs) * M scratch M-vectors (API calls)
 

@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cfloat>
+#include <chrono>
 #include <condition_variable>
 #include <map>
 #include <mutex>
@@ -99,10 +100,36 @@ static double pass_flops(const vampomi_ctx* c, int K) { return (double)c->N * (d
 // ---------------------------------------------------------------------------
 // reductions
 // ---------------------------------------------------------------------------
+// Waits until everything queued on the context's stream has finished: a
+// 1-thread kernel stores the next sequence number into a mapped host word
+// (system-scope release) and the host spins on it — a few microseconds
+// sooner than hipStreamSynchronize's completion path, once per dependency
+// level of the iteration.  Faults are still reported: the spin polls
+// hipStreamQuery, and gives up after 10 minutes.
 vampomi_status host_sync(vampomi_ctx* c) {
-    HIPCHK(hipStreamSynchronize(c->st));
     c->stats.host_syncs++;
-    return VAMPOMI_OK;
+    if (!c->h_flag) {
+        HIPCHK(hipStreamSynchronize(c->st));
+        return VAMPOMI_OK;
+    }
+    const unsigned long long seq = ++c->sync_seq;
+    HIPCHK(vk::signal_host(c->d_flag, seq, c->st));
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint64_t spin = 1;; ++spin) {
+        if (__atomic_load_n(c->h_flag, __ATOMIC_ACQUIRE) == seq) return VAMPOMI_OK;
+        if ((spin & 4095) == 0) {
+            const hipError_t e = hipStreamQuery(c->st);
+            if (e != hipSuccess && e != hipErrorNotReady)
+                return fail(VAMPOMI_ERR_HIP, std::string("stream failed: ") + hipGetErrorString(e));
+            if (e == hipSuccess) {  // finished, flag not seen yet: complete through the runtime
+                HIPCHK(hipStreamSynchronize(c->st));
+                return VAMPOMI_OK;
+            }
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::minutes(10))
+                return fail(VAMPOMI_ERR_HIP, "device did not signal completion within 10 minutes");
+        }
+        __builtin_ia32_pause();
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -188,7 +215,11 @@ vampomi_status DotBatch::add(std::initializer_list<vk::DotTerm> terms, int64_t n
     a.nt = (int)terms.size();
     if (a.nt < 1 || a.nt > vk::kMaxTerms) return fail(VAMPOMI_ERR_ARG, "DotBatch: 1..8 terms");
     int q = 0;
-    for (const auto& t : terms) a.t[q++] = t;
+    for (const auto& t : terms) {
+        a.t[q] = t;
+        if (t.op == vk::SUM) a.t[q].b = t.a;  // the kernel loads both operands of every term
+        ++q;
+    }
     vk::RedOut ro{};
     STCHK(sink(a.nt, sync, out, &ro));
     HIPCHK(vk::dots(a, n, ro, c_->st));
@@ -349,6 +380,8 @@ void release_ctx_resources(vampomi_ctx* c) {
     c->h_scal = nullptr;
     if (c->ticket) (void)hipFree(c->ticket);
     c->ticket = nullptr;
+    if (c->h_flag) (void)hipHostFree(c->h_flag);
+    c->h_flag = nullptr;
     if (c->comm) (void)ncclCommDestroy(c->comm);
     c->comm = nullptr;
     if (c->st) (void)hipStreamDestroy(c->st);
@@ -393,6 +426,9 @@ extern "C" vampomi_status vampomi_open(const vampomi_shard_desc* d, vampomi_ctx*
     STCHK(dev_alloc(&c->scal, SL_TOTAL));
     HIPCHK(hipHostMalloc((void**)&c->h_scal, SL_TOTAL * sizeof(double), hipHostMallocMapped | hipHostMallocCoherent));
     HIPCHK(hipHostGetDevicePointer((void**)&c->d_hscal, c->h_scal, 0));
+    HIPCHK(hipHostMalloc((void**)&c->h_flag, 64, hipHostMallocMapped | hipHostMallocCoherent));
+    *c->h_flag = 0;
+    HIPCHK(hipHostGetDevicePointer((void**)&c->d_flag, c->h_flag, 0));
     HIPCHK(hipMalloc((void**)&c->ticket, 64 * sizeof(unsigned)));
     HIPCHK(hipMemsetAsync(c->ticket, 0, 64 * sizeof(unsigned), c->st));
     STCHK(dev_alloc(&c->nbuf, (size_t)vk::kMaxRhs * c->ld));

@@ -146,6 +146,9 @@ hipError_t se_pvals(int64_t M, const double* r1, double gam1, int64_t N, double*
 // out = x * a
 hipError_t mul_scalar(int64_t n, const double* x, double a, double* out, hipStream_t st);
 
+// ---- host completion flag (system-scope store into mapped host memory) -------
+hipError_t signal_host(unsigned long long* flag, unsigned long long seq, hipStream_t st);
+
 // ---- PCG (vamp::precondCG_solver), K right-hand sides --------------------------
 struct CgVecs {
     double* mu[kMaxRhs];

@@ -39,20 +39,53 @@ __device__ __forceinline__ double block_sum(double v, double* lds4) {
     return ((lds4[0] + lds4[1]) + lds4[2]) + lds4[3];
 }
 
-// Fused finish of a two-stage reduction.  Every block has stored its per-block
-// partials part[blk*nq + q]; the LAST block to arrive (device-scope ticket)
-// sums them in block order, exactly as a separate one-block sum kernel would
-// (so results are bitwise those of the two-launch form), writes out[0..nq)
-// (device memory or mapped host memory) and re-arms the ticket.  Release:
-// fence before the ticket; acquire: fence after it, then agent-scope loads.
+// Fused finish of a two-stage reduction.  Thread 0 of every block publishes
+// its per-block partials with red_put (agent-coherent, write-through stores);
+// red_finish drains them (s_waitcnt) and takes a ticket; the LAST block to
+// arrive sums the partials in block order, exactly as a separate one-block
+// sum kernel would (so results are bitwise those of the two-launch form),
+// writes out[0..nq) (device memory or mapped host memory) and re-arms the
+// ticket.  No __threadfence: an agent-scope fence writes back the XCD's whole
+// L2 (every dirty line of the vectors the kernel just updated), which made
+// the fused kernels slower than the two launches (MI355X_MICROARCH.md,
+// handoff-flag: drained sc1 payload, then the flag).
+__device__ __forceinline__ void red_put(const RedOut& ro, int64_t idx, double v) {
+    __hip_atomic_store(ro.part + idx, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Block sums of nq <= NQ values at once, published with red_put at
+// part[base + q]: every wave reduces all values in registers, ONE barrier,
+// then thread q adds the four wave sums in wave order — the additions of nq
+// separate block_sum calls, with one barrier instead of 2*nq.
+template <int NQ>
+__device__ __forceinline__ void block_put_sums(double (&v)[NQ], int nq, const RedOut& ro, int64_t base) {
+    __shared__ double lds[4 * NQ];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+        if (q < nq) v[q] = wave_sum(v[q]);
+    if (lane == 0) {
+#pragma unroll
+        for (int q = 0; q < NQ; ++q)
+            if (q < nq) lds[w * NQ + q] = v[q];
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < nq) {
+        const int q = threadIdx.x;
+        red_put(ro, base + q, ((lds[q] + lds[NQ + q]) + lds[2 * NQ + q]) + lds[3 * NQ + q]);
+    }
+}
+
 __device__ void red_finish(const RedOut& ro, int nq, double* lds4) {
     __shared__ int is_last;
-    __threadfence();
-    __syncthreads();
-    if (threadIdx.x == 0) is_last = atomicAdd(ro.ticket, 1u) == gridDim.x - 1;
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __builtin_amdgcn_s_waitcnt(0);  // every partial store of this block is acknowledged ...
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __syncthreads();                // ... before the ticket moves
+    if (threadIdx.x == 0)
+        is_last = __hip_atomic_fetch_add(ro.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
     __syncthreads();
     if (!is_last) return;
-    __threadfence();
     const int nblk = (int)gridDim.x;
     for (int q = 0; q < nq; ++q) {
         double s = 0.0;
@@ -631,7 +664,7 @@ __global__ __launch_bounds__(kBlock) void gen_beta_kernel(uint64_t seed, double 
         c = causal ? 1.0 : 0.0;
     }
     c = block_sum(c, lds);
-    if (threadIdx.x == 0) ro.part[blockIdx.x] = c;
+    if (threadIdx.x == 0) red_put(ro, blockIdx.x, c);
     red_finish(ro, 1, lds);
 }
 
@@ -672,39 +705,46 @@ int red_blocks(int64_t n) {
     return (int)b;
 }
 
+// every term loads both operands unconditionally (a SUM term's b is its a,
+// set on the host) so a thread's loads for all terms are in flight together;
+// the op is a per-launch uniform selected per element
+template <int NT>
 __global__ __launch_bounds__(kBlock) void dots_kernel(DotArgs a, int64_t n, RedOut ro) {
     __shared__ double lds[4];
-    double acc[kMaxTerms];
+    double acc[NT];
 #pragma unroll
-    for (int q = 0; q < kMaxTerms; ++q) acc[q] = 0.0;
+    for (int q = 0; q < NT; ++q) acc[q] = 0.0;
     for (int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x; e < n; e += (int64_t)gridDim.x * kBlock) {
+        double va[NT], vb[NT];
 #pragma unroll
-        for (int q = 0; q < kMaxTerms; ++q) {
-            if (q < a.nt) {
-                const DotTerm& t = a.t[q];
-                if (t.op == DOT) {
-                    acc[q] += t.a[e] * t.b[e];
-                } else if (t.op == DIFF2) {
-                    const double d = t.a[e] - t.b[e];
-                    acc[q] += d * d;
-                } else {
-                    acc[q] += t.a[e];
-                }
-            }
+        for (int q = 0; q < NT; ++q) {
+            va[q] = a.t[q].a[e];
+            vb[q] = a.t[q].b[e];
+        }
+#pragma unroll
+        for (int q = 0; q < NT; ++q) {
+            const double d = va[q] - vb[q];
+            const double v = a.t[q].op == DOT ? va[q] * vb[q] : (a.t[q].op == DIFF2 ? d * d : va[q]);
+            acc[q] += v;
         }
     }
-#pragma unroll
-    for (int q = 0; q < kMaxTerms; ++q) {
-        if (q < a.nt) {
-            const double s = block_sum(acc[q], lds);
-            if (threadIdx.x == 0) ro.part[(int64_t)blockIdx.x * a.nt + q] = s;
-        }
-    }
-    red_finish(ro, a.nt, lds);
+    block_put_sums<NT>(acc, NT, ro, (int64_t)blockIdx.x * NT);
+    red_finish(ro, NT, lds);
 }
 
 hipError_t dots(const DotArgs& a, int64_t n, const RedOut& ro, hipStream_t st) {
-    hipLaunchKernelGGL(dots_kernel, dim3(red_blocks(n)), dim3(kBlock), 0, st, a, n, ro);
+    const dim3 g(red_blocks(n)), b(kBlock);
+    switch (a.nt) {
+        case 1: hipLaunchKernelGGL(dots_kernel<1>, g, b, 0, st, a, n, ro); break;
+        case 2: hipLaunchKernelGGL(dots_kernel<2>, g, b, 0, st, a, n, ro); break;
+        case 3: hipLaunchKernelGGL(dots_kernel<3>, g, b, 0, st, a, n, ro); break;
+        case 4: hipLaunchKernelGGL(dots_kernel<4>, g, b, 0, st, a, n, ro); break;
+        case 5: hipLaunchKernelGGL(dots_kernel<5>, g, b, 0, st, a, n, ro); break;
+        case 6: hipLaunchKernelGGL(dots_kernel<6>, g, b, 0, st, a, n, ro); break;
+        case 7: hipLaunchKernelGGL(dots_kernel<7>, g, b, 0, st, a, n, ro); break;
+        case 8: hipLaunchKernelGGL(dots_kernel<8>, g, b, 0, st, a, n, ro); break;
+        default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 
@@ -751,7 +791,7 @@ __global__ __launch_bounds__(kBlock) void denoise_kernel(int64_t M, const double
         acc += gd;
     }
     acc = block_sum(acc, lds);
-    if (threadIdx.x == 0) ro.part[blockIdx.x] = acc;
+    if (threadIdx.x == 0) red_put(ro, blockIdx.x, acc);
     red_finish(ro, 1, lds);
 }
 
@@ -786,7 +826,7 @@ __global__ __launch_bounds__(kBlock) void em_kernel(int64_t M, const double* __r
                                     exp(-(r * r) / 2 * a.max_sigma / a.noise_var / (a.noise_var + a.max_sigma)) /
                                     sum_of_elems);
     double s = block_sum(valid ? pin : 0.0, lds);
-    if (threadIdx.x == 0) ro.part[(int64_t)blockIdx.x * Q] = s;
+    if (threadIdx.x == 0) red_put(ro, (int64_t)blockIdx.x * Q, s);
     for (int j = 1; j < L; ++j) {
         const double beta = em_num(a, r, j) / sum_of_elems;
         const double g = a.gam1 * r / (1 / a.vars[j] + a.gam1);
@@ -794,8 +834,8 @@ __global__ __launch_bounds__(kBlock) void em_kernel(int64_t M, const double* __r
         const double sb = block_sum(valid ? beta * pin : 0.0, lds);
         const double sg = block_sum(valid ? gam * pin : 0.0, lds);
         if (threadIdx.x == 0) {
-            ro.part[(int64_t)blockIdx.x * Q + j] = sb;
-            ro.part[(int64_t)blockIdx.x * Q + (L - 1) + j] = sg;
+            red_put(ro, (int64_t)blockIdx.x * Q + j, sb);
+            red_put(ro, (int64_t)blockIdx.x * Q + (L - 1) + j, sg);
         }
     }
     red_finish(ro, Q, lds);
@@ -890,14 +930,7 @@ __global__ __launch_bounds__(kBlock) void cg_init_kernel(int K, int64_t M, CgVec
             }
         }
     }
-    for (int q = 0; q < 2 * K; ++q) {
-        double v = 0.0;
-#pragma unroll
-        for (int t = 0; t < 2 * kMaxRhs; ++t)
-            if (t == q) v = acc[t];
-        const double s = block_sum(v, lds);
-        if (threadIdx.x == 0) ro.part[(int64_t)blockIdx.x * 2 * K + q] = s;
-    }
+    block_put_sums<2 * kMaxRhs>(acc, 2 * K, ro, (int64_t)blockIdx.x * 2 * K);
     red_finish(ro, 2 * K, lds);
 }
 
@@ -932,14 +965,7 @@ __global__ __launch_bounds__(kBlock) void cg_update_kernel(int K, int64_t M, CgV
             }
         }
     }
-    for (int q = 0; q < 3 * K; ++q) {
-        double v = 0.0;
-#pragma unroll
-        for (int t = 0; t < 3 * kMaxRhs; ++t)
-            if (t == q) v = acc[t];
-        const double s = block_sum(v, lds);
-        if (threadIdx.x == 0) ro.part[(int64_t)blockIdx.x * 3 * K + q] = s;
-    }
+    block_put_sums<3 * kMaxRhs>(acc, 3 * K, ro, (int64_t)blockIdx.x * 3 * K);
     red_finish(ro, 3 * K, lds);
 }
 
@@ -1021,7 +1047,7 @@ __global__ __launch_bounds__(kBlock) void probit_denoise_kernel(int64_t N, const
         acc += 1 - ratio / den * (s * c + ratio);
     }
     acc = block_sum(acc, lds);
-    if (threadIdx.x == 0) ro.part[blockIdx.x] = acc;
+    if (threadIdx.x == 0) red_put(ro, blockIdx.x, acc);
     red_finish(ro, 1, lds);
 }
 
@@ -1050,10 +1076,7 @@ __global__ __launch_bounds__(kBlock) void confusion_kernel(int64_t N, int nz, co
                 cnt[4 * k + 3] += 1;
         }
     }
-    for (int q = 0; q < 4 * nz; ++q) {
-        const double s = block_sum(cnt[q], lds);
-        if (threadIdx.x == 0) ro.part[(int64_t)blockIdx.x * 4 * nz + q] = s;
-    }
+    block_put_sums<8>(cnt, 4 * nz, ro, (int64_t)blockIdx.x * 4 * nz);
     red_finish(ro, 4 * nz, lds);
 }
 
@@ -1314,6 +1337,17 @@ __global__ void mul_scalar_kernel(int64_t n, const double* __restrict__ x, doubl
 hipError_t mul_scalar(int64_t n, const double* x, double a, double* out, hipStream_t st) {
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(mul_scalar_kernel, dim3((unsigned)cdiv(n, kBlock)), dim3(kBlock), 0, st, n, x, a, out);
+    return hipGetLastError();
+}
+
+// completion flag for the host: a system-scope release store of seq into
+// mapped host memory, after everything earlier on the stream
+__global__ void signal_kernel(unsigned long long* flag, unsigned long long seq) {
+    __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+hipError_t signal_host(unsigned long long* flag, unsigned long long seq, hipStream_t st) {
+    hipLaunchKernelGGL(signal_kernel, dim3(1), dim3(1), 0, st, flag, seq);
     return hipGetLastError();
 }
 
