@@ -262,11 +262,9 @@ vampomi_status ax_dev(vampomi_ctx* c, int K, const double* const* x, double* out
     if (c->timing) {
         t.a = ev_get(c);
         t.b = ev_get(c);
-        HIPCHK(hipEventRecord(t.a, c->st));
     }
-    HIPCHK(vk::ax_partial(c->shard(), c->axp, K, xs, c->ax_part, c->st));
+    HIPCHK(vk::ax_partial(c->shard(), c->axp, K, xs, c->ax_part, c->st, vk::Timing{t.a, t.b}));
     if (c->timing) {
-        HIPCHK(hipEventRecord(t.b, c->st));
         t.cls = 0;
         t.K = K;
         t.bytes = pass_bytes(c, K);
@@ -301,11 +299,9 @@ vampomi_status atx_dev(vampomi_ctx* c, int K, const double* const* u, double* co
     if (c->timing) {
         t.a = ev_get(c);
         t.b = ev_get(c);
-        HIPCHK(hipEventRecord(t.a, c->st));
     }
-    HIPCHK(vk::atx(c->shard(), K, us, os, 1.0 / c->sqrtN, mode, tau, gam2, ps, nullptr, c->st));
+    HIPCHK(vk::atx(c->shard(), K, us, os, 1.0 / c->sqrtN, mode, tau, gam2, ps, nullptr, c->st, vk::Timing{t.a, t.b}));
     if (c->timing) {
-        HIPCHK(hipEventRecord(t.b, c->st));
         t.cls = 1;
         t.K = K;
         t.bytes = pass_bytes(c, K);
@@ -872,11 +868,9 @@ extern "C" vampomi_status vampomi_assoc_loo(vampomi_ctx* c, const double* est, d
     if (c->timing) {
         t.a = ev_get(c);
         t.b = ev_get(c);
-        HIPCHK(hipEventRecord(t.a, c->st));
     }
-    HIPCHK(vk::loo_sums(c->shard(), ymod, x1, std::sqrt((double)N), st, c->st));  // data.cpp:393-416
+    HIPCHK(vk::loo_sums(c->shard(), ymod, x1, std::sqrt((double)N), st, c->st, vk::Timing{t.a, t.b}));  // :393-416
     if (c->timing) {
-        HIPCHK(hipEventRecord(t.b, c->st));
         t.cls = 2;
         t.K = 1;
         // raw X once, ymod, x1, the five sums; per element 1 div, 2 mul + 1 add

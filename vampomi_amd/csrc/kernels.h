@@ -14,6 +14,8 @@ constexpr int kMaxTerms = 8;   // dot-product terms per reduction launch
 constexpr int kRedBlocks = 1024;  // max partial blocks of a reduction
 
 struct CPtrs { const double* p[kMaxRhs]; };
+// optional HIP events recorded by a launch's own dispatch (hipExtLaunchKernelGGL)
+struct Timing { hipEvent_t start = nullptr, stop = nullptr; };
 // Destination of a fused two-stage reduction (see red_finish in kernels.hip):
 // per-block partials in part, the final sums in out[0..nq) (device memory or
 // mapped host memory), ticket a zeroed device counter the kernel re-arms.
@@ -44,7 +46,8 @@ int ax_variant_count();
 bool set_ax_variant(int v);   // development hook (tools/kbench.py)
 int atx_variant_count();
 bool set_atx_variant(int v);
-hipError_t ax_partial(const Shard& s, const AxPlan& pl, int K, CPtrs x, double* part, hipStream_t st);
+hipError_t ax_partial(const Shard& s, const AxPlan& pl, int K, CPtrs x, double* part, hipStream_t st,
+                      const Timing& tm = Timing{});
 // out_k[j] = sum_c part[c][k][j]; if div > 0 then out_k[j] /= div
 hipError_t ax_reduce(const AxPlan& pl, int K, int64_t N, int64_t ld, const double* part, Ptrs out,
                      double div, hipStream_t st);
@@ -58,7 +61,7 @@ hipError_t vec_div(int K, int64_t n, int64_t ld, Ptrs v, double div, hipStream_t
 int atx_blocks(int64_t M, int K);
 std::string kernel_name(int which, int K, int mode);  // as rocprofv3 prints it
 hipError_t atx(const Shard& s, int K, CPtrs u, Ptrs out, double scale, int mode, double tau,
-               double gam2, CPtrs p, double* dp_part, hipStream_t st);
+               double gam2, CPtrs p, double* dp_part, hipStream_t st, const Timing& tm = Timing{});
 
 // ---- marker statistics (data::compute_markers_statistics) ----------------
 hipError_t marker_stats(const double* X, int64_t ld, int64_t N, int64_t M, double nonas,
@@ -135,7 +138,7 @@ hipError_t probit_p1(uint64_t seed, int64_t N, double* p1, hipStream_t st);
 // stats[5j + {0..4}] = sum X, sum X^2, sum X*ym, sum ym, sum ym^2 over the
 // samples of marker j (RAW X), ym = ymod + X / sqrtN * x1[j]  (data::pvals_loo)
 hipError_t loo_sums(const Shard& s, const double* ymod, const double* x1, double sqrtN, double* stats,
-                    hipStream_t st);
+                    hipStream_t st, const Timing& tm = Timing{});
 std::string loo_kernel_name();
 int loo_variant_count();
 bool set_loo_variant(int v);  // development hook (tools/kbench.py)

@@ -9,6 +9,8 @@
 // run and independent of the rank count's effect on scheduling.
 #include "kernels.h"
 
+#include <hip/hip_ext.h>
+
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -312,35 +314,39 @@ AxPlan ax_plan(int64_t N, int64_t M) {
     return p;
 }
 
+// launches go through hipExtLaunchKernelGGL: the optional start / stop events
+// are written by the kernel's own dispatch (no extra marker packets around it)
 template <int K, int R, int U, bool NT, bool IL = false>
-static void launch_ax(const Shard& s, const AxPlan& pl, CPtrs x, double* part, hipStream_t st) {
-    hipLaunchKernelGGL((ax_partial_kernel<K, R, U, NT, IL>), dim3(pl.tiles, pl.nchunks), dim3(kBlock), 0, st, s.X,
-                       s.ld, s.N, s.M, s.mave, s.msig, x, pl.chunk, part);
+static void launch_ax(const Shard& s, const AxPlan& pl, CPtrs x, double* part, hipStream_t st, const Timing& tm) {
+    hipExtLaunchKernelGGL((ax_partial_kernel<K, R, U, NT, IL>), dim3(pl.tiles, pl.nchunks), dim3(kBlock), 0, st,
+                          tm.start, tm.stop, 0, s.X, s.ld, s.N, s.M, s.mave, s.msig, x, pl.chunk, part);
 }
 
 template <int K>
-static bool launch_ax_v(int v, const Shard& s, const AxPlan& pl, CPtrs x, double* part, hipStream_t st) {
+static bool launch_ax_v(int v, const Shard& s, const AxPlan& pl, CPtrs x, double* part, hipStream_t st,
+                        const Timing& tm) {
     switch (v) {
-        case 0: launch_ax<K, 2, 8, true>(s, pl, x, part, st); return true;
-        case 1: launch_ax<K, 2, 8, false>(s, pl, x, part, st); return true;
-        case 2: launch_ax<K, 4, 4, true>(s, pl, x, part, st); return true;
-        case 3: launch_ax<K, 4, 8, true>(s, pl, x, part, st); return true;
-        case 4: launch_ax<K, 8, 4, true>(s, pl, x, part, st); return true;
-        case 5: launch_ax<K, 2, 8, true, true>(s, pl, x, part, st); return true;
-        case 6: launch_ax<K, 2, 4, true, true>(s, pl, x, part, st); return true;
-        case 7: launch_ax<K, 4, 4, true, true>(s, pl, x, part, st); return true;
-        case 8: launch_ax<K, 2, 12, true, true>(s, pl, x, part, st); return true;
+        case 0: launch_ax<K, 2, 8, true>(s, pl, x, part, st, tm); return true;
+        case 1: launch_ax<K, 2, 8, false>(s, pl, x, part, st, tm); return true;
+        case 2: launch_ax<K, 4, 4, true>(s, pl, x, part, st, tm); return true;
+        case 3: launch_ax<K, 4, 8, true>(s, pl, x, part, st, tm); return true;
+        case 4: launch_ax<K, 8, 4, true>(s, pl, x, part, st, tm); return true;
+        case 5: launch_ax<K, 2, 8, true, true>(s, pl, x, part, st, tm); return true;
+        case 6: launch_ax<K, 2, 4, true, true>(s, pl, x, part, st, tm); return true;
+        case 7: launch_ax<K, 4, 4, true, true>(s, pl, x, part, st, tm); return true;
+        case 8: launch_ax<K, 2, 12, true, true>(s, pl, x, part, st, tm); return true;
         default: return false;
     }
 }
 
-hipError_t ax_partial(const Shard& s, const AxPlan& pl, int K, CPtrs x, double* part, hipStream_t st) {
+hipError_t ax_partial(const Shard& s, const AxPlan& pl, int K, CPtrs x, double* part, hipStream_t st,
+                      const Timing& tm) {
     bool ok = false;
     switch (K) {
-        case 1: ok = launch_ax_v<1>(pl.variant, s, pl, x, part, st); break;
-        case 2: ok = launch_ax_v<2>(pl.variant, s, pl, x, part, st); break;
-        case 3: ok = launch_ax_v<3>(pl.variant, s, pl, x, part, st); break;
-        case 4: ok = launch_ax_v<4>(pl.variant, s, pl, x, part, st); break;
+        case 1: ok = launch_ax_v<1>(pl.variant, s, pl, x, part, st, tm); break;
+        case 2: ok = launch_ax_v<2>(pl.variant, s, pl, x, part, st, tm); break;
+        case 3: ok = launch_ax_v<3>(pl.variant, s, pl, x, part, st, tm); break;
+        case 4: ok = launch_ax_v<4>(pl.variant, s, pl, x, part, st, tm); break;
         default: break;
     }
     if (!ok) return hipErrorInvalidValue;
@@ -533,43 +539,44 @@ int atx_blocks(int64_t M, int K) { return (int)cdiv(M, 4 * kAtxVariants[atx_vari
 
 template <int G, int K, int MODE, int UJ, bool NT>
 static void launch_atx(const Shard& s, CPtrs u, Ptrs out, double scale, double tau, double gam2, CPtrs p,
-                       double* dp_part, hipStream_t st) {
-    hipLaunchKernelGGL((atx_kernel<G, K, MODE, UJ, NT>), dim3((unsigned)cdiv(s.M, 4 * G)), dim3(kBlock), 0, st, s.X,
-                       s.ld, s.N, s.M, s.mave, s.msig, u, out, scale, tau, gam2, p, dp_part);
+                       double* dp_part, hipStream_t st, const Timing& tm) {
+    hipExtLaunchKernelGGL((atx_kernel<G, K, MODE, UJ, NT>), dim3((unsigned)cdiv(s.M, 4 * G)), dim3(kBlock), 0, st,
+                          tm.start, tm.stop, 0, s.X, s.ld, s.N, s.M, s.mave, s.msig, u, out, scale, tau, gam2, p,
+                          dp_part);
 }
 
 template <int K, int MODE>
 static bool launch_atx_v(int v, const Shard& s, CPtrs u, Ptrs out, double scale, double tau, double gam2, CPtrs p,
-                         double* dp, hipStream_t st) {
+                         double* dp, hipStream_t st, const Timing& tm) {
     switch (v) {
-        case 0: launch_atx<4, K, MODE, 2, true>(s, u, out, scale, tau, gam2, p, dp, st); return true;
-        case 1: launch_atx<4, K, MODE, 2, false>(s, u, out, scale, tau, gam2, p, dp, st); return true;
-        case 2: launch_atx<2, K, MODE, 2, true>(s, u, out, scale, tau, gam2, p, dp, st); return true;
-        case 3: launch_atx<8, K, MODE, 2, true>(s, u, out, scale, tau, gam2, p, dp, st); return true;
-        case 4: launch_atx<4, K, MODE, 4, true>(s, u, out, scale, tau, gam2, p, dp, st); return true;
-        case 5: launch_atx<4, K, MODE, 1, true>(s, u, out, scale, tau, gam2, p, dp, st); return true;
-        case 6: launch_atx<8, K, MODE, 1, true>(s, u, out, scale, tau, gam2, p, dp, st); return true;
-        case 7: launch_atx<2, K, MODE, 4, true>(s, u, out, scale, tau, gam2, p, dp, st); return true;
+        case 0: launch_atx<4, K, MODE, 2, true>(s, u, out, scale, tau, gam2, p, dp, st, tm); return true;
+        case 1: launch_atx<4, K, MODE, 2, false>(s, u, out, scale, tau, gam2, p, dp, st, tm); return true;
+        case 2: launch_atx<2, K, MODE, 2, true>(s, u, out, scale, tau, gam2, p, dp, st, tm); return true;
+        case 3: launch_atx<8, K, MODE, 2, true>(s, u, out, scale, tau, gam2, p, dp, st, tm); return true;
+        case 4: launch_atx<4, K, MODE, 4, true>(s, u, out, scale, tau, gam2, p, dp, st, tm); return true;
+        case 5: launch_atx<4, K, MODE, 1, true>(s, u, out, scale, tau, gam2, p, dp, st, tm); return true;
+        case 6: launch_atx<8, K, MODE, 1, true>(s, u, out, scale, tau, gam2, p, dp, st, tm); return true;
+        case 7: launch_atx<2, K, MODE, 4, true>(s, u, out, scale, tau, gam2, p, dp, st, tm); return true;
         default: return false;
     }
 }
 
 hipError_t atx(const Shard& s, int K, CPtrs u, Ptrs out, double scale, int mode, double tau, double gam2, CPtrs p,
-               double* dp_part, hipStream_t st) {
+               double* dp_part, hipStream_t st, const Timing& tm) {
     const int v = atx_variant_for(K);
     bool ok = false;
     if (mode == 0) {
         switch (K) {
-            case 1: ok = launch_atx_v<1, 0>(v, s, u, out, scale, tau, gam2, p, dp_part, st); break;
-            case 2: ok = launch_atx_v<2, 0>(v, s, u, out, scale, tau, gam2, p, dp_part, st); break;
-            case 3: ok = launch_atx_v<3, 0>(v, s, u, out, scale, tau, gam2, p, dp_part, st); break;
+            case 1: ok = launch_atx_v<1, 0>(v, s, u, out, scale, tau, gam2, p, dp_part, st, tm); break;
+            case 2: ok = launch_atx_v<2, 0>(v, s, u, out, scale, tau, gam2, p, dp_part, st, tm); break;
+            case 3: ok = launch_atx_v<3, 0>(v, s, u, out, scale, tau, gam2, p, dp_part, st, tm); break;
             default: break;
         }
     } else {
         switch (K) {
-            case 1: ok = launch_atx_v<1, 1>(v, s, u, out, scale, tau, gam2, p, dp_part, st); break;
-            case 2: ok = launch_atx_v<2, 1>(v, s, u, out, scale, tau, gam2, p, dp_part, st); break;
-            case 3: ok = launch_atx_v<3, 1>(v, s, u, out, scale, tau, gam2, p, dp_part, st); break;
+            case 1: ok = launch_atx_v<1, 1>(v, s, u, out, scale, tau, gam2, p, dp_part, st, tm); break;
+            case 2: ok = launch_atx_v<2, 1>(v, s, u, out, scale, tau, gam2, p, dp_part, st, tm); break;
+            case 3: ok = launch_atx_v<3, 1>(v, s, u, out, scale, tau, gam2, p, dp_part, st, tm); break;
             default: break;
         }
     }
@@ -1214,23 +1221,23 @@ std::string loo_kernel_name() {
 
 template <int G, int UJ, bool FD>
 static void launch_loo(const Shard& s, const double* ymod, const double* x1, double sqrtN, double* stats,
-                       hipStream_t st) {
-    hipLaunchKernelGGL((loo_kernel<G, UJ, FD>), dim3((unsigned)cdiv(s.M, 4 * G)), dim3(kBlock), 0, st, s.X, s.ld,
-                       s.N, s.M, ymod, x1, sqrtN, stats);
+                       hipStream_t st, const Timing& tm) {
+    hipExtLaunchKernelGGL((loo_kernel<G, UJ, FD>), dim3((unsigned)cdiv(s.M, 4 * G)), dim3(kBlock), 0, st, tm.start,
+                          tm.stop, 0, s.X, s.ld, s.N, s.M, ymod, x1, sqrtN, stats);
 }
 
 hipError_t loo_sums(const Shard& s, const double* ymod, const double* x1, double sqrtN, double* stats,
-                    hipStream_t st) {
+                    hipStream_t st, const Timing& tm) {
     if (s.M <= 0) return hipSuccess;
     switch (g_loo_variant) {
-        case 0: launch_loo<4, 2, true>(s, ymod, x1, sqrtN, stats, st); break;
-        case 1: launch_loo<4, 2, false>(s, ymod, x1, sqrtN, stats, st); break;
-        case 2: launch_loo<2, 2, true>(s, ymod, x1, sqrtN, stats, st); break;
-        case 3: launch_loo<8, 1, true>(s, ymod, x1, sqrtN, stats, st); break;
-        case 4: launch_loo<4, 1, true>(s, ymod, x1, sqrtN, stats, st); break;
-        case 5: launch_loo<4, 4, true>(s, ymod, x1, sqrtN, stats, st); break;
-        case 6: launch_loo<2, 4, true>(s, ymod, x1, sqrtN, stats, st); break;
-        case 7: launch_loo<8, 2, true>(s, ymod, x1, sqrtN, stats, st); break;
+        case 0: launch_loo<4, 2, true>(s, ymod, x1, sqrtN, stats, st, tm); break;
+        case 1: launch_loo<4, 2, false>(s, ymod, x1, sqrtN, stats, st, tm); break;
+        case 2: launch_loo<2, 2, true>(s, ymod, x1, sqrtN, stats, st, tm); break;
+        case 3: launch_loo<8, 1, true>(s, ymod, x1, sqrtN, stats, st, tm); break;
+        case 4: launch_loo<4, 1, true>(s, ymod, x1, sqrtN, stats, st, tm); break;
+        case 5: launch_loo<4, 4, true>(s, ymod, x1, sqrtN, stats, st, tm); break;
+        case 6: launch_loo<2, 4, true>(s, ymod, x1, sqrtN, stats, st, tm); break;
+        case 7: launch_loo<8, 2, true>(s, ymod, x1, sqrtN, stats, st, tm); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
