@@ -217,6 +217,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local)  # torch's own context on this rank's GPU, not on GPU 0
     n = world
     if world > 1:
         dist.init_process_group("gloo")
