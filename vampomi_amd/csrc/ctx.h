@@ -97,6 +97,8 @@ struct vampomi_ctx {
 vampomi_status dev_alloc(double** p, size_t n);
 void dev_free(double*& p);
 vampomi_status host_sync(vampomi_ctx* c);
+// spins until the context's host flag reaches seq (stores from the stream)
+vampomi_status wait_flag(vampomi_ctx* c, unsigned long long seq);
 vampomi_status allreduce_dev(vampomi_ctx* c, double* buf, size_t n);
 void resolve_timing(vampomi_ctx* c);
 void release_ctx_resources(vampomi_ctx* c);
@@ -135,6 +137,7 @@ class DotBatch {
     };
     vampomi_ctx* c_;
     int nsync_ = 0, nlocal_ = 0;
+    unsigned long long last_seq_ = 0;  // one rank: flag value the last reduction kernel stores
     std::vector<Sink> sinks_;
 };
 

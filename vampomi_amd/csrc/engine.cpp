@@ -100,23 +100,17 @@ static double pass_flops(const vampomi_ctx* c, int K) { return (double)c->N * (d
 // ---------------------------------------------------------------------------
 // reductions
 // ---------------------------------------------------------------------------
-// Waits until everything queued on the context's stream has finished: a
-// 1-thread kernel stores the next sequence number into a mapped host word
-// (system-scope release) and the host spins on it — a few microseconds
-// sooner than hipStreamSynchronize's completion path, once per dependency
-// level of the iteration.  Faults are still reported: the spin polls
-// hipStreamQuery, and gives up after 10 minutes.
-vampomi_status host_sync(vampomi_ctx* c) {
-    c->stats.host_syncs++;
-    if (!c->h_flag) {
-        HIPCHK(hipStreamSynchronize(c->st));
-        return VAMPOMI_OK;
-    }
-    const unsigned long long seq = ++c->sync_seq;
-    HIPCHK(vk::signal_host(c->d_flag, seq, c->st));
+// Host waits without hipStreamSynchronize's completion path: the stream
+// stores increasing sequence numbers into a mapped host word (system-scope
+// release) and the host spins on it — a few microseconds sooner, once per
+// dependency level of the iteration.  host_sync waits for everything queued
+// (a 1-thread kernel stores the flag); a one-rank DotBatch waits for its last
+// reduction kernel, whose last block stores the flag itself.  Faults are
+// still reported: the spin polls hipStreamQuery, and gives up after 10 min.
+vampomi_status wait_flag(vampomi_ctx* c, unsigned long long seq) {
     const auto t0 = std::chrono::steady_clock::now();
     for (uint64_t spin = 1;; ++spin) {
-        if (__atomic_load_n(c->h_flag, __ATOMIC_ACQUIRE) == seq) return VAMPOMI_OK;
+        if (__atomic_load_n(c->h_flag, __ATOMIC_ACQUIRE) >= seq) return VAMPOMI_OK;
         if ((spin & 4095) == 0) {
             const hipError_t e = hipStreamQuery(c->st);
             if (e != hipSuccess && e != hipErrorNotReady)
@@ -130,6 +124,17 @@ vampomi_status host_sync(vampomi_ctx* c) {
         }
         __builtin_ia32_pause();
     }
+}
+
+vampomi_status host_sync(vampomi_ctx* c) {
+    c->stats.host_syncs++;
+    if (!c->h_flag) {
+        HIPCHK(hipStreamSynchronize(c->st));
+        return VAMPOMI_OK;
+    }
+    const unsigned long long seq = ++c->sync_seq;
+    HIPCHK(vk::signal_host(c->d_flag, seq, c->st));
+    return wait_flag(c, seq);
 }
 
 // ---------------------------------------------------------------------------
@@ -205,6 +210,12 @@ vampomi_status DotBatch::sink(int nq, bool sync, double* out, vk::RedOut* ro) {
     ro->part = c_->red_part;
     ro->out = (c_->use_comm ? c_->scal : c_->d_hscal) + base + used;
     ro->ticket = c_->ticket;
+    ro->flag = nullptr;
+    ro->seq = 0;
+    if (!c_->use_comm && c_->h_flag) {  // results land in host memory: the kernel flags their arrival
+        ro->flag = c_->d_flag;
+        ro->seq = last_seq_ = ++c_->sync_seq;
+    }
     sinks_.push_back(Sink{base + used, nq, out});
     used += nq;
     return VAMPOMI_OK;
@@ -237,11 +248,17 @@ vampomi_status DotBatch::flush() {
             HIPCHK(hipMemcpyAsync(c_->h_scal + SL_LOCAL, c_->scal + SL_LOCAL, sizeof(double) * nlocal_,
                                   hipMemcpyDeviceToHost, c_->st));
     }
-    STCHK(host_sync(c_));
+    if (!c_->use_comm && last_seq_) {
+        c_->stats.host_syncs++;
+        STCHK(wait_flag(c_, last_seq_));
+    } else {
+        STCHK(host_sync(c_));
+    }
     for (const Sink& k : sinks_)
         for (int i = 0; i < k.count; ++i) k.out[i] = c_->h_scal[k.slot + i];
     sinks_.clear();
     nsync_ = nlocal_ = 0;
+    last_seq_ = 0;
     return VAMPOMI_OK;
 }
 

@@ -18,8 +18,15 @@ struct CPtrs { const double* p[kMaxRhs]; };
 struct Timing { hipEvent_t start = nullptr, stop = nullptr; };
 // Destination of a fused two-stage reduction (see red_finish in kernels.hip):
 // per-block partials in part, the final sums in out[0..nq) (device memory or
-// mapped host memory), ticket a zeroed device counter the kernel re-arms.
-struct RedOut { double* part; double* out; unsigned* ticket; };
+// mapped host memory), ticket a zeroed device counter the kernel re-arms;
+// flag (may be null): the last block stores seq there (system scope, after out)
+struct RedOut {
+    double* part;
+    double* out;
+    unsigned* ticket;
+    unsigned long long* flag;
+    unsigned long long seq;
+};
 struct Ptrs { double* p[kMaxRhs]; };
 
 // The device-resident marker shard: M columns (markers) of N samples, column

@@ -96,7 +96,11 @@ __device__ void red_finish(const RedOut& ro, int nq, double* lds4) {
         s = block_sum(s, lds4);
         if (threadIdx.x == 0) ro.out[q] = s;
     }
-    if (threadIdx.x == 0) __hip_atomic_store(ro.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) {
+        __hip_atomic_store(ro.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // host completion flag: the results above are visible to the host first
+        if (ro.flag) __hip_atomic_store(ro.flag, ro.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 __device__ __forceinline__ v2d ld_stream(const double* p) {
