@@ -1,0 +1,88 @@
+"""GPU parity in corners the default runs do not reach: the PCG entry point
+with a warm start and with the Onsager stop (vamp::precondCG_solver,
+src/vamp.cpp:664-757, restated in numpy below), and VAMP runs with very few
+markers (one A.x chunk, fewer markers than one A^T wave group) and with N
+much smaller or larger than Mt."""
+import numpy as np
+import pytest
+
+from conftest import relerr
+from _data import make_problem
+
+pytestmark = pytest.mark.gpu
+
+va = pytest.importorskip("vampomi_amd")
+from oracle import pyoracle as O  # noqa: E402  (checker)
+
+
+def pcg_numpy(X, mave, msig, v, mu0, tau, gam2, onsager, max_iter, tol):
+    """precondCG_solver, line by line (numpy dots; the engine's differ only in
+    summation order)."""
+    N = X.shape[1]
+
+    def lmmse(u):
+        if not np.any(u):
+            return np.zeros_like(u)
+        return tau * O.atx(X, mave, msig, O.ax(X, mave, msig, u)) + gam2 * u
+
+    diag = tau * (N - 1) / N + gam2
+    mu = mu0.copy()
+    r = v - lmmse(mu)
+    z = r / diag
+    p = z.copy()
+    prev, its = 0.0, 0
+    norm_v = np.sqrt(v @ v)
+    for i in range(max_iter):
+        its = i + 1
+        d = lmmse(p)
+        rz = r @ z
+        alpha = rz / (d @ p)
+        mu = mu + alpha * p
+        if onsager:
+            ons = gam2 * (v @ mu)
+            rel = abs((ons - prev) / ons) if ons != 0 else 1
+            if rel < 1e-8:
+                break
+            prev = ons
+        beta = rz ** -1
+        r = r - d * alpha
+        z = r / diag
+        beta *= r @ z
+        p = z + beta * p
+        if np.sqrt(r @ r) / norm_v < tol:
+            break
+    return mu, its
+
+
+@pytest.mark.parametrize("warm,onsager", [(False, False), (True, False), (False, True), (True, True)])
+def test_pcg_entry_point(warm, onsager):
+    N, Mt = 700, 1300
+    X, _, _ = make_problem(N, Mt, seed=9)
+    mave, msig = O.marker_stats(X)
+    rng = np.random.default_rng(4)
+    v = rng.normal(size=Mt)
+    mu0 = rng.normal(size=Mt) * 0.1 if warm else np.zeros(Mt)
+    tau, gam2 = 1.7, 0.4
+    ref, its = pcg_numpy(X, mave, msig, v, mu0, tau, gam2, onsager, 200, 1e-9)
+    with va.Data(N, Mt) as d:
+        d.load_meth(X)
+        mu, it = d.pcg(v, tau, gam2, mu0=mu0 if warm else None, onsager=onsager, tol=1e-9, max_iter=200)
+    assert it == its
+    assert relerr(mu, ref) < 1e-11
+
+
+@pytest.mark.parametrize("N,Mt", [(500, 40), (300, 7), (64, 3000), (6000, 120)])
+def test_vamp_shapes(N, Mt):
+    X, y, beta = make_problem(N, Mt, seed=2)
+    kw = dict(max_iter=8, stop_criteria_thr=0.0)
+    ref = O.vamp_infere(X, y, Mt, true_signal=beta, **kw)
+    with va.Data(N, Mt) as d:
+        d.load_meth(X)
+        d.set_phen(y, standardize=False)
+        v = va.Vamp(d, va.VampOptions(**kw), true_signal=beta)
+        v.infere(keep_hist=True)
+        s = v.summary()
+        x1 = v.x1_hist[: s["iterations"], : d.M]
+    assert s["cg_iters"] == ref["cg_iters"].tolist() and s["ons_iters"] == ref["ons_iters"].tolist()
+    for k in range(s["iterations"]):
+        assert relerr(x1[k], ref["x1_hist"][k]) <= 1e-10, k
