@@ -239,16 +239,24 @@ vampomi_status DotBatch::add(std::initializer_list<vk::DotTerm> terms, int64_t n
 
 vampomi_status DotBatch::flush() {
     if (sinks_.empty()) return VAMPOMI_OK;
-    if (c_->use_comm) {  // slots in device memory: all-reduce the synced ones, then one copy each
+    if (c_->use_comm) {  // slots in device memory: all-reduce the synced ones, then publish both ranges
         if (nsync_ > 0) STCHK(allreduce_dev(c_, c_->scal + SL_SYNC, (size_t)nsync_));
-        if (nsync_ > 0)
-            HIPCHK(hipMemcpyAsync(c_->h_scal + SL_SYNC, c_->scal + SL_SYNC, sizeof(double) * nsync_,
-                                  hipMemcpyDeviceToHost, c_->st));
-        if (nlocal_ > 0)
-            HIPCHK(hipMemcpyAsync(c_->h_scal + SL_LOCAL, c_->scal + SL_LOCAL, sizeof(double) * nlocal_,
-                                  hipMemcpyDeviceToHost, c_->st));
-    }
-    if (!c_->use_comm && last_seq_) {
+        if (c_->h_flag) {
+            const unsigned long long seq = ++c_->sync_seq;
+            HIPCHK(vk::publish_host(c_->scal + SL_SYNC, nsync_, c_->d_hscal + SL_SYNC, c_->scal + SL_LOCAL, nlocal_,
+                                    c_->d_hscal + SL_LOCAL, c_->d_flag, seq, c_->st));
+            c_->stats.host_syncs++;
+            STCHK(wait_flag(c_, seq));
+        } else {
+            if (nsync_ > 0)
+                HIPCHK(hipMemcpyAsync(c_->h_scal + SL_SYNC, c_->scal + SL_SYNC, sizeof(double) * nsync_,
+                                      hipMemcpyDeviceToHost, c_->st));
+            if (nlocal_ > 0)
+                HIPCHK(hipMemcpyAsync(c_->h_scal + SL_LOCAL, c_->scal + SL_LOCAL, sizeof(double) * nlocal_,
+                                      hipMemcpyDeviceToHost, c_->st));
+            STCHK(host_sync(c_));
+        }
+    } else if (last_seq_) {
         c_->stats.host_syncs++;
         STCHK(wait_flag(c_, last_seq_));
     } else {

@@ -1362,4 +1362,20 @@ hipError_t signal_host(unsigned long long* flag, unsigned long long seq, hipStre
     return hipGetLastError();
 }
 
+// multi-rank DotBatch results: after the all-reduce, copy the synced and the
+// local slot ranges into mapped host memory, then raise the host flag
+__global__ void publish_kernel(const double* __restrict__ a, int na, double* __restrict__ ha, const double* __restrict__ b,
+                               int nb, double* __restrict__ hb, unsigned long long* flag, unsigned long long seq) {
+    for (int i = threadIdx.x; i < na; i += blockDim.x) ha[i] = a[i];
+    for (int i = threadIdx.x; i < nb; i += blockDim.x) hb[i] = b[i];
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+hipError_t publish_host(const double* a, int na, double* ha, const double* b, int nb, double* hb,
+                        unsigned long long* flag, unsigned long long seq, hipStream_t st) {
+    hipLaunchKernelGGL(publish_kernel, dim3(1), dim3(256), 0, st, a, na, ha, b, nb, hb, flag, seq);
+    return hipGetLastError();
+}
+
 }  // namespace vk
