@@ -19,6 +19,7 @@
  *   vamp::lmmse_mult           src/vamp.cpp:645-662     -> vampomi_lmmse_mult (COLLECTIVE)
  *   vamp::precondCG_solver     src/vamp.cpp:664-757     -> vampomi_pcg      (COLLECTIVE)
  *   vamp::g1 / vamp::g1d       src/vamp.cpp:440-492     -> vampomi_denoise  (COLLECTIVE: alpha1 sum)
+ *   vamp::updatePrior          src/vamp.cpp:531-643     -> vampomi_update_prior (COLLECTIVE)
  *   vamp::g1_bin_class / g1d_bin_class
  *        src/vamp_probit.cpp:469-488                    -> vampomi_denoise_bin
  *   vamp::vamp + vamp::infere / infere_linear / infere_bin_class
@@ -142,6 +143,14 @@ vampomi_status vampomi_pcg(vampomi_ctx* ctx, const double* v, const double* mu0,
 vampomi_status vampomi_denoise(vampomi_ctx* ctx, const double* r1, double gam1, const double* probs,
                                const double* vars, int L, double* x1, double* x1d, double* sum_d,
                                int mem);
+
+/* vamp::updatePrior (src/vamp.cpp:531-643): EM_max_iter EM passes over r1 (this
+ * shard's M values) at noise precision gam1 for the mixture (*L, probs, vars;
+ * vars ALREADY multiplied by N), then the merging of variances closer than
+ * merge_vars_thr; the mixture is updated in place (*L may shrink). COLLECTIVE */
+vampomi_status vampomi_update_prior(vampomi_ctx* ctx, const double* r1, double gam1, int* L, double* probs,
+                                    double* vars, int EM_max_iter, double EM_err_thr, int learn_vars,
+                                    double merge_vars_thr, int mem);
 
 /* probit z-denoiser: z1[i] = g1_bin_class(p1[i], tau1, y[i]) with the context's
  * phenotype y (raw 0/1), *sum_d = sum_i g1d_bin_class(p1[i], tau1, y[i]) (local:

@@ -98,6 +98,8 @@ def load() -> C.CDLL:
         lib.orc_assoc_loo.argtypes = [C.POINTER(Problem), p, p, p]
         lib.orc_assoc_se.argtypes = [p, i64, d, i64, p]
         lib.orc_test_metrics.argtypes = [C.POINTER(Problem), p, p]
+        lib.orc_update_prior.restype = C.c_int
+        lib.orc_update_prior.argtypes = [C.POINTER(Problem), p, d, C.POINTER(Params), C.POINTER(C.c_int), p, p]
         _lib = lib
     return _lib
 
@@ -222,6 +224,24 @@ def test_metrics(X: np.ndarray, y: np.ndarray, est: np.ndarray, alpha_scale: flo
 
 
 test_metrics.__test__ = False  # not a pytest test
+
+
+def update_prior(r1: np.ndarray, gam1: float, probs, vars_scaled, N: int, Mt: Optional[int] = None,
+                 EM_max_iter=1, EM_err_thr=1e-2, learn_vars=1, merge_vars_thr=0.5):
+    """updatePrior (src/vamp.cpp:531-643) on one shard's r1: returns (probs, vars)."""
+    lib = load()
+    r1 = np.ascontiguousarray(r1, dtype=np.float64)
+    M = len(r1)
+    pb = Problem(N=N, Mt=Mt or M, M=M, S=0, ld=N, rank=0, nranks=1, X=None, mave=None, msig=None, y=None,
+                 true_signal=None, x1hat_init=None, allreduce=ALLREDUCE_FN(), user=None)
+    pr = Params(EM_max_iter=EM_max_iter, EM_err_thr=EM_err_thr, learn_vars=learn_vars, merge_vars_thr=merge_vars_thr)
+    L = C.c_int(len(probs))
+    pp, vv = np.zeros(MAX_L), np.zeros(MAX_L)
+    pp[: L.value] = probs
+    vv[: L.value] = vars_scaled
+    if lib.orc_update_prior(C.byref(pb), _p(r1), gam1, C.byref(pr), C.byref(L), _p(pp), _p(vv)) != 0:
+        raise ValueError("bad mixture")
+    return pp[: L.value].copy(), vv[: L.value].copy()
 
 
 def assoc_se(r1: np.ndarray, gam1: float, N: int) -> np.ndarray:

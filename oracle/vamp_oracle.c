@@ -1320,3 +1320,34 @@ void orc_test_metrics(const orc_problem* pb, const double* est, double* out) {
     free(z);
     free(d);
 }
+
+/* updatePrior alone (src/vamp.cpp:531-643), for tests: r1 (M local values),
+ * gam1, the mixture (*L, probs, vars multiplied by N) updated in place */
+int orc_update_prior(const orc_problem* pb, const double* r1, double gam1, const orc_params* prm, int* L,
+                     double* probs, double* vars) {
+    orc_vamp s;
+    memset(&s, 0, sizeof s);
+    s.pb = pb;
+    s.N = pb->N;
+    s.M = pb->M;
+    s.Mt = pb->Mt;
+    s.L = *L;
+    if (s.L < 1 || s.L > ORC_MAX_L) return -1;
+    for (int j = 0; j < s.L; ++j) {
+        s.probs[j] = probs[j];
+        s.vars[j] = vars[j];
+    }
+    s.gam1 = gam1;
+    s.r1 = (double*)r1;
+    s.EM_max_iter = prm->EM_max_iter;
+    s.EM_err_thr = prm->EM_err_thr;
+    s.learn_vars = prm->learn_vars;
+    s.merge_vars_thr = prm->merge_vars_thr;
+    update_prior(&s);
+    *L = s.L;
+    for (int j = 0; j < s.L; ++j) {
+        probs[j] = s.probs[j];
+        vars[j] = s.vars[j];
+    }
+    return 0;
+}

@@ -163,6 +163,11 @@ void orc_assoc_se(const double* r1, int64_t M, double gam1, int64_t N, double* p
  * out[0] = R2 test, out[1] = z correlation test (squared) */
 void orc_test_metrics(const orc_problem* pb, const double* est, double* out);
 
+/* updatePrior alone (src/vamp.cpp:531-643): uses prm's EM_max_iter,
+ * EM_err_thr, learn_vars, merge_vars_thr; vars multiplied by N */
+int orc_update_prior(const orc_problem* pb, const double* r1, double gam1, const orc_params* prm, int* L,
+                     double* probs, double* vars);
+
 /* ---- output writers (src/utilities.cpp:241-249, 366-401) ---- */
 int orc_store_vec(const char* path, const double* v, int64_t S, int64_t M);
 int orc_csv_header(const char* path, const char* const* fields, int n);

@@ -86,3 +86,18 @@ def test_vamp_shapes(N, Mt):
     assert s["cg_iters"] == ref["cg_iters"].tolist() and s["ons_iters"] == ref["ons_iters"].tolist()
     for k in range(s["iterations"]):
         assert relerr(x1[k], ref["x1_hist"][k]) <= 1e-10, k
+
+
+@pytest.mark.parametrize("em,lv,merge", [(1, 1, 0.5), (3, 1, 0.5), (4, 0, 0.0), (2, 1, 5.0)])
+def test_update_prior_entry_point(em, lv, merge):
+    N, Mt = 900, 2100
+    X, _, _ = make_problem(N, Mt, seed=12)
+    rng = np.random.default_rng(em)
+    r1 = np.concatenate([rng.normal(size=Mt - 300) * 0.02, rng.normal(size=300) * 0.4])
+    vars_s = np.array(O.DEFAULT_VARS) * N
+    po, vo = O.update_prior(r1, 35.0, O.DEFAULT_PROBS, vars_s, N, EM_max_iter=em, learn_vars=lv, merge_vars_thr=merge)
+    with va.Data(N, Mt) as d:
+        d.load_meth(X)
+        p, v = d.update_prior(r1, 35.0, O.DEFAULT_PROBS, vars_s, EM_max_iter=em, learn_vars=lv, merge_vars_thr=merge)
+    assert len(p) == len(po)
+    assert np.allclose(p, po, rtol=1e-12, atol=0) and np.allclose(v, vo, rtol=1e-12, atol=0)

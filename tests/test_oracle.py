@@ -169,3 +169,37 @@ def test_vamp_oracle_shard_invariance(P, model):
         assert r["ons_iters"].tolist() == one["ons_iters"].tolist()
         assert r["L"].tolist() == one["L"].tolist()
         assert np.allclose(r["params"], one["params"], rtol=1e-11 if model == "linear" else 1e-5)
+
+
+def test_update_prior_one_em_pass_numpy():
+    """updatePrior (src/vamp.cpp:531-643), one EM pass without merging, against
+    a numpy restatement of the responsibilities and moment updates."""
+    rng = np.random.default_rng(3)
+    N = 800
+    r1 = np.concatenate([rng.normal(size=700) * 0.02, rng.normal(size=300) * 0.3])
+    gam1 = 40.0
+    probs = np.array([0.9, 0.06, 0.04])
+    vars_ = np.array([0.0, 1e-3, 5e-2]) * N
+    p, v = O.update_prior(r1, gam1, probs, vars_, N, EM_max_iter=1, merge_vars_thr=0.0)
+    nv = 1 / gam1
+    lam = 1 - probs[0]
+    om = probs[1:] / lam
+    vmax = vars_.max()
+    num = lam * om[None, :] * np.exp(-(r1[:, None] ** 2) / 2 * (vmax - vars_[None, 1:]) / (vars_[None, 1:] + nv)
+                                     / (vmax + nv)) / np.sqrt(vars_[None, 1:] + nv) / np.sqrt(2 * np.pi)
+    s = num.sum(1)
+    beta = num / s[:, None]
+    pin = 1 / (1 + (1 - lam) / np.sqrt(2 * np.pi * nv) * np.exp(-(r1 ** 2) / 2 * vmax / nv / (nv + vmax)) / s)
+    lam_new = pin.sum() / len(r1)
+    g = gam1 * r1[:, None] / (1 / vars_[None, 1:] + gam1)
+    vv = 1 / (1 / vars_[1:] + gam1)
+    gam = beta * (g ** 2 + vv[None, :])
+    res = (beta * pin[:, None]).sum(0)
+    res_g = (gam * pin[:, None]).sum(0)
+    exp_v = np.concatenate([[0.0], res_g / res])
+    exp_p = np.concatenate([[1 - lam_new], lam_new * res / pin.sum()])
+    assert np.allclose(v, exp_v, rtol=1e-12) and np.allclose(p, exp_p, rtol=1e-12)
+    # merging: equal slabs collapse into one component carrying both weights
+    p2, v2 = O.update_prior(r1, gam1, [0.9, 0.05, 0.05], np.array([0.0, 1e-3, 1e-3]) * N, N, EM_max_iter=1,
+                            learn_vars=0)
+    assert len(p2) == 2 and abs(p2.sum() - 1) < 1e-12

@@ -224,6 +224,19 @@ class Data:
         check(self._lib.vampomi_assoc_se(self.ctx, _dp(r1), gam1, _dp(pv), MEM_HOST))
         return pv[: self.M]
 
+    def update_prior(self, r1: np.ndarray, gam1: float, probs, vars_scaled, EM_max_iter: int = 1,
+                     EM_err_thr: float = 1e-2, learn_vars: int = 1, merge_vars_thr: float = 0.5):
+        """vamp::updatePrior (src/vamp.cpp:531-643); vars multiplied by N. Returns (probs, vars)."""
+        r1 = np.ascontiguousarray(r1, dtype=np.float64)
+        L = C.c_int(len(probs))
+        pr = np.zeros(MAX_L)
+        va_ = np.zeros(MAX_L)
+        pr[: L.value] = probs
+        va_[: L.value] = vars_scaled
+        check(self._lib.vampomi_update_prior(self.ctx, _dp(r1), gam1, C.byref(L), _dp(pr), _dp(va_), EM_max_iter,
+                                             EM_err_thr, learn_vars, merge_vars_thr, MEM_HOST))
+        return pr[: L.value].copy(), va_[: L.value].copy()
+
     def denoise_bin(self, p1: np.ndarray, tau1: float):
         """g1_bin_class / g1d_bin_class over the phenotype (src/vamp_probit.cpp:469-488): (z1, sum of g1d)."""
         p1 = np.ascontiguousarray(p1, dtype=np.float64)

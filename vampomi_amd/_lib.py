@@ -120,6 +120,8 @@ SIGNATURES = {
     "vampomi_test_metrics": (C.c_int, [_P, _P, C.POINTER(C.c_double), C.POINTER(C.c_double), C.c_int]),
     "vampomi_assoc_loo": (C.c_int, [_P, _P, _P, _P, C.c_int]),
     "vampomi_assoc_se": (C.c_int, [_P, _P, C.c_double, _P, C.c_int]),
+    "vampomi_update_prior": (C.c_int, [_P, _P, C.c_double, C.POINTER(C.c_int), _P, _P, C.c_int, C.c_double,
+                                        C.c_int, C.c_double, C.c_int]),
     "vampomi_denoise_bin": (C.c_int, [_P, _P, C.c_double, _P, C.POINTER(C.c_double), C.c_int]),
     "vampomi_denoise": (C.c_int, [_P, _P, C.c_double, _P, _P, C.c_int, _P, _P, C.POINTER(C.c_double), C.c_int]),
     "vampomi_params_default": (None, [C.POINTER(Params)]),

@@ -55,6 +55,14 @@ struct VampRun {
     ~VampRun();
 };
 
+struct EmParams {
+    int EM_max_iter;
+    double EM_err_thr;
+    int learn_vars;
+    double merge_vars_thr;
+    int verbosity;
+};
+vampomi_status update_prior(vampomi_ctx* c, const EmParams& P, Mixture& m, double gam1, const double* r1);
 vampomi_status update_prior(vampomi_ctx* c, const VampRun& R, Mixture& m, double gam1, const double* r1);
 vampomi_status denoise_into(vampomi_ctx* c, const Mixture& m, double gam1, const double* r1, double* x1,
                             const double* x1_prev, bool damp, double rho, double* x1d, DotBatch& b, double* sum_out);

@@ -42,13 +42,18 @@ vampomi_ctx::~vampomi_ctx() {
 
 // updatePrior (src/vamp.cpp:531-643) on mixture m, from r1 and gam1
 vampomi_status update_prior(vampomi_ctx* c, const VampRun& R, Mixture& m, double gam1, const double* r1) {
+    const EmParams ep{R.prm.EM_max_iter, R.prm.EM_err_thr, R.prm.learn_vars, R.prm.merge_vars_thr, R.prm.verbosity};
+    return update_prior(c, ep, m, gam1, r1);
+}
+
+vampomi_status update_prior(vampomi_ctx* c, const EmParams& P, Mixture& m, double gam1, const double* r1) {
     const double noise_var = 1 / gam1;
     double lambda = 1 - m.probs[0];
     double omegas[VAMPOMI_MAX_L];
     for (int j = 0; j < m.L; ++j) omegas[j] = m.probs[j];
     for (int j = 1; j < m.L; ++j) omegas[j] /= lambda;
     std::vector<double> sums(2 * VAMPOMI_MAX_L);
-    for (int emit = 0; emit < R.prm.EM_max_iter; ++emit) {
+    for (int emit = 0; emit < P.EM_max_iter; ++emit) {
         const int L = m.L;
         double max_sigma = m.vars[0];
         for (int j = 1; j < L; ++j) max_sigma = smax(max_sigma, m.vars[j]);  // std::max_element
@@ -78,7 +83,7 @@ vampomi_status update_prior(vampomi_ctx* c, const VampRun& R, Mixture& m, double
         for (int j = 0; j < L - 1; ++j) {
             const double res_total = sums[1 + j];
             const double res_gammas_total = sums[L + j];
-            if (R.prm.learn_vars == 1) m.vars[j + 1] = res_gammas_total / res_total;
+            if (P.learn_vars == 1) m.vars[j + 1] = res_gammas_total / res_total;
             omegas[j + 1] = res_total / sum_of_pin;
             m.probs[j + 1] = lambda * omegas[j + 1];
         }
@@ -91,15 +96,15 @@ vampomi_status update_prior(vampomi_ctx* c, const VampRun& R, Mixture& m, double
             nvar += m.vars[j] * m.vars[j];
         }
         const double dist_probs = std::sqrt(dprob / nprob), dist_vars = std::sqrt(dvar / nvar);
-        if (R.prm.verbosity == 1 && c->rank == 0)
+        if (P.verbosity == 1 && c->rank == 0)
             std::printf("it = %d: dist_probs = %g & dist_vars = %g\n", emit, dist_probs, dist_vars);
-        if (dist_probs < R.prm.EM_err_thr && dist_vars < R.prm.EM_err_thr) break;
+        if (dist_probs < P.EM_err_thr && dist_vars < P.EM_err_thr) break;
     }
     // merging close variances (:626-642)
     for (int j = 0; j < m.L; ++j) {
         for (int k = j + 1; k < m.L; ++k) {
             const double denom = m.vars[j] != 0 ? smin(m.vars[j], m.vars[k]) : 1e-7;
-            if (std::fabs(m.vars[j] - m.vars[k]) / denom < R.prm.merge_vars_thr) {
+            if (std::fabs(m.vars[j] - m.vars[k]) / denom < P.merge_vars_thr) {
                 const double sum2probs = m.probs[j] + m.probs[k];
                 for (int q = k; q + 1 < m.L; ++q) {
                     m.vars[q] = m.vars[q + 1];
@@ -494,4 +499,34 @@ extern "C" void vampomi_params_default(vampomi_params* p) {
     p->seed = 0x5EED5EEDULL;
     p->batch_rhs = 1;
     p->model = "linear";
+}
+
+// vamp::updatePrior (src/vamp.cpp:531-643) on its own: EM for the
+// spike-and-slab prior from r1 (this shard's slice) at noise precision gam1,
+// then the merging of close variances.  vars are multiplied by N, as the
+// reference keeps them (src/vamp.cpp:87-88).  COLLECTIVE.
+extern "C" vampomi_status vampomi_update_prior(vampomi_ctx* c, const double* r1, double gam1, int* L, double* probs,
+                                               double* vars, int EM_max_iter, double EM_err_thr, int learn_vars,
+                                               double merge_vars_thr, int mem) {
+    if (!c || !L || !probs || !vars || (!r1 && c->M > 0)) return fail(VAMPOMI_ERR_ARG, "null argument");
+    if (*L < 1 || *L > VAMPOMI_MAX_L) return fail(VAMPOMI_ERR_ARG, "number of mixture components out of range");
+    HIPCHK(hipSetDevice(c->device));
+    double* rin = c->mbuf;
+    if (c->M > 0)
+        HIPCHK(hipMemcpyAsync(rin, r1, (size_t)c->M * 8,
+                              mem == VAMPOMI_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, c->st));
+    Mixture m;
+    m.L = *L;
+    for (int j = 0; j < m.L; ++j) {
+        m.probs[j] = probs[j];
+        m.vars[j] = vars[j];
+    }
+    const EmParams ep{EM_max_iter, EM_err_thr, learn_vars, merge_vars_thr, 0};
+    STCHK(update_prior(c, ep, m, gam1, rin));
+    *L = m.L;
+    for (int j = 0; j < m.L; ++j) {
+        probs[j] = m.probs[j];
+        vars[j] = m.vars[j];
+    }
+    return VAMPOMI_OK;
 }
