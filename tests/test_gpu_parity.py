@@ -280,7 +280,7 @@ def test_every_kernel_variant_is_correct():
     lib = va.load()
     with va.Data(N, Mt) as d:
         d.load_meth(X)
-        for which, nvar in ((0, 9), (1, 8)):
+        for which, nvar in ((0, 7), (1, 8)):
             for v in range(nvar):
                 _lib.check(lib.vampomi_dev_set_variant(d.ctx, which, v))
                 if which == 0:

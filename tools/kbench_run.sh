@@ -1,6 +1,5 @@
 set -u
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
-timeout -k 10 300 python tools/kbench.py 10000 50000 20 ax > gpurun_out/kbench_ax_c2.log 2>&1 || exit $?
-grep -E "^ax " gpurun_out/kbench_ax_c2.log
-timeout -k 10 300 python tools/kbench.py 50000 50000 6 ax > gpurun_out/kbench_ax_c4.log 2>&1 || exit $?
-grep -E "^ax " gpurun_out/kbench_ax_c4.log
+run() { timeout -k 10 300 python tools/kbench.py $1 $2 $3 ax > gpurun_out/kbn.log 2>&1 || { cat gpurun_out/kbn.log; exit 1; }
+  echo "N=$1 Mt=$2: $(grep -E '^ax 0 ' gpurun_out/kbn.log | cut -c6-)"; }
+run 100000 20000 8; run 50000 125000 4; run 200000 31250 4; run 25000 250000 4; run 100000 62500 4

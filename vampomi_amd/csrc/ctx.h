@@ -69,7 +69,7 @@ struct vampomi_ctx {
     bool have_X = false, have_y = false;
 
     vk::AxPlan axp{};
-    double* ax_part = nullptr;  // nchunks x kMaxRhs x ld partial sums of A.x
+    double* ax_part = nullptr;  // nslots x kMaxRhs x ld partial sums of A.x
     double* red_part = nullptr;  // per-block partials of every reduction
     size_t red_cap = 0;
     double* scal = nullptr;     // device scalars (SL_*)

@@ -439,7 +439,7 @@ extern "C" vampomi_status vampomi_open(const vampomi_shard_desc* d, vampomi_ctx*
     STCHK(dev_alloc(&c->msig, Mx));
     STCHK(dev_alloc(&c->y, c->ld));
     HIPCHK(hipMemsetAsync(c->y, 0, c->ld * 8, c->st));
-    STCHK(dev_alloc(&c->ax_part, (size_t)c->axp.nchunks * vk::kMaxRhs * c->ld));
+    STCHK(dev_alloc(&c->ax_part, (size_t)c->axp.nslots * vk::kMaxRhs * c->ld));
     c->red_cap = std::max<size_t>({(size_t)vk::kRedBlocks * 3 * vk::kMaxRhs,
                                    (size_t)((Mx + 255) / 256) * (1 + 2 * (vk::kMaxL - 1)),
                                    (size_t)(Mx / 8 + 1) * vk::kMaxRhs, (size_t)4096});  // ATx partials at G >= 2
@@ -985,9 +985,9 @@ extern "C" vampomi_status vampomi_dev_set_variant(vampomi_ctx* c, int which, int
     if (which == 0) {
         if (!vk::set_ax_variant(variant)) return fail(VAMPOMI_ERR_ARG, "no such A.x variant");
         const vk::AxPlan np = vk::ax_plan(c->N, std::max<int64_t>(c->M, 1));
-        if (np.nchunks > c->axp.nchunks) {
+        if (np.nslots > c->axp.nslots) {
             dev_free(c->ax_part);
-            STCHK(dev_alloc(&c->ax_part, (size_t)np.nchunks * vk::kMaxRhs * c->ld));
+            STCHK(dev_alloc(&c->ax_part, (size_t)np.nslots * vk::kMaxRhs * c->ld));
         }
         c->axp = np;
     } else if (which == 1) {

@@ -39,15 +39,23 @@ struct Shard {
 };
 
 // ---- A.x : two-stage, deterministic --------------------------------------
-// Stage 1 (ax_partial): a workgroup owns a row tile and a chunk of
-// markers, accumulates in registers, writes part[chunk][k][ld].  Stage 2
-// (ax_reduce): sums the chunks in index order.
+// Stage 1 (ax_partial): the (row tile, marker) segments, tile-major, are
+// cut into equal stripes, one per workgroup (two per CU); each tile a stripe
+// touches gets its own partial slot, written to part[slot][k][ld].  Stage 2
+// (ax_reduce): sums every tile's slots in marker order.
 struct AxPlan {
     int variant;      // row/unroll variant (tuning table in kernels.hip)
-    int tiles;        // ceil(N / rows per tile)
-    int nchunks;      // marker chunks (grid.y)
-    int64_t chunk;    // markers per chunk
+    int64_t rows;     // rows per tile
+    int64_t tiles;    // ceil(N / rows)
+    int64_t total;    // tiles * M segments
+    int64_t span;     // segments per workgroup
+    int groups;       // workgroups (grid)
+    int nslots;       // partial slots of the busiest tile (part holds nslots x kMaxRhs x ld)
 };
+// partial slots tile t uses: the workgroups whose stripe meets it
+inline int64_t ax_slots(const AxPlan& p, int64_t M, int64_t t) {
+    return ((t + 1) * M - 1) / p.span - (t * M) / p.span + 1;
+}
 AxPlan ax_plan(int64_t N, int64_t M);
 int ax_variant_count();
 bool set_ax_variant(int v);   // development hook (tools/kbench.py)

@@ -9,6 +9,8 @@
 // run and independent of the rank count's effect on scheduling.
 #include "kernels.h"
 
+#include <cstdlib>
+
 #include <hip/hip_ext.h>
 
 #include <hip/hip_runtime.h>
@@ -163,60 +165,72 @@ static inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 // ---------------------------------------------------------------------------
 // A.x   (data::Ax, src/data.cpp:340-373)
 // ---------------------------------------------------------------------------
-// Workgroup (tile, chunk): a tile of 256*R rows x the markers of one chunk.
-// Wave w owns the contiguous slab of 64*R rows [tile0 + 64*R*w, ...); its lane
-// l owns rows 2l + 128q (q < R/2), i.e. each 16-byte load instruction reads
-// 1 KiB contiguous, and the workgroup streams 2*R KiB of every marker column.
-// U markers are loaded before any arithmetic (U*R/2 16-byte loads in flight
-// per lane).  Per-sample summation order within a chunk is the reference's:
-// markers in index order, acc += (x - mave_i) * (msig_i * x_i).
-template <int K, int R, int U, bool NT, bool IL>
+// Stripe plan.  The rows are cut into tiles of 256*R; the tile-major space of
+// (tile, marker) segments, tiles*M of them, is cut into G equal contiguous
+// stripes of `span` segments, one per workgroup, with G = two workgroups per
+// CU: one resident round in which every CU carries the same load (a tile x
+// chunk grid leaves some CUs a third workgroup whenever tiles*chunks is not a
+// multiple of the CU count, and those set the kernel's time).  A stripe is
+// one or more pieces (tile t, markers [a, b)); the piece of tile t streamed by
+// workgroup g lands in partial slot g - g_lo(t) of that tile, where
+// g_lo(t) = floor(t*M / span).  The plan does not depend on the batch width K,
+// so batched and solo passes sum identically.
+//
+// Within a piece, wave w owns the contiguous slab of 64*R rows
+// [tile0 + 64*R*w, ...); lane l owns rows 2l + 128q (q < R/2), i.e. each
+// 16-byte load instruction reads 1 KiB contiguous, and the workgroup streams
+// 2*R KiB of every marker column.  U markers are loaded before any
+// arithmetic (U*R/2 16-byte loads in flight per lane).  Per-sample summation
+// order within a piece is the reference's: markers in index order,
+// acc += (x - mave_i) * (msig_i * x_i).
+template <int K, int R, int U, bool NT>
 __global__ __launch_bounds__(kBlock) void ax_partial_kernel(const double* __restrict__ X, int64_t ld,
                                                             int64_t N, int64_t M,
                                                             const double* __restrict__ mave,
                                                             const double* __restrict__ msig, CPtrs xs,
-                                                            int64_t chunk, double* __restrict__ part) {
+                                                            int64_t total, int64_t span,
+                                                            double* __restrict__ part) {
     constexpr int P = R / 2;  // 16-byte pieces per lane per marker
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int64_t j0 = (int64_t)blockIdx.x * (kBlock * R) + (int64_t)wave * (64 * R) + 2 * lane;
-    // IL: chunk c owns markers c, c+nch, c+2nch, ... (all workgroups stream
-    // through the same narrow window of columns together: TLB/DRAM locality);
-    // otherwise chunk c owns the contiguous range [c*chunk, (c+1)*chunk)
-    const int64_t nch = gridDim.y;
-    const int64_t i0 = IL ? (int64_t)blockIdx.y : (int64_t)blockIdx.y * chunk;
-    const int64_t istep = IL ? nch : 1;
-    const int64_t i1 = IL ? M : ((i0 + chunk < M) ? i0 + chunk : M);
-    bool ok[P];
-    int64_t off[P];  // invalid pieces read row 0 of the column (in bounds) and are discarded at the store
+    const int64_t g = blockIdx.x;
+    int64_t pos = g * span;
+    const int64_t end = (pos + span < total) ? pos + span : total;
+    while (pos < end) {
+        const int64_t t = pos / M;
+        const int64_t i0 = pos - t * M;
+        const int64_t i1 = (i0 + (end - pos) < M) ? i0 + (end - pos) : M;
+        pos += i1 - i0;
+        const int64_t slot = g - (t * M) / span;
+        const int64_t j0 = t * (kBlock * R) + (int64_t)wave * (64 * R) + 2 * lane;
+        if (j0 >= N) continue;
+        bool ok[P];
+        int64_t off[P];  // invalid pieces read row 0 of the column (in bounds) and are discarded at the store
 #pragma unroll
-    for (int q = 0; q < P; ++q) {
-        ok[q] = j0 + 128 * q < N;
-        off[q] = ok[q] ? 128 * q : -j0;
-    }
-    double acc[K][R];
+        for (int q = 0; q < P; ++q) {
+            ok[q] = j0 + 128 * q < N;
+            off[q] = ok[q] ? 128 * q : -j0;
+        }
+        double acc[K][R];
 #pragma unroll
-    for (int k = 0; k < K; ++k)
+        for (int k = 0; k < K; ++k)
 #pragma unroll
-        for (int r = 0; r < R; ++r) acc[k][r] = 0.0;
-    if (ok[0]) {
+            for (int r = 0; r < R; ++r) acc[k][r] = 0.0;
         const double* col = X + i0 * ld + j0;
-        const int64_t cstep = istep * ld;
         int64_t i = i0;
-        for (; i + (U - 1) * istep < i1; i += U * istep) {
+        for (; i + (U - 1) < i1; i += U) {
             v2d xv[U][P];
 #pragma unroll
             for (int u = 0; u < U; ++u)
 #pragma unroll
                 for (int q = 0; q < P; ++q)
-                    xv[u][q] = NT ? ld_stream(col + (int64_t)u * cstep + off[q]) : ld2(col + (int64_t)u * cstep + off[q]);
+                    xv[u][q] = NT ? ld_stream(col + (int64_t)u * ld + off[q]) : ld2(col + (int64_t)u * ld + off[q]);
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                const int64_t iu = i + u * istep;
-                const double ave = mave[iu];
-                const double sg = msig[iu];
+                const double ave = mave[i + u];
+                const double sg = msig[i + u];
 #pragma unroll
                 for (int k = 0; k < K; ++k) {
-                    const double w = sg * xs.p[k][iu];
+                    const double w = sg * xs.p[k][i + u];
 #pragma unroll
                     for (int q = 0; q < P; ++q) {
                         acc[k][2 * q] += (xv[u][q].x - ave) * w;
@@ -224,9 +238,9 @@ __global__ __launch_bounds__(kBlock) void ax_partial_kernel(const double* __rest
                     }
                 }
             }
-            col += (int64_t)U * cstep;
+            col += (int64_t)U * ld;
         }
-        for (; i < i1; i += istep) {
+        for (; i < i1; ++i) {
             v2d xv[P];
 #pragma unroll
             for (int q = 0; q < P; ++q) xv[q] = NT ? ld_stream(col + off[q]) : ld2(col + off[q]);
@@ -241,9 +255,9 @@ __global__ __launch_bounds__(kBlock) void ax_partial_kernel(const double* __rest
                     acc[k][2 * q + 1] += (xv[q].y - ave) * w;
                 }
             }
-            col += cstep;
+            col += ld;
         }
-        double* dst = part + (int64_t)blockIdx.y * K * ld + j0;
+        double* dst = part + slot * K * ld + j0;
 #pragma unroll
         for (int k = 0; k < K; ++k)
 #pragma unroll
@@ -257,13 +271,12 @@ __global__ __launch_bounds__(kBlock) void ax_partial_kernel(const double* __rest
 }
 
 // tuning table (rows per lane R, markers in flight U, nontemporal loads)
-struct AxVariant { int R, U; bool NT, IL; };
+struct AxVariant { int R, U; bool NT; };
 static constexpr AxVariant kAxVariants[] = {
-    {2, 8, true, false}, {2, 8, false, false}, {4, 4, true, false}, {4, 8, true, false}, {8, 4, true, false},
-    {2, 8, true, true},  {2, 4, true, true},   {4, 4, true, true},  {2, 12, true, true},
+    {2, 8, true}, {2, 8, false}, {4, 4, true}, {4, 8, true}, {8, 4, true}, {2, 4, true}, {2, 12, true},
 };
 static constexpr int kNumAxVariants = sizeof(kAxVariants) / sizeof(kAxVariants[0]);
-static int g_ax_variant = 0;  // R=2, U=8, nontemporal, one full round of resident workgroups: best at every K (tools/kbench.py)
+static int g_ax_variant = 0;  // R=2, U=8, nontemporal (tools/kbench.py)
 
 int ax_variant_count() { return kNumAxVariants; }
 bool set_ax_variant(int v) {
@@ -272,58 +285,38 @@ bool set_ax_variant(int v) {
     return true;
 }
 
-template <int K>
-static const void* ax_fn(int v) {
-    switch (v) {
-        case 0: return (const void*)ax_partial_kernel<K, 2, 8, true, false>;
-        case 1: return (const void*)ax_partial_kernel<K, 2, 8, false, false>;
-        case 2: return (const void*)ax_partial_kernel<K, 4, 4, true, false>;
-        case 3: return (const void*)ax_partial_kernel<K, 4, 8, true, false>;
-        case 4: return (const void*)ax_partial_kernel<K, 8, 4, true, false>;
-        case 5: return (const void*)ax_partial_kernel<K, 2, 8, true, true>;
-        case 6: return (const void*)ax_partial_kernel<K, 2, 4, true, true>;
-        case 7: return (const void*)ax_partial_kernel<K, 4, 4, true, true>;
-        default: return (const void*)ax_partial_kernel<K, 2, 12, true, true>;
-    }
-}
-
-// resident workgroups of the K=2 kernel (the common batch width) on the device
-static int64_t ax_resident_slots(int v) {
-    int dev = 0, cus = 0, per_cu = 0;
+static int device_cus() {
+    int dev = 0, cus = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-        return 2048;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ax_fn<2>(v), kBlock, 0) != hipSuccess || per_cu <= 0)
-        return 2048;
-    return (int64_t)cus * per_cu;
+        return 256;
+    return cus;
 }
 
 AxPlan ax_plan(int64_t N, int64_t M) {
     AxPlan p;
     p.variant = g_ax_variant;
-    p.tiles = (int)cdiv(N, (int64_t)kBlock * kAxVariants[p.variant].R);
-    // whole rounds of resident workgroups (no partly filled last round), >= 2048 workgroups;
-    // the plan is the same for every batch width K, so batched and solo passes sum identically
-    const int64_t slots = ax_resident_slots(p.variant);
-    const int64_t rounds = cdiv(2048, slots);
-    int64_t target = rounds * slots;
-    int64_t nch = target / p.tiles > 0 ? target / p.tiles : 1;
-    int64_t maxch = M / 64 > 0 ? M / 64 : 1;  // at least 64 markers per chunk
-    if (nch > maxch) nch = maxch;
-    if (nch < 1) nch = 1;
-    p.chunk = cdiv(M, nch);
-    if (p.chunk < 1) p.chunk = 1;
-    p.nchunks = (int)cdiv(M, p.chunk);
-    if (p.nchunks < 1) p.nchunks = 1;
+    p.rows = (int64_t)kBlock * kAxVariants[p.variant].R;
+    p.tiles = cdiv(N, p.rows);
+    p.total = p.tiles * M;
+    int64_t wpc = 2;  // workgroups per CU
+    if (const char* f = std::getenv("VAMPOMI_AX_WPC")) wpc = std::max(1, std::atoi(f));  // tuning experiments
+    int64_t G = std::min<int64_t>(wpc * device_cus(), cdiv(p.total, 64));  // >= 64 segments per stripe
+    if (G < 1) G = 1;
+    p.span = cdiv(p.total, G);
+    p.groups = (int)cdiv(p.total, p.span);
+    int64_t ns = 1;
+    for (int64_t t = 0; t < p.tiles; ++t) ns = std::max(ns, ax_slots(p, M, t));
+    p.nslots = (int)ns;
     return p;
 }
 
 // launches go through hipExtLaunchKernelGGL: the optional start / stop events
 // are written by the kernel's own dispatch (no extra marker packets around it)
-template <int K, int R, int U, bool NT, bool IL = false>
+template <int K, int R, int U, bool NT>
 static void launch_ax(const Shard& s, const AxPlan& pl, CPtrs x, double* part, hipStream_t st, const Timing& tm) {
-    hipExtLaunchKernelGGL((ax_partial_kernel<K, R, U, NT, IL>), dim3(pl.tiles, pl.nchunks), dim3(kBlock), 0, st,
-                          tm.start, tm.stop, 0, s.X, s.ld, s.N, s.M, s.mave, s.msig, x, pl.chunk, part);
+    hipExtLaunchKernelGGL((ax_partial_kernel<K, R, U, NT>), dim3(pl.groups), dim3(kBlock), 0, st, tm.start,
+                          tm.stop, 0, s.X, s.ld, s.N, s.M, s.mave, s.msig, x, pl.total, pl.span, part);
 }
 
 template <int K>
@@ -335,16 +328,17 @@ static bool launch_ax_v(int v, const Shard& s, const AxPlan& pl, CPtrs x, double
         case 2: launch_ax<K, 4, 4, true>(s, pl, x, part, st, tm); return true;
         case 3: launch_ax<K, 4, 8, true>(s, pl, x, part, st, tm); return true;
         case 4: launch_ax<K, 8, 4, true>(s, pl, x, part, st, tm); return true;
-        case 5: launch_ax<K, 2, 8, true, true>(s, pl, x, part, st, tm); return true;
-        case 6: launch_ax<K, 2, 4, true, true>(s, pl, x, part, st, tm); return true;
-        case 7: launch_ax<K, 4, 4, true, true>(s, pl, x, part, st, tm); return true;
-        case 8: launch_ax<K, 2, 12, true, true>(s, pl, x, part, st, tm); return true;
+        case 5: launch_ax<K, 2, 4, true>(s, pl, x, part, st, tm); return true;
+        case 6: launch_ax<K, 2, 12, true>(s, pl, x, part, st, tm); return true;
         default: return false;
     }
 }
 
 hipError_t ax_partial(const Shard& s, const AxPlan& pl, int K, CPtrs x, double* part, hipStream_t st,
                       const Timing& tm) {
+    if (pl.rows != (int64_t)kBlock * kAxVariants[pl.variant].R || pl.total != pl.tiles * s.M ||
+        pl.tiles * pl.rows < s.N)
+        return hipErrorInvalidValue;  // plan made for another shape
     bool ok = false;
     switch (K) {
         case 1: ok = launch_ax_v<1>(pl.variant, s, pl, x, part, st, tm); break;
@@ -357,12 +351,14 @@ hipError_t ax_partial(const Shard& s, const AxPlan& pl, int K, CPtrs x, double* 
     return hipGetLastError();
 }
 
-// Stage 2: out_k[j] = sum over chunks of part[c][k][j].  A 512-thread block
-// covers 64 consecutive samples (one wave per chunk group, coalesced across
-// lanes); group g sums its contiguous chunk range in index order, then the 8
-// group sums are added in group order: a fixed tree, short dependent chains.
+// Stage 2: out_k[j] = sum over tile(j)'s slots of part[s][k][j].  A 512-thread
+// block covers 64 consecutive samples (one wave per slot group, coalesced
+// across lanes); group q sums its contiguous slot range in index order, then
+// the 8 group sums are added in group order: a fixed tree, short dependent
+// chains.
 constexpr int kRedGroups = 8;
-__global__ __launch_bounds__(64 * kRedGroups) void ax_reduce_kernel(int K, int64_t N, int64_t ld, int nchunks,
+__global__ __launch_bounds__(64 * kRedGroups) void ax_reduce_kernel(int K, int64_t N, int64_t ld, int64_t M,
+                                                                    int64_t rows, int64_t span,
                                                                     const double* __restrict__ part, Ptrs out,
                                                                     double div) {
     __shared__ double lds[kRedGroups][64];
@@ -371,8 +367,10 @@ __global__ __launch_bounds__(64 * kRedGroups) void ax_reduce_kernel(int K, int64
     const bool valid = e < (int64_t)K * N;
     const int k = valid ? (int)(e / N) : 0;
     const int64_t j = valid ? e - (int64_t)k * N : 0;
-    const int per = (nchunks + kRedGroups - 1) / kRedGroups;
-    const int c0 = g * per, c1 = (c0 + per < nchunks) ? c0 + per : nchunks;
+    const int64_t t = j / rows;
+    const int nslots = (int)(((t + 1) * M - 1) / span - (t * M) / span + 1);
+    const int per = (nslots + kRedGroups - 1) / kRedGroups;
+    const int c0 = g * per, c1 = (c0 + per < nslots) ? c0 + per : nslots;
     const int64_t stride = (int64_t)K * ld;
     const double* p = part + (int64_t)k * ld + j;
     double s = 0.0;
@@ -391,11 +389,11 @@ __global__ __launch_bounds__(64 * kRedGroups) void ax_reduce_kernel(int K, int64
     lds[g][lane] = s;
     __syncthreads();
     if (g == 0 && valid) {
-        double t = lds[0][lane];
+        double t2 = lds[0][lane];
 #pragma unroll
-        for (int q = 1; q < kRedGroups; ++q) t += lds[q][lane];
-        if (div > 0.0) t /= div;  // src/data.cpp:369-370: Ax_total[i] /= sqrt(N)
-        out.p[k][j] = t;
+        for (int q = 1; q < kRedGroups; ++q) t2 += lds[q][lane];
+        if (div > 0.0) t2 /= div;  // src/data.cpp:369-370: Ax_total[i] /= sqrt(N)
+        out.p[k][j] = t2;
     }
 }
 
@@ -403,7 +401,7 @@ hipError_t ax_reduce(const AxPlan& pl, int K, int64_t N, int64_t ld, const doubl
                      hipStream_t st) {
     const int64_t n = (int64_t)K * N;
     hipLaunchKernelGGL(ax_reduce_kernel, dim3((unsigned)cdiv(n, 64)), dim3(64 * kRedGroups), 0, st, K, N, ld,
-                       pl.nchunks, part, out, div);
+                       pl.total / pl.tiles, pl.rows, pl.span, part, out, div);
     return hipGetLastError();
 }
 
@@ -530,8 +528,7 @@ std::string kernel_name(int which, int K, int mode) {
     char b[160];
     if (which == 0) {
         const AxVariant& v = kAxVariants[g_ax_variant];
-        std::snprintf(b, sizeof b, "ax_partial_kernel<%d, %d, %d, %s, %s>", K, v.R, v.U, v.NT ? "true" : "false",
-                      v.IL ? "true" : "false");
+        std::snprintf(b, sizeof b, "ax_partial_kernel<%d, %d, %d, %s>", K, v.R, v.U, v.NT ? "true" : "false");
     } else {
         const AtxVariant& v = kAtxVariants[atx_variant_for(K)];
         std::snprintf(b, sizeof b, "atx_kernel<%d, %d, %d, %d, %s>", v.G, K, mode, v.UJ, v.NT ? "true" : "false");
