@@ -39,23 +39,24 @@ struct Shard {
 };
 
 // ---- A.x : two-stage, deterministic --------------------------------------
-// Stage 1 (ax_partial): the (row tile, marker) segments, tile-major, are
-// cut into equal stripes, one per workgroup (two per CU); each tile a stripe
-// touches gets its own partial slot, written to part[slot][k][ld].  Stage 2
-// (ax_reduce): sums every tile's slots in marker order.
+// Stage 1 (ax_partial): the (row tile, marker) segments are split into equal
+// shares, one per workgroup (two per CU): a fixed fraction of one or two
+// tiles in every marker band (band plan), or a contiguous tile-major stripe;
+// each tile a workgroup touches gets its own partial slot, written to
+// part[slot][k][ld].  Stage 2 (ax_reduce): sums every tile's slots in order.
 struct AxPlan {
     int variant;      // row/unroll variant (tuning table in kernels.hip)
     int64_t rows;     // rows per tile
     int64_t tiles;    // ceil(N / rows)
     int64_t total;    // tiles * M segments
-    int64_t span;     // segments per workgroup
+    int64_t span;     // stripe plan: segments per workgroup
+    int64_t nband;    // band plan: marker bands (0: stripe plan)
+    int64_t sa, sb;   // tile t's first slot-owning workgroup is t*sa/sb
     int groups;       // workgroups (grid)
     int nslots;       // partial slots of the busiest tile (part holds nslots x kMaxRhs x ld)
 };
-// partial slots tile t uses: the workgroups whose stripe meets it
-inline int64_t ax_slots(const AxPlan& p, int64_t M, int64_t t) {
-    return ((t + 1) * M - 1) / p.span - (t * M) / p.span + 1;
-}
+// partial slots tile t uses: the workgroups whose share meets it
+inline int64_t ax_slots(const AxPlan& p, int64_t t) { return ((t + 1) * p.sa - 1) / p.sb - (t * p.sa) / p.sb + 1; }
 AxPlan ax_plan(int64_t N, int64_t M);
 int ax_variant_count();
 bool set_ax_variant(int v);   // development hook (tools/kbench.py)

@@ -165,34 +165,153 @@ static inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 // ---------------------------------------------------------------------------
 // A.x   (data::Ax, src/data.cpp:340-373)
 // ---------------------------------------------------------------------------
-// Stripe plan.  The rows are cut into tiles of 256*R; the tile-major space of
-// (tile, marker) segments, tiles*M of them, is cut into G equal contiguous
-// stripes of `span` segments, one per workgroup, with G = two workgroups per
-// CU: one resident round in which every CU carries the same load (a tile x
-// chunk grid leaves some CUs a third workgroup whenever tiles*chunks is not a
-// multiple of the CU count, and those set the kernel's time).  A stripe is
-// one or more pieces (tile t, markers [a, b)); the piece of tile t streamed by
-// workgroup g lands in partial slot g - g_lo(t) of that tile, where
-// g_lo(t) = floor(t*M / span).  The plan does not depend on the batch width K,
-// so batched and solo passes sum identically.
+// Work split.  The rows are cut into tiles of 256*R, and the (tile, marker)
+// segments, tiles*M of them, into G equal shares, one per workgroup, with
+// G = two workgroups per CU: one resident round in which every CU carries the
+// same load (a tile x chunk grid leaves some CUs a third workgroup whenever
+// tiles*chunks is not a multiple of the CU count, and those set the kernel's
+// time).  Two layouts of the shares:
+//  * band plan (tiles <= G): the markers are cut into bands of about 64 MiB
+//    of columns, and workgroup g owns the same fraction [g*tiles, (g+1)*tiles)
+//    / G of the tile-major (tile, marker-in-band) space of every band: one or
+//    two tiles, a run of each band's columns per tile.  All workgroups walk
+//    the bands together, so the reads in flight stay inside one band (page
+//    translation and DRAM locality: equal contiguous stripes spread over a
+//    50 GB matrix ran 4% slower).  A band's column boundaries are dithered
+//    per band so floor rounding does not favour the same workgroups.
+//  * stripe plan (tiles > G): workgroup g owns the contiguous stripe
+//    [g*span, (g+1)*span) of the tile-major space (whole tiles, in order).
+// Either way the piece of tile t that workgroup g streams lands in partial
+// slot g - lo(t) of that tile, lo(t) = t*sa/sb ((sa, sb) = (G, tiles) for
+// bands, (M, span) for stripes).  The plan does not depend on the batch width
+// K, so batched and solo passes sum identically.
 //
 // Within a piece, wave w owns the contiguous slab of 64*R rows
 // [tile0 + 64*R*w, ...); lane l owns rows 2l + 128q (q < R/2), i.e. each
 // 16-byte load instruction reads 1 KiB contiguous, and the workgroup streams
 // 2*R KiB of every marker column.  U markers are loaded before any
 // arithmetic (U*R/2 16-byte loads in flight per lane).  Per-sample summation
-// order within a piece is the reference's: markers in index order,
+// order within a slot is the reference's: markers in index order,
 // acc += (x - mave_i) * (msig_i * x_i).
+template <int K, int R, int U, bool NT>
+__device__ __forceinline__ void ax_piece(const double* __restrict__ X, int64_t ld, int64_t N,
+                                         const double* __restrict__ mave, const double* __restrict__ msig,
+                                         const CPtrs& xs, int64_t j0, int64_t i0, int64_t i1, double (&acc)[K][R]) {
+    constexpr int P = R / 2;  // 16-byte pieces per lane per marker
+    int64_t off[P];  // invalid pieces read row 0 of the column (in bounds) and are discarded at the store
+#pragma unroll
+    for (int q = 0; q < P; ++q) off[q] = (j0 + 128 * q < N) ? 128 * q : -j0;
+    const double* col = X + i0 * ld + j0;
+    int64_t i = i0;
+    for (; i + (U - 1) < i1; i += U) {
+        v2d xv[U][P];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int q = 0; q < P; ++q)
+                xv[u][q] = NT ? ld_stream(col + (int64_t)u * ld + off[q]) : ld2(col + (int64_t)u * ld + off[q]);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const double ave = mave[i + u];
+            const double sg = msig[i + u];
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const double w = sg * xs.p[k][i + u];
+#pragma unroll
+                for (int q = 0; q < P; ++q) {
+                    acc[k][2 * q] += (xv[u][q].x - ave) * w;
+                    acc[k][2 * q + 1] += (xv[u][q].y - ave) * w;
+                }
+            }
+        }
+        col += (int64_t)U * ld;
+    }
+    for (; i < i1; ++i) {
+        v2d xv[P];
+#pragma unroll
+        for (int q = 0; q < P; ++q) xv[q] = NT ? ld_stream(col + off[q]) : ld2(col + off[q]);
+        const double ave = mave[i];
+        const double sg = msig[i];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const double w = sg * xs.p[k][i];
+#pragma unroll
+            for (int q = 0; q < P; ++q) {
+                acc[k][2 * q] += (xv[q].x - ave) * w;
+                acc[k][2 * q + 1] += (xv[q].y - ave) * w;
+            }
+        }
+        col += ld;
+    }
+}
+
+template <int K, int R>
+__device__ __forceinline__ void ax_store(double* __restrict__ part, int64_t slot, int64_t ld, int64_t N, int64_t j0,
+                                         const double (&acc)[K][R]) {
+    double* dst = part + slot * K * ld + j0;
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+#pragma unroll
+        for (int q = 0; q < R / 2; ++q) {
+            if (j0 + 128 * q < N) {
+                dst[(int64_t)k * ld + 128 * q] = acc[k][2 * q];
+                if (j0 + 128 * q + 1 < N) dst[(int64_t)k * ld + 128 * q + 1] = acc[k][2 * q + 1];
+            }
+        }
+}
+
+template <int K, int R>
+__device__ __forceinline__ void ax_zero(double (&acc)[K][R]) {
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc[k][r] = 0.0;
+}
+
 template <int K, int R, int U, bool NT>
 __global__ __launch_bounds__(kBlock) void ax_partial_kernel(const double* __restrict__ X, int64_t ld,
                                                             int64_t N, int64_t M,
                                                             const double* __restrict__ mave,
                                                             const double* __restrict__ msig, CPtrs xs,
-                                                            int64_t total, int64_t span,
+                                                            int64_t tiles, int64_t span, int64_t nband,
                                                             double* __restrict__ part) {
-    constexpr int P = R / 2;  // 16-byte pieces per lane per marker
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int64_t g = blockIdx.x;
+    const int64_t g = blockIdx.x, G = gridDim.x;
+    const int64_t slab = (int64_t)wave * (64 * R) + 2 * lane;  // row offset inside a tile
+    double acc[K][R];
+    if (nband > 0) {
+        // band plan: u-space [g*tiles, (g+1)*tiles) over tiles of G units each
+        const int64_t ulo = g * tiles, uhi = ulo + tiles;
+        const int64_t tA = ulo / G;
+        const int64_t xa0 = ulo - tA * G, xa1 = ((uhi < (tA + 1) * G) ? uhi : (tA + 1) * G) - tA * G;
+        const bool hasB = uhi > (tA + 1) * G;
+        const int64_t xb1 = uhi - (tA + 1) * G;
+        const int64_t jA = tA * (kBlock * R) + slab, jB = jA + kBlock * R;
+        double accB[K][R];
+        ax_zero<K, R>(acc);
+        ax_zero<K, R>(accB);
+        // boundaries in whole groups of U markers (full-width load trips); the
+        // last group boundary stands for M (the M % U leftover markers)
+        const int64_t Mu = M / U;
+        for (int64_t p = 0; p < nband; ++p) {
+            const int64_t c = p * Mu / nband, w = (p + 1) * Mu / nband - c;
+            const int64_t phi = (int64_t)(((uint64_t)p * 0x9E3779B97F4A7C15ULL) >> 40) % G;  // dither in [0, G)
+            if (jA < N) {
+                const int64_t u0 = c + (xa0 * w + phi) / G, u1 = c + (xa1 * w + phi) / G;
+                ax_piece<K, R, U, NT>(X, ld, N, mave, msig, xs, jA, u0 == Mu ? M : u0 * U, u1 == Mu ? M : u1 * U,
+                                      acc);
+            }
+            if (hasB && jB < N) {
+                const int64_t u1 = c + (xb1 * w + phi) / G;
+                ax_piece<K, R, U, NT>(X, ld, N, mave, msig, xs, jB, c * U, u1 == Mu ? M : u1 * U, accB);
+            }
+        }
+        if (jA < N) ax_store<K, R>(part, g - (tA * G) / tiles, ld, N, jA, acc);
+        if (hasB && jB < N) ax_store<K, R>(part, g - ((tA + 1) * G) / tiles, ld, N, jB, accB);
+        return;
+    }
+    // stripe plan
+    const int64_t total = tiles * M;
     int64_t pos = g * span;
     const int64_t end = (pos + span < total) ? pos + span : total;
     while (pos < end) {
@@ -200,73 +319,11 @@ __global__ __launch_bounds__(kBlock) void ax_partial_kernel(const double* __rest
         const int64_t i0 = pos - t * M;
         const int64_t i1 = (i0 + (end - pos) < M) ? i0 + (end - pos) : M;
         pos += i1 - i0;
-        const int64_t slot = g - (t * M) / span;
-        const int64_t j0 = t * (kBlock * R) + (int64_t)wave * (64 * R) + 2 * lane;
+        const int64_t j0 = t * (kBlock * R) + slab;
         if (j0 >= N) continue;
-        bool ok[P];
-        int64_t off[P];  // invalid pieces read row 0 of the column (in bounds) and are discarded at the store
-#pragma unroll
-        for (int q = 0; q < P; ++q) {
-            ok[q] = j0 + 128 * q < N;
-            off[q] = ok[q] ? 128 * q : -j0;
-        }
-        double acc[K][R];
-#pragma unroll
-        for (int k = 0; k < K; ++k)
-#pragma unroll
-            for (int r = 0; r < R; ++r) acc[k][r] = 0.0;
-        const double* col = X + i0 * ld + j0;
-        int64_t i = i0;
-        for (; i + (U - 1) < i1; i += U) {
-            v2d xv[U][P];
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-#pragma unroll
-                for (int q = 0; q < P; ++q)
-                    xv[u][q] = NT ? ld_stream(col + (int64_t)u * ld + off[q]) : ld2(col + (int64_t)u * ld + off[q]);
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const double ave = mave[i + u];
-                const double sg = msig[i + u];
-#pragma unroll
-                for (int k = 0; k < K; ++k) {
-                    const double w = sg * xs.p[k][i + u];
-#pragma unroll
-                    for (int q = 0; q < P; ++q) {
-                        acc[k][2 * q] += (xv[u][q].x - ave) * w;
-                        acc[k][2 * q + 1] += (xv[u][q].y - ave) * w;
-                    }
-                }
-            }
-            col += (int64_t)U * ld;
-        }
-        for (; i < i1; ++i) {
-            v2d xv[P];
-#pragma unroll
-            for (int q = 0; q < P; ++q) xv[q] = NT ? ld_stream(col + off[q]) : ld2(col + off[q]);
-            const double ave = mave[i];
-            const double sg = msig[i];
-#pragma unroll
-            for (int k = 0; k < K; ++k) {
-                const double w = sg * xs.p[k][i];
-#pragma unroll
-                for (int q = 0; q < P; ++q) {
-                    acc[k][2 * q] += (xv[q].x - ave) * w;
-                    acc[k][2 * q + 1] += (xv[q].y - ave) * w;
-                }
-            }
-            col += ld;
-        }
-        double* dst = part + slot * K * ld + j0;
-#pragma unroll
-        for (int k = 0; k < K; ++k)
-#pragma unroll
-            for (int q = 0; q < P; ++q) {
-                if (ok[q]) {
-                    dst[(int64_t)k * ld + 128 * q] = acc[k][2 * q];
-                    if (j0 + 128 * q + 1 < N) dst[(int64_t)k * ld + 128 * q + 1] = acc[k][2 * q + 1];
-                }
-            }
+        ax_zero<K, R>(acc);
+        ax_piece<K, R, U, NT>(X, ld, N, mave, msig, xs, j0, i0, i1, acc);
+        ax_store<K, R>(part, g - (t * M) / span, ld, N, j0, acc);
     }
 }
 
@@ -299,14 +356,27 @@ AxPlan ax_plan(int64_t N, int64_t M) {
     p.rows = (int64_t)kBlock * kAxVariants[p.variant].R;
     p.tiles = cdiv(N, p.rows);
     p.total = p.tiles * M;
-    int64_t wpc = 2;  // workgroups per CU
-    if (const char* f = std::getenv("VAMPOMI_AX_WPC")) wpc = std::max(1, std::atoi(f));  // tuning experiments
-    int64_t G = std::min<int64_t>(wpc * device_cus(), cdiv(p.total, 64));  // >= 64 segments per stripe
+    // tuning experiments: VAMPOMI_AX_WPC workgroups per CU, VAMPOMI_AX_BANDSEG
+    // segments per workgroup per band (0: stripe plan)
+    int64_t wpc = 2, bandseg = 32;
+    if (const char* f = std::getenv("VAMPOMI_AX_WPC")) wpc = std::max(1, std::atoi(f));
+    if (const char* f = std::getenv("VAMPOMI_AX_BANDSEG")) bandseg = std::max(0, std::atoi(f));
+    int64_t G = std::min<int64_t>(wpc * device_cus(), cdiv(p.total, 64));  // >= 64 segments per workgroup
     if (G < 1) G = 1;
     p.span = cdiv(p.total, G);
-    p.groups = (int)cdiv(p.total, p.span);
+    if (p.tiles <= G && bandseg > 0 && M >= (int64_t)kAxVariants[p.variant].U) {
+        p.groups = (int)G;
+        p.nband = std::max<int64_t>(1, std::min<int64_t>(M / kAxVariants[p.variant].U, p.total / (bandseg * G)));
+        p.sa = G;
+        p.sb = p.tiles;
+    } else {
+        p.groups = (int)cdiv(p.total, p.span);
+        p.nband = 0;
+        p.sa = M;
+        p.sb = p.span;
+    }
     int64_t ns = 1;
-    for (int64_t t = 0; t < p.tiles; ++t) ns = std::max(ns, ax_slots(p, M, t));
+    for (int64_t t = 0; t < p.tiles; ++t) ns = std::max(ns, ax_slots(p, t));
     p.nslots = (int)ns;
     return p;
 }
@@ -316,7 +386,7 @@ AxPlan ax_plan(int64_t N, int64_t M) {
 template <int K, int R, int U, bool NT>
 static void launch_ax(const Shard& s, const AxPlan& pl, CPtrs x, double* part, hipStream_t st, const Timing& tm) {
     hipExtLaunchKernelGGL((ax_partial_kernel<K, R, U, NT>), dim3(pl.groups), dim3(kBlock), 0, st, tm.start,
-                          tm.stop, 0, s.X, s.ld, s.N, s.M, s.mave, s.msig, x, pl.total, pl.span, part);
+                          tm.stop, 0, s.X, s.ld, s.N, s.M, s.mave, s.msig, x, pl.tiles, pl.span, pl.nband, part);
 }
 
 template <int K>
@@ -357,8 +427,8 @@ hipError_t ax_partial(const Shard& s, const AxPlan& pl, int K, CPtrs x, double* 
 // the 8 group sums are added in group order: a fixed tree, short dependent
 // chains.
 constexpr int kRedGroups = 8;
-__global__ __launch_bounds__(64 * kRedGroups) void ax_reduce_kernel(int K, int64_t N, int64_t ld, int64_t M,
-                                                                    int64_t rows, int64_t span,
+__global__ __launch_bounds__(64 * kRedGroups) void ax_reduce_kernel(int K, int64_t N, int64_t ld, int64_t sa,
+                                                                    int64_t rows, int64_t sb,
                                                                     const double* __restrict__ part, Ptrs out,
                                                                     double div) {
     __shared__ double lds[kRedGroups][64];
@@ -368,7 +438,7 @@ __global__ __launch_bounds__(64 * kRedGroups) void ax_reduce_kernel(int K, int64
     const int k = valid ? (int)(e / N) : 0;
     const int64_t j = valid ? e - (int64_t)k * N : 0;
     const int64_t t = j / rows;
-    const int nslots = (int)(((t + 1) * M - 1) / span - (t * M) / span + 1);
+    const int nslots = (int)(((t + 1) * sa - 1) / sb - (t * sa) / sb + 1);
     const int per = (nslots + kRedGroups - 1) / kRedGroups;
     const int c0 = g * per, c1 = (c0 + per < nslots) ? c0 + per : nslots;
     const int64_t stride = (int64_t)K * ld;
@@ -401,7 +471,7 @@ hipError_t ax_reduce(const AxPlan& pl, int K, int64_t N, int64_t ld, const doubl
                      hipStream_t st) {
     const int64_t n = (int64_t)K * N;
     hipLaunchKernelGGL(ax_reduce_kernel, dim3((unsigned)cdiv(n, 64)), dim3(64 * kRedGroups), 0, st, K, N, ld,
-                       pl.total / pl.tiles, pl.rows, pl.span, part, out, div);
+                       pl.sa, pl.rows, pl.sb, part, out, div);
     return hipGetLastError();
 }
 
