@@ -268,8 +268,9 @@ vampomi_status vampomi_dev_set_variant(vampomi_ctx* ctx, int which, int variant)
 /* average device time (HIP events) of `reps` back-to-back launches, K RHS */
 vampomi_status vampomi_dev_time_pass(vampomi_ctx* ctx, int which, int K, int reps, double* avg_ms);
 /* the kernel (as rocprofv3 names it) that pass `which` with K RHS launches now
- * (mode 1: A^T.u with the lmmse_mult epilogue; which = 2: the association-test
- * pass of vampomi_assoc_loo) */
+ * (mode 1: the CG form, i.e. A^T.u with the lmmse_mult epilogue, A.x with the
+ * fused direction update; which = 2: the association-test pass of
+ * vampomi_assoc_loo) */
 vampomi_status vampomi_dev_kernel_name(int which, int K, int mode, char* out, int cap);
 
 #ifdef __cplusplus

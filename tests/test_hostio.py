@@ -83,3 +83,15 @@ def test_fma_corrected_division_is_the_ieee_quotient(tmp_path):
                     "-o", str(exe), "-lm"], check=True)
     bad, tot = map(int, run(str(exe), 400000).split())
     assert tot > 5_000_000 and bad == 0
+
+
+def test_pow_minus_one_is_within_one_ulp_of_the_reciprocal(tmp_path):
+    """The device CG step forms beta = (1/rz_old) * rz_new where the reference
+    writes pow(rz_old, -1) (src/vamp.cpp:731).  glibc's pow is not correctly
+    rounded: it differs from the IEEE reciprocal on a small fraction of inputs,
+    by one ulp at most (a 1e-16 relative change of the CG direction)."""
+    exe = tmp_path / "powm1"
+    subprocess.run(["gcc", "-O2", "-ffp-contract=off", os.path.join(ROOT, "tests", "powm1_check.c"),
+                    "-o", str(exe), "-lm"], check=True)
+    bad, tot, maxulp = map(int, run(str(exe), 4000000).split())
+    assert tot > 3_000_000 and maxulp <= 1 and bad < 0.01 * tot

@@ -48,7 +48,8 @@ struct TimedLaunch {
 
 // scalar slots in ctx->scal: <d,p> of the fused lmmse epilogue, then the
 // synced (summed over ranks) and local halves of a DotBatch
-enum : int { SL_DP = 0, SL_SYNC = 16, SL_NSYNC = 256, SL_LOCAL = SL_SYNC + SL_NSYNC, SL_NLOCAL = 128,
+// (SL_CG: the 3K sums of a CG step, decided on the device)
+enum : int { SL_DP = 0, SL_CG = 4, SL_SYNC = 16, SL_NSYNC = 256, SL_LOCAL = SL_SYNC + SL_NSYNC, SL_NLOCAL = 128,
              SL_TOTAL = 512, SL_BARRIER = SL_TOTAL - 1 };
 
 struct vampomi_ctx {
@@ -79,6 +80,9 @@ struct vampomi_ctx {
     unsigned long long* h_flag = nullptr;  // mapped host word the stream stores sync sequence numbers into
     unsigned long long* d_flag = nullptr;
     unsigned long long sync_seq = 0;
+    vk::CgState* cgs = nullptr;     // device-side CG control (pcg.cpp)
+    vk::CgMirror* h_cgm = nullptr;  // its mapped host mirror, and the mirror's device address
+    vk::CgMirror* d_cgm = nullptr;
     double* nbuf = nullptr;     // kMaxRhs * ld scratch N-vectors (API calls)
     double* mbuf = nullptr;     // (2*kMaxRhs) * M scratch M-vectors (API calls)
 
@@ -105,11 +109,15 @@ void release_ctx_resources(vampomi_ctx* c);
 
 // ---- operators on device buffers ---------------------------------------------
 // out_k = A x_k (K <= 4), outputs at outbase + k*ld (one all-reduce). COLLECTIVE
-vampomi_status ax_dev(vampomi_ctx* c, int K, const double* const* x, double* outbase);
+// fu (may be null): fused direction update and gate (vk::AxFuse)
+vampomi_status ax_dev(vampomi_ctx* c, int K, const double* const* x, double* outbase,
+                      const vk::AxFuse* fu = nullptr);
 // out_k = A^T u_k (mode 0) or tau*A^T u_k + gam2*p_k with <out_k,p_k> summed over
-// ranks into scal[SL_DP + k] (mode 1).  u_k: ld-padded N-vectors.
+// ranks into scal[SL_DP + k] (mode 1).  u_k: ld-padded N-vectors.  gate: as in
+// vk::AxFuse; zf/beta (may be null): p_k stands for fma(beta[k], p_k, zf_k)
 vampomi_status atx_dev(vampomi_ctx* c, int K, const double* const* u, double* const* out, int mode, double tau,
-                       double gam2, const double* const* p);
+                       double gam2, const double* const* p, const int* gate = nullptr,
+                       const double* const* zf = nullptr, const double* beta = nullptr);
 // d_k = tau*A^T A v_k + gam2*v_k (lmmse_mult), <d_k,v_k> in scal[SL_DP+k]. COLLECTIVE
 vampomi_status lmmse_dev(vampomi_ctx* c, int K, const double* const* v, double* const* d, double tau, double gam2,
                          double* nscratch);

@@ -275,7 +275,7 @@ vampomi_status DotBatch::flush() {
 // ---------------------------------------------------------------------------
 // out_k = Ax(x_k) for K <= 4; outputs at outbase + k*ld (contiguous so that one
 // all-reduce carries them all).  COLLECTIVE.
-vampomi_status ax_dev(vampomi_ctx* c, int K, const double* const* x, double* outbase) {
+vampomi_status ax_dev(vampomi_ctx* c, int K, const double* const* x, double* outbase, const vk::AxFuse* fu) {
     if (!c->have_X) return fail(VAMPOMI_ERR_STATE, "Ax before the methylation data was loaded");
     vk::CPtrs xs{};
     vk::Ptrs os{};
@@ -288,7 +288,9 @@ vampomi_status ax_dev(vampomi_ctx* c, int K, const double* const* x, double* out
         t.a = ev_get(c);
         t.b = ev_get(c);
     }
-    HIPCHK(vk::ax_partial(c->shard(), c->axp, K, xs, c->ax_part, c->st, vk::Timing{t.a, t.b}));
+    const vk::AxFuse none{};
+    const vk::AxFuse& f = fu ? *fu : none;
+    HIPCHK(vk::ax_partial(c->shard(), c->axp, K, xs, c->ax_part, c->st, vk::Timing{t.a, t.b}, f));
     if (c->timing) {
         t.cls = 0;
         t.K = K;
@@ -298,9 +300,9 @@ vampomi_status ax_dev(vampomi_ctx* c, int K, const double* const* x, double* out
     }
     c->stats.a_passes_exec++;
     if (!c->use_comm) {
-        HIPCHK(vk::ax_reduce(c->axp, K, c->N, c->ld, c->ax_part, os, c->sqrtN, c->st));
+        HIPCHK(vk::ax_reduce(c->axp, K, c->N, c->ld, c->ax_part, os, c->sqrtN, c->st, f.gate));
     } else {
-        HIPCHK(vk::ax_reduce(c->axp, K, c->N, c->ld, c->ax_part, os, 0.0, c->st));
+        HIPCHK(vk::ax_reduce(c->axp, K, c->N, c->ld, c->ax_part, os, 0.0, c->st, f.gate));
         STCHK(allreduce_dev(c, outbase, (size_t)K * c->ld));  // src/data.cpp:367
         HIPCHK(vk::vec_div(K, c->N, c->ld, os, c->sqrtN, c->st));
     }
@@ -310,22 +312,25 @@ vampomi_status ax_dev(vampomi_ctx* c, int K, const double* const* x, double* out
 // out_k = ATx(u_k) (mode 0) or tau*ATx(u_k) + gam2*p_k with <out_k,p_k> summed
 // over ranks into ctx->scal[SL_DP + k] (mode 1).  u_k are ld-padded N-vectors.
 vampomi_status atx_dev(vampomi_ctx* c, int K, const double* const* u, double* const* out, int mode,
-                              double tau, double gam2, const double* const* p) {
+                              double tau, double gam2, const double* const* p, const int* gate,
+                              const double* const* zf, const double* beta) {
     if (!c->have_X) return fail(VAMPOMI_ERR_STATE, "ATx before the methylation data was loaded");
     if (c->M <= 0) return VAMPOMI_OK;
-    vk::CPtrs us{}, ps{};
+    vk::CPtrs us{}, ps{}, zs{};
     vk::Ptrs os{};
     for (int k = 0; k < K; ++k) {
         us.p[k] = u[k];
         os.p[k] = out[k];
         ps.p[k] = p ? p[k] : nullptr;
+        zs.p[k] = zf ? zf[k] : nullptr;
     }
     TimedLaunch t{};
     if (c->timing) {
         t.a = ev_get(c);
         t.b = ev_get(c);
     }
-    HIPCHK(vk::atx(c->shard(), K, us, os, 1.0 / c->sqrtN, mode, tau, gam2, ps, nullptr, c->st, vk::Timing{t.a, t.b}));
+    HIPCHK(vk::atx(c->shard(), K, us, os, 1.0 / c->sqrtN, mode, tau, gam2, ps, c->st, vk::Timing{t.a, t.b}, gate, zs,
+                   zf ? beta : nullptr));
     if (c->timing) {
         t.cls = 1;
         t.K = K;
@@ -340,8 +345,9 @@ vampomi_status atx_dev(vampomi_ctx* c, int K, const double* const* u, double* co
         // bitwise the same whether it runs alone or batched with another
         vk::DotArgs a{};
         a.nt = K;
-        for (int k = 0; k < K; ++k) a.t[k] = vk::DotTerm{out[k], p[k], vk::DOT};
-        HIPCHK(vk::dots(a, c->M, vk::RedOut{c->red_part, c->scal + SL_DP, c->ticket}, c->st));
+        for (int k = 0; k < K; ++k)
+            a.t[k] = zf ? vk::DotTerm{out[k], p[k], vk::PUPD, zf[k], beta + k} : vk::DotTerm{out[k], p[k], vk::DOT};
+        HIPCHK(vk::dots(a, c->M, vk::RedOut{c->red_part, c->scal + SL_DP, c->ticket, nullptr, 0, gate}, c->st));
         STCHK(allreduce_dev(c, c->scal + SL_DP, K));
     }
     return VAMPOMI_OK;
@@ -403,6 +409,10 @@ void release_ctx_resources(vampomi_ctx* c) {
     c->ticket = nullptr;
     if (c->h_flag) (void)hipHostFree(c->h_flag);
     c->h_flag = nullptr;
+    if (c->h_cgm) (void)hipHostFree(c->h_cgm);
+    c->h_cgm = nullptr;
+    if (c->cgs) (void)hipFree(c->cgs);
+    c->cgs = nullptr;
     if (c->comm) (void)ncclCommDestroy(c->comm);
     c->comm = nullptr;
     if (c->st) (void)hipStreamDestroy(c->st);
@@ -455,6 +465,11 @@ extern "C" vampomi_status vampomi_open(const vampomi_shard_desc* d, vampomi_ctx*
     STCHK(dev_alloc(&c->nbuf, (size_t)vk::kMaxRhs * c->ld));
     HIPCHK(hipMemsetAsync(c->nbuf, 0, (size_t)vk::kMaxRhs * c->ld * 8, c->st));
     STCHK(dev_alloc(&c->mbuf, (size_t)2 * vk::kMaxRhs * Mx));
+    HIPCHK(hipMalloc((void**)&c->cgs, sizeof(vk::CgState)));
+    HIPCHK(hipMemsetAsync(c->cgs, 0, sizeof(vk::CgState), c->st));
+    HIPCHK(hipHostMalloc((void**)&c->h_cgm, sizeof(vk::CgMirror), hipHostMallocMapped | hipHostMallocCoherent));
+    std::memset(c->h_cgm, 0, sizeof(vk::CgMirror));
+    HIPCHK(hipHostGetDevicePointer((void**)&c->d_cgm, c->h_cgm, 0));
     // VAMPOMI_FORCE_RCCL=1 runs a 1-rank job through the multi-rank code path
     // (RCCL communicator, all-reduces, post-reduce division) so that path can
     // be exercised on a single GPU
@@ -1018,7 +1033,7 @@ extern "C" vampomi_status vampomi_dev_time_pass(vampomi_ctx* c, int which, int K
         if (which == 0)
             HIPCHK(vk::ax_partial(c->shard(), c->axp, K, in, c->ax_part, c->st));
         else if (which == 1)
-            HIPCHK(vk::atx(c->shard(), K, in, out, 1.0 / c->sqrtN, 0, 0.0, 0.0, vk::CPtrs{}, c->red_part, c->st));
+            HIPCHK(vk::atx(c->shard(), K, in, out, 1.0 / c->sqrtN, 0, 0.0, 0.0, vk::CPtrs{}, c->st));
         else  // association pass: ymod = nbuf slot 0, x1 = mbuf slot 0, sums in mbuf slots 3..7
             HIPCHK(vk::loo_sums(c->shard(), c->nbuf, c->mbuf, c->sqrtN, c->mbuf + 3 * Mx, c->st));
     }

@@ -19,13 +19,15 @@ struct Timing { hipEvent_t start = nullptr, stop = nullptr; };
 // Destination of a fused two-stage reduction (see red_finish in kernels.hip):
 // per-block partials in part, the final sums in out[0..nq) (device memory or
 // mapped host memory), ticket a zeroed device counter the kernel re-arms;
-// flag (may be null): the last block stores seq there (system scope, after out)
+// flag (may be null): the last block stores seq there (system scope, after out);
+// gate (may be null): the launch does nothing while *gate == 0
 struct RedOut {
     double* part;
     double* out;
     unsigned* ticket;
-    unsigned long long* flag;
-    unsigned long long seq;
+    unsigned long long* flag = nullptr;
+    unsigned long long seq = 0;
+    const int* gate = nullptr;
 };
 struct Ptrs { double* p[kMaxRhs]; };
 
@@ -62,22 +64,33 @@ int ax_variant_count();
 bool set_ax_variant(int v);   // development hook (tools/kbench.py)
 int atx_variant_count();
 bool set_atx_variant(int v);
+// Optional fusion into the A.x pass (the CG direction update of the previous
+// step): with z set, the pass multiplies x_k = fma(beta[k], p_k, z_k), where
+// p_k is the `x` argument (every consumer of the new direction forms it the
+// same way; cg_update stores it).  gate (may be null): no work while *gate == 0.
+struct AxFuse {
+    CPtrs z{};
+    const double* beta = nullptr;  // device
+    const int* gate = nullptr;
+};
 hipError_t ax_partial(const Shard& s, const AxPlan& pl, int K, CPtrs x, double* part, hipStream_t st,
-                      const Timing& tm = Timing{});
+                      const Timing& tm = Timing{}, const AxFuse& fu = AxFuse{});
 // out_k[j] = sum_c part[c][k][j]; if div > 0 then out_k[j] /= div
 hipError_t ax_reduce(const AxPlan& pl, int K, int64_t N, int64_t ld, const double* part, Ptrs out,
-                     double div, hipStream_t st);
+                     double div, hipStream_t st, const int* gate = nullptr);
 // out_k[j] /= div (after the cross-rank all-reduce)
 hipError_t vec_div(int K, int64_t n, int64_t ld, Ptrs v, double div, hipStream_t st);
 
 // ---- A^T.u : one wave per group of markers --------------------------------
 // mode 0: out_k[i] = (msig_i * dot_k(i)) * scale
 // mode 1 (lmmse_mult): out_k[i] = ((msig_i*dot)*scale)*tau + gam2*p_k[i]
-// (dp_part is unused; <out_k, p_k> is a separate fixed-geometry reduction)
+// (<out_k, p_k> is a separate fixed-geometry reduction); gate as in AxFuse
 int atx_blocks(int64_t M, int K);
 std::string kernel_name(int which, int K, int mode);  // as rocprofv3 prints it
+// zf/beta (mode 1, may be null): the epilogue's p_k is fma(beta[k], p_k, zf_k)
 hipError_t atx(const Shard& s, int K, CPtrs u, Ptrs out, double scale, int mode, double tau,
-               double gam2, CPtrs p, double* dp_part, hipStream_t st, const Timing& tm = Timing{});
+               double gam2, CPtrs p, hipStream_t st, const Timing& tm = Timing{}, const int* gate = nullptr,
+               CPtrs zf = CPtrs{}, const double* beta = nullptr);
 
 // ---- marker statistics (data::compute_markers_statistics) ----------------
 hipError_t marker_stats(const double* X, int64_t ld, int64_t N, int64_t M, double nonas,
@@ -94,8 +107,15 @@ hipError_t scale_vec(int64_t n, double* v, double a, hipStream_t st);
 hipError_t add_noise(uint64_t seed, int64_t N, double sd, double* y, hipStream_t st);
 
 // ---- reductions --------------------------------------------------------------
-enum DotOp { DOT = 0, DIFF2 = 1, SUM = 2 };
-struct DotTerm { const double* a; const double* b; int op; };
+// PUPD: a . fma(*beta, b, c) (a CG step's <d, p> with p = z + beta p fused)
+enum DotOp { DOT = 0, DIFF2 = 1, SUM = 2, PUPD = 3 };
+struct DotTerm {
+    const double* a;
+    const double* b;
+    int op;
+    const double* c = nullptr;
+    const double* beta = nullptr;
+};
 struct DotArgs { DotTerm t[kMaxTerms]; int nt; };
 int red_blocks(int64_t n);
 // ro.out[q] = term q summed over [0, n): per-block partials, then the blocks'
@@ -185,13 +205,32 @@ struct CgVecs {
 // r = v - d (or v, or v - (atx0*tau + gam2*mu)), z = r/diag, p = z;
 // <r,z>, <v,v> per system in ro.out (2K values)
 hipError_t cg_init(int K, int64_t M, const CgVecs& c, double diag, const RedOut& ro, hipStream_t st);
-// alpha_k = rz[k] / dp_dev[k]; mu += alpha p; r -= d alpha; z = r/diag;
-// <r,z>, <r,r>, <v,mu> in ro.out (3K values, ordered k-major)
-struct CgScalars { double rz[kMaxRhs]; };
-hipError_t cg_update(int K, int64_t M, const CgVecs& c, double diag, CgScalars rz, const double* dp_dev,
-                     const RedOut& ro, hipStream_t st);
-// p = z + beta_k p
-struct CgBeta { double beta[kMaxRhs]; };
-hipError_t cg_pupdate(int K, int64_t M, const CgVecs& c, CgBeta b, hipStream_t st);
+// Device-side CG control.  The scalar recurrences of a CG step (alpha, the
+// Onsager and residual stops, beta) run on the device from a CgState, so the
+// host can queue the next step before this one's sums are known: every launch
+// of a step is gated on `any` (a step queued after the last system stopped
+// does nothing).  `mirror` (mapped host memory) receives any/iters, then the
+// step's flag.
+struct CgState {
+    double rz[kMaxRhs], vv[kMaxRhs], prev_ons[kMaxRhs], beta[kMaxRhs];
+    double gam2, tol;
+    int active[kMaxRhs], iters[kMaxRhs], onsager[kMaxRhs];
+    int K, any;
+};
+struct CgMirror {
+    int any;
+    int iters[kMaxRhs];
+};
+// *dst = init (one thread)
+hipError_t cg_start(const CgState& init, CgState* dst, hipStream_t st);
+// for active k: [fuse: p = fma(beta_k, p, z), stored] alpha_k = rz[k] / dp_dev[k];
+// mu += alpha p; r -= d alpha; z = r/diag; <r,z>, <r,r>, <v,mu> in ro.out (3K
+// values, k-major; zeros for stopped systems); gated on cs->any
+hipError_t cg_update(int K, int64_t M, const CgVecs& c, double diag, const CgState* cs, const double* dp_dev,
+                     int fuse, const RedOut& ro, hipStream_t st);
+// step `it`'s decisions from red (the 3K sums of cg_update, summed over ranks),
+// src/vamp.cpp:700-750; then mirror and flag (stored even when gated off)
+hipError_t cg_decide(CgState* cs, const double* red, int it, CgMirror* mirror, unsigned long long* flag,
+                     unsigned long long seq, hipStream_t st);
 
 }  // namespace vk

@@ -193,10 +193,15 @@ static inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 // arithmetic (U*R/2 16-byte loads in flight per lane).  Per-sample summation
 // order within a slot is the reference's: markers in index order,
 // acc += (x - mave_i) * (msig_i * x_i).
-template <int K, int R, int U, bool NT>
+// x_k[i] of the pass: p_k[i], or with fusion (FU) fma(beta_k, p_k[i], z_k[i])
+// (the CG direction update, src/vamp.cpp:738-739, as every consumer of the new
+// direction forms it).  The kernel stores nothing but its partials, so the
+// compiler keeps the per-marker loads scalar.
+template <int K, int R, int U, bool NT, bool FU>
 __device__ __forceinline__ void ax_piece(const double* __restrict__ X, int64_t ld, int64_t N,
                                          const double* __restrict__ mave, const double* __restrict__ msig,
-                                         const CPtrs& xs, int64_t j0, int64_t i0, int64_t i1, double (&acc)[K][R]) {
+                                         const CPtrs& xs, const AxFuse& fu, const double (&bk)[K], int64_t j0,
+                                         int64_t i0, int64_t i1, double (&acc)[K][R]) {
     constexpr int P = R / 2;  // 16-byte pieces per lane per marker
     int64_t off[P];  // invalid pieces read row 0 of the column (in bounds) and are discarded at the store
 #pragma unroll
@@ -210,13 +215,19 @@ __device__ __forceinline__ void ax_piece(const double* __restrict__ X, int64_t l
 #pragma unroll
             for (int q = 0; q < P; ++q)
                 xv[u][q] = NT ? ld_stream(col + (int64_t)u * ld + off[q]) : ld2(col + (int64_t)u * ld + off[q]);
+        double xk[U][K];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+                xk[u][k] = FU ? __builtin_fma(bk[k], xs.p[k][i + u], fu.z.p[k][i + u]) : xs.p[k][i + u];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const double ave = mave[i + u];
             const double sg = msig[i + u];
 #pragma unroll
             for (int k = 0; k < K; ++k) {
-                const double w = sg * xs.p[k][i + u];
+                const double w = sg * xk[u][k];
 #pragma unroll
                 for (int q = 0; q < P; ++q) {
                     acc[k][2 * q] += (xv[u][q].x - ave) * w;
@@ -230,11 +241,14 @@ __device__ __forceinline__ void ax_piece(const double* __restrict__ X, int64_t l
         v2d xv[P];
 #pragma unroll
         for (int q = 0; q < P; ++q) xv[q] = NT ? ld_stream(col + off[q]) : ld2(col + off[q]);
+        double xk[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) xk[k] = FU ? __builtin_fma(bk[k], xs.p[k][i], fu.z.p[k][i]) : xs.p[k][i];
         const double ave = mave[i];
         const double sg = msig[i];
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            const double w = sg * xs.p[k][i];
+            const double w = sg * xk[k];
 #pragma unroll
             for (int q = 0; q < P; ++q) {
                 acc[k][2 * q] += (xv[q].x - ave) * w;
@@ -268,15 +282,19 @@ __device__ __forceinline__ void ax_zero(double (&acc)[K][R]) {
         for (int r = 0; r < R; ++r) acc[k][r] = 0.0;
 }
 
-template <int K, int R, int U, bool NT>
+template <int K, int R, int U, bool NT, bool FU>
 __global__ __launch_bounds__(kBlock) void ax_partial_kernel(const double* __restrict__ X, int64_t ld,
                                                             int64_t N, int64_t M,
                                                             const double* __restrict__ mave,
                                                             const double* __restrict__ msig, CPtrs xs,
                                                             int64_t tiles, int64_t span, int64_t nband,
-                                                            double* __restrict__ part) {
+                                                            double* __restrict__ part, AxFuse fu) {
+    if (fu.gate && !*fu.gate) return;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t g = blockIdx.x, G = gridDim.x;
+    double bk[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) bk[k] = FU ? fu.beta[k] : 0.0;
     const int64_t slab = (int64_t)wave * (64 * R) + 2 * lane;  // row offset inside a tile
     double acc[K][R];
     if (nband > 0) {
@@ -298,12 +316,13 @@ __global__ __launch_bounds__(kBlock) void ax_partial_kernel(const double* __rest
             const int64_t phi = (int64_t)(((uint64_t)p * 0x9E3779B97F4A7C15ULL) >> 40) % G;  // dither in [0, G)
             if (jA < N) {
                 const int64_t u0 = c + (xa0 * w + phi) / G, u1 = c + (xa1 * w + phi) / G;
-                ax_piece<K, R, U, NT>(X, ld, N, mave, msig, xs, jA, u0 == Mu ? M : u0 * U, u1 == Mu ? M : u1 * U,
-                                      acc);
+                ax_piece<K, R, U, NT, FU>(X, ld, N, mave, msig, xs, fu, bk, jA, u0 == Mu ? M : u0 * U,
+                                      u1 == Mu ? M : u1 * U, acc);
             }
             if (hasB && jB < N) {
                 const int64_t u1 = c + (xb1 * w + phi) / G;
-                ax_piece<K, R, U, NT>(X, ld, N, mave, msig, xs, jB, c * U, u1 == Mu ? M : u1 * U, accB);
+                ax_piece<K, R, U, NT, FU>(X, ld, N, mave, msig, xs, fu, bk, jB, c * U, u1 == Mu ? M : u1 * U,
+                                      accB);
             }
         }
         if (jA < N) ax_store<K, R>(part, g - (tA * G) / tiles, ld, N, jA, acc);
@@ -322,7 +341,7 @@ __global__ __launch_bounds__(kBlock) void ax_partial_kernel(const double* __rest
         const int64_t j0 = t * (kBlock * R) + slab;
         if (j0 >= N) continue;
         ax_zero<K, R>(acc);
-        ax_piece<K, R, U, NT>(X, ld, N, mave, msig, xs, j0, i0, i1, acc);
+        ax_piece<K, R, U, NT, FU>(X, ld, N, mave, msig, xs, fu, bk, j0, i0, i1, acc);
         ax_store<K, R>(part, g - (t * M) / span, ld, N, j0, acc);
     }
 }
@@ -384,37 +403,44 @@ AxPlan ax_plan(int64_t N, int64_t M) {
 // launches go through hipExtLaunchKernelGGL: the optional start / stop events
 // are written by the kernel's own dispatch (no extra marker packets around it)
 template <int K, int R, int U, bool NT>
-static void launch_ax(const Shard& s, const AxPlan& pl, CPtrs x, double* part, hipStream_t st, const Timing& tm) {
-    hipExtLaunchKernelGGL((ax_partial_kernel<K, R, U, NT>), dim3(pl.groups), dim3(kBlock), 0, st, tm.start,
-                          tm.stop, 0, s.X, s.ld, s.N, s.M, s.mave, s.msig, x, pl.tiles, pl.span, pl.nband, part);
+static void launch_ax(const Shard& s, const AxPlan& pl, CPtrs x, double* part, hipStream_t st, const Timing& tm,
+                      const AxFuse& fu) {
+    if (fu.z.p[0])
+        hipExtLaunchKernelGGL((ax_partial_kernel<K, R, U, NT, true>), dim3(pl.groups), dim3(kBlock), 0, st, tm.start,
+                              tm.stop, 0, s.X, s.ld, s.N, s.M, s.mave, s.msig, x, pl.tiles, pl.span, pl.nband, part,
+                              fu);
+    else
+        hipExtLaunchKernelGGL((ax_partial_kernel<K, R, U, NT, false>), dim3(pl.groups), dim3(kBlock), 0, st,
+                              tm.start, tm.stop, 0, s.X, s.ld, s.N, s.M, s.mave, s.msig, x, pl.tiles, pl.span,
+                              pl.nband, part, fu);
 }
 
 template <int K>
 static bool launch_ax_v(int v, const Shard& s, const AxPlan& pl, CPtrs x, double* part, hipStream_t st,
-                        const Timing& tm) {
+                        const Timing& tm, const AxFuse& fu) {
     switch (v) {
-        case 0: launch_ax<K, 2, 8, true>(s, pl, x, part, st, tm); return true;
-        case 1: launch_ax<K, 2, 8, false>(s, pl, x, part, st, tm); return true;
-        case 2: launch_ax<K, 4, 4, true>(s, pl, x, part, st, tm); return true;
-        case 3: launch_ax<K, 4, 8, true>(s, pl, x, part, st, tm); return true;
-        case 4: launch_ax<K, 8, 4, true>(s, pl, x, part, st, tm); return true;
-        case 5: launch_ax<K, 2, 4, true>(s, pl, x, part, st, tm); return true;
-        case 6: launch_ax<K, 2, 12, true>(s, pl, x, part, st, tm); return true;
+        case 0: launch_ax<K, 2, 8, true>(s, pl, x, part, st, tm, fu); return true;
+        case 1: launch_ax<K, 2, 8, false>(s, pl, x, part, st, tm, fu); return true;
+        case 2: launch_ax<K, 4, 4, true>(s, pl, x, part, st, tm, fu); return true;
+        case 3: launch_ax<K, 4, 8, true>(s, pl, x, part, st, tm, fu); return true;
+        case 4: launch_ax<K, 8, 4, true>(s, pl, x, part, st, tm, fu); return true;
+        case 5: launch_ax<K, 2, 4, true>(s, pl, x, part, st, tm, fu); return true;
+        case 6: launch_ax<K, 2, 12, true>(s, pl, x, part, st, tm, fu); return true;
         default: return false;
     }
 }
 
 hipError_t ax_partial(const Shard& s, const AxPlan& pl, int K, CPtrs x, double* part, hipStream_t st,
-                      const Timing& tm) {
+                      const Timing& tm, const AxFuse& fu) {
     if (pl.rows != (int64_t)kBlock * kAxVariants[pl.variant].R || pl.total != pl.tiles * s.M ||
         pl.tiles * pl.rows < s.N)
         return hipErrorInvalidValue;  // plan made for another shape
     bool ok = false;
     switch (K) {
-        case 1: ok = launch_ax_v<1>(pl.variant, s, pl, x, part, st, tm); break;
-        case 2: ok = launch_ax_v<2>(pl.variant, s, pl, x, part, st, tm); break;
-        case 3: ok = launch_ax_v<3>(pl.variant, s, pl, x, part, st, tm); break;
-        case 4: ok = launch_ax_v<4>(pl.variant, s, pl, x, part, st, tm); break;
+        case 1: ok = launch_ax_v<1>(pl.variant, s, pl, x, part, st, tm, fu); break;
+        case 2: ok = launch_ax_v<2>(pl.variant, s, pl, x, part, st, tm, fu); break;
+        case 3: ok = launch_ax_v<3>(pl.variant, s, pl, x, part, st, tm, fu); break;
+        case 4: ok = launch_ax_v<4>(pl.variant, s, pl, x, part, st, tm, fu); break;
         default: break;
     }
     if (!ok) return hipErrorInvalidValue;
@@ -430,7 +456,8 @@ constexpr int kRedGroups = 8;
 __global__ __launch_bounds__(64 * kRedGroups) void ax_reduce_kernel(int K, int64_t N, int64_t ld, int64_t sa,
                                                                     int64_t rows, int64_t sb,
                                                                     const double* __restrict__ part, Ptrs out,
-                                                                    double div) {
+                                                                    double div, const int* gate) {
+    if (gate && !*gate) return;
     __shared__ double lds[kRedGroups][64];
     const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
     const int64_t e = (int64_t)blockIdx.x * 64 + lane;
@@ -468,10 +495,10 @@ __global__ __launch_bounds__(64 * kRedGroups) void ax_reduce_kernel(int K, int64
 }
 
 hipError_t ax_reduce(const AxPlan& pl, int K, int64_t N, int64_t ld, const double* part, Ptrs out, double div,
-                     hipStream_t st) {
+                     hipStream_t st, const int* gate) {
     const int64_t n = (int64_t)K * N;
     hipLaunchKernelGGL(ax_reduce_kernel, dim3((unsigned)cdiv(n, 64)), dim3(64 * kRedGroups), 0, st, K, N, ld,
-                       pl.sa, pl.rows, pl.sb, part, out, div);
+                       pl.sa, pl.rows, pl.sb, part, out, div, gate);
     return hipGetLastError();
 }
 
@@ -502,7 +529,9 @@ __global__ __launch_bounds__(kBlock) void atx_kernel(const double* __restrict__ 
                                                      const double* __restrict__ mave,
                                                      const double* __restrict__ msig, CPtrs u, Ptrs out,
                                                      double scale, double tau, double gam2, CPtrs pv,
-                                                     double* __restrict__ /*unused*/) {
+                                                     const int* __restrict__ gate, CPtrs zf,
+                                                     const double* __restrict__ beta) {
+    if (gate && !*gate) return;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t m0 = ((int64_t)blockIdx.x * 4 + wave) * G;
     double acc[G][K];
@@ -566,8 +595,9 @@ __global__ __launch_bounds__(kBlock) void atx_kernel(const double* __restrict__ 
                 double val = msig[m] * dot;  // sigma_inv * dpa
                 val *= scale;                // ATx[mloc] *= 1/sqrt(N)
                 if (MODE == 1) {
-                    val *= tau;              // res[i] *= tau
-                    val += gam2 * pv.p[k][m];  // res[i] += gam2 * v[i]
+                    const double pk = zf.p[0] ? __builtin_fma(beta[k], pv.p[k][m], zf.p[k][m]) : pv.p[k][m];
+                    val *= tau;        // res[i] *= tau
+                    val += gam2 * pk;  // res[i] += gam2 * v[i]
                 }
                 out.p[k][m] = val;
             }
@@ -598,7 +628,8 @@ std::string kernel_name(int which, int K, int mode) {
     char b[160];
     if (which == 0) {
         const AxVariant& v = kAxVariants[g_ax_variant];
-        std::snprintf(b, sizeof b, "ax_partial_kernel<%d, %d, %d, %s>", K, v.R, v.U, v.NT ? "true" : "false");
+        std::snprintf(b, sizeof b, "ax_partial_kernel<%d, %d, %d, %s, %s>", K, v.R, v.U, v.NT ? "true" : "false",
+                      mode == 1 ? "true" : "false");
     } else {
         const AtxVariant& v = kAtxVariants[atx_variant_for(K)];
         std::snprintf(b, sizeof b, "atx_kernel<%d, %d, %d, %d, %s>", v.G, K, mode, v.UJ, v.NT ? "true" : "false");
@@ -610,44 +641,44 @@ int atx_blocks(int64_t M, int K) { return (int)cdiv(M, 4 * kAtxVariants[atx_vari
 
 template <int G, int K, int MODE, int UJ, bool NT>
 static void launch_atx(const Shard& s, CPtrs u, Ptrs out, double scale, double tau, double gam2, CPtrs p,
-                       double* dp_part, hipStream_t st, const Timing& tm) {
+                       const int* gate, CPtrs zf, const double* beta, hipStream_t st, const Timing& tm) {
     hipExtLaunchKernelGGL((atx_kernel<G, K, MODE, UJ, NT>), dim3((unsigned)cdiv(s.M, 4 * G)), dim3(kBlock), 0, st,
                           tm.start, tm.stop, 0, s.X, s.ld, s.N, s.M, s.mave, s.msig, u, out, scale, tau, gam2, p,
-                          dp_part);
+                          gate, zf, beta);
 }
 
 template <int K, int MODE>
 static bool launch_atx_v(int v, const Shard& s, CPtrs u, Ptrs out, double scale, double tau, double gam2, CPtrs p,
-                         double* dp, hipStream_t st, const Timing& tm) {
+                         const int* gate, CPtrs zf, const double* beta, hipStream_t st, const Timing& tm) {
     switch (v) {
-        case 0: launch_atx<4, K, MODE, 2, true>(s, u, out, scale, tau, gam2, p, dp, st, tm); return true;
-        case 1: launch_atx<4, K, MODE, 2, false>(s, u, out, scale, tau, gam2, p, dp, st, tm); return true;
-        case 2: launch_atx<2, K, MODE, 2, true>(s, u, out, scale, tau, gam2, p, dp, st, tm); return true;
-        case 3: launch_atx<8, K, MODE, 2, true>(s, u, out, scale, tau, gam2, p, dp, st, tm); return true;
-        case 4: launch_atx<4, K, MODE, 4, true>(s, u, out, scale, tau, gam2, p, dp, st, tm); return true;
-        case 5: launch_atx<4, K, MODE, 1, true>(s, u, out, scale, tau, gam2, p, dp, st, tm); return true;
-        case 6: launch_atx<8, K, MODE, 1, true>(s, u, out, scale, tau, gam2, p, dp, st, tm); return true;
-        case 7: launch_atx<2, K, MODE, 4, true>(s, u, out, scale, tau, gam2, p, dp, st, tm); return true;
+        case 0: launch_atx<4, K, MODE, 2, true>(s, u, out, scale, tau, gam2, p, gate, zf, beta, st, tm); return true;
+        case 1: launch_atx<4, K, MODE, 2, false>(s, u, out, scale, tau, gam2, p, gate, zf, beta, st, tm); return true;
+        case 2: launch_atx<2, K, MODE, 2, true>(s, u, out, scale, tau, gam2, p, gate, zf, beta, st, tm); return true;
+        case 3: launch_atx<8, K, MODE, 2, true>(s, u, out, scale, tau, gam2, p, gate, zf, beta, st, tm); return true;
+        case 4: launch_atx<4, K, MODE, 4, true>(s, u, out, scale, tau, gam2, p, gate, zf, beta, st, tm); return true;
+        case 5: launch_atx<4, K, MODE, 1, true>(s, u, out, scale, tau, gam2, p, gate, zf, beta, st, tm); return true;
+        case 6: launch_atx<8, K, MODE, 1, true>(s, u, out, scale, tau, gam2, p, gate, zf, beta, st, tm); return true;
+        case 7: launch_atx<2, K, MODE, 4, true>(s, u, out, scale, tau, gam2, p, gate, zf, beta, st, tm); return true;
         default: return false;
     }
 }
 
 hipError_t atx(const Shard& s, int K, CPtrs u, Ptrs out, double scale, int mode, double tau, double gam2, CPtrs p,
-               double* dp_part, hipStream_t st, const Timing& tm) {
+               hipStream_t st, const Timing& tm, const int* gate, CPtrs zf, const double* beta) {
     const int v = atx_variant_for(K);
     bool ok = false;
     if (mode == 0) {
         switch (K) {
-            case 1: ok = launch_atx_v<1, 0>(v, s, u, out, scale, tau, gam2, p, dp_part, st, tm); break;
-            case 2: ok = launch_atx_v<2, 0>(v, s, u, out, scale, tau, gam2, p, dp_part, st, tm); break;
-            case 3: ok = launch_atx_v<3, 0>(v, s, u, out, scale, tau, gam2, p, dp_part, st, tm); break;
+            case 1: ok = launch_atx_v<1, 0>(v, s, u, out, scale, tau, gam2, p, gate, zf, beta, st, tm); break;
+            case 2: ok = launch_atx_v<2, 0>(v, s, u, out, scale, tau, gam2, p, gate, zf, beta, st, tm); break;
+            case 3: ok = launch_atx_v<3, 0>(v, s, u, out, scale, tau, gam2, p, gate, zf, beta, st, tm); break;
             default: break;
         }
     } else {
         switch (K) {
-            case 1: ok = launch_atx_v<1, 1>(v, s, u, out, scale, tau, gam2, p, dp_part, st, tm); break;
-            case 2: ok = launch_atx_v<2, 1>(v, s, u, out, scale, tau, gam2, p, dp_part, st, tm); break;
-            case 3: ok = launch_atx_v<3, 1>(v, s, u, out, scale, tau, gam2, p, dp_part, st, tm); break;
+            case 1: ok = launch_atx_v<1, 1>(v, s, u, out, scale, tau, gam2, p, gate, zf, beta, st, tm); break;
+            case 2: ok = launch_atx_v<2, 1>(v, s, u, out, scale, tau, gam2, p, gate, zf, beta, st, tm); break;
+            case 3: ok = launch_atx_v<3, 1>(v, s, u, out, scale, tau, gam2, p, gate, zf, beta, st, tm); break;
             default: break;
         }
     }
@@ -788,7 +819,11 @@ int red_blocks(int64_t n) {
 // the op is a per-launch uniform selected per element
 template <int NT>
 __global__ __launch_bounds__(kBlock) void dots_kernel(DotArgs a, int64_t n, RedOut ro) {
+    if (ro.gate && !*ro.gate) return;
     __shared__ double lds[4];
+    double bt[NT];
+#pragma unroll
+    for (int q = 0; q < NT; ++q) bt[q] = a.t[q].op == PUPD ? *a.t[q].beta : 0.0;
     double acc[NT];
 #pragma unroll
     for (int q = 0; q < NT; ++q) acc[q] = 0.0;
@@ -797,12 +832,13 @@ __global__ __launch_bounds__(kBlock) void dots_kernel(DotArgs a, int64_t n, RedO
 #pragma unroll
         for (int q = 0; q < NT; ++q) {
             va[q] = a.t[q].a[e];
-            vb[q] = a.t[q].b[e];
+            vb[q] = a.t[q].op == PUPD ? __builtin_fma(bt[q], a.t[q].b[e], a.t[q].c[e]) : a.t[q].b[e];
         }
 #pragma unroll
         for (int q = 0; q < NT; ++q) {
             const double d = va[q] - vb[q];
-            const double v = a.t[q].op == DOT ? va[q] * vb[q] : (a.t[q].op == DIFF2 ? d * d : va[q]);
+            const int op = a.t[q].op;
+            const double v = (op == DOT || op == PUPD) ? va[q] * vb[q] : (op == DIFF2 ? d * d : va[q]);
             acc[q] += v;
         }
     }
@@ -1017,20 +1053,39 @@ hipError_t cg_init(int K, int64_t M, const CgVecs& c, double diag, const RedOut&
     return hipGetLastError();
 }
 
-__global__ __launch_bounds__(kBlock) void cg_update_kernel(int K, int64_t M, CgVecs c, double diag, CgScalars rz,
-                                                           const double* __restrict__ dp_dev, RedOut ro) {
+__global__ void cg_start_kernel(CgState init, CgState* dst) {
+    if (threadIdx.x == 0) *dst = init;
+}
+
+hipError_t cg_start(const CgState& init, CgState* dst, hipStream_t st) {
+    hipLaunchKernelGGL(cg_start_kernel, dim3(1), dim3(64), 0, st, init, dst);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(kBlock) void cg_update_kernel(int K, int64_t M, CgVecs c, double diag,
+                                                           const CgState* __restrict__ cs,
+                                                           const double* __restrict__ dp_dev, int fuse, RedOut ro) {
+    if (!cs->any) return;
     __shared__ double lds[4];
     double alpha[kMaxRhs];
+    bool on[kMaxRhs];
 #pragma unroll
-    for (int k = 0; k < kMaxRhs; ++k) alpha[k] = k < K ? rz.rz[k] / dp_dev[k] : 0.0;
+    for (int k = 0; k < kMaxRhs; ++k) {
+        on[k] = k < K && cs->active[k];
+        alpha[k] = on[k] ? cs->rz[k] / dp_dev[k] : 0.0;  // :702
+    }
     double acc[3 * kMaxRhs];
 #pragma unroll
     for (int q = 0; q < 3 * kMaxRhs; ++q) acc[q] = 0.0;
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < M; i += (int64_t)gridDim.x * kBlock) {
 #pragma unroll
         for (int k = 0; k < kMaxRhs; ++k) {
-            if (k < K) {
-                const double pi = c.p[k][i];
+            if (on[k]) {
+                double pi = c.p[k][i];
+                if (fuse) {  // p = z + beta p (:738-739)
+                    pi = __builtin_fma(cs->beta[k], pi, c.z[k][i]);
+                    c.p[k][i] = pi;
+                }
                 const double mu = c.mu[k][i] + alpha[k] * pi;  // mu += alpha * p
                 const double r = c.r[k][i] - c.d[k][i] * alpha[k];  // r -= d * alpha
                 const double z = r / diag;
@@ -1047,23 +1102,57 @@ __global__ __launch_bounds__(kBlock) void cg_update_kernel(int K, int64_t M, CgV
     red_finish(ro, 3 * K, lds);
 }
 
-hipError_t cg_update(int K, int64_t M, const CgVecs& c, double diag, CgScalars rz, const double* dp_dev,
-                     const RedOut& ro, hipStream_t st) {
-    hipLaunchKernelGGL(cg_update_kernel, dim3(red_blocks(M)), dim3(kBlock), 0, st, K, M, c, diag, rz, dp_dev, ro);
+hipError_t cg_update(int K, int64_t M, const CgVecs& c, double diag, const CgState* cs, const double* dp_dev,
+                     int fuse, const RedOut& ro, hipStream_t st) {
+    hipLaunchKernelGGL(cg_update_kernel, dim3(red_blocks(M)), dim3(kBlock), 0, st, K, M, c, diag, cs, dp_dev, fuse,
+                       ro);
     return hipGetLastError();
 }
 
-__global__ void cg_pupdate_kernel(int K, int64_t M, CgVecs c, CgBeta b) {
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= M) return;
-#pragma unroll
-    for (int k = 0; k < kMaxRhs; ++k)
-        if (k < K) c.p[k][i] = c.z[k][i] + b.beta[k] * c.p[k][i];
+// one thread: the host loop of vamp::precondCG_solver after each step's sums
+__global__ void cg_decide_kernel(CgState* cs, const double* __restrict__ red, int it, CgMirror* mirror,
+                                 unsigned long long* flag, unsigned long long seq) {
+    if (threadIdx.x != 0) return;
+    if (cs->any) {
+        int any = 0;
+        for (int k = 0; k < cs->K; ++k) {
+            if (!cs->active[k]) continue;
+            cs->iters[k] = it + 1;
+            const double rz_new = red[3 * k], rr = red[3 * k + 1], vmu = red[3 * k + 2];
+            if (cs->onsager[k]) {  // :708-726
+                const double ons = cs->gam2 * vmu;
+                const double rel = ons != 0 ? fabs((ons - cs->prev_ons[k]) / ons) : 1;
+                if (rel < 1e-8) {
+                    cs->active[k] = 0;
+                    continue;
+                }
+                cs->prev_ons[k] = ons;
+            }
+            // :731 pow(rz, -1): the correctly rounded reciprocal; glibc's pow
+            // differs from it by one ulp on ~0.1% of inputs (tests/powm1_check.c)
+            double bt = 1.0 / cs->rz[k];
+            bt *= rz_new;                 // :736
+            cs->rz[k] = rz_new;
+            const double rel_err = sqrt(rr) / sqrt(cs->vv[k]);  // :742-744
+            if (rel_err < cs->tol) {                            // :750
+                cs->active[k] = 0;
+                continue;
+            }
+            cs->beta[k] = bt;
+            any = 1;
+        }
+        cs->any = any;
+    }
+    if (mirror) {
+        mirror->any = cs->any;
+        for (int k = 0; k < kMaxRhs; ++k) mirror->iters[k] = cs->iters[k];
+    }
+    if (flag) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-hipError_t cg_pupdate(int K, int64_t M, const CgVecs& c, CgBeta b, hipStream_t st) {
-    if (M <= 0) return hipSuccess;
-    hipLaunchKernelGGL(cg_pupdate_kernel, dim3((unsigned)cdiv(M, kBlock)), dim3(kBlock), 0, st, K, M, c, b);
+hipError_t cg_decide(CgState* cs, const double* red, int it, CgMirror* mirror, unsigned long long* flag,
+                     unsigned long long seq, hipStream_t st) {
+    hipLaunchKernelGGL(cg_decide_kernel, dim3(1), dim3(64), 0, st, cs, red, it, mirror, flag, seq);
     return hipGetLastError();
 }
 

@@ -5,12 +5,28 @@
 // recurrences: alpha = <r,z>/<d,p>; mu += alpha p; [Onsager stop on
 // gam2<v,mu>]; r -= d alpha; z = r/diag; beta = pow(<r,z>_old,-1)*<r,z>_new;
 // p = z + beta p; stop when ||r||/||v|| < tol.  What is shared is the pass
-// over X: lmmse_mult(p) for all active systems is one A.x and one A^T.u
-// launch with K right-hand sides, so two systems cost 2*max(k1, k2) passes
-// instead of 2*(k1 + k2), with every iterate bitwise equal to a solo solve.
+// over X: lmmse_mult(p) for all systems is one A.x and one A^T.u launch with
+// K right-hand sides, so two systems cost 2*max(k1, k2) passes instead of
+// 2*(k1 + k2), with every iterate bitwise equal to a solo solve.
+//
+// The step's scalar decisions run on the device (vk::cg_decide), so the host
+// never stands between two steps: it queues step i+1 (every launch gated on
+// "some system still active") and only then waits for step i's flag.  The
+// direction update p = z + beta p rides in the next step's kernels.  A step
+// queued after the last system stopped does nothing; its launches are dropped
+// from the stats.
+#include <algorithm>
 #include <cmath>
+#include <cstddef>
+#include <utility>
 
 #include "ctx.h"
+
+// device addresses of CgState fields
+template <class T>
+static T* field(vk::CgState* cs, size_t off) {
+    return reinterpret_cast<T*>(reinterpret_cast<char*>(cs) + off);
+}
 
 vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double tau, double gam2, int max_iter,
                        double tol, double* nscratch, int64_t* ref_passes, DotBatch* init) {
@@ -55,69 +71,87 @@ vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double
     STCHK(b0.sink(2 * K, true, rzvv.data(), &ro));
     HIPCHK(vk::cg_init(K, M, cv, diag, ro, c->st));
     STCHK(b0.flush());
-    std::vector<double> rz(K), vv(K), prev_ons(K, 0.0);
-    std::vector<int> active;
+    vk::CgState s0{};
+    s0.K = K;
+    s0.gam2 = gam2;
+    s0.tol = tol;
+    s0.any = max_iter > 0 ? 1 : 0;
     for (int k = 0; k < K; ++k) {
-        rz[k] = rzvv[2 * k];
-        vv[k] = rzvv[2 * k + 1];
+        s0.rz[k] = rzvv[2 * k];
+        s0.vv[k] = rzvv[2 * k + 1];
+        s0.active[k] = 1;
+        s0.onsager[k] = sys[k]->onsager ? 1 : 0;
         sys[k]->iters = 0;
-        active.push_back(k);
     }
-    std::vector<double> red(3 * vk::kMaxRhs);
-    for (int i = 0; i < max_iter && !active.empty(); ++i) {
-        const int Ka = (int)active.size();
-        vk::CgVecs cu{};
-        vk::CgScalars rzs{};
-        const double* pp[vk::kMaxRhs];
-        double* dd[vk::kMaxRhs];
-        for (int a = 0; a < Ka; ++a) {
-            CgSystem* s = sys[active[a]];
-            cu.mu[a] = s->mu;
-            cu.r[a] = s->r;
-            cu.z[a] = s->z;
-            cu.p[a] = s->p;
-            cu.d[a] = s->d;
-            cu.v[a] = s->v;
-            rzs.rz[a] = rz[active[a]];
-            pp[a] = s->p;
-            dd[a] = s->d;
+    if (max_iter <= 0) return VAMPOMI_OK;
+    HIPCHK(vk::cg_start(s0, c->cgs, c->st));
+    const int* gate = field<int>(c->cgs, offsetof(vk::CgState, any));
+    const double* beta = field<double>(c->cgs, offsetof(vk::CgState, beta));
+    const double* pp[vk::kMaxRhs];
+    const double* zz[vk::kMaxRhs];
+    double* dd[vk::kMaxRhs];
+    for (int k = 0; k < K; ++k) {
+        pp[k] = sys[k]->p;
+        zz[k] = sys[k]->z;
+        dd[k] = sys[k]->d;
+    }
+    vk::CgVecs cu{};
+    for (int k = 0; k < K; ++k) {
+        cu.mu[k] = sys[k]->mu;
+        cu.r[k] = sys[k]->r;
+        cu.z[k] = sys[k]->z;
+        cu.p[k] = sys[k]->p;
+        cu.d[k] = sys[k]->d;
+        cu.v[k] = sys[k]->v;
+    }
+    // queues CG step i; *seq: the sequence number its decision stores.  From
+    // step 1 on, the direction update p = z + beta p (:738-739) of the step
+    // before is fused into this step's kernels: the A.x pass, the lmmse_mult
+    // epilogue and <d,p> form it on the fly, cg_update stores it.
+    auto enqueue = [&](int i, unsigned long long* seq) -> vampomi_status {
+        const bool fuse = i > 0;
+        vk::AxFuse fu{};
+        fu.gate = gate;
+        if (fuse) {
+            for (int k = 0; k < K; ++k) fu.z.p[k] = zz[k];
+            fu.beta = beta;
         }
-        // d = lmmse_mult(p)   (:700); <d,p> lands in scal[SL_DP + a]
-        STCHK(lmmse_dev(c, Ka, pp, dd, tau, gam2, nscratch));
-        if (ref_passes) *ref_passes += 2 * (int64_t)Ka;
-        DotBatch b(c);
-        vk::RedOut rou{};
-        STCHK(b.sink(3 * Ka, true, red.data(), &rou));
-        HIPCHK(vk::cg_update(Ka, M, cu, diag, rzs, c->scal + SL_DP, rou, c->st));
-        STCHK(b.flush());
-        std::vector<int> still;
-        vk::CgVecs pv{};
-        vk::CgBeta beta{};
-        int np = 0;
-        for (int a = 0; a < Ka; ++a) {
-            const int k = active[a];
-            CgSystem* s = sys[k];
-            s->iters = i + 1;
-            const double rz_new = red[3 * a], rr = red[3 * a + 1], vmu = red[3 * a + 2];
-            if (s->onsager) {  // :708-726
-                const double ons = gam2 * vmu;
-                const double rel = ons != 0 ? std::fabs((ons - prev_ons[k]) / ons) : 1;
-                if (rel < 1e-8) continue;
-                prev_ons[k] = ons;
+        // d = lmmse_mult(p) (:700); <d,p> lands in scal[SL_DP + k]
+        STCHK(ax_dev(c, K, pp, nscratch, &fu));
+        const double* u[vk::kMaxRhs];
+        for (int k = 0; k < K; ++k) u[k] = nscratch + (int64_t)k * c->ld;
+        STCHK(atx_dev(c, K, u, dd, 1, tau, gam2, pp, gate, fuse ? zz : nullptr, beta));
+        const vk::RedOut ro{c->red_part, c->scal + SL_CG, c->ticket, nullptr, 0, gate};
+        HIPCHK(vk::cg_update(K, M, cu, diag, c->cgs, c->scal + SL_DP, fuse ? 1 : 0, ro, c->st));
+        STCHK(allreduce_dev(c, c->scal + SL_CG, (size_t)(3 * K)));
+        *seq = ++c->sync_seq;
+        HIPCHK(vk::cg_decide(c->cgs, c->scal + SL_CG, i, c->d_cgm, c->d_flag, *seq, c->st));
+        return VAMPOMI_OK;
+    };
+    unsigned long long prev = 0, cur = 0;
+    STCHK(enqueue(0, &prev));
+    for (int i = 1;; ++i) {
+        const size_t mark = c->pending.size();
+        const int64_t passes = c->stats.a_passes_exec;
+        if (i < max_iter) STCHK(enqueue(i, &cur));
+        c->stats.host_syncs++;
+        STCHK(wait_flag(c, prev));  // step i-1 decided
+        if (!c->h_cgm->any || i >= max_iter) {
+            if (i < max_iter) {  // step i was queued in vain: it did nothing
+                for (size_t q = mark; q < c->pending.size(); ++q) {
+                    c->ev_pool.push_back(c->pending[q].a);
+                    c->ev_pool.push_back(c->pending[q].b);
+                }
+                c->pending.resize(mark);
+                c->stats.a_passes_exec = passes;
             }
-            double bt = std::pow(rz[k], -1);  // :731
-            bt *= rz_new;                      // :736
-            rz[k] = rz_new;
-            const double rel_err = std::sqrt(rr) / std::sqrt(vv[k]);  // :742-744
-            if (rel_err < tol) continue;                               // :750
-            still.push_back(k);
-            pv.z[np] = s->z;
-            pv.p[np] = s->p;
-            beta.beta[np] = bt;
-            ++np;
+            break;
         }
-        if (np > 0) HIPCHK(vk::cg_pupdate(np, M, pv, beta, c->st));  // p = z + beta p (:738-739)
-        active.swap(still);
+        prev = cur;
+    }
+    for (int k = 0; k < K; ++k) {
+        sys[k]->iters = c->h_cgm->iters[k];
+        if (ref_passes) *ref_passes += 2 * (int64_t)sys[k]->iters;
     }
     return VAMPOMI_OK;
 }
