@@ -519,7 +519,8 @@ hipError_t vec_div(int K, int64_t n, int64_t /*ld*/, Ptrs v, double div, hipStre
 // ---------------------------------------------------------------------------
 // A^T.u  (data::ATx + data::dot_product, src/data.cpp:294-333)
 // ---------------------------------------------------------------------------
-// A wave owns G consecutive markers; lanes stride the samples two at a time,
+// A wave owns G consecutive markers (workgroups of two waves, dispatched in
+// order: the dispatcher balances the CUs); lanes stride the samples two at a time,
 // so each load instruction reads 1 KiB of one column, UJ such 128-row steps
 // per loop trip.  Every u value loaded serves G markers.  The wave's partial
 // dots are reduced with an xor butterfly; mode 1 fuses the lmmse_mult
@@ -533,7 +534,7 @@ __global__ __launch_bounds__(kBlock) void atx_kernel(const double* __restrict__ 
                                                      const double* __restrict__ beta) {
     if (gate && !*gate) return;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int64_t m0 = ((int64_t)blockIdx.x * 4 + wave) * G;
+    const int64_t m0 = ((int64_t)blockIdx.x * (blockDim.x >> 6) + wave) * G;
     double acc[G][K];
     double mu[G];
     const double* col[G];
@@ -642,7 +643,10 @@ int atx_blocks(int64_t M, int K) { return (int)cdiv(M, 4 * kAtxVariants[atx_vari
 template <int G, int K, int MODE, int UJ, bool NT>
 static void launch_atx(const Shard& s, CPtrs u, Ptrs out, double scale, double tau, double gam2, CPtrs p,
                        const int* gate, CPtrs zf, const double* beta, hipStream_t st, const Timing& tm) {
-    hipExtLaunchKernelGGL((atx_kernel<G, K, MODE, UJ, NT>), dim3((unsigned)cdiv(s.M, 4 * G)), dim3(kBlock), 0, st,
+    // two waves per workgroup: a finer dispatch grain than four (C2: -2..4%,
+    // profiles/r01_kbench_ax_swap.txt); VAMPOMI_ATX_WPB: tuning experiments
+    static const int wpb = std::getenv("VAMPOMI_ATX_WPB") ? std::max(1, std::min(4, std::atoi(std::getenv("VAMPOMI_ATX_WPB")))) : 2;
+    hipExtLaunchKernelGGL((atx_kernel<G, K, MODE, UJ, NT>), dim3((unsigned)cdiv(s.M, wpb * G)), dim3(64 * wpb), 0, st,
                           tm.start, tm.stop, 0, s.X, s.ld, s.N, s.M, s.mave, s.msig, u, out, scale, tau, gam2, p,
                           gate, zf, beta);
 }
@@ -1291,7 +1295,7 @@ __global__ __launch_bounds__(kBlock) void loo_kernel(const double* __restrict__ 
                                                      const double* __restrict__ ymod, const double* __restrict__ x1,
                                                      double sqrtN, double* __restrict__ stats) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int64_t m0 = ((int64_t)blockIdx.x * 4 + wave) * G;
+    const int64_t m0 = ((int64_t)blockIdx.x * (blockDim.x >> 6) + wave) * G;
     const double rinv = 1.0 / sqrtN;
     double acc[G][5];
     double xj[G];
@@ -1382,7 +1386,10 @@ std::string loo_kernel_name() {
 template <int G, int UJ, bool FD>
 static void launch_loo(const Shard& s, const double* ymod, const double* x1, double sqrtN, double* stats,
                        hipStream_t st, const Timing& tm) {
-    hipExtLaunchKernelGGL((loo_kernel<G, UJ, FD>), dim3((unsigned)cdiv(s.M, 4 * G)), dim3(kBlock), 0, st, tm.start,
+    // two waves per workgroup, as A^T.u (C5 shape: 7339 vs 7477 us with four);
+    // VAMPOMI_LOO_WPB: tuning experiments
+    static const int wpb = std::getenv("VAMPOMI_LOO_WPB") ? std::max(1, std::min(4, std::atoi(std::getenv("VAMPOMI_LOO_WPB")))) : 2;
+    hipExtLaunchKernelGGL((loo_kernel<G, UJ, FD>), dim3((unsigned)cdiv(s.M, wpb * G)), dim3(64 * wpb), 0, st, tm.start,
                           tm.stop, 0, s.X, s.ld, s.N, s.M, ymod, x1, sqrtN, stats);
 }
 
