@@ -114,7 +114,7 @@ vampomi_status ax_dev(vampomi_ctx* c, int K, const double* const* x, double* out
                       const vk::AxFuse* fu = nullptr);
 // out_k = A^T u_k (mode 0) or tau*A^T u_k + gam2*p_k with <out_k,p_k> summed over
 // ranks into scal[SL_DP + k] (mode 1).  u_k: ld-padded N-vectors.  gate: as in
-// vk::AxFuse; zf/beta (may be null): p_k stands for fma(beta[k], p_k, zf_k)
+// vk::AxFuse; zf/beta (may be null): p_k stands for zf_k + beta[k]*p_k
 vampomi_status atx_dev(vampomi_ctx* c, int K, const double* const* u, double* const* out, int mode, double tau,
                        double gam2, const double* const* p, const int* gate = nullptr,
                        const double* const* zf = nullptr, const double* beta = nullptr);

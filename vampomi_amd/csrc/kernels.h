@@ -65,7 +65,7 @@ bool set_ax_variant(int v);   // development hook (tools/kbench.py)
 int atx_variant_count();
 bool set_atx_variant(int v);
 // Optional fusion into the A.x pass (the CG direction update of the previous
-// step): with z set, the pass multiplies x_k = fma(beta[k], p_k, z_k), where
+// step): with z set, the pass multiplies x_k = z_k + beta[k]*p_k, where
 // p_k is the `x` argument (every consumer of the new direction forms it the
 // same way; cg_update stores it).  gate (may be null): no work while *gate == 0.
 struct AxFuse {
@@ -87,7 +87,7 @@ hipError_t vec_div(int K, int64_t n, int64_t ld, Ptrs v, double div, hipStream_t
 // (<out_k, p_k> is a separate fixed-geometry reduction); gate as in AxFuse
 int atx_blocks(int64_t M, int K);
 std::string kernel_name(int which, int K, int mode);  // as rocprofv3 prints it
-// zf/beta (mode 1, may be null): the epilogue's p_k is fma(beta[k], p_k, zf_k)
+// zf/beta (mode 1, may be null): the epilogue's p_k is zf_k + beta[k]*p_k
 hipError_t atx(const Shard& s, int K, CPtrs u, Ptrs out, double scale, int mode, double tau,
                double gam2, CPtrs p, hipStream_t st, const Timing& tm = Timing{}, const int* gate = nullptr,
                CPtrs zf = CPtrs{}, const double* beta = nullptr);
@@ -107,7 +107,7 @@ hipError_t scale_vec(int64_t n, double* v, double a, hipStream_t st);
 hipError_t add_noise(uint64_t seed, int64_t N, double sd, double* y, hipStream_t st);
 
 // ---- reductions --------------------------------------------------------------
-// PUPD: a . fma(*beta, b, c) (a CG step's <d, p> with p = z + beta p fused)
+// PUPD: a . (c + *beta * b) (a CG step's <d, p> with p = z + beta p fused)
 enum DotOp { DOT = 0, DIFF2 = 1, SUM = 2, PUPD = 3 };
 struct DotTerm {
     const double* a;
@@ -223,7 +223,7 @@ struct CgMirror {
 };
 // *dst = init (one thread)
 hipError_t cg_start(const CgState& init, CgState* dst, hipStream_t st);
-// for active k: [fuse: p = fma(beta_k, p, z), stored] alpha_k = rz[k] / dp_dev[k];
+// for active k: [fuse: p = z + beta_k p, stored] alpha_k = rz[k] / dp_dev[k];
 // mu += alpha p; r -= d alpha; z = r/diag; <r,z>, <r,r>, <v,mu> in ro.out (3K
 // values, k-major; zeros for stopped systems); gated on cs->any
 hipError_t cg_update(int K, int64_t M, const CgVecs& c, double diag, const CgState* cs, const double* dp_dev,

@@ -193,7 +193,7 @@ static inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 // arithmetic (U*R/2 16-byte loads in flight per lane).  Per-sample summation
 // order within a slot is the reference's: markers in index order,
 // acc += (x - mave_i) * (msig_i * x_i).
-// x_k[i] of the pass: p_k[i], or with fusion (FU) fma(beta_k, p_k[i], z_k[i])
+// x_k[i] of the pass: p_k[i], or with fusion (FU) z_k[i] + beta_k*p_k[i]
 // (the CG direction update, src/vamp.cpp:738-739, as every consumer of the new
 // direction forms it).  The kernel stores nothing but its partials, so the
 // compiler keeps the per-marker loads scalar.
@@ -220,7 +220,7 @@ __device__ __forceinline__ void ax_piece(const double* __restrict__ X, int64_t l
         for (int u = 0; u < U; ++u)
 #pragma unroll
             for (int k = 0; k < K; ++k)
-                xk[u][k] = FU ? __builtin_fma(bk[k], xs.p[k][i + u], fu.z.p[k][i + u]) : xs.p[k][i + u];
+                xk[u][k] = FU ? fu.z.p[k][i + u] + bk[k] * xs.p[k][i + u] : xs.p[k][i + u];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const double ave = mave[i + u];
@@ -243,7 +243,7 @@ __device__ __forceinline__ void ax_piece(const double* __restrict__ X, int64_t l
         for (int q = 0; q < P; ++q) xv[q] = NT ? ld_stream(col + off[q]) : ld2(col + off[q]);
         double xk[K];
 #pragma unroll
-        for (int k = 0; k < K; ++k) xk[k] = FU ? __builtin_fma(bk[k], xs.p[k][i], fu.z.p[k][i]) : xs.p[k][i];
+        for (int k = 0; k < K; ++k) xk[k] = FU ? fu.z.p[k][i] + bk[k] * xs.p[k][i] : xs.p[k][i];
         const double ave = mave[i];
         const double sg = msig[i];
 #pragma unroll
@@ -596,7 +596,7 @@ __global__ __launch_bounds__(kBlock) void atx_kernel(const double* __restrict__ 
                 double val = msig[m] * dot;  // sigma_inv * dpa
                 val *= scale;                // ATx[mloc] *= 1/sqrt(N)
                 if (MODE == 1) {
-                    const double pk = zf.p[0] ? __builtin_fma(beta[k], pv.p[k][m], zf.p[k][m]) : pv.p[k][m];
+                    const double pk = zf.p[0] ? zf.p[k][m] + beta[k] * pv.p[k][m] : pv.p[k][m];
                     val *= tau;        // res[i] *= tau
                     val += gam2 * pk;  // res[i] += gam2 * v[i]
                 }
@@ -836,7 +836,7 @@ __global__ __launch_bounds__(kBlock) void dots_kernel(DotArgs a, int64_t n, RedO
 #pragma unroll
         for (int q = 0; q < NT; ++q) {
             va[q] = a.t[q].a[e];
-            vb[q] = a.t[q].op == PUPD ? __builtin_fma(bt[q], a.t[q].b[e], a.t[q].c[e]) : a.t[q].b[e];
+            vb[q] = a.t[q].op == PUPD ? a.t[q].c[e] + bt[q] * a.t[q].b[e] : a.t[q].b[e];
         }
 #pragma unroll
         for (int q = 0; q < NT; ++q) {
@@ -1087,7 +1087,7 @@ __global__ __launch_bounds__(kBlock) void cg_update_kernel(int K, int64_t M, CgV
             if (on[k]) {
                 double pi = c.p[k][i];
                 if (fuse) {  // p = z + beta p (:738-739)
-                    pi = __builtin_fma(cs->beta[k], pi, c.z[k][i]);
+                    pi = c.z[k][i] + cs->beta[k] * pi;
                     c.p[k][i] = pi;
                 }
                 const double mu = c.mu[k][i] + alpha[k] * pi;  // mu += alpha * p
