@@ -225,9 +225,16 @@ struct CgMirror {
 hipError_t cg_start(const CgState& init, CgState* dst, hipStream_t st);
 // for active k: [fuse: p = z + beta_k p, stored] alpha_k = rz[k] / dp_dev[k];
 // mu += alpha p; r -= d alpha; z = r/diag; <r,z>, <r,r>, <v,mu> in ro.out (3K
-// values, k-major; zeros for stopped systems); gated on cs->any
-hipError_t cg_update(int K, int64_t M, const CgVecs& c, double diag, const CgState* cs, const double* dp_dev,
-                     int fuse, const RedOut& ro, hipStream_t st);
+// values, k-major; zeros for stopped systems); gated on cs->any.  dc.on (one
+// rank: the sums are final): the last block also takes cg_decide's decisions.
+struct CgDecide {
+    int on = 0, it = 0;
+    CgMirror* mirror = nullptr;
+    unsigned long long* flag = nullptr;
+    unsigned long long seq = 0;
+};
+hipError_t cg_update(int K, int64_t M, const CgVecs& c, double diag, CgState* cs, const double* dp_dev, int fuse,
+                     const RedOut& ro, const CgDecide& dc, hipStream_t st);
 // step `it`'s decisions from red (the 3K sums of cg_update, summed over ranks),
 // src/vamp.cpp:700-750; then mirror and flag (stored even when gated off)
 hipError_t cg_decide(CgState* cs, const double* red, int it, CgMirror* mirror, unsigned long long* flag,

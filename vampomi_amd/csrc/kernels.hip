@@ -80,8 +80,15 @@ __device__ __forceinline__ void block_put_sums(double (&v)[NQ], int nq, const Re
     }
 }
 
-__device__ void red_finish(const RedOut& ro, int nq, double* lds4) {
+// The last block sums up to 8 results per round: each thread adds its
+// blocks' partials of every result (blocks in order), then each result is
+// wave-reduced and the four wave sums added in wave order — per result, the
+// operations of block_sum, so the sums are bitwise those of one block_sum per
+// result, with one barrier round per 8 results instead of one per result.
+// Returns true in the last block (after out[] is written; thread 0 wrote it).
+__device__ bool red_finish(const RedOut& ro, int nq, double* /*lds4*/) {
     __shared__ int is_last;
+    __shared__ double lds[4 * 8];
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
     __builtin_amdgcn_s_waitcnt(0);  // every partial store of this block is acknowledged ...
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
@@ -89,20 +96,40 @@ __device__ void red_finish(const RedOut& ro, int nq, double* lds4) {
     if (threadIdx.x == 0)
         is_last = __hip_atomic_fetch_add(ro.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
     __syncthreads();
-    if (!is_last) return;
+    if (!is_last) return false;
     const int nblk = (int)gridDim.x;
-    for (int q = 0; q < nq; ++q) {
-        double s = 0.0;
-        for (int b = threadIdx.x; b < nblk; b += kBlock)
-            s += __hip_atomic_load(ro.part + (int64_t)b * nq + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s = block_sum(s, lds4);
-        if (threadIdx.x == 0) ro.out[q] = s;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int q0 = 0; q0 < nq; q0 += 8) {
+        const int nc = nq - q0 < 8 ? nq - q0 : 8;
+        double s[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) s[c] = 0.0;
+        for (int b = threadIdx.x; b < nblk; b += kBlock) {
+#pragma unroll
+            for (int c = 0; c < 8; ++c)
+                if (c < nc)
+                    s[c] += __hip_atomic_load(ro.part + (int64_t)b * nq + q0 + c, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+        }
+#pragma unroll
+        for (int c = 0; c < 8; ++c)
+            if (c < nc) s[c] = wave_sum(s[c]);
+        __syncthreads();  // lds of the previous round consumed
+        if (lane == 0) {
+#pragma unroll
+            for (int c = 0; c < 8; ++c)
+                if (c < nc) lds[w * 8 + c] = s[c];
+        }
+        __syncthreads();
+        if (threadIdx.x == 0)
+            for (int c = 0; c < nc; ++c) ro.out[q0 + c] = ((lds[c] + lds[8 + c]) + lds[16 + c]) + lds[24 + c];
     }
     if (threadIdx.x == 0) {
         __hip_atomic_store(ro.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         // host completion flag: the results above are visible to the host first
         if (ro.flag) __hip_atomic_store(ro.flag, ro.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
+    return true;
 }
 
 __device__ __forceinline__ v2d ld_stream(const double* p) {
@@ -1066,57 +1093,9 @@ hipError_t cg_start(const CgState& init, CgState* dst, hipStream_t st) {
     return hipGetLastError();
 }
 
-__global__ __launch_bounds__(kBlock) void cg_update_kernel(int K, int64_t M, CgVecs c, double diag,
-                                                           const CgState* __restrict__ cs,
-                                                           const double* __restrict__ dp_dev, int fuse, RedOut ro) {
-    if (!cs->any) return;
-    __shared__ double lds[4];
-    double alpha[kMaxRhs];
-    bool on[kMaxRhs];
-#pragma unroll
-    for (int k = 0; k < kMaxRhs; ++k) {
-        on[k] = k < K && cs->active[k];
-        alpha[k] = on[k] ? cs->rz[k] / dp_dev[k] : 0.0;  // :702
-    }
-    double acc[3 * kMaxRhs];
-#pragma unroll
-    for (int q = 0; q < 3 * kMaxRhs; ++q) acc[q] = 0.0;
-    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < M; i += (int64_t)gridDim.x * kBlock) {
-#pragma unroll
-        for (int k = 0; k < kMaxRhs; ++k) {
-            if (on[k]) {
-                double pi = c.p[k][i];
-                if (fuse) {  // p = z + beta p (:738-739)
-                    pi = c.z[k][i] + cs->beta[k] * pi;
-                    c.p[k][i] = pi;
-                }
-                const double mu = c.mu[k][i] + alpha[k] * pi;  // mu += alpha * p
-                const double r = c.r[k][i] - c.d[k][i] * alpha[k];  // r -= d * alpha
-                const double z = r / diag;
-                c.mu[k][i] = mu;
-                c.r[k][i] = r;
-                c.z[k][i] = z;
-                acc[3 * k] += r * z;
-                acc[3 * k + 1] += r * r;
-                acc[3 * k + 2] += c.v[k][i] * mu;
-            }
-        }
-    }
-    block_put_sums<3 * kMaxRhs>(acc, 3 * K, ro, (int64_t)blockIdx.x * 3 * K);
-    red_finish(ro, 3 * K, lds);
-}
-
-hipError_t cg_update(int K, int64_t M, const CgVecs& c, double diag, const CgState* cs, const double* dp_dev,
-                     int fuse, const RedOut& ro, hipStream_t st) {
-    hipLaunchKernelGGL(cg_update_kernel, dim3(red_blocks(M)), dim3(kBlock), 0, st, K, M, c, diag, cs, dp_dev, fuse,
-                       ro);
-    return hipGetLastError();
-}
-
 // one thread: the host loop of vamp::precondCG_solver after each step's sums
-__global__ void cg_decide_kernel(CgState* cs, const double* __restrict__ red, int it, CgMirror* mirror,
-                                 unsigned long long* flag, unsigned long long seq) {
-    if (threadIdx.x != 0) return;
+__device__ void cg_decide_body(CgState* cs, const double* red, int it, CgMirror* mirror, unsigned long long* flag,
+                               unsigned long long seq) {
     if (cs->any) {
         int any = 0;
         for (int k = 0; k < cs->K; ++k) {
@@ -1152,6 +1131,60 @@ __global__ void cg_decide_kernel(CgState* cs, const double* __restrict__ red, in
         for (int k = 0; k < kMaxRhs; ++k) mirror->iters[k] = cs->iters[k];
     }
     if (flag) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ void cg_decide_kernel(CgState* cs, const double* __restrict__ red, int it, CgMirror* mirror,
+                                 unsigned long long* flag, unsigned long long seq) {
+    if (threadIdx.x == 0) cg_decide_body(cs, red, it, mirror, flag, seq);
+}
+
+__global__ __launch_bounds__(kBlock) void cg_update_kernel(int K, int64_t M, CgVecs c, double diag,
+                                                           CgState* cs, const double* __restrict__ dp_dev, int fuse,
+                                                           RedOut ro, CgDecide dc) {
+    if (!cs->any) return;
+    __shared__ double lds[4];
+    double alpha[kMaxRhs];
+    bool on[kMaxRhs];
+#pragma unroll
+    for (int k = 0; k < kMaxRhs; ++k) {
+        on[k] = k < K && cs->active[k];
+        alpha[k] = on[k] ? cs->rz[k] / dp_dev[k] : 0.0;  // :702
+    }
+    double acc[3 * kMaxRhs];
+#pragma unroll
+    for (int q = 0; q < 3 * kMaxRhs; ++q) acc[q] = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < M; i += (int64_t)gridDim.x * kBlock) {
+#pragma unroll
+        for (int k = 0; k < kMaxRhs; ++k) {
+            if (on[k]) {
+                double pi = c.p[k][i];
+                if (fuse) {  // p = z + beta p (:738-739)
+                    pi = c.z[k][i] + cs->beta[k] * pi;
+                    c.p[k][i] = pi;
+                }
+                const double mu = c.mu[k][i] + alpha[k] * pi;  // mu += alpha * p
+                const double r = c.r[k][i] - c.d[k][i] * alpha[k];  // r -= d * alpha
+                const double z = r / diag;
+                c.mu[k][i] = mu;
+                c.r[k][i] = r;
+                c.z[k][i] = z;
+                acc[3 * k] += r * z;
+                acc[3 * k + 1] += r * r;
+                acc[3 * k + 2] += c.v[k][i] * mu;
+            }
+        }
+    }
+    block_put_sums<3 * kMaxRhs>(acc, 3 * K, ro, (int64_t)blockIdx.x * 3 * K);
+    // one rank: the last block decides the step itself (its sums are final)
+    if (red_finish(ro, 3 * K, lds) && dc.on && threadIdx.x == 0)
+        cg_decide_body(cs, ro.out, dc.it, dc.mirror, dc.flag, dc.seq);
+}
+
+hipError_t cg_update(int K, int64_t M, const CgVecs& c, double diag, CgState* cs, const double* dp_dev, int fuse,
+                     const RedOut& ro, const CgDecide& dc, hipStream_t st) {
+    hipLaunchKernelGGL(cg_update_kernel, dim3(red_blocks(M)), dim3(kBlock), 0, st, K, M, c, diag, cs, dp_dev, fuse,
+                       ro, dc);
+    return hipGetLastError();
 }
 
 hipError_t cg_decide(CgState* cs, const double* red, int it, CgMirror* mirror, unsigned long long* flag,

@@ -122,10 +122,20 @@ vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double
         for (int k = 0; k < K; ++k) u[k] = nscratch + (int64_t)k * c->ld;
         STCHK(atx_dev(c, K, u, dd, 1, tau, gam2, pp, gate, fuse ? zz : nullptr, beta));
         const vk::RedOut ro{c->red_part, c->scal + SL_CG, c->ticket, nullptr, 0, gate};
-        HIPCHK(vk::cg_update(K, M, cu, diag, c->cgs, c->scal + SL_DP, fuse ? 1 : 0, ro, c->st));
-        STCHK(allreduce_dev(c, c->scal + SL_CG, (size_t)(3 * K)));
         *seq = ++c->sync_seq;
-        HIPCHK(vk::cg_decide(c->cgs, c->scal + SL_CG, i, c->d_cgm, c->d_flag, *seq, c->st));
+        vk::CgDecide dc{};
+        if (!c->use_comm) {  // one rank: cg_update's last block decides
+            dc.on = 1;
+            dc.it = i;
+            dc.mirror = c->d_cgm;
+            dc.flag = c->d_flag;
+            dc.seq = *seq;
+        }
+        HIPCHK(vk::cg_update(K, M, cu, diag, c->cgs, c->scal + SL_DP, fuse ? 1 : 0, ro, dc, c->st));
+        if (c->use_comm) {  // the sums are final after the all-reduce
+            STCHK(allreduce_dev(c, c->scal + SL_CG, (size_t)(3 * K)));
+            HIPCHK(vk::cg_decide(c->cgs, c->scal + SL_CG, i, c->d_cgm, c->d_flag, *seq, c->st));
+        }
         return VAMPOMI_OK;
     };
     unsigned long long prev = 0, cur = 0;
