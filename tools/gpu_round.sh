@@ -3,7 +3,8 @@
 # limit; the script stops at the first abnormal exit, i.e. not 0 / 1):
 #   part a: smoke, the GPU tests, C2 (default bench line with CPU baseline,
 #           rocprofv3 kernel stats, PMC traffic), config-4 probit shard (same)
-#   part b: C5 association shard (same), ingest, the C3 shard and config 4 whole
+#   part b: C5 association shard (same), ingest, the C3 shard, config 4 whole
+#           and 240 GB on one GPU (c3big)
 #   gpurun --timeout 1200 -- bash tools/gpu_round.sh a|b
 set -u
 PART=${1:-a}
@@ -45,5 +46,6 @@ else
     step bench_c3 900 python bench.py --config c3 --steps 10 --warmup 2
     prof c3 4
     step bench_c4full 600 python bench.py --config c4full --steps 6 --warmup 2 --no-cpu-baseline
+    step bench_c3big 600 python bench.py --config c3big --steps 4 --warmup 1
 fi
 echo "done"

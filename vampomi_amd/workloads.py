@@ -14,6 +14,9 @@ c4full: configs[3] whole (N=50,000 x Mt=200,000, 80 GB) on any number of
 c5: LOO association test (configs[4], --run-mode association_test
     --pval-method loo): N=100,000 with 62,500 methylation-like markers per
     GPU; n=8 is exactly N=100,000 x Mt=500,000.
+c3big: configs[2]'s samples with 300,000 methylation-like markers per GPU,
+    i.e. 240 GB of the 288 GB HBM3E resident on one MI355X (the
+    1-GPU row at a reduced Mt); n=2 covers Mt=600,000 > configs[2]'s 500,000.
 """
 from __future__ import annotations
 
@@ -29,6 +32,8 @@ def workload(cfg: str, n: int) -> dict:
         return {"workload": "c4-shard", "N": 50000, "Mt": 50000 * n, "kind": GEN_GAUSS, "model": "bin_class"}
     if cfg == "c5":
         return {"workload": "c5-shard", "N": 100000, "Mt": 62500 * n, "kind": GEN_METH, "model": "loo"}
+    if cfg == "c3big":
+        return {"workload": "c3big", "N": 100000, "Mt": 300000 * n, "kind": GEN_METH, "model": "linear"}
     if cfg == "c4full":
         return {"workload": "c4", "N": 50000, "Mt": 200000, "kind": GEN_GAUSS, "model": "bin_class"}
     if n == 1:
