@@ -109,15 +109,18 @@ void release_ctx_resources(vampomi_ctx* c);
 
 // ---- operators on device buffers ---------------------------------------------
 // out_k = A x_k (K <= 4), outputs at outbase + k*ld (one all-reduce). COLLECTIVE
-// fu (may be null): fused direction update and gate (vk::AxFuse)
+// fu (may be null): fused direction update and gate (vk::AxFuse).  tail (may
+// be null; several ranks only): local M-sums all-reduced in the same call,
+// landing at outbase[K*ld + q] (outbase must hold K*ld + tail->nt doubles)
 vampomi_status ax_dev(vampomi_ctx* c, int K, const double* const* x, double* outbase,
-                      const vk::AxFuse* fu = nullptr);
+                      const vk::AxFuse* fu = nullptr, const vk::DotArgs* tail = nullptr);
 // out_k = A^T u_k (mode 0) or tau*A^T u_k + gam2*p_k with <out_k,p_k> summed over
 // ranks into scal[SL_DP + k] (mode 1).  u_k: ld-padded N-vectors.  gate: as in
 // vk::AxFuse; zf/beta (may be null): p_k stands for zf_k + beta[k]*p_k
+// dp = false (mode 1): <out_k,p_k> is not formed (the caller has it otherwise)
 vampomi_status atx_dev(vampomi_ctx* c, int K, const double* const* u, double* const* out, int mode, double tau,
                        double gam2, const double* const* p, const int* gate = nullptr,
-                       const double* const* zf = nullptr, const double* beta = nullptr);
+                       const double* const* zf = nullptr, const double* beta = nullptr, bool dp = true);
 // d_k = tau*A^T A v_k + gam2*v_k (lmmse_mult), <d_k,v_k> in scal[SL_DP+k]. COLLECTIVE
 vampomi_status lmmse_dev(vampomi_ctx* c, int K, const double* const* v, double* const* d, double tau, double gam2,
                          double* nscratch);

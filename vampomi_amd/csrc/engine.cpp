@@ -275,7 +275,8 @@ vampomi_status DotBatch::flush() {
 // ---------------------------------------------------------------------------
 // out_k = Ax(x_k) for K <= 4; outputs at outbase + k*ld (contiguous so that one
 // all-reduce carries them all).  COLLECTIVE.
-vampomi_status ax_dev(vampomi_ctx* c, int K, const double* const* x, double* outbase, const vk::AxFuse* fu) {
+vampomi_status ax_dev(vampomi_ctx* c, int K, const double* const* x, double* outbase, const vk::AxFuse* fu,
+                      const vk::DotArgs* tail) {
     if (!c->have_X) return fail(VAMPOMI_ERR_STATE, "Ax before the methylation data was loaded");
     vk::CPtrs xs{};
     vk::Ptrs os{};
@@ -303,7 +304,12 @@ vampomi_status ax_dev(vampomi_ctx* c, int K, const double* const* x, double* out
         HIPCHK(vk::ax_reduce(c->axp, K, c->N, c->ld, c->ax_part, os, c->sqrtN, c->st, f.gate));
     } else {
         HIPCHK(vk::ax_reduce(c->axp, K, c->N, c->ld, c->ax_part, os, 0.0, c->st, f.gate));
-        STCHK(allreduce_dev(c, outbase, (size_t)K * c->ld));  // src/data.cpp:367
+        size_t n = (size_t)K * c->ld;
+        if (tail) {
+            HIPCHK(vk::dots(*tail, c->M, vk::RedOut{c->red_part, outbase + n, c->ticket, nullptr, 0, f.gate}, c->st));
+            n += (size_t)tail->nt;
+        }
+        STCHK(allreduce_dev(c, outbase, n));  // src/data.cpp:367
         HIPCHK(vk::vec_div(K, c->N, c->ld, os, c->sqrtN, c->st));
     }
     return VAMPOMI_OK;
@@ -313,7 +319,7 @@ vampomi_status ax_dev(vampomi_ctx* c, int K, const double* const* x, double* out
 // over ranks into ctx->scal[SL_DP + k] (mode 1).  u_k are ld-padded N-vectors.
 vampomi_status atx_dev(vampomi_ctx* c, int K, const double* const* u, double* const* out, int mode,
                               double tau, double gam2, const double* const* p, const int* gate,
-                              const double* const* zf, const double* beta) {
+                              const double* const* zf, const double* beta, bool dp) {
     if (!c->have_X) return fail(VAMPOMI_ERR_STATE, "ATx before the methylation data was loaded");
     if (c->M <= 0) return VAMPOMI_OK;
     vk::CPtrs us{}, ps{}, zs{};
@@ -339,7 +345,7 @@ vampomi_status atx_dev(vampomi_ctx* c, int K, const double* const* u, double* co
         c->pending.push_back(t);
     }
     c->stats.a_passes_exec++;
-    if (mode == 1) {
+    if (mode == 1 && dp) {
         // <d_k, p_k> with the fixed-geometry reduction (depends on M only, not on
         // the A^T kernel variant chosen for this K), so a system's CG iterates are
         // bitwise the same whether it runs alone or batched with another

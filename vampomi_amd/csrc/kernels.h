@@ -107,8 +107,9 @@ hipError_t scale_vec(int64_t n, double* v, double a, hipStream_t st);
 hipError_t add_noise(uint64_t seed, int64_t N, double sd, double* y, hipStream_t st);
 
 // ---- reductions --------------------------------------------------------------
-// PUPD: a . (c + *beta * b) (a CG step's <d, p> with p = z + beta p fused)
-enum DotOp { DOT = 0, DIFF2 = 1, SUM = 2, PUPD = 3 };
+// PUPD: a . (c + *beta * b) (a CG step's <d, p> with p = z + beta p fused);
+// SQPUPD: (c + *beta * b)^2 (a is not used; pass b)
+enum DotOp { DOT = 0, DIFF2 = 1, SUM = 2, PUPD = 3, SQPUPD = 4 };
 struct DotTerm {
     const double* a;
     const double* b;
@@ -233,8 +234,10 @@ struct CgDecide {
     unsigned long long* flag = nullptr;
     unsigned long long seq = 0;
 };
-hipError_t cg_update(int K, int64_t M, const CgVecs& c, double diag, CgState* cs, const double* dp_dev, int fuse,
-                     const RedOut& ro, const CgDecide& dc, hipStream_t st);
+// pp_dev (may be null): dp_dev holds |A p_k|^2 and pp_dev |p_k|^2, and
+// <d,p> = tau*|A p|^2 + gam2*|p|^2 (c.tau, c.gam2)
+hipError_t cg_update(int K, int64_t M, const CgVecs& c, double diag, CgState* cs, const double* dp_dev,
+                     const double* pp_dev, int fuse, const RedOut& ro, const CgDecide& dc, hipStream_t st);
 // step `it`'s decisions from red (the 3K sums of cg_update, summed over ranks),
 // src/vamp.cpp:700-750; then mirror and flag (stored even when gated off)
 hipError_t cg_decide(CgState* cs, const double* red, int it, CgMirror* mirror, unsigned long long* flag,

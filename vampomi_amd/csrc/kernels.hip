@@ -854,7 +854,7 @@ __global__ __launch_bounds__(kBlock) void dots_kernel(DotArgs a, int64_t n, RedO
     __shared__ double lds[4];
     double bt[NT];
 #pragma unroll
-    for (int q = 0; q < NT; ++q) bt[q] = a.t[q].op == PUPD ? *a.t[q].beta : 0.0;
+    for (int q = 0; q < NT; ++q) bt[q] = (a.t[q].op == PUPD || a.t[q].op == SQPUPD) ? *a.t[q].beta : 0.0;
     double acc[NT];
 #pragma unroll
     for (int q = 0; q < NT; ++q) acc[q] = 0.0;
@@ -863,13 +863,16 @@ __global__ __launch_bounds__(kBlock) void dots_kernel(DotArgs a, int64_t n, RedO
 #pragma unroll
         for (int q = 0; q < NT; ++q) {
             va[q] = a.t[q].a[e];
-            vb[q] = a.t[q].op == PUPD ? a.t[q].c[e] + bt[q] * a.t[q].b[e] : a.t[q].b[e];
+            vb[q] = (a.t[q].op == PUPD || a.t[q].op == SQPUPD) ? a.t[q].c[e] + bt[q] * a.t[q].b[e] : a.t[q].b[e];
         }
 #pragma unroll
         for (int q = 0; q < NT; ++q) {
             const double d = va[q] - vb[q];
             const int op = a.t[q].op;
-            const double v = (op == DOT || op == PUPD) ? va[q] * vb[q] : (op == DIFF2 ? d * d : va[q]);
+            const double v = (op == DOT || op == PUPD) ? va[q] * vb[q]
+                             : op == SQPUPD            ? vb[q] * vb[q]
+                             : op == DIFF2             ? d * d
+                                                       : va[q];
             acc[q] += v;
         }
     }
@@ -1139,8 +1142,9 @@ __global__ void cg_decide_kernel(CgState* cs, const double* __restrict__ red, in
 }
 
 __global__ __launch_bounds__(kBlock) void cg_update_kernel(int K, int64_t M, CgVecs c, double diag,
-                                                           CgState* cs, const double* __restrict__ dp_dev, int fuse,
-                                                           RedOut ro, CgDecide dc) {
+                                                           CgState* cs, const double* __restrict__ dp_dev,
+                                                           const double* __restrict__ pp_dev, int fuse, RedOut ro,
+                                                           CgDecide dc) {
     if (!cs->any) return;
     __shared__ double lds[4];
     double alpha[kMaxRhs];
@@ -1148,7 +1152,8 @@ __global__ __launch_bounds__(kBlock) void cg_update_kernel(int K, int64_t M, CgV
 #pragma unroll
     for (int k = 0; k < kMaxRhs; ++k) {
         on[k] = k < K && cs->active[k];
-        alpha[k] = on[k] ? cs->rz[k] / dp_dev[k] : 0.0;  // :702
+        const double dp = pp_dev ? c.tau * dp_dev[k] + c.gam2 * pp_dev[k] : dp_dev[k];  // <d,p>
+        alpha[k] = on[k] ? cs->rz[k] / dp : 0.0;  // :702
     }
     double acc[3 * kMaxRhs];
 #pragma unroll
@@ -1180,10 +1185,10 @@ __global__ __launch_bounds__(kBlock) void cg_update_kernel(int K, int64_t M, CgV
         cg_decide_body(cs, ro.out, dc.it, dc.mirror, dc.flag, dc.seq);
 }
 
-hipError_t cg_update(int K, int64_t M, const CgVecs& c, double diag, CgState* cs, const double* dp_dev, int fuse,
-                     const RedOut& ro, const CgDecide& dc, hipStream_t st) {
-    hipLaunchKernelGGL(cg_update_kernel, dim3(red_blocks(M)), dim3(kBlock), 0, st, K, M, c, diag, cs, dp_dev, fuse,
-                       ro, dc);
+hipError_t cg_update(int K, int64_t M, const CgVecs& c, double diag, CgState* cs, const double* dp_dev,
+                     const double* pp_dev, int fuse, const RedOut& ro, const CgDecide& dc, hipStream_t st) {
+    hipLaunchKernelGGL(cg_update_kernel, dim3(red_blocks(M)), dim3(kBlock), 0, st, K, M, c, diag, cs, dp_dev, pp_dev,
+                       fuse, ro, dc);
     return hipGetLastError();
 }
 

@@ -18,6 +18,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstddef>
+#include <cstdlib>
 #include <utility>
 
 #include "ctx.h"
@@ -95,7 +96,13 @@ vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double
         zz[k] = sys[k]->z;
         dd[k] = sys[k]->d;
     }
+    // several ranks: <d,p> rides in the A.x all-reduce (nscratch holds K*ld + K);
+    // VAMPOMI_DP_SEPARATE=1 keeps the one-rank form (tests compare bitwise)
+    static const bool dp_separate = std::getenv("VAMPOMI_DP_SEPARATE") && std::atoi(std::getenv("VAMPOMI_DP_SEPARATE"));
+    const bool split_dp = c->use_comm && K < vk::kMaxRhs && !dp_separate;
     vk::CgVecs cu{};
+    cu.tau = tau;
+    cu.gam2 = gam2;
     for (int k = 0; k < K; ++k) {
         cu.mu[k] = sys[k]->mu;
         cu.r[k] = sys[k]->r;
@@ -116,11 +123,31 @@ vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double
             for (int k = 0; k < K; ++k) fu.z.p[k] = zz[k];
             fu.beta = beta;
         }
-        // d = lmmse_mult(p) (:700); <d,p> lands in scal[SL_DP + k]
-        STCHK(ax_dev(c, K, pp, nscratch, &fu));
+        // d = lmmse_mult(p) (:700).  One rank: <d,p> by a reduction over d and
+        // p into scal[SL_DP + k].  Several ranks: <d,p> = tau*|A p|^2 +
+        // gam2*|p|^2, with the local |p|^2 all-reduced together with A p's
+        // partials and |A p|^2 summed over the replicated N-vector: one
+        // collective per step fewer.
         const double* u[vk::kMaxRhs];
         for (int k = 0; k < K; ++k) u[k] = nscratch + (int64_t)k * c->ld;
-        STCHK(atx_dev(c, K, u, dd, 1, tau, gam2, pp, gate, fuse ? zz : nullptr, beta));
+        const double* pp_dev = nullptr;
+        if (split_dp) {
+            vk::DotArgs tail{};
+            tail.nt = K;
+            for (int k = 0; k < K; ++k)
+                tail.t[k] = fuse ? vk::DotTerm{pp[k], pp[k], vk::SQPUPD, zz[k], beta + k}
+                                 : vk::DotTerm{pp[k], pp[k], vk::DOT};
+            STCHK(ax_dev(c, K, pp, nscratch, &fu, &tail));
+            pp_dev = nscratch + (int64_t)K * c->ld;
+            vk::DotArgs uu{};
+            uu.nt = K;
+            for (int k = 0; k < K; ++k) uu.t[k] = vk::DotTerm{u[k], u[k], vk::DOT};
+            HIPCHK(vk::dots(uu, c->N, vk::RedOut{c->red_part, c->scal + SL_DP, c->ticket, nullptr, 0, gate}, c->st));
+            STCHK(atx_dev(c, K, u, dd, 1, tau, gam2, pp, gate, fuse ? zz : nullptr, beta, false));
+        } else {
+            STCHK(ax_dev(c, K, pp, nscratch, &fu));
+            STCHK(atx_dev(c, K, u, dd, 1, tau, gam2, pp, gate, fuse ? zz : nullptr, beta));
+        }
         const vk::RedOut ro{c->red_part, c->scal + SL_CG, c->ticket, nullptr, 0, gate};
         *seq = ++c->sync_seq;
         vk::CgDecide dc{};
@@ -131,7 +158,7 @@ vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double
             dc.flag = c->d_flag;
             dc.seq = *seq;
         }
-        HIPCHK(vk::cg_update(K, M, cu, diag, c->cgs, c->scal + SL_DP, fuse ? 1 : 0, ro, dc, c->st));
+        HIPCHK(vk::cg_update(K, M, cu, diag, c->cgs, c->scal + SL_DP, pp_dev, fuse ? 1 : 0, ro, dc, c->st));
         if (c->use_comm) {  // the sums are final after the all-reduce
             STCHK(allreduce_dev(c, c->scal + SL_CG, (size_t)(3 * K)));
             HIPCHK(vk::cg_decide(c->cgs, c->scal + SL_CG, i, c->d_cgm, c->d_flag, *seq, c->st));
