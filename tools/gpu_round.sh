@@ -31,7 +31,7 @@ prof() {  # workload steps
 }
 if [ "$PART" = a ]; then
     step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-    step pytest_gpu 900 python -m pytest tests -m gpu -q -rf
+    step pytest_gpu 900 python -u -m pytest tests -m gpu -v -rf --timeout 300 --timeout-method thread
     step bench_c2 400 python bench.py
     prof c2 20
     step pmc_c2 400 bash tools/pmc.sh c2

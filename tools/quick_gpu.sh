@@ -3,7 +3,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 mkdir -p gpurun_out; export TMPDIR=/tmp
-timeout -k 10 900 python -m pytest tests -m gpu -q -rf -x > gpurun_out/pytest_gpu.log 2>&1; rc=$?
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -rf --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; rc=$?
 echo "pytest rc=$rc"; tail -15 gpurun_out/pytest_gpu.log
 if [ $rc -ne 0 ]; then exit $rc; fi
 timeout -k 10 400 python bench.py --no-cpu-baseline > gpurun_out/bench_c2.log 2>&1; rc=$?
