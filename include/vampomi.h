@@ -177,8 +177,12 @@ typedef struct {
     int verbosity;
     const double* true_signal;    /* local slice (M) or NULL => zeros (host) */
     const double* x1hat_init;     /* local slice (M) or NULL => zeros (host) */
-    int batch_rhs;                /* 1 (default): share each A/A^T pass between the x2 and
-                                     Onsager CG solves; 0: run them back to back */
+    int batch_rhs;                /* 2 (default): 1, plus the linear model's updateNoisePrec
+                                     products A^T A x2 / A^T A invQ carried through the CG
+                                     steps (one pass over X fewer per iteration; equal up
+                                     to rounding); 1: share each A/A^T pass between the x2
+                                     and Onsager CG solves (every value bitwise that of 0);
+                                     0: run them back to back */
     const char* model;            /* "linear" (NULL == "linear") or "bin_class" (probit,
                                      src/vamp_probit.cpp; phenotype must be raw 0/1, i.e. read
                                      with standardize = 0; h2/gamw unused; seed also keys the

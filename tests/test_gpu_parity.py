@@ -145,6 +145,26 @@ def test_batched_rhs_bitwise_equal_to_sequential():
     assert a["a_passes_exec"] < b["a_passes_exec"]
 
 
+@pytest.mark.parametrize("N,Mt,its,kind", [(1000, 2000, 30, 0), (700, 1500, 20, 1), (301, 517, 12, 0)])
+def test_recurrence_mode_matches_bitwise_schedule(N, Mt, its, kind):
+    """batch_rhs=2 (default) carries A^T A x2 and A^T A invQ through the CG
+    steps instead of a pass: the same vectors up to rounding, the same
+    integer counts, exactly one executed pass fewer per iteration after the
+    first (iteration 1 has no warm start either way)."""
+    X, y, beta = _problem(N, Mt, kind=kind)
+    a = _gpu_vamp(X, y, beta, Mt, max_iter=its, stop_criteria_thr=0.0, batch_rhs=2)
+    b = _gpu_vamp(X, y, beta, Mt, max_iter=its, stop_criteria_thr=0.0, batch_rhs=1)
+    assert a["cg_iters"] == b["cg_iters"] and a["ons_iters"] == b["ons_iters"] and a["L"] == b["L"]
+    for k in range(its):
+        assert relerr(a["x1_hist"][k], b["x1_hist"][k]) <= 1e-11, f"x1 it {k + 1}"
+        assert relerr(a["r1_hist"][k], b["r1_hist"][k]) <= 1e-11, f"r1 it {k + 1}"
+    assert np.allclose(np.array(a["params"]), np.array(b["params"]), rtol=1e-11, atol=0)
+    assert b["a_passes_exec"] - a["a_passes_exec"] == its
+    assert a["a_passes_ref"] == b["a_passes_ref"]
+    ref = O.vamp_infere(X, y, Mt, true_signal=beta, max_iter=its, stop_criteria_thr=0.0)
+    _assert_parity(a, ref)
+
+
 def test_deterministic_repeat():
     N, Mt = 777, 1234
     X, y, beta = _problem(N, Mt)

@@ -120,7 +120,8 @@ vampomi_status ax_dev(vampomi_ctx* c, int K, const double* const* x, double* out
 // dp = false (mode 1): <out_k,p_k> is not formed (the caller has it otherwise)
 vampomi_status atx_dev(vampomi_ctx* c, int K, const double* const* u, double* const* out, int mode, double tau,
                        double gam2, const double* const* p, const int* gate = nullptr,
-                       const double* const* zf = nullptr, const double* beta = nullptr, bool dp = true);
+                       const double* const* zf = nullptr, const double* beta = nullptr, bool dp = true,
+                       double* const* sraw = nullptr);
 // d_k = tau*A^T A v_k + gam2*v_k (lmmse_mult), <d_k,v_k> in scal[SL_DP+k]. COLLECTIVE
 vampomi_status lmmse_dev(vampomi_ctx* c, int K, const double* const* v, double* const* d, double tau, double gam2,
                          double* nscratch);
@@ -160,6 +161,11 @@ struct CgSystem {
     double* mu = nullptr;          // in: start (if mu0_nonzero), out: solution
     bool mu0_nonzero = false;      // false: start from zeros (lmmse_mult short-circuit)
     const double* atx0 = nullptr;  // optional: A^T(A mu0) computed earlier (saves the start's passes)
+    // optional recurrence (batch_rhs 2): W (device, M) holds A^T A mu0 on entry
+    // (zeros when mu0 = 0) and A^T A mu on return, updated with each step's raw
+    // A^T(A p) kept in S (device, M scratch); W may alias atx0
+    double* W = nullptr;
+    double* S = nullptr;
     bool onsager = false;          // denoiser == 0 in the reference: extra Onsager stop
     int iters = 0;
     double *r = nullptr, *z = nullptr, *p = nullptr, *d = nullptr;  // work vectors (device, M)

@@ -319,14 +319,15 @@ vampomi_status ax_dev(vampomi_ctx* c, int K, const double* const* x, double* out
 // over ranks into ctx->scal[SL_DP + k] (mode 1).  u_k are ld-padded N-vectors.
 vampomi_status atx_dev(vampomi_ctx* c, int K, const double* const* u, double* const* out, int mode,
                               double tau, double gam2, const double* const* p, const int* gate,
-                              const double* const* zf, const double* beta, bool dp) {
+                              const double* const* zf, const double* beta, bool dp, double* const* sraw) {
     if (!c->have_X) return fail(VAMPOMI_ERR_STATE, "ATx before the methylation data was loaded");
     if (c->M <= 0) return VAMPOMI_OK;
     vk::CPtrs us{}, ps{}, zs{};
-    vk::Ptrs os{};
+    vk::Ptrs os{}, ss{};
     for (int k = 0; k < K; ++k) {
         us.p[k] = u[k];
         os.p[k] = out[k];
+        ss.p[k] = sraw ? sraw[k] : nullptr;
         ps.p[k] = p ? p[k] : nullptr;
         zs.p[k] = zf ? zf[k] : nullptr;
     }
@@ -336,7 +337,7 @@ vampomi_status atx_dev(vampomi_ctx* c, int K, const double* const* u, double* co
         t.b = ev_get(c);
     }
     HIPCHK(vk::atx(c->shard(), K, us, os, 1.0 / c->sqrtN, mode, tau, gam2, ps, c->st, vk::Timing{t.a, t.b}, gate, zs,
-                   zf ? beta : nullptr));
+                   zf ? beta : nullptr, ss));
     if (c->timing) {
         t.cls = 1;
         t.K = K;

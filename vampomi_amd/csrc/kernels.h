@@ -87,10 +87,11 @@ hipError_t vec_div(int K, int64_t n, int64_t ld, Ptrs v, double div, hipStream_t
 // (<out_k, p_k> is a separate fixed-geometry reduction); gate as in AxFuse
 int atx_blocks(int64_t M, int K);
 std::string kernel_name(int which, int K, int mode);  // as rocprofv3 prints it
-// zf/beta (mode 1, may be null): the epilogue's p_k is zf_k + beta[k]*p_k
+// zf/beta (mode 1, may be null): the epilogue's p_k is zf_k + beta[k]*p_k;
+// sraw (mode 1, may be null): also stores the raw product (msig_i*dot)*scale
 hipError_t atx(const Shard& s, int K, CPtrs u, Ptrs out, double scale, int mode, double tau,
                double gam2, CPtrs p, hipStream_t st, const Timing& tm = Timing{}, const int* gate = nullptr,
-               CPtrs zf = CPtrs{}, const double* beta = nullptr);
+               CPtrs zf = CPtrs{}, const double* beta = nullptr, Ptrs sraw = Ptrs{});
 
 // ---- marker statistics (data::compute_markers_statistics) ----------------
 hipError_t marker_stats(const double* X, int64_t ld, int64_t N, int64_t M, double nonas,
@@ -202,6 +203,10 @@ struct CgVecs {
     const double* v[kMaxRhs];
     const double* atx0[kMaxRhs];  // init only: A^T(A mu0) computed earlier (then d is ignored)
     double tau, gam2;             // init only, with atx0
+    // cg_update only (may be null): W += alpha * S alongside mu += alpha * p,
+    // S = the step's raw A^T(A p) (atx sraw), so W tracks A^T A mu
+    double* W[kMaxRhs];
+    const double* S[kMaxRhs];
 };
 // r = v - d (or v, or v - (atx0*tau + gam2*mu)), z = r/diag, p = z;
 // <r,z>, <v,v> per system in ro.out (2K values)

@@ -558,7 +558,7 @@ __global__ __launch_bounds__(kBlock) void atx_kernel(const double* __restrict__ 
                                                      const double* __restrict__ msig, CPtrs u, Ptrs out,
                                                      double scale, double tau, double gam2, CPtrs pv,
                                                      const int* __restrict__ gate, CPtrs zf,
-                                                     const double* __restrict__ beta) {
+                                                     const double* __restrict__ beta, Ptrs sraw) {
     if (gate && !*gate) return;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t m0 = ((int64_t)blockIdx.x * (blockDim.x >> 6) + wave) * G;
@@ -622,6 +622,7 @@ __global__ __launch_bounds__(kBlock) void atx_kernel(const double* __restrict__ 
             if (m < M && lane == 0) {
                 double val = msig[m] * dot;  // sigma_inv * dpa
                 val *= scale;                // ATx[mloc] *= 1/sqrt(N)
+                if (MODE == 1 && sraw.p[0]) sraw.p[k][m] = val;  // A^T(A p) itself (CG recurrences)
                 if (MODE == 1) {
                     const double pk = zf.p[0] ? zf.p[k][m] + beta[k] * pv.p[k][m] : pv.p[k][m];
                     val *= tau;        // res[i] *= tau
@@ -669,47 +670,47 @@ int atx_blocks(int64_t M, int K) { return (int)cdiv(M, 4 * kAtxVariants[atx_vari
 
 template <int G, int K, int MODE, int UJ, bool NT>
 static void launch_atx(const Shard& s, CPtrs u, Ptrs out, double scale, double tau, double gam2, CPtrs p,
-                       const int* gate, CPtrs zf, const double* beta, hipStream_t st, const Timing& tm) {
+                       const int* gate, CPtrs zf, const double* beta, Ptrs sraw, hipStream_t st, const Timing& tm) {
     // two waves per workgroup: a finer dispatch grain than four (C2: -2..4%,
     // profiles/r01_kbench_ax_swap.txt); VAMPOMI_ATX_WPB: tuning experiments
     static const int wpb = std::getenv("VAMPOMI_ATX_WPB") ? std::max(1, std::min(4, std::atoi(std::getenv("VAMPOMI_ATX_WPB")))) : 2;
     hipExtLaunchKernelGGL((atx_kernel<G, K, MODE, UJ, NT>), dim3((unsigned)cdiv(s.M, wpb * G)), dim3(64 * wpb), 0, st,
                           tm.start, tm.stop, 0, s.X, s.ld, s.N, s.M, s.mave, s.msig, u, out, scale, tau, gam2, p,
-                          gate, zf, beta);
+                          gate, zf, beta, sraw);
 }
 
 template <int K, int MODE>
 static bool launch_atx_v(int v, const Shard& s, CPtrs u, Ptrs out, double scale, double tau, double gam2, CPtrs p,
-                         const int* gate, CPtrs zf, const double* beta, hipStream_t st, const Timing& tm) {
+                         const int* gate, CPtrs zf, const double* beta, Ptrs sraw, hipStream_t st, const Timing& tm) {
     switch (v) {
-        case 0: launch_atx<4, K, MODE, 2, true>(s, u, out, scale, tau, gam2, p, gate, zf, beta, st, tm); return true;
-        case 1: launch_atx<4, K, MODE, 2, false>(s, u, out, scale, tau, gam2, p, gate, zf, beta, st, tm); return true;
-        case 2: launch_atx<2, K, MODE, 2, true>(s, u, out, scale, tau, gam2, p, gate, zf, beta, st, tm); return true;
-        case 3: launch_atx<8, K, MODE, 2, true>(s, u, out, scale, tau, gam2, p, gate, zf, beta, st, tm); return true;
-        case 4: launch_atx<4, K, MODE, 4, true>(s, u, out, scale, tau, gam2, p, gate, zf, beta, st, tm); return true;
-        case 5: launch_atx<4, K, MODE, 1, true>(s, u, out, scale, tau, gam2, p, gate, zf, beta, st, tm); return true;
-        case 6: launch_atx<8, K, MODE, 1, true>(s, u, out, scale, tau, gam2, p, gate, zf, beta, st, tm); return true;
-        case 7: launch_atx<2, K, MODE, 4, true>(s, u, out, scale, tau, gam2, p, gate, zf, beta, st, tm); return true;
+        case 0: launch_atx<4, K, MODE, 2, true>(s, u, out, scale, tau, gam2, p, gate, zf, beta, sraw, st, tm); return true;
+        case 1: launch_atx<4, K, MODE, 2, false>(s, u, out, scale, tau, gam2, p, gate, zf, beta, sraw, st, tm); return true;
+        case 2: launch_atx<2, K, MODE, 2, true>(s, u, out, scale, tau, gam2, p, gate, zf, beta, sraw, st, tm); return true;
+        case 3: launch_atx<8, K, MODE, 2, true>(s, u, out, scale, tau, gam2, p, gate, zf, beta, sraw, st, tm); return true;
+        case 4: launch_atx<4, K, MODE, 4, true>(s, u, out, scale, tau, gam2, p, gate, zf, beta, sraw, st, tm); return true;
+        case 5: launch_atx<4, K, MODE, 1, true>(s, u, out, scale, tau, gam2, p, gate, zf, beta, sraw, st, tm); return true;
+        case 6: launch_atx<8, K, MODE, 1, true>(s, u, out, scale, tau, gam2, p, gate, zf, beta, sraw, st, tm); return true;
+        case 7: launch_atx<2, K, MODE, 4, true>(s, u, out, scale, tau, gam2, p, gate, zf, beta, sraw, st, tm); return true;
         default: return false;
     }
 }
 
 hipError_t atx(const Shard& s, int K, CPtrs u, Ptrs out, double scale, int mode, double tau, double gam2, CPtrs p,
-               hipStream_t st, const Timing& tm, const int* gate, CPtrs zf, const double* beta) {
+               hipStream_t st, const Timing& tm, const int* gate, CPtrs zf, const double* beta, Ptrs sraw) {
     const int v = atx_variant_for(K);
     bool ok = false;
     if (mode == 0) {
         switch (K) {
-            case 1: ok = launch_atx_v<1, 0>(v, s, u, out, scale, tau, gam2, p, gate, zf, beta, st, tm); break;
-            case 2: ok = launch_atx_v<2, 0>(v, s, u, out, scale, tau, gam2, p, gate, zf, beta, st, tm); break;
-            case 3: ok = launch_atx_v<3, 0>(v, s, u, out, scale, tau, gam2, p, gate, zf, beta, st, tm); break;
+            case 1: ok = launch_atx_v<1, 0>(v, s, u, out, scale, tau, gam2, p, gate, zf, beta, sraw, st, tm); break;
+            case 2: ok = launch_atx_v<2, 0>(v, s, u, out, scale, tau, gam2, p, gate, zf, beta, sraw, st, tm); break;
+            case 3: ok = launch_atx_v<3, 0>(v, s, u, out, scale, tau, gam2, p, gate, zf, beta, sraw, st, tm); break;
             default: break;
         }
     } else {
         switch (K) {
-            case 1: ok = launch_atx_v<1, 1>(v, s, u, out, scale, tau, gam2, p, gate, zf, beta, st, tm); break;
-            case 2: ok = launch_atx_v<2, 1>(v, s, u, out, scale, tau, gam2, p, gate, zf, beta, st, tm); break;
-            case 3: ok = launch_atx_v<3, 1>(v, s, u, out, scale, tau, gam2, p, gate, zf, beta, st, tm); break;
+            case 1: ok = launch_atx_v<1, 1>(v, s, u, out, scale, tau, gam2, p, gate, zf, beta, sraw, st, tm); break;
+            case 2: ok = launch_atx_v<2, 1>(v, s, u, out, scale, tau, gam2, p, gate, zf, beta, sraw, st, tm); break;
+            case 3: ok = launch_atx_v<3, 1>(v, s, u, out, scale, tau, gam2, p, gate, zf, beta, sraw, st, tm); break;
             default: break;
         }
     }
@@ -1173,6 +1174,7 @@ __global__ __launch_bounds__(kBlock) void cg_update_kernel(int K, int64_t M, CgV
                 c.mu[k][i] = mu;
                 c.r[k][i] = r;
                 c.z[k][i] = z;
+                if (c.W[k]) c.W[k][i] = c.W[k][i] + alpha[k] * c.S[k][i];  // A^T A mu, as mu += alpha p
                 acc[3 * k] += r * z;
                 acc[3 * k + 1] += r * r;
                 acc[3 * k + 2] += c.v[k][i] * mu;

@@ -91,11 +91,18 @@ vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double
     const double* pp[vk::kMaxRhs];
     const double* zz[vk::kMaxRhs];
     double* dd[vk::kMaxRhs];
+    double* ss[vk::kMaxRhs];
+    bool recur = false;
     for (int k = 0; k < K; ++k) {
         pp[k] = sys[k]->p;
         zz[k] = sys[k]->z;
         dd[k] = sys[k]->d;
+        ss[k] = sys[k]->S;
+        recur = recur || sys[k]->W;
     }
+    if (recur)  // every system keeps a raw-product slot (the kernel stores all K or none)
+        for (int k = 0; k < K; ++k)
+            if (!ss[k]) return fail(VAMPOMI_ERR_ARG, "pcg: W needs an S scratch vector for every system");
     // several ranks: <d,p> rides in the A.x all-reduce (nscratch holds K*ld + K);
     // VAMPOMI_DP_SEPARATE=1 keeps the one-rank form (tests compare bitwise)
     static const bool dp_separate = std::getenv("VAMPOMI_DP_SEPARATE") && std::atoi(std::getenv("VAMPOMI_DP_SEPARATE"));
@@ -110,6 +117,8 @@ vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double
         cu.p[k] = sys[k]->p;
         cu.d[k] = sys[k]->d;
         cu.v[k] = sys[k]->v;
+        cu.W[k] = sys[k]->W;
+        cu.S[k] = sys[k]->W ? sys[k]->S : nullptr;
     }
     // queues CG step i; *seq: the sequence number its decision stores.  From
     // step 1 on, the direction update p = z + beta p (:738-739) of the step
@@ -143,10 +152,10 @@ vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double
             uu.nt = K;
             for (int k = 0; k < K; ++k) uu.t[k] = vk::DotTerm{u[k], u[k], vk::DOT};
             HIPCHK(vk::dots(uu, c->N, vk::RedOut{c->red_part, c->scal + SL_DP, c->ticket, nullptr, 0, gate}, c->st));
-            STCHK(atx_dev(c, K, u, dd, 1, tau, gam2, pp, gate, fuse ? zz : nullptr, beta, false));
+            STCHK(atx_dev(c, K, u, dd, 1, tau, gam2, pp, gate, fuse ? zz : nullptr, beta, false, recur ? ss : nullptr));
         } else {
             STCHK(ax_dev(c, K, pp, nscratch, &fu));
-            STCHK(atx_dev(c, K, u, dd, 1, tau, gam2, pp, gate, fuse ? zz : nullptr, beta));
+            STCHK(atx_dev(c, K, u, dd, 1, tau, gam2, pp, gate, fuse ? zz : nullptr, beta, true, recur ? ss : nullptr));
         }
         const vk::RedOut ro{c->red_part, c->scal + SL_CG, c->ticket, nullptr, 0, gate};
         *seq = ++c->sync_seq;

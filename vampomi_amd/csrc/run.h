@@ -21,7 +21,9 @@ struct VampRun {
     vampomi_result* res = nullptr;
     bool probit = false;  // model "bin_class"
     bool write = false;
-    bool fuse = true;  // batch_rhs: share passes + prefetch the next denoising step
+    bool fuse = true;  // batch_rhs >= 1: share passes + prefetch the next denoising step
+    bool recur = false;  // batch_rhs == 2: A^T A x2 and A^T A invQ by CG recurrences (no pass)
+    int z1n_slot = 2;    // nb3 slot of the prefetched z1
     std::string out_dir, out_name, p_params, p_metrics, p_prior;
     int it = 0;
     bool stopped = false;
@@ -37,7 +39,7 @@ struct VampRun {
     double *r1 = nullptr, *x1 = nullptr, *x1p = nullptr, *x1n = nullptr, *x1d = nullptr, *r2 = nullptr;
     double *x2 = nullptr, *bern = nullptr, *invQ = nullptr, *v = nullptr, *atxy = nullptr, *ts = nullptr;
     double *tmpM = nullptr, *atx0 = nullptr;
-    double* cgw[8] = {};  // r, z, p, d of the two CG systems
+    double* cgw[10] = {};  // r, z, p, d of the two CG systems; raw A^T A p of each (recur)
     // device N-vectors (ld each)
     double *z1buf = nullptr, *nb3 = nullptr /* A.x2, A.invQ, A.x1_next */, *nsc = nullptr;
     const double* z1 = nullptr;

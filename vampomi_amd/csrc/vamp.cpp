@@ -4,8 +4,8 @@
 // Every vector of the VAMP state lives in HBM; the host keeps the scalars
 // the algorithm branches on.  Per iteration the work is the reference's, in
 // the reference's arithmetic, with three bandwidth reformulations that leave
-// every value bitwise unchanged (tests/test_gpu_parity.py checks batch_rhs=1
-// against batch_rhs=0 bit for bit):
+// every value bitwise unchanged (batch_rhs=1; tests/test_gpu_parity.py checks
+// it against batch_rhs=0 bit for bit):
 //   1. the x2 CG solve and the Onsager CG solve share each pass over X
 //      (pcg.cpp);
 //   2. updateNoisePrec's A.x2 and A.invQ_bern_vec (:508, :518) share one
@@ -17,6 +17,10 @@
 //      (:681) up to the tau / gam2 epilogue applied when those are known.
 // err_measures' A.x2_hat (:826) is the product of (2); A^T y (:303) is
 // computed once.  Scalar reductions are batched per dependency level.
+// batch_rhs=2 (default) replaces the A^T pass of (3) by recurrences: the CG
+// keeps W += alpha*A^T(A p) beside mu += alpha*p for both systems, so the
+// pass count per iteration is 1 + 2*max(k1, k2) instead of 2 + 2*max(k1, k2);
+// the vectors are the same up to rounding (parity within 1e-10, counts exact).
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -199,6 +203,7 @@ extern "C" vampomi_status vampomi_vamp_begin(vampomi_ctx* c, const vampomi_param
     R.res = r;
     R.probit = probit;
     R.fuse = p->batch_rhs != 0;
+    R.recur = p->batch_rhs == 2;
     R.out_dir = p->out_dir ? p->out_dir : "";
     R.out_name = p->out_name ? p->out_name : "";
     R.write = !R.out_dir.empty();
@@ -321,7 +326,7 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
         R.x1n = old;
         R.mix = R.mix_next;
         R.alpha1 = R.alpha1_next;
-        R.z1 = R.nb3 + 2 * ld;
+        R.z1 = R.nb3 + R.z1n_slot * ld;
     }
     R.passes_ref += 1;
     if (res && res->L_hist) res->L_hist[it - 1] = R.mix.L;
@@ -356,6 +361,19 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
     so.d = R.cgw[7];
     if (it == 1) HIPCHK(hipMemsetAsync(R.x2, 0, (size_t)std::max<int64_t>(M, 1) * 8, c->st));
     HIPCHK(hipMemsetAsync(R.invQ, 0, (size_t)std::max<int64_t>(M, 1) * 8, c->st));
+    // batch_rhs 2: updateNoisePrec's A^T(A x2) (the next warm start, :681) and
+    // A^T(A invQ) (the trace, :519) are carried through the CG steps as
+    // W += alpha * A^T(A p) beside mu += alpha * p, instead of one more pass
+    // over X per iteration (mathematically the same vectors; rounding differs)
+    const bool rec = R.recur && R.fuse && (it == 1 || sx.atx0);
+    if (rec) {
+        if (it == 1) HIPCHK(hipMemsetAsync(R.atx0, 0, (size_t)std::max<int64_t>(M, 1) * 8, c->st));
+        HIPCHK(hipMemsetAsync(R.tmpM, 0, (size_t)std::max<int64_t>(M, 1) * 8, c->st));
+        sx.W = R.atx0;  // holds A^T A mu0 on entry (the warm start's product), in place
+        sx.S = R.cgw[8];
+        so.W = R.tmpM;  // invQ starts from zeros
+        so.S = R.cgw[9];
+    }
     if (R.fuse) {
         STCHK(pcg_run(c, {&sx, &so}, R.gamw, R.gam2, R.prm.CG_max_iter, R.prm.CG_err_tol, R.nsc, &R.passes_ref, &e1));
     } else {
@@ -387,9 +405,18 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
     }
 
     // ---- updateNoisePrec (:504-529) + the next z1 in the same pass ----
-    {
+    if (rec) {  // A.x2 and the next z1 in one pass; the A^T products came with the CG
+        const double* xs[2] = {R.x2, R.x1n};
+        STCHK(ax_dev(c, next ? 2 : 1, xs, R.nb3));
+        R.z1n_slot = 1;
+        R.passes_ref += 2;
+        STCHK(fin.add({T(R.nb3, c->y, vk::DIFF2)}, N, false, &R.tn));  // l2_norm2(temp, 0)
+        R.passes_ref += 1;
+        STCHK(fin.add({T(R.bern, R.tmpM)}, M, true, &R.tc));  // <u, A^T A invQ>
+    } else {
         const double* xs[3] = {R.x2, R.invQ, R.x1n};
         STCHK(ax_dev(c, next ? 3 : 2, xs, R.nb3));
+        R.z1n_slot = 2;
         R.passes_ref += 2;
         STCHK(fin.add({T(R.nb3, c->y, vk::DIFF2)}, N, false, &R.tn));  // l2_norm2(temp, 0)
         const double* u[2] = {R.nb3 + ld, R.nb3};  // A.invQ (trace), A.x2 (next warm start)
@@ -497,7 +524,7 @@ extern "C" void vampomi_params_default(vampomi_params* p) {
         p->probs[j] = q[j];
     }
     p->seed = 0x5EED5EEDULL;
-    p->batch_rhs = 1;
+    p->batch_rhs = 2;
     p->model = "linear";
 }
 
