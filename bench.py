@@ -211,7 +211,7 @@ def main():
     ap.add_argument("--seed", type=int, default=20250711)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="skip the HIP-event kernel timing")
-    ap.add_argument("--batch-rhs", type=int, default=2)
+    ap.add_argument("--batch-rhs", type=int, default=3)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

@@ -177,10 +177,13 @@ typedef struct {
     int verbosity;
     const double* true_signal;    /* local slice (M) or NULL => zeros (host) */
     const double* x1hat_init;     /* local slice (M) or NULL => zeros (host) */
-    int batch_rhs;                /* 2 (default): 1, plus the linear model's updateNoisePrec
-                                     products A^T A x2 / A^T A invQ carried through the CG
-                                     steps (one pass over X fewer per iteration; equal up
-                                     to rounding); 1: share each A/A^T pass between the x2
+    int batch_rhs;                /* 3 (default): 2, plus A x2 carried through the CG steps
+                                     and z1 = A x1 in the first CG pass (no pass over X
+                                     outside the CG; equal up to rounding); 2: 1, plus the
+                                     linear model's updateNoisePrec products A^T A x2 /
+                                     A^T A invQ carried through the CG steps (one pass over
+                                     X fewer per iteration; equal up to rounding);
+                                     1: share each A/A^T pass between the x2
                                      and Onsager CG solves (every value bitwise that of 0);
                                      0: run them back to back */
     const char* model;            /* "linear" (NULL == "linear") or "bin_class" (probit,

@@ -147,7 +147,7 @@ def test_batched_rhs_bitwise_equal_to_sequential():
 
 @pytest.mark.parametrize("N,Mt,its,kind", [(1000, 2000, 30, 0), (700, 1500, 20, 1), (301, 517, 12, 0)])
 def test_recurrence_mode_matches_bitwise_schedule(N, Mt, its, kind):
-    """batch_rhs=2 (default) carries A^T A x2 and A^T A invQ through the CG
+    """batch_rhs=2 carries A^T A x2 and A^T A invQ through the CG
     steps instead of a pass: the same vectors up to rounding, the same
     integer counts, exactly one executed pass fewer per iteration after the
     first (iteration 1 has no warm start either way)."""
@@ -160,6 +160,29 @@ def test_recurrence_mode_matches_bitwise_schedule(N, Mt, its, kind):
         assert relerr(a["r1_hist"][k], b["r1_hist"][k]) <= 1e-11, f"r1 it {k + 1}"
     assert np.allclose(np.array(a["params"]), np.array(b["params"]), rtol=1e-11, atol=0)
     assert b["a_passes_exec"] - a["a_passes_exec"] == its
+    assert a["a_passes_ref"] == b["a_passes_ref"]
+    ref = O.vamp_infere(X, y, Mt, true_signal=beta, max_iter=its, stop_criteria_thr=0.0)
+    _assert_parity(a, ref)
+
+
+@pytest.mark.parametrize("N,Mt,its,kind", [(1000, 2000, 30, 0), (700, 1500, 20, 1), (301, 517, 12, 0)])
+def test_ax_recurrence_mode(N, Mt, its, kind):
+    """batch_rhs=3 (default) also carries A x2 through the CG steps (AW +=
+    alpha * A p) and computes z1 = A x1 as one more right-hand side of the first
+    CG pass: no pass outside the CG, 2*max(k1, k2) per iteration, the same
+    integer counts, values within rounding of the bitwise schedule and within
+    the parity bar of the oracle."""
+    X, y, beta = _problem(N, Mt, kind=kind)
+    a = _gpu_vamp(X, y, beta, Mt, max_iter=its, stop_criteria_thr=0.0, batch_rhs=3)
+    b = _gpu_vamp(X, y, beta, Mt, max_iter=its, stop_criteria_thr=0.0, batch_rhs=2)
+    assert a["cg_iters"] == b["cg_iters"] and a["ons_iters"] == b["ons_iters"] and a["L"] == b["L"]
+    for k in range(its):
+        assert relerr(a["x1_hist"][k], b["x1_hist"][k]) <= 1e-11, f"x1 it {k + 1}"
+        assert relerr(a["r1_hist"][k], b["r1_hist"][k]) <= 1e-11, f"r1 it {k + 1}"
+    assert np.allclose(np.array(a["params"]), np.array(b["params"]), rtol=1e-11, atol=0)
+    assert np.allclose(np.array(a["metrics"]), np.array(b["metrics"]), rtol=1e-10, atol=1e-13, equal_nan=True)
+    assert b["a_passes_exec"] - a["a_passes_exec"] == its + 1  # + iteration 1's own z1 pass
+    assert a["a_passes_exec"] == 1 + sum(2 * max(p, q) for p, q in zip(a["cg_iters"], a["ons_iters"]))  # + A^T y
     assert a["a_passes_ref"] == b["a_passes_ref"]
     ref = O.vamp_infere(X, y, Mt, true_signal=beta, max_iter=its, stop_criteria_thr=0.0)
     _assert_parity(a, ref)

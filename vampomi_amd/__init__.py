@@ -293,7 +293,7 @@ class VampOptions:
     out_dir: str = ""
     out_name: str = ""
     verbosity: int = 0
-    batch_rhs: int = 2
+    batch_rhs: int = 3
     model: str = "linear"
 
     def to_struct(self) -> Params:

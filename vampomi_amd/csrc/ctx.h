@@ -166,6 +166,9 @@ struct CgSystem {
     // A^T(A p) kept in S (device, M scratch); W may alias atx0
     double* W = nullptr;
     double* S = nullptr;
+    // optional (batch_rhs 3): AW (device, ld) holds A mu0 on entry (zeros when
+    // mu0 = 0) and A mu on return, updated with each step's A p
+    double* AW = nullptr;
     bool onsager = false;          // denoiser == 0 in the reference: extra Onsager stop
     int iters = 0;
     double *r = nullptr, *z = nullptr, *p = nullptr, *d = nullptr;  // work vectors (device, M)
@@ -173,5 +176,9 @@ struct CgSystem {
 // Solves the systems together: every CG step streams X twice for all still
 // active systems; each keeps its own scalars and stopping rule.  `init` (may
 // be null) is flushed together with the initial residual reductions.
+// extra_x (may be null, device M): ex_out (device, ld) = A extra_x, carried as
+// one more right-hand side of the first step's A.x pass (its own pass if no
+// step runs).  nscratch holds kMaxRhs*ld + kMaxRhs doubles.
 vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double tau, double gam2, int max_iter,
-                       double tol, double* nscratch, int64_t* ref_passes, DotBatch* init);
+                       double tol, double* nscratch, int64_t* ref_passes, DotBatch* init,
+                       const double* extra_x = nullptr, double* ex_out = nullptr);

@@ -207,6 +207,11 @@ struct CgVecs {
     // S = the step's raw A^T(A p) (atx sraw), so W tracks A^T A mu
     double* W[kMaxRhs];
     const double* S[kMaxRhs];
+    // cg_update only (may be null): AW += alpha * AS over nA samples, AS = the
+    // step's A p (the replicated N-vector of the A.x pass), so AW tracks A mu
+    double* AW[kMaxRhs];
+    const double* AS[kMaxRhs];
+    int64_t nA;
 };
 // r = v - d (or v, or v - (atx0*tau + gam2*mu)), z = r/diag, p = z;
 // <r,z>, <v,v> per system in ro.out (2K values)

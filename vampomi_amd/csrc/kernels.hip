@@ -1181,6 +1181,12 @@ __global__ __launch_bounds__(kBlock) void cg_update_kernel(int K, int64_t M, CgV
             }
         }
     }
+    // A mu alongside mu (replicated N-vectors, the same on every rank)
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < c.nA; i += (int64_t)gridDim.x * kBlock) {
+#pragma unroll
+        for (int k = 0; k < kMaxRhs; ++k)
+            if (on[k] && c.AW[k]) c.AW[k][i] = c.AW[k][i] + alpha[k] * c.AS[k][i];
+    }
     block_put_sums<3 * kMaxRhs>(acc, 3 * K, ro, (int64_t)blockIdx.x * 3 * K);
     // one rank: the last block decides the step itself (its sums are final)
     if (red_finish(ro, 3 * K, lds) && dc.on && threadIdx.x == 0)

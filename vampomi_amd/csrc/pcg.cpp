@@ -30,11 +30,19 @@ static T* field(vk::CgState* cs, size_t off) {
 }
 
 vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double tau, double gam2, int max_iter,
-                       double tol, double* nscratch, int64_t* ref_passes, DotBatch* init) {
+                       double tol, double* nscratch, int64_t* ref_passes, DotBatch* init, const double* extra_x,
+                       double* ex_out) {
     const int64_t M = c->M, N = c->N;
     const double diag = tau * (double)(N - 1) / (double)N + gam2;  // :676-677
     const int K = (int)sys.size();
     if (K < 1 || K > vk::kMaxRhs) return fail(VAMPOMI_ERR_ARG, "pcg: 1..4 systems");
+    if (extra_x && (!ex_out || K + 1 >= vk::kMaxRhs)) return fail(VAMPOMI_ERR_ARG, "pcg: extra A.x needs K <= 2");
+    auto extra_alone = [&]() -> vampomi_status {  // no CG step carries it
+        if (!extra_x) return VAMPOMI_OK;
+        STCHK(ax_dev(c, 1, &extra_x, nscratch));
+        HIPCHK(hipMemcpyAsync(ex_out, nscratch, (size_t)N * 8, hipMemcpyDeviceToDevice, c->st));
+        return VAMPOMI_OK;
+    };
     // initial residual r = v - lmmse_mult(mu0)  (:681-684)
     {
         std::vector<CgSystem*> nz;
@@ -84,7 +92,7 @@ vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double
         s0.onsager[k] = sys[k]->onsager ? 1 : 0;
         sys[k]->iters = 0;
     }
-    if (max_iter <= 0) return VAMPOMI_OK;
+    if (max_iter <= 0) return extra_alone();
     HIPCHK(vk::cg_start(s0, c->cgs, c->st));
     const int* gate = field<int>(c->cgs, offsetof(vk::CgState, any));
     const double* beta = field<double>(c->cgs, offsetof(vk::CgState, beta));
@@ -119,6 +127,9 @@ vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double
         cu.v[k] = sys[k]->v;
         cu.W[k] = sys[k]->W;
         cu.S[k] = sys[k]->W ? sys[k]->S : nullptr;
+        cu.AW[k] = sys[k]->AW;
+        cu.AS[k] = nscratch + (int64_t)k * c->ld;  // this step's A p (the A.x pass output)
+        if (sys[k]->AW) cu.nA = N;
     }
     // queues CG step i; *seq: the sequence number its decision stores.  From
     // step 1 on, the direction update p = z + beta p (:738-739) of the step
@@ -139,6 +150,12 @@ vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double
         // collective per step fewer.
         const double* u[vk::kMaxRhs];
         for (int k = 0; k < K; ++k) u[k] = nscratch + (int64_t)k * c->ld;
+        // the first step's pass also carries A.extra_x (one more right-hand side)
+        const double* px[vk::kMaxRhs];
+        for (int k = 0; k < K; ++k) px[k] = pp[k];
+        const bool ex = i == 0 && extra_x;
+        if (ex) px[K] = extra_x;
+        const int KA = ex ? K + 1 : K;
         const double* pp_dev = nullptr;
         if (split_dp) {
             vk::DotArgs tail{};
@@ -146,15 +163,17 @@ vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double
             for (int k = 0; k < K; ++k)
                 tail.t[k] = fuse ? vk::DotTerm{pp[k], pp[k], vk::SQPUPD, zz[k], beta + k}
                                  : vk::DotTerm{pp[k], pp[k], vk::DOT};
-            STCHK(ax_dev(c, K, pp, nscratch, &fu, &tail));
-            pp_dev = nscratch + (int64_t)K * c->ld;
+            STCHK(ax_dev(c, KA, px, nscratch, &fu, &tail));
+            if (ex) HIPCHK(hipMemcpyAsync(ex_out, nscratch + (int64_t)K * c->ld, (size_t)N * 8, hipMemcpyDeviceToDevice, c->st));
+            pp_dev = nscratch + (int64_t)KA * c->ld;
             vk::DotArgs uu{};
             uu.nt = K;
             for (int k = 0; k < K; ++k) uu.t[k] = vk::DotTerm{u[k], u[k], vk::DOT};
             HIPCHK(vk::dots(uu, c->N, vk::RedOut{c->red_part, c->scal + SL_DP, c->ticket, nullptr, 0, gate}, c->st));
             STCHK(atx_dev(c, K, u, dd, 1, tau, gam2, pp, gate, fuse ? zz : nullptr, beta, false, recur ? ss : nullptr));
         } else {
-            STCHK(ax_dev(c, K, pp, nscratch, &fu));
+            STCHK(ax_dev(c, KA, px, nscratch, &fu));
+            if (ex) HIPCHK(hipMemcpyAsync(ex_out, nscratch + (int64_t)K * c->ld, (size_t)N * 8, hipMemcpyDeviceToDevice, c->st));
             STCHK(atx_dev(c, K, u, dd, 1, tau, gam2, pp, gate, fuse ? zz : nullptr, beta, true, recur ? ss : nullptr));
         }
         const vk::RedOut ro{c->red_part, c->scal + SL_CG, c->ticket, nullptr, 0, gate};

@@ -22,7 +22,8 @@ struct VampRun {
     bool probit = false;  // model "bin_class"
     bool write = false;
     bool fuse = true;  // batch_rhs >= 1: share passes + prefetch the next denoising step
-    bool recur = false;  // batch_rhs == 2: A^T A x2 and A^T A invQ by CG recurrences (no pass)
+    bool recur = false;  // batch_rhs >= 2: A^T A x2 and A^T A invQ by CG recurrences (no pass)
+    bool arec = false;   // batch_rhs == 3: also A x2 by a CG recurrence, z1 in the first CG pass
     int z1n_slot = 2;    // nb3 slot of the prefetched z1
     std::string out_dir, out_name, p_params, p_metrics, p_prior;
     int it = 0;
@@ -42,6 +43,7 @@ struct VampRun {
     double* cgw[10] = {};  // r, z, p, d of the two CG systems; raw A^T A p of each (recur)
     // device N-vectors (ld each)
     double *z1buf = nullptr, *nb3 = nullptr /* A.x2, A.invQ, A.x1_next */, *nsc = nullptr;
+    double* ax2 = nullptr;  // arec: A x2, carried from iteration to iteration
     const double* z1 = nullptr;
     int64_t passes_ref = 0;
     // probit (src/vamp_probit.cpp) state

@@ -21,6 +21,10 @@
 // keeps W += alpha*A^T(A p) beside mu += alpha*p for both systems, so the
 // pass count per iteration is 1 + 2*max(k1, k2) instead of 2 + 2*max(k1, k2);
 // the vectors are the same up to rounding (parity within 1e-10, counts exact).
+// batch_rhs=3 (default) also carries A x2 as A x2 += alpha * A p through the
+// CG steps (from the previous iteration's A x2) and computes z1 = A x1_hat as
+// one more right-hand side of the first CG pass, so no pass over X is left
+// outside the CG: 2*max(k1, k2) passes per iteration.
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -32,7 +36,7 @@
 
 VampRun::~VampRun() {
     for (double** p : {&r1, &x1, &x1p, &x1n, &x1d, &r2, &x2, &bern, &invQ, &v, &atxy, &ts, &tmpM, &atx0, &z1buf,
-                       &nb3, &nsc, &p1, &p2, &z1h, &x1s, &x1sn, &x2s})
+                       &nb3, &nsc, &ax2, &p1, &p2, &z1h, &x1s, &x1sn, &x2s})
         dev_free(*p);
     for (auto& p : cgw) dev_free(p);
 }
@@ -183,6 +187,8 @@ static vampomi_status vamp_alloc(vampomi_ctx* c, VampRun& R) {
     STCHK(dev_alloc(&R.z1buf, ld));
     STCHK(dev_alloc(&R.nb3, 3 * ld));
     STCHK(dev_alloc(&R.nsc, vk::kMaxRhs * ld));
+    STCHK(dev_alloc(&R.ax2, ld));
+    HIPCHK(hipMemsetAsync(R.ax2, 0, ld * 8, c->st));
     HIPCHK(hipMemsetAsync(R.z1buf, 0, ld * 8, c->st));
     HIPCHK(hipMemsetAsync(R.nb3, 0, 3 * ld * 8, c->st));
     HIPCHK(hipMemsetAsync(R.nsc, 0, vk::kMaxRhs * ld * 8, c->st));
@@ -203,7 +209,8 @@ extern "C" vampomi_status vampomi_vamp_begin(vampomi_ctx* c, const vampomi_param
     R.res = r;
     R.probit = probit;
     R.fuse = p->batch_rhs != 0;
-    R.recur = p->batch_rhs == 2;
+    R.recur = p->batch_rhs >= 2;
+    R.arec = p->batch_rhs >= 3;
     R.out_dir = p->out_dir ? p->out_dir : "";
     R.out_name = p->out_name ? p->out_name : "";
     R.write = !R.out_dir.empty();
@@ -316,8 +323,10 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
         STCHK(denoise_into(c, R.mix, R.gam1, R.r1, R.x1, R.x1p, it > 1, R.prm.rho, R.x1d, b, &R.sum_d));
         STCHK(b.flush());
         R.alpha1 = R.sum_d / (double)Mt;  // :223
-        const double* xs[1] = {R.x1};
-        STCHK(ax_dev(c, 1, xs, R.z1buf));  // z1 = Ax(x1_hat) (:232)
+        if (!R.arec) {  // (arec: z1 rides in the first CG pass below)
+            const double* xs[1] = {R.x1};
+            STCHK(ax_dev(c, 1, xs, R.z1buf));  // z1 = Ax(x1_hat) (:232)
+        }
         R.z1 = R.z1buf;
     } else {  // prefetched by iteration it-1 (see file comment, item 2)
         double* old = R.x1p;
@@ -326,7 +335,7 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
         R.x1n = old;
         R.mix = R.mix_next;
         R.alpha1 = R.alpha1_next;
-        R.z1 = R.nb3 + R.z1n_slot * ld;
+        R.z1 = R.arec ? R.z1buf : R.nb3 + R.z1n_slot * ld;
     }
     R.passes_ref += 1;
     if (res && res->L_hist) res->L_hist[it - 1] = R.mix.L;
@@ -335,7 +344,7 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
     R.gam2 = smin(smax(R.eta1 - R.gam1, 1e-11), 1e11);  // :255-256
     HIPCHK(vk::lincomb_div(M, R.eta1, R.x1, R.gam1, R.r1, R.gam2, R.r2, c->st));  // r2 (:259-261)
     DotBatch e1(c);
-    STCHK(err_queue(c, R, R.x1, R.z1, e1, R.e1m, R.e1n, R.e1s));  // :272, flushed with the CG start
+    if (!R.arec) STCHK(err_queue(c, R, R.x1, R.z1, e1, R.e1m, R.e1n, R.e1s));  // :272, flushed with the CG start
     R.params[0] = R.alpha1;
     R.params[1] = R.gam1;
 
@@ -374,21 +383,32 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
         so.W = R.tmpM;  // invQ starts from zeros
         so.S = R.cgw[9];
     }
+    // batch_rhs 3: A x2 (updateNoisePrec :508, err_measures :826, and the next
+    // warm start) is carried as AW += alpha * A p beside mu += alpha * p, from
+    // the previous iteration's A x2; z1 = A x1_hat (:232) is one more
+    // right-hand side of the first CG pass
+    const bool arec = R.arec && rec;
+    if (arec) {
+        if (it == 1) HIPCHK(hipMemsetAsync(R.ax2, 0, (size_t)ld * 8, c->st));
+        sx.AW = R.ax2;
+    }
     if (R.fuse) {
-        STCHK(pcg_run(c, {&sx, &so}, R.gamw, R.gam2, R.prm.CG_max_iter, R.prm.CG_err_tol, R.nsc, &R.passes_ref, &e1));
+        STCHK(pcg_run(c, {&sx, &so}, R.gamw, R.gam2, R.prm.CG_max_iter, R.prm.CG_err_tol, R.nsc, &R.passes_ref,
+                      arec ? nullptr : &e1, arec ? R.x1 : nullptr, arec ? R.z1buf : nullptr));
     } else {
         STCHK(pcg_run(c, {&sx}, R.gamw, R.gam2, R.prm.CG_max_iter, R.prm.CG_err_tol, R.nsc, &R.passes_ref, &e1));
         STCHK(pcg_run(c, {&so}, R.gamw, R.gam2, R.prm.CG_max_iter, R.prm.CG_err_tol, R.nsc, &R.passes_ref, nullptr));
     }
-    err_finish(R, R.e1m, R.e1n, R.e1s, 1);
     if (res && res->cg_iters) res->cg_iters[it - 1] = sx.iters;
     if (res && res->ons_iters) res->ons_iters[it - 1] = so.iters;
     {
         DotBatch b(c);
         STCHK(b.add({T(R.bern, R.invQ)}, M, true, &R.a2));
+        if (arec) STCHK(err_queue(c, R, R.x1, R.z1, b, R.e1m, R.e1n, R.e1s));  // :272
         STCHK(b.flush());
         R.alpha2 = R.gam2 * R.a2;  // :498
     }
+    err_finish(R, R.e1m, R.e1n, R.e1s, 1);
     R.eta2 = R.gam2 / R.alpha2;  // :341
     const double gam1_prev = R.gam1;
     R.gam1 = smin(smax(R.eta2 - R.gam2, 1e-11), 1e11);
@@ -405,7 +425,13 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
     }
 
     // ---- updateNoisePrec (:504-529) + the next z1 in the same pass ----
-    if (rec) {  // A.x2 and the next z1 in one pass; the A^T products came with the CG
+    const double* ax2 = R.nb3;  // A.x2_hat
+    if (arec) {  // no pass: A x2 came with the CG, the next z1 comes with the next CG
+        ax2 = R.ax2;
+        R.passes_ref += 3;  // :508, :518, :519
+        STCHK(fin.add({T(R.ax2, c->y, vk::DIFF2)}, N, false, &R.tn));  // l2_norm2(temp, 0)
+        STCHK(fin.add({T(R.bern, R.tmpM)}, M, true, &R.tc));           // <u, A^T A invQ>
+    } else if (rec) {  // A.x2 and the next z1 in one pass; the A^T products came with the CG
         const double* xs[2] = {R.x2, R.x1n};
         STCHK(ax_dev(c, next ? 2 : 1, xs, R.nb3));
         R.z1n_slot = 1;
@@ -425,7 +451,7 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
         R.passes_ref += 1;
         STCHK(fin.add({T(R.bern, R.tmpM)}, M, true, &R.tc));
     }
-    STCHK(err_queue(c, R, R.x2, R.nb3, fin, R.e2m, R.e2n, R.e2s));  // :365 (A.x2_hat of :826 == nb3)
+    STCHK(err_queue(c, R, R.x2, ax2, fin, R.e2m, R.e2n, R.e2s));  // :365 (A.x2_hat of :826)
     R.passes_ref += 1;
     STCHK(fin.add({T(R.x1p, R.x1, vk::DIFF2), T(R.x1p, R.x1p)}, M, true, R.nm));  // NMSE (:409-413)
     STCHK(fin.flush());
@@ -524,7 +550,7 @@ extern "C" void vampomi_params_default(vampomi_params* p) {
         p->probs[j] = q[j];
     }
     p->seed = 0x5EED5EEDULL;
-    p->batch_rhs = 2;
+    p->batch_rhs = 3;
     p->model = "linear";
 }
 
