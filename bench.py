@@ -142,7 +142,7 @@ def bench_assoc(args, d, w, world, rank, t_start):
     for _ in range(args.warmup):
         step()
     d.reset_stats()
-    d.set_timing(not args.no_timing)
+    d.set_timing(not args.no_timing, args.timing_period)
 
     def barrier():
         d.sync()
@@ -211,6 +211,8 @@ def main():
     ap.add_argument("--seed", type=int, default=20250711)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="skip the HIP-event kernel timing")
+    ap.add_argument("--timing-period", type=int, default=4,
+                    help="time one A/A^T launch in this many of each (kernel, K) with HIP events")
     ap.add_argument("--batch-rhs", type=int, default=3)
     args = ap.parse_args()
 
@@ -250,7 +252,7 @@ def main():
         v.step()
     ref0, _ = v.a_passes
     d.reset_stats()
-    d.set_timing(not args.no_timing)
+    d.set_timing(not args.no_timing, args.timing_period)
 
     def barrier():
         d.sync()
@@ -294,7 +296,10 @@ def main():
                 "traffic_unit": "HBM bytes per launch (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, "
                                 f"profiles/{os.path.basename(PMC_FILE.format(w['workload']))})",
                 "algorithmic_bytes_per_launch": int(bytes_per),
-                "kernel": kname, "avg_launch_us": round(avg_ms * 1e3, 2), "launches": int(ks.launches)}
+                "kernel": kname, "avg_launch_us": round(avg_ms * 1e3, 2), "launches": int(ks.launches),
+                "timed_launches": int(ks.launches) // max(1, args.timing_period),
+                "timing": f"HIP events in the dispatch packets of 1 in {max(1, args.timing_period)} launches "
+                          "of each (kernel, K) over the timed region"}
     all_ms = st.ax.ms_total + st.atx.ms_total
     all_bytes = st.ax.bytes_total + st.atx.bytes_total
     line = {

@@ -262,7 +262,9 @@ typedef struct {
     vampomi_kernel_stat loo;      /* association-test pass (vampomi_assoc_loo) */
 } vampomi_stats;
 
-/* enable HIP-event timing of the A/A^T kernels (adds one event pair per launch) */
+/* HIP-event timing of the A/A^T kernels: on = 0 off, 1 every launch, n > 1 one
+ * launch in n of each (kernel class, K), counted n times in the stats (each
+ * timed launch carries an event pair in its dispatch, a few microseconds) */
 vampomi_status vampomi_set_timing(vampomi_ctx* ctx, int on);
 vampomi_status vampomi_get_stats(vampomi_ctx* ctx, vampomi_stats* out);
 vampomi_status vampomi_reset_stats(vampomi_ctx* ctx);

@@ -259,8 +259,10 @@ class Data:
         return x1[: self.M], x1d[: self.M], s.value
 
     # -- measurement --
-    def set_timing(self, on: bool = True):
-        check(self._lib.vampomi_set_timing(self.ctx, 1 if on else 0))
+    def set_timing(self, on: bool = True, period: int = 1):
+        """HIP-event timing of the A/A^T launches; period > 1 times one launch
+        in `period` of each (kernel class, K) and counts it `period` times."""
+        check(self._lib.vampomi_set_timing(self.ctx, (max(1, int(period)) if on else 0)))
 
     def stats(self) -> Stats:
         s = Stats()

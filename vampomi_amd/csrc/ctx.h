@@ -44,6 +44,7 @@ struct TimedLaunch {
     int cls;  // 0 ax, 1 atx, 2 loo
     int K;
     double bytes, flops;
+    int weight;  // launches this sample stands for (the sampling period)
 };
 
 // scalar slots in ctx->scal: <d,p> of the fused lmmse epilogue, then the
@@ -87,6 +88,8 @@ struct vampomi_ctx {
     double* mbuf = nullptr;     // (2*kMaxRhs) * M scratch M-vectors (API calls)
 
     bool timing = false;
+    int tperiod = 1;            // time 1 in tperiod launches of each (class, K)
+    int64_t tcount[3][vk::kMaxRhs] = {};
     std::vector<TimedLaunch> pending;
     std::vector<hipEvent_t> ev_pool;
     vampomi_stats stats{};
@@ -105,6 +108,8 @@ vampomi_status host_sync(vampomi_ctx* c);
 vampomi_status wait_flag(vampomi_ctx* c, unsigned long long seq);
 vampomi_status allreduce_dev(vampomi_ctx* c, double* buf, size_t n);
 void resolve_timing(vampomi_ctx* c);
+// events for this launch of class cls with K right-hand sides, if it is sampled
+TimedLaunch timed_launch(vampomi_ctx* c, int cls, int K);
 void release_ctx_resources(vampomi_ctx* c);
 
 // ---- operators on device buffers ---------------------------------------------

@@ -69,18 +69,27 @@ static hipEvent_t ev_get(vampomi_ctx* c) {
     return e;
 }
 
+TimedLaunch timed_launch(vampomi_ctx* c, int cls, int K) {
+    TimedLaunch t{};
+    if (!c->timing || c->tcount[cls][K - 1]++ % c->tperiod != 0) return t;
+    t.a = ev_get(c);
+    t.b = ev_get(c);
+    t.weight = c->tperiod;
+    return t;
+}
+
 void resolve_timing(vampomi_ctx* c) {
     for (auto& t : c->pending) {
         float ms = 0.f;
         if (hipEventSynchronize(t.b) == hipSuccess && hipEventElapsedTime(&ms, t.a, t.b) == hipSuccess) {
             vampomi_kernel_stat* s = t.cls == 0 ? &c->stats.ax : t.cls == 1 ? &c->stats.atx : &c->stats.loo;
             vampomi_kernel_stat* sk = t.cls == 0 ? &c->stats.ax_k[t.K - 1] : t.cls == 1 ? &c->stats.atx_k[t.K - 1] : nullptr;
-            for (vampomi_kernel_stat* x : {s, sk}) {
+            for (vampomi_kernel_stat* x : {s, sk}) {  // a sample stands for `weight` launches
                 if (!x) continue;
-                x->launches += 1;
-                x->ms_total += ms;
-                x->bytes_total += t.bytes;
-                x->flops_total += t.flops;
+                x->launches += t.weight;
+                x->ms_total += (double)ms * t.weight;
+                x->bytes_total += t.bytes * t.weight;
+                x->flops_total += t.flops * t.weight;
             }
         }
         c->ev_pool.push_back(t.a);
@@ -284,15 +293,11 @@ vampomi_status ax_dev(vampomi_ctx* c, int K, const double* const* x, double* out
         xs.p[k] = x[k];
         os.p[k] = outbase + (int64_t)k * c->ld;
     }
-    TimedLaunch t{};
-    if (c->timing) {
-        t.a = ev_get(c);
-        t.b = ev_get(c);
-    }
+    TimedLaunch t = timed_launch(c, 0, K);
     const vk::AxFuse none{};
     const vk::AxFuse& f = fu ? *fu : none;
     HIPCHK(vk::ax_partial(c->shard(), c->axp, K, xs, c->ax_part, c->st, vk::Timing{t.a, t.b}, f));
-    if (c->timing) {
+    if (t.a) {
         t.cls = 0;
         t.K = K;
         t.bytes = pass_bytes(c, K);
@@ -331,14 +336,10 @@ vampomi_status atx_dev(vampomi_ctx* c, int K, const double* const* u, double* co
         ps.p[k] = p ? p[k] : nullptr;
         zs.p[k] = zf ? zf[k] : nullptr;
     }
-    TimedLaunch t{};
-    if (c->timing) {
-        t.a = ev_get(c);
-        t.b = ev_get(c);
-    }
+    TimedLaunch t = timed_launch(c, 1, K);
     HIPCHK(vk::atx(c->shard(), K, us, os, 1.0 / c->sqrtN, mode, tau, gam2, ps, c->st, vk::Timing{t.a, t.b}, gate, zs,
                    zf ? beta : nullptr, ss));
-    if (c->timing) {
+    if (t.a) {
         t.cls = 1;
         t.K = K;
         t.bytes = pass_bytes(c, K);
@@ -911,13 +912,9 @@ extern "C" vampomi_status vampomi_assoc_loo(vampomi_ctx* c, const double* est, d
     STCHK(ax_dev(c, 1, xs, z1));                                     // :257
     HIPCHK(vk::axpby(N, 1.0, c->y, -1.0, z1, ymod, c->st));          // y_mod = y - z1 (data.cpp:390-391)
     if (ld > N) HIPCHK(hipMemsetAsync(ymod + N, 0, (size_t)(ld - N) * 8, c->st));
-    TimedLaunch t{};
-    if (c->timing) {
-        t.a = ev_get(c);
-        t.b = ev_get(c);
-    }
+    TimedLaunch t = timed_launch(c, 2, 1);
     HIPCHK(vk::loo_sums(c->shard(), ymod, x1, std::sqrt((double)N), st, c->st, vk::Timing{t.a, t.b}));  // :393-416
-    if (c->timing) {
+    if (t.a) {
         t.cls = 2;
         t.K = 1;
         // raw X once, ymod, x1, the five sums; per element 1 div, 2 mul + 1 add
@@ -978,6 +975,9 @@ extern "C" vampomi_status vampomi_assoc_se(vampomi_ctx* c, const double* r1, dou
 extern "C" vampomi_status vampomi_set_timing(vampomi_ctx* c, int on) {
     if (!c) return fail(VAMPOMI_ERR_ARG, "null context");
     c->timing = on != 0;
+    c->tperiod = on > 1 ? on : 1;
+    for (auto& row : c->tcount)
+        for (auto& n : row) n = 0;
     return VAMPOMI_OK;
 }
 
