@@ -49,9 +49,10 @@ struct TimedLaunch {
 
 // scalar slots in ctx->scal: <d,p> of the fused lmmse epilogue, then the
 // synced (summed over ranks) and local halves of a DotBatch
-// (SL_CG: the 3K sums of a CG step, decided on the device)
+// (SL_CG: the 3K sums of a CG step, decided on the device; SL_CGI: the 2K sums
+// of cg_init, read by cg_start_from)
 enum : int { SL_DP = 0, SL_CG = 4, SL_SYNC = 16, SL_NSYNC = 256, SL_LOCAL = SL_SYNC + SL_NSYNC, SL_NLOCAL = 128,
-             SL_TOTAL = 512, SL_BARRIER = SL_TOTAL - 1 };
+             SL_CGI = SL_LOCAL + SL_NLOCAL, SL_TOTAL = 512, SL_BARRIER = SL_TOTAL - 1 };
 
 struct vampomi_ctx {
     int rank = 0, nranks = 1, device = 0;

@@ -234,6 +234,8 @@ struct CgMirror {
 };
 // *dst = init (one thread)
 hipError_t cg_start(const CgState& init, CgState* dst, hipStream_t st);
+// *dst = init with rz[k], vv[k] = sums[2k], sums[2k+1] (cg_init's sums, in device memory)
+hipError_t cg_start_from(const CgState& init, const double* sums, CgState* dst, hipStream_t st);
 // for active k: [fuse: p = z + beta_k p, stored] alpha_k = rz[k] / dp_dev[k];
 // mu += alpha p; r -= d alpha; z = r/diag; <r,z>, <r,r>, <v,mu> in ro.out (3K
 // values, k-major; zeros for stopped systems); gated on cs->any.  dc.on (one

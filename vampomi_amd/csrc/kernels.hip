@@ -1097,6 +1097,20 @@ hipError_t cg_start(const CgState& init, CgState* dst, hipStream_t st) {
     return hipGetLastError();
 }
 
+__global__ void cg_start_from_kernel(CgState init, const double* __restrict__ sums, CgState* dst) {
+    if (threadIdx.x != 0) return;
+    for (int k = 0; k < init.K; ++k) {
+        init.rz[k] = sums[2 * k];
+        init.vv[k] = sums[2 * k + 1];
+    }
+    *dst = init;
+}
+
+hipError_t cg_start_from(const CgState& init, const double* sums, CgState* dst, hipStream_t st) {
+    hipLaunchKernelGGL(cg_start_from_kernel, dim3(1), dim3(64), 0, st, init, sums, dst);
+    return hipGetLastError();
+}
+
 // one thread: the host loop of vamp::precondCG_solver after each step's sums
 __device__ void cg_decide_body(CgState* cs, const double* red, int it, CgMirror* mirror, unsigned long long* flag,
                                unsigned long long seq) {
@@ -1159,33 +1173,60 @@ __global__ __launch_bounds__(kBlock) void cg_update_kernel(int K, int64_t M, CgV
     double acc[3 * kMaxRhs];
 #pragma unroll
     for (int q = 0; q < 3 * kMaxRhs; ++q) acc[q] = 0.0;
+    double beta[kMaxRhs];
+#pragma unroll
+    for (int k = 0; k < kMaxRhs; ++k) beta[k] = fuse && on[k] ? cs->beta[k] : 0.0;
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < M; i += (int64_t)gridDim.x * kBlock) {
+        // every load of the element first (the vectors may alias as far as the
+        // compiler knows: loads after a store would wait for it)
+        double pv[kMaxRhs], zv[kMaxRhs], muv[kMaxRhs], rv[kMaxRhs], dv[kMaxRhs], vv[kMaxRhs], wv[kMaxRhs],
+            sv[kMaxRhs];
 #pragma unroll
         for (int k = 0; k < kMaxRhs; ++k) {
             if (on[k]) {
-                double pi = c.p[k][i];
+                pv[k] = c.p[k][i];
+                zv[k] = fuse ? c.z[k][i] : 0.0;
+                muv[k] = c.mu[k][i];
+                rv[k] = c.r[k][i];
+                dv[k] = c.d[k][i];
+                vv[k] = c.v[k][i];
+                wv[k] = c.W[k] ? c.W[k][i] : 0.0;
+                sv[k] = c.W[k] ? c.S[k][i] : 0.0;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kMaxRhs; ++k) {
+            if (on[k]) {
+                double pi = pv[k];
                 if (fuse) {  // p = z + beta p (:738-739)
-                    pi = c.z[k][i] + cs->beta[k] * pi;
+                    pi = zv[k] + beta[k] * pi;
                     c.p[k][i] = pi;
                 }
-                const double mu = c.mu[k][i] + alpha[k] * pi;  // mu += alpha * p
-                const double r = c.r[k][i] - c.d[k][i] * alpha[k];  // r -= d * alpha
+                const double mu = muv[k] + alpha[k] * pi;  // mu += alpha * p
+                const double r = rv[k] - dv[k] * alpha[k];  // r -= d * alpha
                 const double z = r / diag;
                 c.mu[k][i] = mu;
                 c.r[k][i] = r;
                 c.z[k][i] = z;
-                if (c.W[k]) c.W[k][i] = c.W[k][i] + alpha[k] * c.S[k][i];  // A^T A mu, as mu += alpha p
+                if (c.W[k]) c.W[k][i] = wv[k] + alpha[k] * sv[k];  // A^T A mu, as mu += alpha p
                 acc[3 * k] += r * z;
                 acc[3 * k + 1] += r * r;
-                acc[3 * k + 2] += c.v[k][i] * mu;
+                acc[3 * k + 2] += vv[k] * mu;
             }
         }
     }
     // A mu alongside mu (replicated N-vectors, the same on every rank)
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < c.nA; i += (int64_t)gridDim.x * kBlock) {
+        double aw[kMaxRhs], as[kMaxRhs];
 #pragma unroll
         for (int k = 0; k < kMaxRhs; ++k)
-            if (on[k] && c.AW[k]) c.AW[k][i] = c.AW[k][i] + alpha[k] * c.AS[k][i];
+            if (on[k] && c.AW[k]) {
+                aw[k] = c.AW[k][i];
+                as[k] = c.AS[k][i];
+            }
+#pragma unroll
+        for (int k = 0; k < kMaxRhs; ++k)
+            if (on[k] && c.AW[k]) c.AW[k][i] = aw[k] + alpha[k] * as[k];
     }
     block_put_sums<3 * kMaxRhs>(acc, 3 * K, ro, (int64_t)blockIdx.x * 3 * K);
     // one rank: the last block decides the step itself (its sums are final)

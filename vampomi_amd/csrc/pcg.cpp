@@ -73,27 +73,35 @@ vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double
         cv.atx0[k] = s->mu0_nonzero ? s->atx0 : nullptr;
         cv.d[k] = (s->mu0_nonzero && !s->atx0) ? s->d : nullptr;
     }
-    std::vector<double> rzvv(2 * K);
-    DotBatch local(c);
-    DotBatch& b0 = init ? *init : local;
-    vk::RedOut ro{};
-    STCHK(b0.sink(2 * K, true, rzvv.data(), &ro));
-    HIPCHK(vk::cg_init(K, M, cv, diag, ro, c->st));
-    STCHK(b0.flush());
     vk::CgState s0{};
     s0.K = K;
     s0.gam2 = gam2;
     s0.tol = tol;
     s0.any = max_iter > 0 ? 1 : 0;
     for (int k = 0; k < K; ++k) {
-        s0.rz[k] = rzvv[2 * k];
-        s0.vv[k] = rzvv[2 * k + 1];
         s0.active[k] = 1;
         s0.onsager[k] = sys[k]->onsager ? 1 : 0;
         sys[k]->iters = 0;
     }
-    if (max_iter <= 0) return extra_alone();
-    HIPCHK(vk::cg_start(s0, c->cgs, c->st));
+    if (init) {  // the caller's reductions resolve together with <r,z>, <v,v> (one host wait)
+        std::vector<double> rzvv(2 * K);
+        vk::RedOut ro{};
+        STCHK(init->sink(2 * K, true, rzvv.data(), &ro));
+        HIPCHK(vk::cg_init(K, M, cv, diag, ro, c->st));
+        STCHK(init->flush());
+        for (int k = 0; k < K; ++k) {
+            s0.rz[k] = rzvv[2 * k];
+            s0.vv[k] = rzvv[2 * k + 1];
+        }
+        if (max_iter <= 0) return extra_alone();
+        HIPCHK(vk::cg_start(s0, c->cgs, c->st));
+    } else {  // <r,z>, <v,v> stay on the device: the CgState is built there, no host wait
+        const vk::RedOut ro{c->red_part, c->scal + SL_CGI, c->ticket, nullptr, 0, nullptr};
+        HIPCHK(vk::cg_init(K, M, cv, diag, ro, c->st));
+        STCHK(allreduce_dev(c, c->scal + SL_CGI, (size_t)(2 * K)));
+        if (max_iter <= 0) return extra_alone();
+        HIPCHK(vk::cg_start_from(s0, c->scal + SL_CGI, c->cgs, c->st));
+    }
     const int* gate = field<int>(c->cgs, offsetof(vk::CgState, any));
     const double* beta = field<double>(c->cgs, offsetof(vk::CgState, beta));
     const double* pp[vk::kMaxRhs];
