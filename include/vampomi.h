@@ -177,7 +177,11 @@ typedef struct {
     int verbosity;
     const double* true_signal;    /* local slice (M) or NULL => zeros (host) */
     const double* x1hat_init;     /* local slice (M) or NULL => zeros (host) */
-    int batch_rhs;                /* 3 (default): 2, plus A x2 carried through the CG steps
+    int batch_rhs;                /* 4 (default): 3, and each CG step reads X ONCE: A^T q
+                                     and A d from the same pass, with q = A p and A r
+                                     carried as N-vector recurrences (one A.x pass per
+                                     solve for A r0; equal up to rounding);
+                                     3: 2, plus A x2 carried through the CG steps
                                      and z1 = A x1 in the first CG pass (no pass over X
                                      outside the CG; equal up to rounding); 2: 1, plus the
                                      linear model's updateNoisePrec products A^T A x2 /
@@ -260,6 +264,8 @@ typedef struct {
     int64_t a_passes_exec;
     int64_t host_syncs;
     vampomi_kernel_stat loo;      /* association-test pass (vampomi_assoc_loo) */
+    vampomi_kernel_stat op;       /* one-pass CG operator (A^T q and A d, batch_rhs 4) */
+    vampomi_kernel_stat op_k[4];
 } vampomi_stats;
 
 /* HIP-event timing of the A/A^T kernels: on = 0 off, 1 every launch, n > 1 one
@@ -271,7 +277,7 @@ vampomi_status vampomi_reset_stats(vampomi_ctx* ctx);
 
 /* ---- development hooks (kernel tuning; not part of the reference interface) ----
  * which: 0 = A.x partial-sum kernel, 1 = A^T.u kernel, 2 = association-test pass
- * (K = 1).  Variants index the
+ * (K = 1), 3 = one-pass CG operator (K = 1, 2).  Variants index the
  * tuning tables in vampomi_amd/csrc/kernels.hip; variant 0 is the default. */
 vampomi_status vampomi_dev_set_variant(vampomi_ctx* ctx, int which, int variant);
 /* average device time (HIP events) of `reps` back-to-back launches, K RHS */

@@ -188,6 +188,31 @@ def test_ax_recurrence_mode(N, Mt, its, kind):
     _assert_parity(a, ref)
 
 
+@pytest.mark.parametrize("N,Mt,its,kind", [(1000, 2000, 30, 0), (4099, 3001, 12, 1), (301, 517, 12, 0),
+                                            (10000, 2500, 8, 0)])
+def test_onepass_mode(N, Mt, its, kind):
+    """batch_rhs=4 reads X once per CG step (A^T q and A d in one pass, q = A p
+    and A r carried as N-vector recurrences): the same integer counts as
+    batch_rhs=3, values within rounding of it and within the parity bar of the
+    oracle, and 1 + max(k1, k2) executed passes per iteration (A r0 with z1,
+    then one per CG step).  N > 2048 exercises the tile exchange between the
+    workgroups of a team."""
+    X, y, beta = _problem(N, Mt, kind=kind)
+    a = _gpu_vamp(X, y, beta, Mt, max_iter=its, stop_criteria_thr=0.0, batch_rhs=4)
+    b = _gpu_vamp(X, y, beta, Mt, max_iter=its, stop_criteria_thr=0.0, batch_rhs=3)
+    errs = [max(relerr(a["x1_hist"][k], b["x1_hist"][k]), relerr(a["r1_hist"][k], b["r1_hist"][k]))
+            for k in range(its)]
+    print("onepass vs batch_rhs=3, max rel err per iteration:", ["%.1e" % e for e in errs])
+    assert a["cg_iters"] == b["cg_iters"] and a["ons_iters"] == b["ons_iters"] and a["L"] == b["L"]
+    assert max(errs) <= 1e-11
+    assert np.allclose(np.array(a["params"]), np.array(b["params"]), rtol=1e-11, atol=0)
+    assert np.allclose(np.array(a["metrics"]), np.array(b["metrics"]), rtol=1e-10, atol=1e-13, equal_nan=True)
+    assert a["a_passes_exec"] == 1 + sum(1 + max(p, q) for p, q in zip(a["cg_iters"], a["ons_iters"]))  # + A^T y
+    assert a["a_passes_ref"] == b["a_passes_ref"]
+    ref = O.vamp_infere(X, y, Mt, true_signal=beta, max_iter=its, stop_criteria_thr=0.0)
+    _assert_parity(a, ref)
+
+
 def test_deterministic_repeat():
     N, Mt = 777, 1234
     X, y, beta = _problem(N, Mt)

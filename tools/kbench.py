@@ -52,6 +52,18 @@ for which, name, Ks, nvar in ((0, "ax", (1, 2, 3), 7), (1, "atx", (1, 2), 8)):
         res[name][v] = row
         print(name, v, json.dumps(row), flush=True)
     _lib.check(lib.vampomi_dev_set_variant(d.ctx, which, 0))
+if "op" in only:  # the one-pass CG operator (A^T q and A d from one read of X)
+    res["op"] = {}
+    for v in range(1):
+        row = {"kernel": va.kernel_name(3, 2, N)}
+        for K in (1, 2):
+            ms = C.c_double()
+            _lib.check(lib.vampomi_dev_time_pass(d.ctx, 3, K, 2, C.byref(ms)))
+            _lib.check(lib.vampomi_dev_time_pass(d.ctx, 3, K, reps, C.byref(ms)))
+            b = 8.0 * N * Mt + 8.0 * K * N + 8.0 * (2 + K) * Mt
+            row[f"K{K}"] = {"us": round(ms.value * 1e3, 1), "GBs": round(b / (ms.value * 1e-3) / 1e9, 1)}
+        res["op"][v] = row
+        print("op", v, json.dumps(row), flush=True)
 if "loo" in only:
     d.set_phen(rng.normal(size=N), standardize=False)
     est = rng.normal(size=Mt) * 1e-3

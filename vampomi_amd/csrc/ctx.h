@@ -41,7 +41,7 @@ struct LoopbackComm;  // engine.cpp: test-only in-process communicator
 
 struct TimedLaunch {
     hipEvent_t a, b;
-    int cls;  // 0 ax, 1 atx, 2 loo
+    int cls;  // 0 ax, 1 atx, 2 loo, 3 one-pass operator
     int K;
     double bytes, flops;
     int weight;  // launches this sample stands for (the sampling period)
@@ -85,12 +85,17 @@ struct vampomi_ctx {
     vk::CgState* cgs = nullptr;     // device-side CG control (pcg.cpp)
     vk::CgMirror* h_cgm = nullptr;  // its mapped host mirror, and the mirror's device address
     vk::CgMirror* d_cgm = nullptr;
+    // one-pass CG operator (batch_rhs 4; allocated on first use, pcg.cpp)
+    vk::OpPlan opp{};
+    int cus = 0;                // compute units of the device (the operator's grid)
+    double* op_part = nullptr;  // opp.nslots x kMaxRhs x ld partial A d
+    double* op_nvec = nullptr;  // 3 x kMaxRhs x ld: A r, q = A p, A d (+ <d,p> tail)
     double* nbuf = nullptr;     // kMaxRhs * ld scratch N-vectors (API calls)
     double* mbuf = nullptr;     // (2*kMaxRhs) * M scratch M-vectors (API calls)
 
     bool timing = false;
     int tperiod = 1;            // time 1 in tperiod launches of each (class, K)
-    int64_t tcount[3][vk::kMaxRhs] = {};
+    int64_t tcount[4][vk::kMaxRhs] = {};
     std::vector<TimedLaunch> pending;
     std::vector<hipEvent_t> ev_pool;
     vampomi_stats stats{};
@@ -185,6 +190,14 @@ struct CgSystem {
 // extra_x (may be null, device M): ex_out (device, ld) = A extra_x, carried as
 // one more right-hand side of the first step's A.x pass (its own pass if no
 // step runs).  nscratch holds kMaxRhs*ld + kMaxRhs doubles.
+// onepass (K <= 2): every CG step reads X once (vk::atax; A r0 by one A.x pass
+// per solve, which also carries extra_x); otherwise two passes per step.
 vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double tau, double gam2, int max_iter,
                        double tol, double* nscratch, int64_t* ref_passes, DotBatch* init,
-                       const double* extra_x = nullptr, double* ex_out = nullptr);
+                       const double* extra_x = nullptr, double* ex_out = nullptr, bool onepass = false);
+// allocates the one-pass operator's buffers (idempotent)
+vampomi_status op_prepare(vampomi_ctx* c);
+// d_k = tau*A^T q_k + gam2*p_k and A d_k (into op_nvec's A d block, /sqrt(N),
+// summed over ranks with <d_k,p_k> at its tail; one rank: <d_k,p_k> in
+// scal[SL_DP+k]) from one pass over X.  COLLECTIVE
+vampomi_status op_dev(vampomi_ctx* c, int K, const vk::OpArgs& a, const int* gate);

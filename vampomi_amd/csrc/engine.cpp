@@ -82,8 +82,14 @@ void resolve_timing(vampomi_ctx* c) {
     for (auto& t : c->pending) {
         float ms = 0.f;
         if (hipEventSynchronize(t.b) == hipSuccess && hipEventElapsedTime(&ms, t.a, t.b) == hipSuccess) {
-            vampomi_kernel_stat* s = t.cls == 0 ? &c->stats.ax : t.cls == 1 ? &c->stats.atx : &c->stats.loo;
-            vampomi_kernel_stat* sk = t.cls == 0 ? &c->stats.ax_k[t.K - 1] : t.cls == 1 ? &c->stats.atx_k[t.K - 1] : nullptr;
+            vampomi_kernel_stat* s = t.cls == 0   ? &c->stats.ax
+                                     : t.cls == 1 ? &c->stats.atx
+                                     : t.cls == 3 ? &c->stats.op
+                                                  : &c->stats.loo;
+            vampomi_kernel_stat* sk = t.cls == 0   ? &c->stats.ax_k[t.K - 1]
+                                      : t.cls == 1 ? &c->stats.atx_k[t.K - 1]
+                                      : t.cls == 3 ? &c->stats.op_k[t.K - 1]
+                                                   : nullptr;
             for (vampomi_kernel_stat* x : {s, sk}) {  // a sample stands for `weight` launches
                 if (!x) continue;
                 x->launches += t.weight;
@@ -361,6 +367,59 @@ vampomi_status atx_dev(vampomi_ctx* c, int K, const double* const* u, double* co
     return VAMPOMI_OK;
 }
 
+// ---------------------------------------------------------------------------
+// one-pass CG operator (batch_rhs 4)
+// ---------------------------------------------------------------------------
+vampomi_status op_prepare(vampomi_ctx* c) {
+    if (c->op_nvec) return VAMPOMI_OK;
+    if (c->cus <= 0) HIPCHK(hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, c->device));
+    c->opp = vk::op_plan(c->N, c->M, c->cus);
+    STCHK(dev_alloc(&c->op_part, (size_t)c->opp.nslots * vk::kMaxRhs * c->ld));
+    STCHK(dev_alloc(&c->op_nvec, (size_t)3 * vk::kMaxRhs * c->ld));
+    HIPCHK(hipMemsetAsync(c->op_nvec, 0, (size_t)3 * vk::kMaxRhs * c->ld * 8, c->st));
+    return VAMPOMI_OK;
+}
+
+// one operator launch: X once, the K q-vectors (as A r and q_old), mave/msig,
+// p, z and d, plus the K A d partials written once per workgroup
+static double op_bytes(const vampomi_ctx* c, int K) {
+    return pass_bytes(c, K) + 8.0 * K * (double)c->N + 8.0 * 2 * K * (double)c->M +
+           8.0 * K * (double)c->N * (double)c->opp.nslots;
+}
+
+vampomi_status op_dev(vampomi_ctx* c, int K, const vk::OpArgs& a, const int* gate) {
+    if (!c->have_X) return fail(VAMPOMI_ERR_STATE, "A before the methylation data was loaded");
+    if (!vk::op_supported(c->N, K)) return fail(VAMPOMI_ERR_ARG, "one-pass operator: K <= 2 and K*N <= 20000");
+    STCHK(op_prepare(c));
+    double* ad = c->op_nvec + (int64_t)2 * vk::kMaxRhs * c->ld;
+    vk::OpArgs x = a;
+    x.part = c->op_part;
+    x.scale = 1.0 / c->sqrtN;
+    // <d,p>: one rank into scal[SL_DP+k]; several: behind the A d block, all-reduced with it
+    x.ro = vk::RedOut{c->red_part, c->use_comm ? ad + (int64_t)K * c->ld : c->scal + SL_DP, c->ticket, nullptr, 0,
+                      gate};
+    TimedLaunch t = timed_launch(c, 3, K);
+    HIPCHK(vk::atax(c->shard(), c->opp, K, x, c->st, vk::Timing{t.a, t.b}, gate));
+    if (t.a) {
+        t.cls = 3;
+        t.K = K;
+        t.bytes = op_bytes(c, K);
+        t.flops = 2.0 * pass_flops(c, K);
+        c->pending.push_back(t);
+    }
+    c->stats.a_passes_exec++;
+    vk::Ptrs os{};
+    for (int k = 0; k < K; ++k) os.p[k] = ad + (int64_t)k * c->ld;
+    if (!c->use_comm) {
+        HIPCHK(vk::op_reduce(c->opp, K, c->N, c->ld, c->op_part, os, c->sqrtN, c->st, gate));
+    } else {
+        HIPCHK(vk::op_reduce(c->opp, K, c->N, c->ld, c->op_part, os, 0.0, c->st, gate));
+        STCHK(allreduce_dev(c, ad, (size_t)K * c->ld + K));  // src/data.cpp:367
+        HIPCHK(vk::vec_div(K, c->N, c->ld, os, c->sqrtN, c->st));
+    }
+    return VAMPOMI_OK;
+}
+
 // d_k = tau*A^T A v_k + gam2*v_k (lmmse_mult, src/vamp.cpp:645-662) for K
 // vectors that are not all-zero; <d_k, v_k> lands in scal[SL_DP+k]. COLLECTIVE
 vampomi_status lmmse_dev(vampomi_ctx* c, int K, const double* const* v, double* const* d, double tau,
@@ -409,7 +468,8 @@ void release_ctx_resources(vampomi_ctx* c) {
     resolve_timing(c);
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
     c->ev_pool.clear();
-    for (double** p : {&c->X, &c->mave, &c->msig, &c->y, &c->ax_part, &c->red_part, &c->scal, &c->nbuf, &c->mbuf})
+    for (double** p : {&c->X, &c->mave, &c->msig, &c->y, &c->ax_part, &c->red_part, &c->scal, &c->nbuf, &c->mbuf,
+                       &c->op_part, &c->op_nvec})
         dev_free(*p);
     if (c->h_scal) (void)hipHostFree(c->h_scal);
     c->h_scal = nullptr;
@@ -1021,10 +1081,11 @@ extern "C" vampomi_status vampomi_dev_set_variant(vampomi_ctx* c, int which, int
 }
 
 extern "C" vampomi_status vampomi_dev_time_pass(vampomi_ctx* c, int which, int K, int reps, double* avg_ms) {
-    if (!c || !avg_ms || K < 1 || K > (which == 0 ? 4 : which == 1 ? 3 : 1) || reps < 1)
+    if (!c || !avg_ms || K < 1 || K > (which == 0 ? 4 : which == 1 ? 3 : which == 3 ? 2 : 1) || reps < 1)
         return fail(VAMPOMI_ERR_ARG, "bad argument");
     if (!c->have_X) return fail(VAMPOMI_ERR_STATE, "no methylation data loaded");
     HIPCHK(hipSetDevice(c->device));
+    if (which == 3) STCHK(op_prepare(c));
     const int64_t Mx = std::max<int64_t>(c->M, 1);
     vk::CPtrs in{};
     vk::Ptrs out{};
@@ -1041,6 +1102,20 @@ extern "C" vampomi_status vampomi_dev_time_pass(vampomi_ctx* c, int which, int K
             HIPCHK(vk::ax_partial(c->shard(), c->axp, K, in, c->ax_part, c->st));
         else if (which == 1)
             HIPCHK(vk::atx(c->shard(), K, in, out, 1.0 / c->sqrtN, 0, 0.0, 0.0, vk::CPtrs{}, c->st));
+        else if (which == 3) {  // the operator on q = nbuf/1, p = mbuf slots 0..1, d into slots 2..3
+            vk::OpArgs x{};
+            for (int k = 0; k < K; ++k) {
+                x.ar.p[k] = c->nbuf + k * c->ld;
+                x.p.p[k] = c->mbuf + k * Mx;
+                x.d.p[k] = c->mbuf + (2 + k) * Mx;
+            }
+            x.diag = 1.0;
+            x.scale = 1.0 / c->sqrtN;
+            x.tau = 1.0;
+            x.part = c->op_part;
+            x.ro = vk::RedOut{c->red_part, c->scal + SL_DP, c->ticket, nullptr, 0, nullptr};
+            HIPCHK(vk::atax(c->shard(), c->opp, K, x, c->st));
+        }
         else  // association pass: ymod = nbuf slot 0, x1 = mbuf slot 0, sums in mbuf slots 3..7
             HIPCHK(vk::loo_sums(c->shard(), c->nbuf, c->mbuf, c->sqrtN, c->mbuf + 3 * Mx, c->st));
     }
@@ -1056,7 +1131,10 @@ extern "C" vampomi_status vampomi_dev_time_pass(vampomi_ctx* c, int which, int K
 
 extern "C" vampomi_status vampomi_dev_kernel_name(int which, int K, int mode, char* out, int cap) {
     if (!out || cap < 1) return fail(VAMPOMI_ERR_ARG, "bad buffer");
-    const std::string n = which == 2 ? vk::loo_kernel_name() : vk::kernel_name(which, K, mode);
+    // which = 3: mode carries N (the operator's instantiation depends on it)
+    const std::string n = which == 2   ? vk::loo_kernel_name()
+                          : which == 3 ? vk::op_kernel_name(K, mode)
+                                       : vk::kernel_name(which, K, mode);
     std::snprintf(out, (size_t)cap, "%s", n.c_str());
     return VAMPOMI_OK;
 }

@@ -93,6 +93,38 @@ hipError_t atx(const Shard& s, int K, CPtrs u, Ptrs out, double scale, int mode,
                double gam2, CPtrs p, hipStream_t st, const Timing& tm = Timing{}, const int* gate = nullptr,
                CPtrs zf = CPtrs{}, const double* beta = nullptr, Ptrs sraw = Ptrs{});
 
+// ---- one-pass CG operator: A^T q and A d from ONE read of X ----------------
+// A CG step needs d = tau*A^T(A p) + gam2*p.  With q = A p carried as an
+// N-vector recurrence (q = A r/diag + beta*q_old, A r -= alpha*A d), the pass
+// over X computes, per marker i, t_i = (msig_i*sum_j (X_ij - mave_i) q_j)/sqrt(N)
+// and d_i = tau*t_i + gam2*p_i, and while the column is still in registers
+// accumulates (A d)_j += (X_ij - mave_i)*(msig_i*d_i): A^T and A in one read.
+// One workgroup per CU owns whole columns; q lives in LDS, so K*N <= 20,000
+// (op_supported); larger problems keep the two-pass CG step.
+struct OpPlan {
+    int grid;       // workgroups (one per CU, at most M)
+    int S;          // 16-byte loads per lane per column: ceil(N / 1024)
+    int64_t nslots; // partial A d slots (grid x kMaxRhs x ld)
+};
+bool op_supported(int64_t N, int K);
+OpPlan op_plan(int64_t N, int64_t M, int cus);
+struct OpArgs {
+    CPtrs ar, qo;       // q_k = ar_k/diag [+ beta_k*qo_k when fuse] (N-space, replicated)
+    CPtrs p, z;         // p_k [= z_k + beta_k*p_k when fuse] (M-space)
+    const double* beta; // device (CgState.beta)
+    int fuse;
+    double diag, scale, tau, gam2;
+    Ptrs d, sraw;       // d_k (M); sraw_k = t_k (may be null)
+    double* part;       // grid x kMaxRhs x ld partial A d (before the sum over workgroups)
+    RedOut ro;          // <d_k, p_k> summed over the shard (K values)
+};
+std::string op_kernel_name(int K, int64_t N);
+hipError_t atax(const Shard& s, const OpPlan& pl, int K, const OpArgs& a, hipStream_t st, const Timing& tm = Timing{},
+                const int* gate = nullptr);
+// out_k[j] = sum_b part[b][k][j] (workgroups in order); if div > 0 then /= div
+hipError_t op_reduce(const OpPlan& pl, int K, int64_t N, int64_t ld, const double* part, Ptrs out, double div,
+                     hipStream_t st, const int* gate = nullptr);
+
 // ---- marker statistics (data::compute_markers_statistics) ----------------
 hipError_t marker_stats(const double* X, int64_t ld, int64_t N, int64_t M, double nonas,
                         double alpha_scale, double* mave, double* msig, hipStream_t st);
@@ -212,6 +244,12 @@ struct CgVecs {
     double* AW[kMaxRhs];
     const double* AS[kMaxRhs];
     int64_t nA;
+    // cg_update only, one-pass operator (may be null): over nA samples,
+    // q = AR/diag [+ beta*Q when fuse] is stored in Q (the step's A p, as the
+    // pass formed it), AW += alpha*q, AR -= AD*alpha (A r tracks r -= d*alpha)
+    double* Q[kMaxRhs];
+    double* AR[kMaxRhs];
+    const double* AD[kMaxRhs];
 };
 // r = v - d (or v, or v - (atx0*tau + gam2*mu)), z = r/diag, p = z;
 // <r,z>, <v,v> per system in ro.out (2K values)

@@ -9,6 +9,7 @@
 // run and independent of the rank count's effect on scheduling.
 #include "kernels.h"
 
+#include <algorithm>
 #include <cstdlib>
 
 #include <hip/hip_ext.h>
@@ -719,6 +720,283 @@ hipError_t atx(const Shard& s, int K, CPtrs u, Ptrs out, double scale, int mode,
 }
 
 // ---------------------------------------------------------------------------
+// One-pass CG operator (kernels.h: atax).  A^T q (data::ATx,
+// src/data.cpp:294-333, with the lmmse_mult epilogue src/vamp.cpp:656-659)
+// and A d (data::Ax, src/data.cpp:340-373) from one read of X.
+// ---------------------------------------------------------------------------
+// One workgroup per CU (kOpWaves waves) owns whole columns: markers
+// [b*M/grid, (b+1)*M/grid).  Wave w, lane l owns rows 1024*s + 128*w + 2l
+// (+1), s < S = ceil(N/1024): every load instruction reads 1 KiB contiguous
+// of one column.  Per marker i (a column of X in registers, the next one
+// loading):
+//   t_i = msig_i * sum_j (X_ij - mave_i) q_j * scale   (the wave partials
+//         meet in LDS, one barrier; every wave sums them in wave order)
+//   d_i = t_i*tau + gam2*p_i,  c_i = msig_i*d_i
+//   acc_j += (X_ij - mave_i) * c_i                      (registers)
+// q = A r/diag [+ beta*q_old] is formed once per launch into LDS (K*N
+// doubles, each thread only ever reads its own rows: no barrier), so
+// K*N <= kOpLdsDoubles.  The column is read from HBM once for both products;
+// the workgroup's A d partial (K*N) goes to its slot, op_reduce sums the
+// slots in order.  Summation orders are fixed, results bitwise reproducible.
+static constexpr int kOpWaves = 8;
+static constexpr int kOpThreads = 64 * kOpWaves;
+static constexpr int kOpRows = 128 * kOpWaves;   // rows per load step of the workgroup
+static constexpr int kOpMaxS = 10;               // rows per workgroup <= kOpRows*kOpMaxS = 10,240
+static constexpr int64_t kOpLdsDoubles = 20000;  // q in LDS: 160,000 B of the CU's 160 KiB
+
+bool op_supported(int64_t N, int K) {
+    return K >= 1 && K <= 2 && N >= 1 && K * (N + (N & 1)) <= kOpLdsDoubles && (N + kOpRows - 1) / kOpRows <= kOpMaxS;
+}
+
+OpPlan op_plan(int64_t N, int64_t M, int cus) {
+    OpPlan p{};
+    p.S = (int)std::max<int64_t>(1, (N + kOpRows - 1) / kOpRows);
+    p.grid = (int)std::max<int64_t>(1, std::min<int64_t>(cus, M));
+    p.nslots = p.grid;
+    return p;
+}
+
+// one column in registers: its X rows and the marker's scalars
+template <int K, int S>
+struct OpCol {
+    v2d x[S];
+    double mu, sg, p[K], z[K];
+};
+
+template <int K, int S>
+__global__ __launch_bounds__(kOpThreads) void atax_kernel(const double* __restrict__ X, int64_t ld, int64_t N,
+                                                          int64_t M, const double* __restrict__ mave,
+                                                          const double* __restrict__ msig, OpArgs a,
+                                                          const int* __restrict__ gate) {
+    if (gate && !*gate) return;
+    extern __shared__ double q_lds[];  // K x NL (rows of this thread only), then 2 x kOpWaves x K partials
+    const int64_t NL = N + (N & 1);    // even row stride: 16-byte aligned pairs
+    double* s_part = q_lds + (int64_t)K * NL;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t mb = (int64_t)blockIdx.x * M / gridDim.x, me = (int64_t)(blockIdx.x + 1) * M / gridDim.x;
+    // row of this thread in step s: jb + kOpRows*s (recomputed, not kept in registers)
+    const int jb = 128 * wave + 2 * lane;
+    const int n32 = (int)N;
+#define OP_J(s) (jb + kOpRows * (s))
+#define OP_OK(s) (OP_J(s) < n32)
+    v2d acc[K][S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            acc[k][s] = v2d{0.0, 0.0};
+            if (!OP_OK(s)) continue;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int jj = OP_J(s) + h;
+                if (jj < N) {
+                    double q = a.ar.p[k][jj] / a.diag;              // A z = A r / diag
+                    if (a.fuse) q = q + a.beta[k] * a.qo.p[k][jj];  // A p = A z + beta A p
+                    q_lds[(int64_t)k * NL + jj] = q;
+                }
+            }
+        }
+    }
+    double bk[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) bk[k] = a.fuse ? a.beta[k] : 0.0;
+    double dpacc[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) dpacc[k] = 0.0;
+    OpCol<K, S> cb[2];
+    auto load = [&](OpCol<K, S>& c, int64_t m) {
+        const char* col = reinterpret_cast<const char*>(X + m * ld);
+#pragma unroll
+        for (int s = 0; s < S; ++s)
+            c.x[s] = OP_OK(s) ? __builtin_nontemporal_load(reinterpret_cast<const v2d*>(col + (unsigned)(OP_J(s) * 8)))
+                              : v2d{0.0, 0.0};
+        c.mu = mave[m];
+        c.sg = msig[m];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            c.p[k] = a.p.p[k][m];
+            c.z[k] = a.fuse ? a.z.p[k][m] : 0.0;
+        }
+    };
+    // dot partials of column c -> s_part[par][wave][k]
+    auto dots = [&](const OpCol<K, S>& c, int par) {
+        double v[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            double t = 0.0;
+#pragma unroll
+            for (int s = 0; s < S; ++s) {
+                if (!OP_OK(s)) continue;
+                const v2d q = *reinterpret_cast<const v2d*>(q_lds + (int64_t)k * NL + OP_J(s));  // .y unused at j+1 == N
+                t += (c.x[s].x - c.mu) * q.x;
+                if (OP_J(s) + 1 < n32) t += (c.x[s].y - c.mu) * q.y;
+            }
+            v[k] = wave_sum(t);
+        }
+        if (lane == 0) {
+#pragma unroll
+            for (int k = 0; k < K; ++k) s_part[(par * kOpWaves + wave) * K + k] = v[k];
+        }
+    };
+    // the column's d (all waves, identically) and acc += (x - mave)*msig*d
+    auto finish = [&](const OpCol<K, S>& c, int64_t m, int par) {
+        double cc[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            double dot = 0.0;
+#pragma unroll
+            for (int w = 0; w < kOpWaves; ++w) dot += s_part[(par * kOpWaves + w) * K + k];
+            double t = c.sg * dot;  // sigma_inv * dpa
+            t *= a.scale;           // ATx[mloc] *= 1/sqrt(N)
+            double pk = c.p[k];
+            if (a.fuse) pk = c.z[k] + bk[k] * pk;  // p = z + beta p
+            double val = t * a.tau;  // res[i] *= tau
+            val += a.gam2 * pk;      // res[i] += gam2 * v[i]
+            if (threadIdx.x == 0) {
+                if (a.sraw.p[0]) a.sraw.p[k][m] = t;
+                a.d.p[k][m] = val;
+            }
+            dpacc[k] += val * pk;
+            cc[k] = c.sg * val;  // Ax: (x - mave) * (msig * x_i)
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+#pragma unroll
+            for (int s = 0; s < S; ++s) {
+                acc[k][s].x += (c.x[s].x - c.mu) * cc[k];
+                acc[k][s].y += (c.x[s].y - c.mu) * cc[k];
+            }
+    };
+    // two columns in registers: m is finished while m+1 is dotted and m+2 loads
+    int64_t m = mb;
+    if (m < me) {
+        load(cb[0], m);
+        if (m + 1 < me) load(cb[1], m + 1);
+        dots(cb[0], 0);
+        __syncthreads();
+        for (; m < me; m += 2) {
+            finish(cb[0], m, 0);
+            if (m + 2 < me) load(cb[0], m + 2);
+            if (m + 1 < me) {
+                dots(cb[1], 1);
+                __syncthreads();
+                finish(cb[1], m + 1, 1);
+                if (m + 3 < me) load(cb[1], m + 3);
+            }
+            if (m + 2 < me) {
+                dots(cb[0], 0);
+                __syncthreads();
+            }
+        }
+    }
+    // this workgroup's partial A d
+    double* dst = a.part + (int64_t)blockIdx.x * kMaxRhs * ld;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+        if (!OP_OK(s)) continue;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            dst[(int64_t)k * ld + OP_J(s)] = acc[k][s].x;
+            if (OP_J(s) + 1 < n32) dst[(int64_t)k * ld + OP_J(s) + 1] = acc[k][s].y;
+        }
+    }
+#undef OP_J
+#undef OP_OK
+    // <d_k, p_k>: this workgroup's sums over its markers in order (every
+    // thread holds them), then the last workgroup adds them in block order
+    const RedOut& ro = a.ro;
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) red_put(ro, (int64_t)blockIdx.x * K + k, dpacc[k]);
+    }
+    if (wave != 0) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    unsigned old = 0;
+    if (lane == 0) old = __hip_atomic_fetch_add(ro.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    old = __shfl(old, 0, 64);
+    if (old != gridDim.x - 1) return;
+    const int nblk = (int)gridDim.x;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        double t = 0.0;
+        for (int b = lane; b < nblk; b += 64)
+            t += __hip_atomic_load(ro.part + (int64_t)b * K + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        t = wave_sum(t);
+        if (lane == 0) ro.out[k] = t;
+    }
+    if (lane == 0) __hip_atomic_store(ro.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+std::string op_kernel_name(int K, int64_t N) {
+    char b[96];
+    std::snprintf(b, sizeof b, "atax_kernel<%d, %d>", K, (int)std::max<int64_t>(1, (N + kOpRows - 1) / kOpRows));
+    return b;
+}
+
+template <int K, int S>
+static void launch_op(const Shard& s, const OpPlan& pl, const OpArgs& a, hipStream_t st, const Timing& tm,
+                      const int* gate) {
+    const size_t lds = ((size_t)K * (s.N + (s.N & 1)) + 2 * kOpWaves * K) * sizeof(double);
+    static bool attr = false;
+    if (!attr) {  // more than 64 KiB of dynamic LDS must be allowed explicitly
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&atax_kernel<K, S>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr = true;
+    }
+    hipExtLaunchKernelGGL((atax_kernel<K, S>), dim3(pl.grid), dim3(kOpThreads), lds, st, tm.start, tm.stop, 0, s.X,
+                          s.ld, s.N, s.M, s.mave, s.msig, a, gate);
+}
+
+template <int K>
+static bool launch_op_s(int S, const Shard& s, const OpPlan& pl, const OpArgs& a, hipStream_t st, const Timing& tm,
+                        const int* gate) {
+    switch (S) {
+        case 1: launch_op<K, 1>(s, pl, a, st, tm, gate); return true;
+        case 2: launch_op<K, 2>(s, pl, a, st, tm, gate); return true;
+        case 3: launch_op<K, 3>(s, pl, a, st, tm, gate); return true;
+        case 4: launch_op<K, 4>(s, pl, a, st, tm, gate); return true;
+        case 5: launch_op<K, 5>(s, pl, a, st, tm, gate); return true;
+        default: return false;
+    }
+}
+
+hipError_t atax(const Shard& s, const OpPlan& pl, int K, const OpArgs& a, hipStream_t st, const Timing& tm,
+                const int* gate) {
+    if (!op_supported(s.N, K) || pl.S != (int)std::max<int64_t>(1, (s.N + kOpRows - 1) / kOpRows)) return hipErrorInvalidValue;
+    if (s.M <= 0) return hipSuccess;
+    bool ok = false;
+    switch (K) {
+        case 1: ok = launch_op_s<1>(pl.S, s, pl, a, st, tm, gate); break;
+        case 2: ok = launch_op_s<2>(pl.S, s, pl, a, st, tm, gate); break;
+        default: break;
+    }
+    if (!ok) return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
+__global__ void op_reduce_kernel(int K, int64_t N, int64_t ld, int nslots, const double* __restrict__ part, Ptrs out,
+                                 double div, const int* __restrict__ gate) {
+    if (gate && !*gate) return;
+    const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (e >= (int64_t)K * N) return;
+    const int k = (int)(e / N);
+    const int64_t j = e - (int64_t)k * N;
+    double s = 0.0;
+    for (int t = 0; t < nslots; ++t) s += part[((int64_t)t * kMaxRhs + k) * ld + j];
+    if (div > 0) s /= div;
+    out.p[k][j] = s;
+}
+
+hipError_t op_reduce(const OpPlan& pl, int K, int64_t N, int64_t ld, const double* part, Ptrs out, double div,
+                     hipStream_t st, const int* gate) {
+    const int64_t n = (int64_t)K * N;
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(op_reduce_kernel, dim3((unsigned)cdiv(n, kBlock)), dim3(kBlock), 0, st, K, N, ld, (int)pl.nslots,
+                       part, out, div, gate);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
 // marker statistics (src/data.cpp:233-283): one wave per marker, two passes
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(kBlock) void stats_kernel(const double* __restrict__ X, int64_t ld, int64_t N, int64_t M,
@@ -1216,6 +1494,28 @@ __global__ __launch_bounds__(kBlock) void cg_update_kernel(int K, int64_t M, CgV
         }
     }
     // A mu alongside mu (replicated N-vectors, the same on every rank)
+    if (c.Q[0]) {  // one-pass operator: q (the step's A p) from A r, then A r -= A d * alpha
+        for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < c.nA; i += (int64_t)gridDim.x * kBlock) {
+            double ar[kMaxRhs], qo[kMaxRhs], ad[kMaxRhs], aw[kMaxRhs];
+#pragma unroll
+            for (int k = 0; k < kMaxRhs; ++k)
+                if (on[k]) {
+                    ar[k] = c.AR[k][i];
+                    qo[k] = fuse ? c.Q[k][i] : 0.0;
+                    ad[k] = c.AD[k][i];
+                    aw[k] = c.AW[k] ? c.AW[k][i] : 0.0;
+                }
+#pragma unroll
+            for (int k = 0; k < kMaxRhs; ++k)
+                if (on[k]) {
+                    double q = ar[k] / diag;  // A z = A r / diag
+                    if (fuse) q = q + beta[k] * qo[k];  // A p = A z + beta A p
+                    c.Q[k][i] = q;
+                    if (c.AW[k]) c.AW[k][i] = aw[k] + alpha[k] * q;
+                    c.AR[k][i] = ar[k] - ad[k] * alpha[k];
+                }
+        }
+    } else
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < c.nA; i += (int64_t)gridDim.x * kBlock) {
         double aw[kMaxRhs], as[kMaxRhs];
 #pragma unroll

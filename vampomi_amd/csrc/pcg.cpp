@@ -29,9 +29,37 @@ static T* field(vk::CgState* cs, size_t off) {
     return reinterpret_cast<T*>(reinterpret_cast<char*>(cs) + off);
 }
 
+// the host loop shared by both forms: queue step i+1, then wait for step i's
+// decision; a step queued after the last system stopped is dropped from the stats
+template <class Enqueue>
+static vampomi_status cg_loop(vampomi_ctx* c, int max_iter, Enqueue&& enqueue) {
+    unsigned long long prev = 0, cur = 0;
+    STCHK(enqueue(0, &prev));
+    for (int i = 1;; ++i) {
+        const size_t mark = c->pending.size();
+        const int64_t passes = c->stats.a_passes_exec;
+        if (i < max_iter) STCHK(enqueue(i, &cur));
+        c->stats.host_syncs++;
+        STCHK(wait_flag(c, prev));  // step i-1 decided
+        if (!c->h_cgm->any || i >= max_iter) {
+            if (i < max_iter) {  // step i was queued in vain: it did nothing
+                for (size_t q = mark; q < c->pending.size(); ++q) {
+                    c->ev_pool.push_back(c->pending[q].a);
+                    c->ev_pool.push_back(c->pending[q].b);
+                }
+                c->pending.resize(mark);
+                c->stats.a_passes_exec = passes;
+            }
+            break;
+        }
+        prev = cur;
+    }
+    return VAMPOMI_OK;
+}
+
 vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double tau, double gam2, int max_iter,
                        double tol, double* nscratch, int64_t* ref_passes, DotBatch* init, const double* extra_x,
-                       double* ex_out) {
+                       double* ex_out, bool onepass) {
     const int64_t M = c->M, N = c->N;
     const double diag = tau * (double)(N - 1) / (double)N + gam2;  // :676-677
     const int K = (int)sys.size();
@@ -104,6 +132,85 @@ vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double
     }
     const int* gate = field<int>(c->cgs, offsetof(vk::CgState, any));
     const double* beta = field<double>(c->cgs, offsetof(vk::CgState, beta));
+    if (onepass && vk::op_supported(N, K) && c->have_X) {
+        // ---- one pass over X per CG step (vk::atax) ----
+        // A r0 for every system (and A extra_x) by one A.x pass; then each step
+        // forms q = A p = A r/diag + beta*q_old on the fly, streams X once for
+        // d = tau*A^T q + gam2*p and A d, and cg_update carries A r -= alpha*A d
+        STCHK(op_prepare(c));
+        double* AR = c->op_nvec;
+        double* Q = c->op_nvec + (int64_t)vk::kMaxRhs * c->ld;
+        const double* AD = c->op_nvec + (int64_t)2 * vk::kMaxRhs * c->ld;
+        const double* px[vk::kMaxRhs];
+        for (int k = 0; k < K; ++k) px[k] = sys[k]->r;
+        if (extra_x) px[K] = extra_x;
+        STCHK(ax_dev(c, extra_x ? K + 1 : K, px, AR));
+        if (extra_x) HIPCHK(hipMemcpyAsync(ex_out, AR + (int64_t)K * c->ld, (size_t)N * 8, hipMemcpyDeviceToDevice, c->st));
+        vk::CgVecs cu{};
+        cu.tau = tau;
+        cu.gam2 = gam2;
+        cu.nA = N;
+        for (int k = 0; k < K; ++k) {
+            cu.mu[k] = sys[k]->mu;
+            cu.r[k] = sys[k]->r;
+            cu.z[k] = sys[k]->z;
+            cu.p[k] = sys[k]->p;
+            cu.d[k] = sys[k]->d;
+            cu.v[k] = sys[k]->v;
+            cu.W[k] = sys[k]->W;
+            cu.S[k] = sys[k]->W ? sys[k]->S : nullptr;
+            cu.AW[k] = sys[k]->AW;
+            cu.Q[k] = Q + (int64_t)k * c->ld;
+            cu.AR[k] = AR + (int64_t)k * c->ld;
+            cu.AD[k] = AD + (int64_t)k * c->ld;
+        }
+        bool rec = false;
+        for (int k = 0; k < K; ++k) rec = rec || sys[k]->W;
+        if (rec)
+            for (int k = 0; k < K; ++k)
+                if (!sys[k]->S) return fail(VAMPOMI_ERR_ARG, "pcg: W needs an S scratch vector for every system");
+        auto enqueue = [&](int i, unsigned long long* seq) -> vampomi_status {
+            const bool fuse = i > 0;
+            vk::OpArgs a{};
+            for (int k = 0; k < K; ++k) {
+                a.ar.p[k] = cu.AR[k];
+                a.qo.p[k] = cu.Q[k];
+                a.p.p[k] = sys[k]->p;
+                a.z.p[k] = sys[k]->z;
+                a.d.p[k] = sys[k]->d;
+                a.sraw.p[k] = rec ? sys[k]->S : nullptr;
+            }
+            a.beta = beta;
+            a.fuse = fuse ? 1 : 0;
+            a.diag = diag;
+            a.tau = tau;
+            a.gam2 = gam2;
+            STCHK(op_dev(c, K, a, gate));
+            const double* dp = c->use_comm ? AD + (int64_t)K * c->ld : c->scal + SL_DP;
+            const vk::RedOut ro{c->red_part, c->scal + SL_CG, c->ticket, nullptr, 0, gate};
+            *seq = ++c->sync_seq;
+            vk::CgDecide dc{};
+            if (!c->use_comm) {
+                dc.on = 1;
+                dc.it = i;
+                dc.mirror = c->d_cgm;
+                dc.flag = c->d_flag;
+                dc.seq = *seq;
+            }
+            HIPCHK(vk::cg_update(K, M, cu, diag, c->cgs, dp, nullptr, fuse ? 1 : 0, ro, dc, c->st));
+            if (c->use_comm) {
+                STCHK(allreduce_dev(c, c->scal + SL_CG, (size_t)(3 * K)));
+                HIPCHK(vk::cg_decide(c->cgs, c->scal + SL_CG, i, c->d_cgm, c->d_flag, *seq, c->st));
+            }
+            return VAMPOMI_OK;
+        };
+        STCHK(cg_loop(c, max_iter, enqueue));
+        for (int k = 0; k < K; ++k) {
+            sys[k]->iters = c->h_cgm->iters[k];
+            if (ref_passes) *ref_passes += 2 * (int64_t)sys[k]->iters;
+        }
+        return VAMPOMI_OK;
+    }
     const double* pp[vk::kMaxRhs];
     const double* zz[vk::kMaxRhs];
     double* dd[vk::kMaxRhs];
@@ -201,27 +308,7 @@ vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double
         }
         return VAMPOMI_OK;
     };
-    unsigned long long prev = 0, cur = 0;
-    STCHK(enqueue(0, &prev));
-    for (int i = 1;; ++i) {
-        const size_t mark = c->pending.size();
-        const int64_t passes = c->stats.a_passes_exec;
-        if (i < max_iter) STCHK(enqueue(i, &cur));
-        c->stats.host_syncs++;
-        STCHK(wait_flag(c, prev));  // step i-1 decided
-        if (!c->h_cgm->any || i >= max_iter) {
-            if (i < max_iter) {  // step i was queued in vain: it did nothing
-                for (size_t q = mark; q < c->pending.size(); ++q) {
-                    c->ev_pool.push_back(c->pending[q].a);
-                    c->ev_pool.push_back(c->pending[q].b);
-                }
-                c->pending.resize(mark);
-                c->stats.a_passes_exec = passes;
-            }
-            break;
-        }
-        prev = cur;
-    }
+    STCHK(cg_loop(c, max_iter, enqueue));
     for (int k = 0; k < K; ++k) {
         sys[k]->iters = c->h_cgm->iters[k];
         if (ref_passes) *ref_passes += 2 * (int64_t)sys[k]->iters;

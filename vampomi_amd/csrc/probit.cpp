@@ -153,7 +153,7 @@ vampomi_status probit_step(vampomi_ctx* c, VampRun& R) {
     HIPCHK(hipMemsetAsync(R.invQ, 0, Mb, c->st));
     if (R.fuse) {
         STCHK(pcg_run(c, {&sx, &so}, R.tau2, R.gam2, R.prm.CG_max_iter, R.prm.CG_err_tol, R.nsc, &R.passes_ref,
-                      nullptr));
+                      nullptr, nullptr, nullptr, R.onepass));
     } else {
         STCHK(pcg_run(c, {&sx}, R.tau2, R.gam2, R.prm.CG_max_iter, R.prm.CG_err_tol, R.nsc, &R.passes_ref, nullptr));
         STCHK(pcg_run(c, {&so}, R.tau2, R.gam2, R.prm.CG_max_iter, R.prm.CG_err_tol, R.nsc, &R.passes_ref, nullptr));

@@ -23,7 +23,8 @@ struct VampRun {
     bool write = false;
     bool fuse = true;  // batch_rhs >= 1: share passes + prefetch the next denoising step
     bool recur = false;  // batch_rhs >= 2: A^T A x2 and A^T A invQ by CG recurrences (no pass)
-    bool arec = false;   // batch_rhs == 3: also A x2 by a CG recurrence, z1 in the first CG pass
+    bool arec = false;   // batch_rhs >= 3: also A x2 by a CG recurrence, z1 in the first CG pass
+    bool onepass = false;  // batch_rhs >= 4: each CG step reads X once (vk::atax)
     int z1n_slot = 2;    // nb3 slot of the prefetched z1
     std::string out_dir, out_name, p_params, p_metrics, p_prior;
     int it = 0;

@@ -211,6 +211,7 @@ extern "C" vampomi_status vampomi_vamp_begin(vampomi_ctx* c, const vampomi_param
     R.fuse = p->batch_rhs != 0;
     R.recur = p->batch_rhs >= 2;
     R.arec = p->batch_rhs >= 3;
+    R.onepass = p->batch_rhs >= 4;
     R.out_dir = p->out_dir ? p->out_dir : "";
     R.out_name = p->out_name ? p->out_name : "";
     R.write = !R.out_dir.empty();
@@ -394,7 +395,7 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
     }
     if (R.fuse) {
         STCHK(pcg_run(c, {&sx, &so}, R.gamw, R.gam2, R.prm.CG_max_iter, R.prm.CG_err_tol, R.nsc, &R.passes_ref,
-                      arec ? nullptr : &e1, arec ? R.x1 : nullptr, arec ? R.z1buf : nullptr));
+                      arec ? nullptr : &e1, arec ? R.x1 : nullptr, arec ? R.z1buf : nullptr, R.onepass));
     } else {
         STCHK(pcg_run(c, {&sx}, R.gamw, R.gam2, R.prm.CG_max_iter, R.prm.CG_err_tol, R.nsc, &R.passes_ref, &e1));
         STCHK(pcg_run(c, {&so}, R.gamw, R.gam2, R.prm.CG_max_iter, R.prm.CG_err_tol, R.nsc, &R.passes_ref, nullptr));
