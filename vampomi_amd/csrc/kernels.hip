@@ -956,6 +956,11 @@ static bool launch_op_s(int S, const Shard& s, const OpPlan& pl, const OpArgs& a
         case 3: launch_op<K, 3>(s, pl, a, st, tm, gate); return true;
         case 4: launch_op<K, 4>(s, pl, a, st, tm, gate); return true;
         case 5: launch_op<K, 5>(s, pl, a, st, tm, gate); return true;
+        case 6: launch_op<K, 6>(s, pl, a, st, tm, gate); return true;
+        case 7: launch_op<K, 7>(s, pl, a, st, tm, gate); return true;
+        case 8: launch_op<K, 8>(s, pl, a, st, tm, gate); return true;
+        case 9: launch_op<K, 9>(s, pl, a, st, tm, gate); return true;
+        case 10: launch_op<K, 10>(s, pl, a, st, tm, gate); return true;
         default: return false;
     }
 }
