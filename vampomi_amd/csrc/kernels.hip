@@ -738,14 +738,14 @@ hipError_t atx(const Shard& s, int K, CPtrs u, Ptrs out, double scale, int mode,
 // K*N <= kOpLdsDoubles.  The column is read from HBM once for both products;
 // the workgroup's A d partial (K*N) goes to its slot, op_reduce sums the
 // slots in order.  Summation orders are fixed, results bitwise reproducible.
-static constexpr int kOpWaves = 8;
+static constexpr int kOpWaves = 8;               // 2 per SIMD: <= 256 VGPRs
 static constexpr int kOpThreads = 64 * kOpWaves;
 static constexpr int kOpRows = 128 * kOpWaves;   // rows per load step of the workgroup
 static constexpr int kOpMaxS = 10;               // rows per workgroup <= kOpRows*kOpMaxS = 10,240
-static constexpr int64_t kOpLdsDoubles = 20000;  // q in LDS: 160,000 B of the CU's 160 KiB
+static constexpr int64_t kOpLdsDoubles = 20480 - 2 - 2 * kOpWaves * 2;  // the CU's 160 KiB of LDS
 
 bool op_supported(int64_t N, int K) {
-    return K >= 1 && K <= 2 && N >= 1 && K * (N + (N & 1)) <= kOpLdsDoubles && (N + kOpRows - 1) / kOpRows <= kOpMaxS;
+    return K >= 1 && K <= 2 && N >= 1 && K * (N + 2) <= kOpLdsDoubles && (N + kOpRows - 1) / kOpRows <= kOpMaxS;
 }
 
 OpPlan op_plan(int64_t N, int64_t M, int cus) {
@@ -756,11 +756,11 @@ OpPlan op_plan(int64_t N, int64_t M, int cus) {
     return p;
 }
 
-// one column in registers: its X rows and the marker's scalars
+// one column in registers: its X rows and the marker's mean
 template <int K, int S>
 struct OpCol {
     v2d x[S];
-    double mu, sg, p[K], z[K];
+    double mu;
 };
 
 template <int K, int S>
@@ -769,9 +769,12 @@ __global__ __launch_bounds__(kOpThreads) void atax_kernel(const double* __restri
                                                           const double* __restrict__ msig, OpArgs a,
                                                           const int* __restrict__ gate) {
     if (gate && !*gate) return;
-    extern __shared__ double q_lds[];  // K x NL (rows of this thread only), then 2 x kOpWaves x K partials
-    const int64_t NL = N + (N & 1);    // even row stride: 16-byte aligned pairs
-    double* s_part = q_lds + (int64_t)K * NL;
+    // LDS: q (K x NL; each thread only ever touches its own rows), a zero
+    // pair, then 2 x kOpWaves x K dot partials
+    extern __shared__ double q_lds[];
+    const int NL = (int)N + 1 + ((int)N & 1);  // even stride; q[N] = 0 (the odd-N pad row)
+    const int zslot = K * NL;
+    double* s_part = q_lds + zslot + 2;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int64_t mb = (int64_t)blockIdx.x * M / gridDim.x, me = (int64_t)(blockIdx.x + 1) * M / gridDim.x;
     // row of this thread in step s: jb + kOpRows*s (recomputed, not kept in registers)
@@ -779,6 +782,12 @@ __global__ __launch_bounds__(kOpThreads) void atax_kernel(const double* __restri
     const int n32 = (int)N;
 #define OP_J(s) (jb + kOpRows * (s))
 #define OP_OK(s) (OP_J(s) < n32)
+    if (threadIdx.x == 0) {  // rows past N meet q = 0: the zero pair, and q[N] for odd N
+        q_lds[zslot] = 0.0;
+        q_lds[zslot + 1] = 0.0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) q_lds[k * NL + n32] = 0.0;
+    }
     v2d acc[K][S];
 #pragma unroll
     for (int s = 0; s < S; ++s) {
@@ -792,46 +801,51 @@ __global__ __launch_bounds__(kOpThreads) void atax_kernel(const double* __restri
                 if (jj < N) {
                     double q = a.ar.p[k][jj] / a.diag;              // A z = A r / diag
                     if (a.fuse) q = q + a.beta[k] * a.qo.p[k][jj];  // A p = A z + beta A p
-                    q_lds[(int64_t)k * NL + jj] = q;
+                    q_lds[k * NL + jj] = q;
                 }
             }
         }
     }
+    __syncthreads();  // the zero pair and q[N] (thread 0) are read by other threads
     double bk[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) bk[k] = a.fuse ? a.beta[k] : 0.0;
     double dpacc[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) dpacc[k] = 0.0;
-    OpCol<K, S> cb[2];
+    // columns in registers: three where they fit beside acc, else two
+    constexpr int NB = K * S <= 16 ? 3 : 2;
+    OpCol<K, S> cb[NB];
     auto load = [&](OpCol<K, S>& c, int64_t m) {
         const char* col = reinterpret_cast<const char*>(X + m * ld);
 #pragma unroll
         for (int s = 0; s < S; ++s)
-            c.x[s] = OP_OK(s) ? __builtin_nontemporal_load(reinterpret_cast<const v2d*>(col + (unsigned)(OP_J(s) * 8)))
-                              : v2d{0.0, 0.0};
+            if (OP_OK(s)) c.x[s] = __builtin_nontemporal_load(reinterpret_cast<const v2d*>(col + (unsigned)(OP_J(s) * 8)));
         c.mu = mave[m];
-        c.sg = msig[m];
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            c.p[k] = a.p.p[k][m];
-            c.z[k] = a.fuse ? a.z.p[k][m] : 0.0;
-        }
     };
     // dot partials of column c -> s_part[par][wave][k]
     auto dots = [&](const OpCol<K, S>& c, int par) {
         double v[K];
 #pragma unroll
-        for (int k = 0; k < K; ++k) {
-            double t = 0.0;
+        for (int k = 0; k < K; ++k) v[k] = 0.0;
 #pragma unroll
-            for (int s = 0; s < S; ++s) {
-                if (!OP_OK(s)) continue;
-                const v2d q = *reinterpret_cast<const v2d*>(q_lds + (int64_t)k * NL + OP_J(s));  // .y unused at j+1 == N
-                t += (c.x[s].x - c.mu) * q.x;
-                if (OP_J(s) + 1 < n32) t += (c.x[s].y - c.mu) * q.y;
+        for (int s = 0; s < S; ++s) {
+            if (!OP_OK(s)) continue;
+            const double dx = c.x[s].x - c.mu, dy = c.x[s].y - c.mu;
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const v2d q = *reinterpret_cast<const v2d*>(q_lds + k * NL + OP_J(s));  // q[N] = 0 for odd N
+                v[k] += dx * q.x;
+                v[k] += dy * q.y;
             }
-            v[k] = wave_sum(t);
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {  // the K butterflies interleaved: their exchanges fly together
+            double t[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) t[k] = __shfl_xor(v[k], o, 64);
+#pragma unroll
+            for (int k = 0; k < K; ++k) v[k] += t[k];
         }
         if (lane == 0) {
 #pragma unroll
@@ -840,16 +854,17 @@ __global__ __launch_bounds__(kOpThreads) void atax_kernel(const double* __restri
     };
     // the column's d (all waves, identically) and acc += (x - mave)*msig*d
     auto finish = [&](const OpCol<K, S>& c, int64_t m, int par) {
+        const double sg = msig[m];
         double cc[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             double dot = 0.0;
 #pragma unroll
             for (int w = 0; w < kOpWaves; ++w) dot += s_part[(par * kOpWaves + w) * K + k];
-            double t = c.sg * dot;  // sigma_inv * dpa
-            t *= a.scale;           // ATx[mloc] *= 1/sqrt(N)
-            double pk = c.p[k];
-            if (a.fuse) pk = c.z[k] + bk[k] * pk;  // p = z + beta p
+            double t = sg * dot;  // sigma_inv * dpa
+            t *= a.scale;         // ATx[mloc] *= 1/sqrt(N)
+            double pk = a.p.p[k][m];
+            if (a.fuse) pk = a.z.p[k][m] + bk[k] * pk;  // p = z + beta p
             double val = t * a.tau;  // res[i] *= tau
             val += a.gam2 * pk;      // res[i] += gam2 * v[i]
             if (threadIdx.x == 0) {
@@ -857,35 +872,53 @@ __global__ __launch_bounds__(kOpThreads) void atax_kernel(const double* __restri
                 a.d.p[k][m] = val;
             }
             dpacc[k] += val * pk;
-            cc[k] = c.sg * val;  // Ax: (x - mave) * (msig * x_i)
+            cc[k] = sg * val;  // Ax: (x - mave) * (msig * x_i)
         }
 #pragma unroll
-        for (int k = 0; k < K; ++k)
+        for (int s = 0; s < S; ++s) {
+            if (!OP_OK(s)) continue;
+            const double dx = c.x[s].x - c.mu, dy = c.x[s].y - c.mu;
 #pragma unroll
-            for (int s = 0; s < S; ++s) {
-                acc[k][s].x += (c.x[s].x - c.mu) * cc[k];
-                acc[k][s].y += (c.x[s].y - c.mu) * cc[k];
+            for (int k = 0; k < K; ++k) {
+                acc[k][s].x += dx * cc[k];
+                acc[k][s].y += dy * cc[k];
             }
+        }
     };
-    // two columns in registers: m is finished while m+1 is dotted and m+2 loads
-    int64_t m = mb;
-    if (m < me) {
-        load(cb[0], m);
-        if (m + 1 < me) load(cb[1], m + 1);
+    // NB columns in registers: m is finished while m+1 .. m+NB-1 load; the
+    // buffer m frees takes m+NB.  Dot partials alternate between two LDS slots.
+    auto step = [&](OpCol<K, S>& cur, OpCol<K, S>& nxt, int64_t m, int par) {
+        finish(cur, m, par);
+        if (m + NB < me) load(cur, m + NB);
+        if (m + 1 < me) {
+            dots(nxt, par ^ 1);
+            __syncthreads();
+        }
+    };
+    if (mb < me) {
+#pragma unroll
+        for (int b = 0; b < NB; ++b)
+            if (mb + b < me) load(cb[b], mb + b);
         dots(cb[0], 0);
         __syncthreads();
-        for (; m < me; m += 2) {
-            finish(cb[0], m, 0);
-            if (m + 2 < me) load(cb[0], m + 2);
-            if (m + 1 < me) {
-                dots(cb[1], 1);
-                __syncthreads();
-                finish(cb[1], m + 1, 1);
-                if (m + 3 < me) load(cb[1], m + 3);
-            }
-            if (m + 2 < me) {
-                dots(cb[0], 0);
-                __syncthreads();
+        int par = 0;
+        for (int64_t m = mb; m < me; m += NB) {
+            step(cb[0], cb[1], m, par);
+            par ^= 1;
+            if constexpr (NB == 2) {
+                if (m + 1 < me) {
+                    step(cb[1], cb[0], m + 1, par);
+                    par ^= 1;
+                }
+            } else {
+                if (m + 1 < me) {
+                    step(cb[1], cb[2 % NB], m + 1, par);
+                    par ^= 1;
+                }
+                if (m + 2 < me) {
+                    step(cb[2 % NB], cb[0], m + 2, par);
+                    par ^= 1;
+                }
             }
         }
     }
@@ -936,7 +969,7 @@ std::string op_kernel_name(int K, int64_t N) {
 template <int K, int S>
 static void launch_op(const Shard& s, const OpPlan& pl, const OpArgs& a, hipStream_t st, const Timing& tm,
                       const int* gate) {
-    const size_t lds = ((size_t)K * (s.N + (s.N & 1)) + 2 * kOpWaves * K) * sizeof(double);
+    const size_t lds = ((size_t)K * (s.N + 1 + (s.N & 1)) + 2 + 2 * kOpWaves * K) * sizeof(double);
     static bool attr = false;
     if (!attr) {  // more than 64 KiB of dynamic LDS must be allowed explicitly
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&atax_kernel<K, S>),
