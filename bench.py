@@ -10,8 +10,8 @@ iterations run; W are untimed.
 
 Workloads (synthetic, generated on the device):
   c2 (default)  N=10,000 x Mt=50,000 i.i.d. Gaussian design (BASELINE configs[1]);
-                with --gpus n > 1: weak scaling at constant per-GPU bytes and
-                constant aspect ratio: N = 10,000*sqrt(n), Mt = 50,000*sqrt(n).
+                with --gpus n > 1: weak scaling over markers (the reference's
+                own sharding): N = 10,000, Mt = 50,000*n, 4 GB per GPU.
   c3            per-GPU shard of configs[2] (N=100,000 x 62,500 markers per GPU,
                 methylation-like); at n=8 it is N=100,000 x Mt=500,000.
   c4            probit model (configs[3], src/vamp_probit.cpp): N=50,000 x 50,000
@@ -213,7 +213,7 @@ def main():
     ap.add_argument("--no-timing", action="store_true", help="skip the HIP-event kernel timing")
     ap.add_argument("--timing-period", type=int, default=4,
                     help="time one A/A^T launch in this many of each (kernel, K) with HIP events")
-    ap.add_argument("--batch-rhs", type=int, default=3)
+    ap.add_argument("--batch-rhs", type=int, default=4)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -278,14 +278,16 @@ def main():
     it_s = args.steps / el
     # dominant kernel: the (class, batch width) with the most device time
     cands = []
-    for which, arr in ((0, st.ax_k), (1, st.atx_k)):
+    for which, arr in ((0, st.ax_k), (1, st.atx_k), (3, st.op_k)):
         for k in range(4):
             if arr[k].launches:
                 cands.append((arr[k].ms_total, which, k + 1, arr[k]))
     roof = None
     if cands:
         ms, which, K, ks = max(cands, key=lambda c: c[0])
-        kname = va.kernel_name(which, K, 1)  # A^T.u in the CG carries the lmmse_mult epilogue (mode 1)
+        # A^T.u in the CG carries the lmmse_mult epilogue (mode 1); the one-pass
+        # operator's instantiation depends on N (passed as mode)
+        kname = va.kernel_name(which, K, N if which == 3 else 1)
         avg_ms = ks.ms_total / ks.launches
         bytes_per = ks.bytes_total / ks.launches
         achieved = bytes_per / (avg_ms * 1e-3) / 1e9
@@ -300,8 +302,8 @@ def main():
                 "timed_launches": int(ks.launches) // max(1, args.timing_period),
                 "timing": f"HIP events in the dispatch packets of 1 in {max(1, args.timing_period)} launches "
                           "of each (kernel, K) over the timed region"}
-    all_ms = st.ax.ms_total + st.atx.ms_total
-    all_bytes = st.ax.bytes_total + st.atx.bytes_total
+    all_ms = st.ax.ms_total + st.atx.ms_total + st.op.ms_total
+    all_bytes = st.ax.bytes_total + st.atx.bytes_total + st.op.bytes_total
     line = {
         "metric": "VAMP iterations/s (+ achieved HBM GB/s of the A/A^T kernels)",
         "value": round(n * it_s, 4),

@@ -69,7 +69,7 @@ def test_params_default_is_the_reference_cli_default():
     assert (p.EM_max_iter, p.EM_err_thr, p.rho, p.learn_vars, p.learn_prior_delay) == (1, 1e-2, 0.5, 1, 1)
     assert (p.stop_criteria_thr, p.merge_vars_thr, p.L) == (0.01, 0.5, 10)
     assert list(p.vars[:10]) == [0, 1e-06, 6e-06, 3e-05, 2e-04, 1e-03, 6e-03, 3e-02, 2e-01, 1e+00]
-    assert p.probs[0] == 0.99 and p.probs[9] == 3.90625e-05 and p.batch_rhs == 3
+    assert p.probs[0] == 0.99 and p.probs[9] == 3.90625e-05 and p.batch_rhs == 4
     q = _lib.Params()
     va.load().vampomi_params_default(C.byref(q))
     assert q.model == b"linear" and q.max_iter == 50

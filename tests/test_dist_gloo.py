@@ -86,6 +86,6 @@ def test_bench_weak_scaling_workloads_keep_per_gpu_bytes():
         w = workload("c2", n)
         per_gpu = w["N"] * w["Mt"] / n
         assert abs(per_gpu / (10000 * 50000) - 1) < 1e-3
-        assert abs(w["Mt"] / w["N"] - 5) < 1e-3
+        assert w["N"] == 10000  # markers sharded, as the reference's ranks shard them
     w8 = workload("c3", 8)
     assert (w8["N"], w8["Mt"]) == (100000, 500000)

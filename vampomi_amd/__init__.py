@@ -295,7 +295,7 @@ class VampOptions:
     out_dir: str = ""
     out_name: str = ""
     verbosity: int = 0
-    batch_rhs: int = 3
+    batch_rhs: int = 4
     model: str = "linear"
 
     def to_struct(self) -> Params:

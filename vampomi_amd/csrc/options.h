@@ -24,7 +24,7 @@ struct Options {
     std::vector<int> test_iter_range{1, 50};
     // engine extensions (not in the reference): Bernoulli seed, RHS batching
     unsigned long long seed = 0x5EED5EEDULL;
-    int batch_rhs = 3;
+    int batch_rhs = 4;
 };
 
 // Parses argv exactly like Options::read_command_line_options + check_options:

@@ -551,7 +551,7 @@ extern "C" void vampomi_params_default(vampomi_params* p) {
         p->probs[j] = q[j];
     }
     p->seed = 0x5EED5EEDULL;
-    p->batch_rhs = 3;
+    p->batch_rhs = 4;
     p->model = "linear";
 }
 
