@@ -1012,25 +1012,40 @@ hipError_t atax(const Shard& s, const OpPlan& pl, int K, const OpArgs& a, hipStr
     return hipGetLastError();
 }
 
-__global__ void op_reduce_kernel(int K, int64_t N, int64_t ld, int nslots, const double* __restrict__ part, Ptrs out,
-                                 double div, const int* __restrict__ gate) {
+// 64 samples per workgroup; its 8 waves sum contiguous eighths of the slots
+// (in slot order) and wave 0 adds the eighths in order: a fixed order, and
+// 64x more loads in flight than one thread per sample
+static constexpr int kOpRedWaves = 8;
+__global__ __launch_bounds__(64 * kOpRedWaves) void op_reduce_kernel(int K, int64_t N, int64_t ld, int nslots,
+                                                                     const double* __restrict__ part, Ptrs out,
+                                                                     double div, const int* __restrict__ gate) {
     if (gate && !*gate) return;
-    const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (e >= (int64_t)K * N) return;
-    const int k = (int)(e / N);
-    const int64_t j = e - (int64_t)k * N;
+    __shared__ double lds[kOpRedWaves][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t e = (int64_t)blockIdx.x * 64 + lane;
+    const bool ok = e < (int64_t)K * N;
+    const int k = ok ? (int)(e / N) : 0;
+    const int64_t j = ok ? e - (int64_t)k * N : 0;
+    const int t0 = w * nslots / kOpRedWaves, t1 = (w + 1) * nslots / kOpRedWaves;
     double s = 0.0;
-    for (int t = 0; t < nslots; ++t) s += part[((int64_t)t * kMaxRhs + k) * ld + j];
-    if (div > 0) s /= div;
-    out.p[k][j] = s;
+    if (ok)
+        for (int t = t0; t < t1; ++t) s += part[((int64_t)t * kMaxRhs + k) * ld + j];
+    lds[w][lane] = s;
+    __syncthreads();
+    if (w != 0 || !ok) return;
+    double r = lds[0][lane];
+#pragma unroll
+    for (int q = 1; q < kOpRedWaves; ++q) r += lds[q][lane];
+    if (div > 0) r /= div;
+    out.p[k][j] = r;
 }
 
 hipError_t op_reduce(const OpPlan& pl, int K, int64_t N, int64_t ld, const double* part, Ptrs out, double div,
                      hipStream_t st, const int* gate) {
     const int64_t n = (int64_t)K * N;
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(op_reduce_kernel, dim3((unsigned)cdiv(n, kBlock)), dim3(kBlock), 0, st, K, N, ld, (int)pl.nslots,
-                       part, out, div, gate);
+    hipLaunchKernelGGL(op_reduce_kernel, dim3((unsigned)cdiv(n, 64)), dim3(64 * kOpRedWaves), 0, st, K, N, ld,
+                       (int)pl.nslots, part, out, div, gate);
     return hipGetLastError();
 }
 
