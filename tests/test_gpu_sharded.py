@@ -10,6 +10,7 @@ must match the single-rank GPU run (linear) or the oracle's bars (probit,
 association tests)."""
 import os
 import threading
+import time
 
 import numpy as np
 import pytest
@@ -23,7 +24,7 @@ va = pytest.importorskip("vampomi_amd")
 from oracle import pyoracle as O  # noqa: E402  (checker)
 
 
-def run_ranks(monkeypatch, P, N, Mt, fn, timeout=600):
+def run_ranks(monkeypatch, P, N, Mt, fn, timeout=100):
     """fn(rank, data) on P threads, one context each; returns the results by rank."""
     monkeypatch.setenv("VAMPOMI_COMM", "loopback")
     cid = os.urandom(va.UNIQUE_ID_BYTES)
@@ -38,8 +39,10 @@ def run_ranks(monkeypatch, P, N, Mt, fn, timeout=600):
 
     th = [threading.Thread(target=work, args=(r,), daemon=True) for r in range(P)]
     [t.start() for t in th]
-    [t.join(timeout) for t in th]
-    assert not any(t.is_alive() for t in th), "a rank is stuck in a collective"
+    deadline = time.monotonic() + timeout
+    [t.join(max(0.0, deadline - time.monotonic())) for t in th]
+    stuck = [r for r, t in enumerate(th) if t.is_alive()]
+    assert not stuck, f"ranks {stuck} stuck in a collective; errors of the others: {errs}"
     assert not errs, errs
     return res
 

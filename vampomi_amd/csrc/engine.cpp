@@ -201,8 +201,11 @@ static vampomi_status loopback_allreduce(vampomi_ctx* c, double* buf, size_t n) 
             lb.arrived = 0;
             ++lb.gen;
             lb.cv.notify_all();
-        } else {
-            lb.cv.wait(g, [&] { return lb.gen != my_gen; });
+        } else if (!lb.cv.wait_for(g, std::chrono::seconds(60), [&] { return lb.gen != my_gen; })) {
+            // a rank that failed (or took another branch) never arrives: end
+            // this rank with an error instead of waiting forever
+            --lb.arrived;
+            return fail(VAMPOMI_ERR_STATE, "loopback all-reduce: not every rank arrived within 60 s");
         }
         mine = lb.out;  // lb.out is only rewritten once every rank has arrived again
     }
