@@ -1,110 +1,182 @@
 """bench.py — VAMP iterations/s + HBM GB/s on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c3big|c4|c4full|c5] [--no-cpu-baseline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config auto|c2|c3full|c3|c3big|c4|c4full|c5]
+                    [--no-cpu-baseline]
 
 A "step" is one VAMP iteration (src/vamp.cpp:148-428) of the linear model
-(or src/vamp_probit.cpp:68-463 of the probit model for c4)
-over the whole synthetic problem, with every vector and the fp64 design
-matrix already resident in HBM.  --stop-criteria-thr is 0, so exactly W+K
-iterations run; W are untimed.
+(or src/vamp_probit.cpp:68-463 of the probit model for c4) over the whole
+synthetic problem, with every vector and the fp64 design matrix already
+resident in HBM.  --stop-criteria-thr is 0, so exactly W+K iterations run; W
+are untimed.
 
-Workloads (synthetic, generated on the device, see DESIGN.md §Measurement):
-  c2 (default)  N=10,000 x Mt=50,000 i.i.d. Gaussian design (BASELINE configs[1]);
-                with --gpus n > 1: weak scaling over markers (the reference's
-                own sharding): N = 10,000, Mt = 50,000*n, 4 GB per GPU.
-  c3            per-GPU shard of configs[2] (N=100,000 x 62,500 markers per GPU,
-                methylation-like); at n=8 it is N=100,000 x Mt=500,000.
-  c4            probit model (configs[3], src/vamp_probit.cpp): N=50,000 x 50,000
-                markers per GPU, binary phenotype; at n=4 it is N=50,000 x Mt=200,000.
-  c4full        configs[3] whole on any n (80 GB: fits one MI355X).
-  c5            LOO association test (configs[4]): N=100,000 x 62,500 methylation-
-                like markers per GPU; at n=8 it is N=100,000 x Mt=500,000.  A step
-                is one whole test (A.x of the estimate, then the per-marker pass
-                and the p-values); value = markers tested per second.
+Workloads (synthetic, generated on the device, see DESIGN.md §5):
+  auto (default)  n = 1: c2; n > 1: c3full (the metric's own problem).
+  c2      N=10,000 x Mt=50,000 i.i.d. Gaussian design (BASELINE configs[1]);
+          with n > 1: weak scaling over markers (the reference's own
+          sharding): N = 10,000, Mt = 50,000*n, 4 GB per GPU ("c2-weak").
+  c3full  N=100,000 x Mt=500,000 methylation-like (configs[2], 400 GB) fixed,
+          markers sharded over n >= 2 GPUs (strong scaling; 200 GB per GPU at
+          n = 2, 50 GB at n = 8); value = iterations/s of the whole problem.
+  c3      per-GPU shard of configs[2] (N=100,000 x 62,500 markers per GPU);
+          weak; at n=8 it is exactly configs[2].
+  c3big   N=100,000 x 300,000 markers per GPU (240 GB resident on one GPU).
+  c4      probit model (configs[3]): N=50,000 x 50,000 markers per GPU; n=4
+          is exactly configs[3].  c4full: configs[3] whole (80 GB) on any n.
+  c5      LOO association test (configs[4]): N=100,000 x 62,500 markers per
+          GPU; n=8 is exactly configs[4]; value = markers tested per second.
 
-value = n_gpus * iterations/s ("shard-iterations/s": VAMP iterations over one
-GPU's shard; at n=1 exactly iterations/s of the workload).  Multi-GPU: one
-process per GPU (torchrun), RCCL communicator inside libvampomi for the data
-path, torch.distributed (gloo) only for the id broadcast, barriers and the
-max-over-ranks time.
+Multi-GPU: one process per GPU.  Under torchrun (WORLD_SIZE set) this process
+is one rank; with `--gpus N` and no WORLD_SIZE it starts N rank processes
+itself (127.0.0.1 rendezvous) before touching the GPU and exits with their
+status; rank 0 prints the line.  The data path uses libvampomi's RCCL
+communicator; torch.distributed (gloo) only broadcasts its id, runs the
+barriers and takes the max-over-ranks time.
 """
 from __future__ import annotations
 
 import argparse
 import json
-import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-import numpy as np  # noqa: E402
-import torch  # noqa: E402  (imported before libvampomi: one HIP runtime)
-import torch.distributed as dist  # noqa: E402
-
-import vampomi_amd as va  # noqa: E402
-from vampomi_amd.workloads import workload  # noqa: E402
-
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 PMC_FILE = os.path.join(ROOT, "profiles", "r01_pmc_traffic_{}.json")
+PMC_FILES = [os.path.join(ROOT, "profiles", f) for f in ("r02_pmc_traffic_{}.json", "r01_pmc_traffic_{}.json")]
 
 
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=48)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="auto", choices=["auto", "c2", "c3full", "c3", "c3big", "c4", "c4full", "c5"])
+    ap.add_argument("--seed", type=int, default=20250711)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=45.0, help="seconds of host time for the CPU baseline")
+    ap.add_argument("--no-timing", action="store_true", help="skip the HIP-event kernel timing")
+    ap.add_argument("--timing-period", type=int, default=4,
+                    help="time one A/A^T launch in this many of each (kernel, K) with HIP events")
+    ap.add_argument("--batch-rhs", type=int, default=4)
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher / rendezvous / max-over-ranks path only: no GPU work (CPU tests)")
+    return ap.parse_args(argv)
+
+
+# ---------------------------------------------------------------------------
+# launcher: `python bench.py --gpus N` outside torchrun
+# ---------------------------------------------------------------------------
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int, argv) -> int:
+    """Start n rank processes of this script (RANK / LOCAL_RANK / WORLD_SIZE /
+    MASTER_* set; one GPU each).  Runs before this process imports torch or
+    touches the GPU.  Rank 0 prints the JSON line on the shared stdout.  If a
+    rank fails, the others are stopped; returns the first failing rank's code."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), VAMPOMI_RUN_ID=f"bench-{os.getpid()}-{port}")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in live:  # a rank failed: do not leave the others waiting in a collective
+                    q.kill()
+        time.sleep(0.05)
+    return rc
+
+
+# ---------------------------------------------------------------------------
+# measurement helpers
+# ---------------------------------------------------------------------------
 def pmc_traffic(kernel: str, workload: str):
     """HBM bytes per launch of `kernel` on `workload` from the committed
     rocprofv3 --pmc summary (tools/pmc.sh: FETCH_SIZE x2 gfx950 correction +
-    WRITE_SIZE); None when that workload was not profiled."""
-    try:
-        import json as _j
+    WRITE_SIZE), newest round first; (bytes, file) or (None, None)."""
+    for pat in PMC_FILES:
+        f = pat.format(workload)
+        try:
+            for name, d in json.load(open(f)).items():
+                if kernel in name:
+                    return d.get("traffic_bytes_per_launch"), os.path.relpath(f, ROOT)
+        except Exception:
+            continue
+    return None, None
 
-        for name, d in _j.load(open(PMC_FILE.format(workload))).items():
-            if kernel in name:
-                return d.get("traffic_bytes_per_launch")
-    except Exception:
-        return None
-    return None
+
+def roofline(ks, kname: str, workload: str, period: int) -> dict:
+    """The dominant kernel's achieved GB/s: algorithmic bytes per launch (exact
+    count) over its average launch time (HIP events recorded in
+    the dispatch packets of the sampled launches, on the stream they run on)."""
+    avg_ms = ks.ms_timed / ks.timed
+    bytes_per = ks.bytes_total / ks.launches
+    achieved = bytes_per / (avg_ms * 1e-3) / 1e9
+    traffic, tfile = pmc_traffic(kname, workload)
+    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": int(traffic) if traffic else None,
+            "traffic_unit": f"HBM bytes per launch (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, {tfile})"
+            if tfile else None,
+            "algorithmic_bytes_per_launch": int(bytes_per), "kernel": kname,
+            "avg_launch_us": round(avg_ms * 1e3, 2), "launches": int(ks.launches), "timed_launches": int(ks.timed),
+            "timing": f"HIP events in the dispatch packets of 1 in {max(1, period)} launches of each (kernel, K) "
+                      "over the timed region; launch counts exact"}
 
 
-def cpu_baseline(d: "va.Data", w: dict, beta: np.ndarray, seed: int, budget_s: float = 20.0) -> dict:
-    """The CPU oracle (C restatement, OpenMP) on a bounded sample of the same workload."""
+def cpu_baseline(d, w: dict, beta, seed: int, warmup: int, steps: int, gpu_ref_passes: float,
+                 budget_s: float) -> dict:
+    """The CPU oracle (C restatement, OpenMP) on the same workload.  Where
+    W + k iterations fit the budget, it times the GPU's own window, iterations
+    W+1..W+k (k <= K); otherwise it times iterations 1-2 per
+    reference-equivalent A-pass and projects the GPU window's pass count."""
+    import numpy as np  # noqa: F401
     from oracle import pyoracle as O
 
     threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    N, Mt = w["N"], w["Mt"]
+    N, Mt, model = w["N"], w["Mt"], w.get("model", "linear")
     t0 = time.perf_counter()
     X = O.generate_markers(seed, w["kind"], N, 0, Mt)  # bit-identical to the device shard
     tgen = time.perf_counter() - t0
     y = d.get_phen()
-    # two iterations first to size the sample (iteration 1 of the probit model
-    # is a single CG step, unrepresentative alone), then a fresh run of k
-    t0 = time.perf_counter()
-    model = w.get("model", "linear")
-    r1 = O.vamp_infere(X, y, Mt, true_signal=beta, max_iter=2, stop_criteria_thr=0.0, keep_hist=False, model=model)
-    t1 = (time.perf_counter() - t0) / 2
-    k = max(2, min(10, int(budget_s / max(t1, 1e-3))))
-    if k > 2:
-        t0 = time.perf_counter()
-        r = O.vamp_infere(X, y, Mt, true_signal=beta, max_iter=k, stop_criteria_thr=0.0, keep_hist=False,
+    probe = O.vamp_infere(X, y, Mt, true_signal=beta, max_iter=2, stop_criteria_thr=0.0, keep_hist=False, model=model)
+    t_it = probe["it_end_s"][-1] / 2
+    k = max(0, min(steps, int((budget_s - warmup * t_it) / max(t_it, 1e-3))))
+    base = {"unit": "VAMP iterations/s", "cores": threads, "kind": "port"}
+    if k >= 2:
+        r = O.vamp_infere(X, y, Mt, true_signal=beta, max_iter=warmup + k, stop_criteria_thr=0.0, keep_hist=False,
                           model=model)
-        tk = time.perf_counter() - t0
-    else:
-        r, tk = r1, 2 * t1
-    passes = int(r["a_passes"])
-    return {
-        "value": k / tk,
-        "unit": "VAMP iterations/s",
-        "cores": threads,
-        "kind": "port",
-        "sample": f"iterations 1-{k} of {w['workload']} (N={N}, Mt={Mt}) on {threads} OpenMP threads; "
-                  f"{passes} A/A^T passes = {passes * 8.0 * N * Mt / tk / 1e9:.1f} GB/s effective; "
-                  f"data generation ({tgen:.1f} s) not timed",
-        "cg_iters": [int(a) for a in r["cg_iters"]],
-        "ons_iters": [int(a) for a in r["ons_iters"]],
-    }
+        end = r["it_end_s"]
+        win = end[warmup + k - 1] - (end[warmup - 1] if warmup > 0 else 0.0)
+        return dict(base, value=k / win,
+                    sample=f"iterations {warmup + 1}-{warmup + k} of {w['workload']} (N={N}, Mt={Mt}), the GPU "
+                           f"window's first {k}, on {threads} OpenMP threads; data generation ({tgen:.1f} s) and "
+                           f"iterations 1-{warmup} not timed",
+                    cg_iters=[int(a) for a in r["cg_iters"][warmup:]], ons_iters=[int(a) for a in r["ons_iters"][warmup:]])
+    per_pass = probe["it_end_s"][-1] / max(int(probe["a_passes"]), 1)
+    return dict(base, value=1.0 / (per_pass * gpu_ref_passes), projected=True,
+                sample=f"iterations 1-2 of {w['workload']} (N={N}, Mt={Mt}) on {threads} OpenMP threads: "
+                       f"{per_pass * 1e3:.1f} ms per reference-equivalent A-pass, times the GPU window's "
+                       f"{gpu_ref_passes:.2f} passes per iteration (W + k iterations exceed the {budget_s:.0f} s budget)")
 
 
-def cpu_baseline_assoc(d: "va.Data", w: dict, est: np.ndarray, seed: int) -> dict:
+def cpu_baseline_assoc(d, w: dict, est, seed: int) -> dict:
     """The oracle's LOO test (OpenMP) on the first Ms markers of the same workload."""
     from oracle import pyoracle as O
 
@@ -121,16 +193,80 @@ def cpu_baseline_assoc(d: "va.Data", w: dict, est: np.ndarray, seed: int) -> dic
                       f"{threads} OpenMP threads, {el:.1f} s"}
 
 
-def bench_assoc(args, d, w, world, rank, t_start):
+# ---------------------------------------------------------------------------
+# the runs
+# ---------------------------------------------------------------------------
+class Ranks:
+    """torch.distributed (gloo) for the id broadcast, barriers and max-over-ranks time."""
+
+    def __init__(self):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        import torch.distributed as dist
+
+        self.dist = dist
+        if self.world > 1:
+            dist.init_process_group("gloo")
+
+    def max(self, v: float) -> float:
+        if self.world == 1:
+            return v
+        import torch
+
+        t = torch.tensor([v], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum(self, v: float) -> float:
+        if self.world == 1:
+            return v
+        import torch
+
+        t = torch.tensor([v], dtype=torch.float64)
+        self.dist.all_reduce(t)
+        return float(t.item())
+
+    def barrier(self):
+        if self.world > 1:
+            self.dist.barrier()
+
+    def close(self):
+        if self.world > 1:
+            self.dist.destroy_process_group()
+
+
+def dry_run(args, R: Ranks):
+    """The launcher, rendezvous, barrier and max-over-ranks path without a GPU."""
+    R.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        time.sleep(0.001)
+    R.barrier()
+    el = R.max(time.perf_counter() - t0)
+    seen = int(R.sum(1.0))
+    if R.rank == 0:
+        print(json.dumps({"metric": "dry run", "value": 0.0, "unit": "none", "n_gpus": R.world, "steps": args.steps,
+                          "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3),
+                          "ranks_seen": seen, "dry_run": True}), flush=True)
+    R.close()
+
+
+def bench_assoc(args, d, w, R: Ranks, t_start):
     """--config c5: the LOO association test (src/main_meth.cpp:245-264) on
     device-resident inputs; a step is one whole test."""
     import ctypes as C
+
+    import numpy as np
+    import torch
+
+    import vampomi_amd as va
 
     N, Mt = w["N"], w["Mt"]
     beta = d.simulate_phen(args.seed + 1, lam=0.1, h2=0.5)
     t_setup = time.perf_counter() - t_start
     est = beta * 0.9 / np.sqrt(N)  # an estimate file's values (x1_hat / sqrt(N))
-    dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+    dev = torch.device("cuda", R.local)
     e_t = torch.from_numpy(est).to(dev)
     p_t = torch.zeros(max(d.M, 1), dtype=torch.float64, device=dev)
     lib = va.load()
@@ -147,97 +283,77 @@ def bench_assoc(args, d, w, world, rank, t_start):
     def barrier():
         d.sync()
         torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
+        R.barrier()
 
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     barrier()
-    el = time.perf_counter() - t0
+    el = R.max(time.perf_counter() - t0)
     st = d.stats()
-    if world > 1:
-        t = torch.tensor([el], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
     roof = None
-    if st.loo.launches:
-        ks = st.loo
-        kname = va.kernel_name(2, 1, 0)
-        avg_ms = ks.ms_total / ks.launches
-        bytes_per = ks.bytes_total / ks.launches
-        achieved = bytes_per / (avg_ms * 1e-3) / 1e9
-        traffic = pmc_traffic(kname, w["workload"])
-        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": int(traffic) if traffic else None,
-                "traffic_unit": "HBM bytes per launch (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, "
-                                f"profiles/{os.path.basename(PMC_FILE.format(w['workload']))})",
-                "algorithmic_bytes_per_launch": int(bytes_per), "kernel": kname,
-                "avg_launch_us": round(avg_ms * 1e3, 2), "launches": int(ks.launches),
-                "ax_avg_launch_us": round(st.ax.ms_total / max(st.ax.launches, 1) * 1e3, 2)}
+    if st.loo.timed:
+        roof = roofline(st.loo, d.kernel_name(2, 1, 0), w["workload"], args.timing_period)
+        roof["ax_avg_launch_us"] = round(st.ax.ms_timed / max(st.ax.timed, 1) * 1e3, 2)
     line = {
         "metric": "LOO association test: markers tested/s (+ achieved HBM GB/s of the per-marker pass)",
         "value": round(Mt * args.steps / el, 1),
         "unit": "markers/s",
-        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "n_gpus": R.world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(el / args.steps * 1e3, 3),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "f64", "data": "synthetic (index-keyed dyadic generator, generated in HBM)",
         "config": {"workload": w["workload"], "model": "association_test loo", "N": N, "Mt": Mt, "M_per_gpu": d.M,
-                   "design": "methylation-like", "parallelism": f"markers sharded over {world} GPU(s)"},
+                   "design": "methylation-like", "parallelism": f"markers sharded over {R.world} GPU(s)"},
         "roofline": roof,
         "setup_s": round(t_setup, 2),
         "cpu_baseline": None,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if R.rank == 0 and R.world == 1 and not args.no_cpu_baseline:
         try:
             line["cpu_baseline"] = cpu_baseline_assoc(d, w, est, args.seed)
         except Exception as e:
             line["cpu_baseline"] = {"error": repr(e)}
     d.close()
-    if rank == 0:
+    if R.rank == 0:
         print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    R.close()
 
 
 def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=48)
-    ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c3big", "c4", "c4full", "c5"])
-    ap.add_argument("--seed", type=int, default=20250711)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-timing", action="store_true", help="skip the HIP-event kernel timing")
-    ap.add_argument("--timing-period", type=int, default=4,
-                    help="time one A/A^T launch in this many of each (kernel, K) with HIP events")
-    ap.add_argument("--batch-rhs", type=int, default=4)
-    args = ap.parse_args()
+    args = parse_args()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # start the ranks before this process touches the GPU (or imports torch)
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch  # noqa: F401  (before libvampomi: one HIP runtime per process)
+
+    R = Ranks()
+    if args.dry_run:
+        return dry_run(args, R)
+    if args.gpus != R.world:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={R.world}: launch one process per GPU")
+
+    import vampomi_amd as va
+    from vampomi_amd.workloads import workload
+
     if torch.cuda.is_available():
-        torch.cuda.set_device(local)  # torch's own context on this rank's GPU, not on GPU 0
-    n = world
-    if world > 1:
-        dist.init_process_group("gloo")
+        torch.cuda.set_device(R.local)  # torch's own context on this rank's GPU, not on GPU 0
+    n = R.world
     w = workload(args.config, n)
     N, Mt = w["N"], w["Mt"]
-
     comm_id = None
-    if world > 1:
-        obj = [va.comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
+    if n > 1:
+        obj = [va.comm_unique_id() if R.rank == 0 else None]
+        R.dist.broadcast_object_list(obj, src=0)
         comm_id = obj[0]
-    d = va.Data(N, Mt, rank=rank, nranks=world, comm_id=comm_id, device=local)
+    d = va.Data(N, Mt, rank=R.rank, nranks=n, comm_id=comm_id, device=R.local)
     t0 = time.perf_counter()
     d.generate(args.seed, w["kind"])
     model = w.get("model", "linear")
     if model == "loo":
-        return bench_assoc(args, d, w, world, rank, t0)
+        return bench_assoc(args, d, w, R, t0)
     if model == "bin_class":
         beta = d.simulate_phen_binary(args.seed + 1, lam=0.1, h2=0.8)
     else:
@@ -257,88 +373,74 @@ def main():
     def barrier():
         d.sync()
         torch.cuda.synchronize() if torch.cuda.is_available() else None
-        if world > 1:
-            dist.barrier()
+        R.barrier()
 
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         v.step()
     barrier()
-    el = time.perf_counter() - t0
+    el = R.max(time.perf_counter() - t0)
     st = d.stats()
     ref1, _ = v.a_passes
     summ = v.summary()
     v.end()
-    if world > 1:
-        t = torch.tensor([el], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
 
     it_s = args.steps / el
+    strong = w.get("scaling") == "strong"
     # dominant kernel: the (class, batch width) with the most device time
     cands = []
     for which, arr in ((0, st.ax_k), (1, st.atx_k), (3, st.op_k)):
         for k in range(4):
-            if arr[k].launches:
+            if arr[k].timed:
                 cands.append((arr[k].ms_total, which, k + 1, arr[k]))
     roof = None
     if cands:
-        ms, which, K, ks = max(cands, key=lambda c: c[0])
+        _, which, K, ks = max(cands, key=lambda c: c[0])
         # A^T.u in the CG carries the lmmse_mult epilogue (mode 1); the one-pass
         # operator's instantiation depends on N (passed as mode)
-        kname = va.kernel_name(which, K, N if which == 3 else 1)
-        avg_ms = ks.ms_total / ks.launches
-        bytes_per = ks.bytes_total / ks.launches
-        achieved = bytes_per / (avg_ms * 1e-3) / 1e9
-        traffic = pmc_traffic(kname, w["workload"])
-        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": int(traffic) if traffic else None,
-                "traffic_unit": "HBM bytes per launch (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, "
-                                f"profiles/{os.path.basename(PMC_FILE.format(w['workload']))})",
-                "algorithmic_bytes_per_launch": int(bytes_per),
-                "kernel": kname, "avg_launch_us": round(avg_ms * 1e3, 2), "launches": int(ks.launches),
-                "timed_launches": int(ks.launches) // max(1, args.timing_period),
-                "timing": f"HIP events in the dispatch packets of 1 in {max(1, args.timing_period)} launches "
-                          "of each (kernel, K) over the timed region"}
+        roof = roofline(ks, d.kernel_name(which, K, N if which == 3 else 1), w["workload"], args.timing_period)
     all_ms = st.ax.ms_total + st.atx.ms_total + st.op.ms_total
     all_bytes = st.ax.bytes_total + st.atx.bytes_total + st.op.bytes_total
+    ref_passes = (ref1 - ref0) / args.steps
     line = {
         "metric": "VAMP iterations/s (+ achieved HBM GB/s of the A/A^T kernels)",
-        "value": round(n * it_s, 4),
-        "unit": "shard-iterations/s" if n > 1 else "iterations/s",
+        "value": round(it_s if strong else n * it_s, 4),
+        "unit": "iterations/s" if (strong or n == 1) else "shard-iterations/s",
         "n_gpus": n, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(el / args.steps * 1e3, 3),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "higher_is_better": True, "scaling": "strong" if strong else "weak", "vs_baseline": None,
         "dtype": "f64", "data": "synthetic (index-keyed dyadic generator, generated in HBM)",
         "config": {"workload": w["workload"], "model": model, "N": N, "Mt": Mt, "M_per_gpu": d.M,
                    "design": "gaussian" if w["kind"] == va.GEN_GAUSS else "methylation-like",
                    "iterations_timed": f"{args.warmup + 1}-{args.warmup + args.steps}",
-                   "parallelism": f"markers sharded over {n} GPU(s), RCCL all-reduce"},
+                   "parallelism": f"markers sharded over {n} GPU(s)" + (", RCCL all-reduce" if n > 1 else ""),
+                   "comm": {"backend": "rccl" if n > 1 else "none", "nranks": d.nranks}},
         "roofline": roof,
         "hbm_gbs_all_A_kernels": round(all_bytes / (all_ms * 1e-3) / 1e9, 1) if all_ms > 0 else None,
         "passes_exec_per_step": round(st.a_passes_exec / args.steps, 2),  # stats reset at the timed region
-        "passes_ref_per_step": round((ref1 - ref0) / args.steps, 2),
+        "passes_ref_per_step": round(ref_passes, 2),
         "a_kernel_frac_of_step": round(all_ms * 1e-3 / el, 3) if el > 0 else None,
         "cg_iters": summ["cg_iters"][args.warmup:], "ons_iters": summ["ons_iters"][args.warmup:],
         "setup_s": round(t_setup, 2),
         "cpu_baseline": None,
     }
-    if rank == 0 and n == 1 and not args.no_cpu_baseline and w["workload"] == "c3big":
-        # the oracle's leg generates the whole matrix on the host (240 GB): the
-        # c3 line carries the CPU baseline for the same samples and marker kind
+    if model == "bin_class":
+        line["parity_note"] = ("probit: x1_hat/r1 parity bar is max(1e-10, 10x the oracle's own rank-count spread), "
+                               "integers exact (DESIGN.md §3)")
+    if R.rank == 0 and n == 1 and not args.no_cpu_baseline and w["workload"] == "c3big":
+        # the oracle's leg would generate the whole 240 GB matrix on the host
         line["cpu_baseline"] = {"skipped": "240 GB matrix; see the --config c3 line (same N, 62,500-marker shard)"}
-    elif rank == 0 and n == 1 and not args.no_cpu_baseline:
+    elif R.rank == 0 and n == 1 and not args.no_cpu_baseline:
         try:
-            line["cpu_baseline"] = cpu_baseline(d, w, beta, args.seed)
+            line["cpu_baseline"] = cpu_baseline(d, w, beta, args.seed, args.warmup, args.steps, ref_passes,
+                                                args.cpu_budget)
         except Exception as e:  # reported, never fatal for the GPU number
             line["cpu_baseline"] = {"error": repr(e)}
     d.close()
-    if rank == 0:
+    if R.rank == 0:
         print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    R.close()
 
 
 if __name__ == "__main__":

@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define VAMPOMI_ABI_VERSION 2
+#define VAMPOMI_ABI_VERSION 3
 #define VAMPOMI_MAX_L 64          /* mixture components */
 #define VAMPOMI_UNIQUE_ID_BYTES 128
 
@@ -97,6 +97,16 @@ void vampomi_close(vampomi_ctx* ctx);
 vampomi_status vampomi_shard_info(const vampomi_ctx* ctx, int64_t* M, int64_t* S, int64_t* ld);
 vampomi_status vampomi_sync(vampomi_ctx* ctx);          /* drain the context's stream */
 vampomi_status vampomi_barrier(vampomi_ctx* ctx);       /* COLLECTIVE: RCCL barrier + drain */
+/* COLLECTIVE: *all_ok = 1 iff local_ok != 0 on every rank.  How ranks agree on
+   a rank-local outcome (a file read) before the next collective; the
+   reference's rank-local exits (exit(1), throw) leave the other MPI ranks
+   blocked in MPI_Allreduce instead. */
+vampomi_status vampomi_all_ok(vampomi_ctx* ctx, int local_ok, int* all_ok);
+/* After a rank-local failure: poisons the test-only loopback communicator
+   (every rank's pending and later collectives fail at once) or aborts the RCCL
+   communicator, so no rank waits for this one.  Every COLLECTIVE entry point
+   does this itself when it fails. */
+vampomi_status vampomi_comm_abort(vampomi_ctx* ctx);
 
 /* ---- data ingest (data::data) ---- */
 /* marker-major fp64 file (README.md:15): this shard's bytes [S*N*8, (S+M)*N*8) */
@@ -250,10 +260,12 @@ vampomi_status vampomi_test_metrics(vampomi_ctx* ctx, const double* est, double*
 
 /* ---- measurement ---- */
 typedef struct {
-    int64_t launches;             /* kernel launches of this class */
-    double ms_total;              /* device time between HIP events around them */
-    double bytes_total;           /* algorithmic HBM bytes */
+    int64_t launches;             /* kernel launches of this class that did work (exact) */
+    double ms_total;              /* their device time: ms_timed / timed x launches */
+    double bytes_total;           /* algorithmic HBM bytes of those launches */
     double flops_total;
+    int64_t timed;                /* launches timed with HIP events (vampomi_set_timing) */
+    double ms_timed;              /* device time of the timed launches */
 } vampomi_kernel_stat;
 
 typedef struct {
@@ -269,8 +281,9 @@ typedef struct {
 } vampomi_stats;
 
 /* HIP-event timing of the A/A^T kernels: on = 0 off, 1 every launch, n > 1 one
- * launch in n of each (kernel class, K), counted n times in the stats (each
- * timed launch carries an event pair in its dispatch, a few microseconds) */
+ * launch in n of each (kernel class, K) (each timed launch carries an event
+ * pair in its dispatch, a few microseconds).  Launch counts and bytes in the
+ * stats are always exact; ms_total extrapolates the timed average to them. */
 vampomi_status vampomi_set_timing(vampomi_ctx* ctx, int on);
 vampomi_status vampomi_get_stats(vampomi_ctx* ctx, vampomi_stats* out);
 vampomi_status vampomi_reset_stats(vampomi_ctx* ctx);
@@ -278,7 +291,9 @@ vampomi_status vampomi_reset_stats(vampomi_ctx* ctx);
 /* ---- development hooks (kernel tuning; not part of the reference interface) ----
  * which: 0 = A.x partial-sum kernel, 1 = A^T.u kernel, 2 = association-test pass
  * (K = 1), 3 = one-pass CG operator (K = 1, 2).  Variants index the
- * tuning tables in vampomi_amd/csrc/kernels.hip; variant 0 is the default. */
+ * tuning tables in vampomi_amd/csrc/kernels.hip and are settings of this
+ * context only; the defaults are 0 (A.x), -1 (A^T.u: the per-K choice) and 2
+ * (association pass). */
 vampomi_status vampomi_dev_set_variant(vampomi_ctx* ctx, int which, int variant);
 /* average device time (HIP events) of `reps` back-to-back launches, K RHS */
 vampomi_status vampomi_dev_time_pass(vampomi_ctx* ctx, int which, int K, int reps, double* avg_ms);
@@ -286,7 +301,7 @@ vampomi_status vampomi_dev_time_pass(vampomi_ctx* ctx, int which, int K, int rep
  * (mode 1: the CG form, i.e. A^T.u with the lmmse_mult epilogue, A.x with the
  * fused direction update; which = 2: the association-test pass of
  * vampomi_assoc_loo) */
-vampomi_status vampomi_dev_kernel_name(int which, int K, int mode, char* out, int cap);
+vampomi_status vampomi_dev_kernel_name(const vampomi_ctx* ctx, int which, int K, int mode, char* out, int cap);
 
 #ifdef __cplusplus
 }

@@ -41,7 +41,8 @@ class Result(C.Structure):
                 ("L_hist", C.c_void_p), ("params", C.c_void_p), ("metrics", C.c_void_p),
                 ("x1_hist", C.c_void_p), ("r1_hist", C.c_void_p), ("x1_final", C.c_void_p),
                 ("probs_final", C.c_void_p), ("vars_final", C.c_void_p), ("L_final", C.c_int),
-                ("a_passes", C.c_int64), ("prior_hist", C.c_void_p)]
+                ("a_passes", C.c_int64), ("prior_hist", C.c_void_p), ("it_wall", C.c_void_p),
+                ("wall_start", C.c_double)]
 
 
 _lib = None
@@ -318,9 +319,10 @@ def vamp_infere(X: np.ndarray, y: np.ndarray, Mt: int, S: int = 0, rank: int = 0
     r1h = np.zeros((max_iter, max(M, 1))) if keep_hist else None
     x1f = np.zeros(max(M, 1))
     pf, vf = np.zeros(MAX_L), np.zeros(MAX_L)
+    wall = np.zeros(max_iter)
     res = Result(cg_iters=_p(cg), ons_iters=_p(ons), L_hist=_p(Lh), params=_p(params), metrics=_p(metrics),
                  x1_hist=_p(x1h), r1_hist=_p(r1h), x1_final=_p(x1f), probs_final=_p(pf), vars_final=_p(vf),
-                 prior_hist=_p(prior))
+                 prior_hist=_p(prior), it_wall=_p(wall))
     fn = lib.orc_vamp_infere_probit if probit else lib.orc_vamp_infere_linear
     rc = fn(C.byref(pb), C.byref(pr), C.byref(res))
     if rc != 0:
@@ -329,7 +331,9 @@ def vamp_infere(X: np.ndarray, y: np.ndarray, Mt: int, S: int = 0, rank: int = 0
     out = {"iterations": n, "cg_iters": cg[:n].copy(), "ons_iters": ons[:n].copy(), "L": Lh[:n].copy(),
            "params": params[:n].copy(), "metrics": metrics[:n].copy(), "x1_final": x1f[:M].copy(),
            "probs_final": pf[:res.L_final].copy(), "vars_final": vf[:res.L_final].copy(), "a_passes": res.a_passes,
-           "mave": mave, "msig": msig}
+           "mave": mave, "msig": msig,
+           # seconds from the start of iteration 1 to the end of each iteration (timing only)
+           "it_end_s": wall[:n] - res.wall_start}
     if probit:
         out["prior"] = prior[:n].copy()
     if keep_hist:

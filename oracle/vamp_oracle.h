@@ -123,6 +123,8 @@ typedef struct {
     int L_final;
     int64_t a_passes;           /* reference-equivalent A/A^T passes executed */
     double* prior_hist;         /* probit: 1 + 2*ORC_MAX_L per iteration: L, probs, vars (x N) */
+    double* it_wall;            /* omp_get_wtime() at the end of each iteration (timing only; may be NULL) */
+    double wall_start;          /* omp_get_wtime() before iteration 1 */
 } orc_result;
 
 /* returns 0 on success */

@@ -3,6 +3,9 @@
 //   harness csv <path> <it> <v1> <v2> ...   (creates header "h0, h1.." when it == 0)
 //   harness bin <path> <S> <v1> <v2> ...
 //   harness phen <path> <standardize>       (prints the parsed values, %.17g)
+//   harness rdzv-pub <path> <id-text>       (rank 0 of the CLI: publish, nonce from the environment)
+//   harness rdzv-get <path> <not_before> <timeout_ms>  (another rank: prints the id text or TIMEOUT)
+//   harness rdzv-rm <path>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -40,6 +43,25 @@ int main(int argc, char** argv) {
         }
         if (std::atoi(argv[3])) vio::standardize_phen(y);
         for (double v : y) std::printf("%.17g\n", v);
+        return 0;
+    }
+    if (cmd == "rdzv-pub") {
+        char id[128] = {0};
+        std::strncpy(id, argv[3], sizeof id - 1);
+        return vio::rdzv_publish(path, vio::rdzv_nonce(), id, (int)sizeof id) ? 0 : 1;
+    }
+    if (cmd == "rdzv-get") {
+        char id[128] = {0};
+        if (!vio::rdzv_fetch(path, vio::rdzv_nonce(), std::strtod(argv[3], nullptr), id, (int)sizeof id,
+                             std::atoi(argv[4]))) {
+            std::printf("TIMEOUT\n");
+            return 0;
+        }
+        std::printf("%s\n", id);
+        return 0;
+    }
+    if (cmd == "rdzv-rm") {
+        vio::rdzv_remove(path);
         return 0;
     }
     return 2;

@@ -29,7 +29,7 @@ def test_every_declared_symbol_is_exported_and_bound():
     for n in names:
         assert hasattr(lib, n), n
     assert names == set(_lib.SIGNATURES), names ^ set(_lib.SIGNATURES)
-    assert va.load().vampomi_abi_version() == 2
+    assert va.load().vampomi_abi_version() == 3
 
 
 def test_struct_layout_matches_header(tmp_path):

@@ -355,7 +355,12 @@ def test_every_kernel_variant_is_correct():
                     assert relerr(d.Ax(x), ax_ref) < 1e-13, ("ax", v)
                 else:
                     assert relerr(d.ATx(u), atx_ref) < 1e-13, ("atx", v)
-            _lib.check(lib.vampomi_dev_set_variant(d.ctx, which, 0))
+        # variants are settings of this context only: a fresh one runs the defaults
+        with va.Data(N, Mt) as e:
+            e.load_meth(X)
+            assert e.kernel_name(1, 2, 1) != d.kernel_name(1, 2, 1)
+            assert e.kernel_name(1, 2, 1) == "atx_kernel<4, 2, 1, 4, true>"  # the per-K default (G=4, UJ=4)
+            assert relerr(e.ATx(u), atx_ref) < 1e-13
 
 
 def test_rccl_code_path_single_rank(tmp_path):

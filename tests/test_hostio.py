@@ -95,3 +95,47 @@ def test_pow_minus_one_is_within_one_ulp_of_the_reciprocal(tmp_path):
                     "-o", str(exe), "-lm"], check=True)
     bad, tot, maxulp = map(int, run(str(exe), 4000000).split())
     assert tot > 3_000_000 and maxulp <= 1 and bad < 0.01 * tot
+
+
+def test_cli_rendezvous_never_reads_an_earlier_jobs_file(harness, tmp_path):
+    """main_meth.exe's rank rendezvous (vio::rdzv_*): a second job into the same
+    out-dir must not pick up the first job's RCCL id, with a run nonce (torchrun
+    / VAMPOMI_RUN_ID) or without one (file age), and rank 0 removes the file once
+    the communicator is up."""
+    import time
+
+    path = str(tmp_path / ".out.rdzv")
+
+    def env(**kw):
+        e = {k: v for k, v in os.environ.items()
+             if k not in ("VAMPOMI_RUN_ID", "TORCHELASTIC_RUN_ID", "MASTER_ADDR", "MASTER_PORT")}
+        e.update(kw)
+        return e
+
+    def get(not_before, timeout_ms, **kw):
+        return subprocess.run([harness, "rdzv-get", path, str(not_before), str(timeout_ms)], capture_output=True,
+                              text=True, check=True, env=env(**kw)).stdout.strip()
+
+    def pub(idtext, **kw):
+        subprocess.run([harness, "rdzv-pub", path, idtext], check=True, env=env(**kw))
+
+    # job 1 (nonce A) leaves its file behind (e.g. it crashed before clean-up)
+    pub("job-one", VAMPOMI_RUN_ID="A")
+    assert get(0, 2000, VAMPOMI_RUN_ID="A") == "job-one"
+    # job 2 (nonce B): its ranks must wait for ITS rank 0, not read job 1's id
+    assert get(0, 300, VAMPOMI_RUN_ID="B") == "TIMEOUT"
+    pub("job-two", VAMPOMI_RUN_ID="B")
+    assert get(0, 2000, VAMPOMI_RUN_ID="B") == "job-two"
+    # torchrun's run id and the master address serve as nonces too
+    pub("job-three", TORCHELASTIC_RUN_ID="t3")
+    assert get(0, 300, TORCHELASTIC_RUN_ID="t2") == "TIMEOUT"
+    assert get(0, 2000, TORCHELASTIC_RUN_ID="t3") == "job-three"
+    pub("job-four", MASTER_ADDR="127.0.0.1", MASTER_PORT="29511")
+    assert get(0, 300, MASTER_ADDR="127.0.0.1", MASTER_PORT="29512") == "TIMEOUT"
+    # no nonce at all: a file older than the job is ignored
+    pub("old")
+    assert get(time.time() + 5, 300) == "TIMEOUT"
+    assert get(time.time() - 60, 2000) == "old"
+    # rank 0 removes the file after communicator init
+    subprocess.run([harness, "rdzv-rm", path], check=True)
+    assert not os.path.exists(path)

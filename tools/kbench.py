@@ -55,7 +55,7 @@ for which, name, Ks, nvar in ((0, "ax", (1, 2, 3), 7), (1, "atx", (1, 2), 8)):
 if "op" in only:  # the one-pass CG operator (A^T q and A d from one read of X)
     res["op"] = {}
     for v in range(1):
-        row = {"kernel": va.kernel_name(3, 2, N)}
+        row = {"kernel": d.kernel_name(3, 2, N)}
         for K in (1, 2):
             ms = C.c_double()
             _lib.check(lib.vampomi_dev_time_pass(d.ctx, 3, K, 2, C.byref(ms)))
@@ -76,7 +76,7 @@ if "loo" in only:
         _lib.check(lib.vampomi_dev_time_pass(d.ctx, 2, 1, 2, C.byref(ms)))
         _lib.check(lib.vampomi_dev_time_pass(d.ctx, 2, 1, reps, C.byref(ms)))
         b = 8.0 * N * Mt + 8.0 * N + 48.0 * Mt
-        row = {"kernel": va.kernel_name(2, 1, 0), "bitwise_eq_v0": bool(np.array_equal(st, ref)),
+        row = {"kernel": d.kernel_name(2, 1, 0), "bitwise_eq_v0": bool(np.array_equal(st, ref)),
                "us": round(ms.value * 1e3, 1), "GBs": round(b / (ms.value * 1e-3) / 1e9, 1)}
         res["loo"][v] = row
         print("loo", v, json.dumps(row), flush=True)

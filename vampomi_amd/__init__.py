@@ -38,14 +38,6 @@ def divide_work(Mt: int, nranks: int, rank: int):
     return M.value, S.value, Mm.value
 
 
-def kernel_name(which: int, K: int, mode: int = 0) -> str:
-    """rocprofv3 name of the A.x (which=0) / A^T.u (which=1) kernel launched for K RHS,
-    or of the association-test pass (which=2)."""
-    buf = C.create_string_buffer(256)
-    check(load().vampomi_dev_kernel_name(which, K, mode, buf, 256))
-    return buf.value.decode()
-
-
 def comm_unique_id() -> bytes:
     """RCCL unique id (rank 0 creates it, the caller broadcasts it)."""
     buf = (C.c_ubyte * UNIQUE_ID_BYTES)()
@@ -259,6 +251,28 @@ class Data:
         return x1[: self.M], x1d[: self.M], s.value
 
     # -- measurement --
+    def kernel_name(self, which: int, K: int, mode: int = 0) -> str:
+        """rocprofv3 name of the kernel this context launches for pass ``which``
+        (0 A.x, 1 A^T.u, 2 association test, 3 one-pass CG operator with mode = N)
+        with K right-hand sides, under its current variant settings."""
+        buf = C.create_string_buffer(256)
+        check(self._lib.vampomi_dev_kernel_name(self.ctx, which, K, mode, buf, 256))
+        return buf.value.decode()
+
+    def set_variant(self, which: int, variant: int):
+        """Development hook: this context's kernel variant for pass ``which``."""
+        check(self._lib.vampomi_dev_set_variant(self.ctx, which, variant))
+
+    def all_ok(self, local_ok: bool) -> bool:
+        """COLLECTIVE: True iff local_ok on every rank."""
+        out = C.c_int()
+        check(self._lib.vampomi_all_ok(self.ctx, 1 if local_ok else 0, C.byref(out)))
+        return bool(out.value)
+
+    def comm_abort(self):
+        """Poison (loopback) / abort (RCCL) the job's communicator after a local failure."""
+        check(self._lib.vampomi_comm_abort(self.ctx))
+
     def set_timing(self, on: bool = True, period: int = 1):
         """HIP-event timing of the A/A^T launches; period > 1 times one launch
         in `period` of each (kernel class, K) and counts it `period` times."""

@@ -80,7 +80,7 @@ class Result(C.Structure):
 
 class KernelStat(C.Structure):
     _fields_ = [("launches", C.c_int64), ("ms_total", C.c_double), ("bytes_total", C.c_double),
-                ("flops_total", C.c_double)]
+                ("flops_total", C.c_double), ("timed", C.c_int64), ("ms_timed", C.c_double)]
 
 
 class Stats(C.Structure):
@@ -135,7 +135,9 @@ SIGNATURES = {
     "vampomi_reset_stats": (C.c_int, [_P]),
     "vampomi_dev_set_variant": (C.c_int, [_P, C.c_int, C.c_int]),
     "vampomi_dev_time_pass": (C.c_int, [_P, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_double)]),
-    "vampomi_dev_kernel_name": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_char_p, C.c_int]),
+    "vampomi_dev_kernel_name": (C.c_int, [_P, C.c_int, C.c_int, C.c_int, C.c_char_p, C.c_int]),
+    "vampomi_all_ok": (C.c_int, [_P, C.c_int, C.POINTER(C.c_int)]),
+    "vampomi_comm_abort": (C.c_int, [_P]),
 }
 
 _lib = None

@@ -36,6 +36,15 @@ vampomi_status fail(vampomi_status s, const std::string& msg);
     } while (0)
 
 // ---- the context ------------------------------------------------------------
+struct vampomi_ctx;
+// Marks a COLLECTIVE entry point on this thread: an error raised inside it
+// (fail()) aborts the context's communicator first (comm_abort), so that the
+// other ranks fail at their next collective instead of waiting for this one.
+struct CollScope {
+    explicit CollScope(vampomi_ctx* c);
+    ~CollScope();
+    vampomi_ctx* prev;
+};
 struct VampRun;
 struct LoopbackComm;  // engine.cpp: test-only in-process communicator
 
@@ -44,7 +53,6 @@ struct TimedLaunch {
     int cls;  // 0 ax, 1 atx, 2 loo, 3 one-pass operator
     int K;
     double bytes, flops;
-    int weight;  // launches this sample stands for (the sampling period)
 };
 
 // scalar slots in ctx->scal: <d,p> of the fused lmmse epilogue, then the
@@ -52,7 +60,7 @@ struct TimedLaunch {
 // (SL_CG: the 3K sums of a CG step, decided on the device; SL_CGI: the 2K sums
 // of cg_init, read by cg_start_from)
 enum : int { SL_DP = 0, SL_CG = 4, SL_SYNC = 16, SL_NSYNC = 256, SL_LOCAL = SL_SYNC + SL_NSYNC, SL_NLOCAL = 128,
-             SL_CGI = SL_LOCAL + SL_NLOCAL, SL_TOTAL = 512, SL_BARRIER = SL_TOTAL - 1 };
+             SL_CGI = SL_LOCAL + SL_NLOCAL, SL_CHECK = SL_CGI + 16, SL_AGREE = SL_CHECK + 8, SL_TOTAL = 512, SL_BARRIER = SL_TOTAL - 1 };
 
 struct vampomi_ctx {
     int rank = 0, nranks = 1, device = 0;
@@ -63,6 +71,8 @@ struct vampomi_ctx {
     ncclComm_t comm = nullptr;
     bool use_comm = false;  // nranks > 1 (or VAMPOMI_FORCE_RCCL): all-reduces through RCCL
     std::shared_ptr<LoopbackComm> loopback;  // VAMPOMI_COMM=loopback: ranks are threads of one process
+    uint64_t coll_seq = 0;  // collectives issued so far (divergence checks)
+    bool aborted = false;   // comm_abort ran: no further collective
 
     double* X = nullptr;     // M columns x ld, marker-major, pad rows zero
     double* mave = nullptr;
@@ -72,6 +82,7 @@ struct vampomi_ctx {
     bool have_X = false, have_y = false;
 
     vk::AxPlan axp{};
+    int atx_variant = vk::kAtxDefault, loo_variant = vk::kLooDefault;  // per context (dev hooks)
     double* ax_part = nullptr;  // nslots x kMaxRhs x ld partial sums of A.x
     double* red_part = nullptr;  // per-block partials of every reduction
     size_t red_cap = 0;
@@ -112,10 +123,25 @@ void dev_free(double*& p);
 vampomi_status host_sync(vampomi_ctx* c);
 // spins until the context's host flag reaches seq (stores from the stream)
 vampomi_status wait_flag(vampomi_ctx* c, unsigned long long seq);
-vampomi_status allreduce_dev(vampomi_ctx* c, double* buf, size_t n);
+// SUM all-reduce of n doubles over the ranks (nothing on one rank). COLLECTIVE:
+// every rank must make the same calls in the same order; site/line identify
+// the call for the divergence checks (loopback always, RCCL with
+// VAMPOMI_COLL_CHECK=1)
+vampomi_status allreduce_dev(vampomi_ctx* c, double* buf, size_t n, const char* site = __builtin_FUNCTION(),
+                             int line = __builtin_LINE());
+// *total = local summed over the ranks (one all-reduce; *total = local on one
+// rank).  COLLECTIVE: how ranks agree on a decision that started rank-local
+vampomi_status sum_over_ranks(vampomi_ctx* c, double local, double* total, const char* site = __builtin_FUNCTION(),
+                              int line = __builtin_LINE());
+// poisons (loopback) or aborts (RCCL) the communicator after a rank-local error
+void comm_abort(vampomi_ctx* c, const std::string& why);
 void resolve_timing(vampomi_ctx* c);
-// events for this launch of class cls with K right-hand sides, if it is sampled
-TimedLaunch timed_launch(vampomi_ctx* c, int cls, int K);
+// counts a launch of class cls with K right-hand sides (bytes, flops: its
+// algorithmic work); returns HIP events for it if it is sampled (else nulls)
+TimedLaunch launch_stat(vampomi_ctx* c, int cls, int K, double bytes, double flops);
+// forgets the counts since `before` and the samples queued since pending_mark
+// (the gated launches of a CG step queued after the solve had stopped)
+void drop_launches(vampomi_ctx* c, size_t pending_mark, const vampomi_stats& before);
 void release_ctx_resources(vampomi_ctx* c);
 
 // ---- operators on device buffers ---------------------------------------------

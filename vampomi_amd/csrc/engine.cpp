@@ -36,9 +36,14 @@
 // errors and device memory
 // ---------------------------------------------------------------------------
 static thread_local std::string g_err;
+static thread_local vampomi_ctx* g_coll_ctx = nullptr;  // innermost CollScope of this thread
+
+CollScope::CollScope(vampomi_ctx* c) : prev(g_coll_ctx) { g_coll_ctx = c; }
+CollScope::~CollScope() { g_coll_ctx = prev; }
 
 vampomi_status fail(vampomi_status s, const std::string& msg) {
     g_err = msg;
+    if (g_coll_ctx && g_coll_ctx->use_comm && !g_coll_ctx->aborted) comm_abort(g_coll_ctx, msg);
     return s;
 }
 
@@ -69,12 +74,43 @@ static hipEvent_t ev_get(vampomi_ctx* c) {
     return e;
 }
 
-TimedLaunch timed_launch(vampomi_ctx* c, int cls, int K) {
+// algorithmic bytes / flops of one pass with K right-hand sides (SURVEY §8(d)):
+// X once, the K N-vectors, mave/msig and the K M-vectors; (x - mu) once per
+// element and one fma per right-hand side.
+static double pass_bytes(const vampomi_ctx* c, int K) {
+    return 8.0 * (double)c->N * (double)c->M + 8.0 * K * (double)c->N + 8.0 * (2.0 + K) * (double)c->M;
+}
+static double pass_flops(const vampomi_ctx* c, int K) { return (double)c->N * (double)c->M * (1.0 + 2.0 * K); }
+
+static vampomi_kernel_stat* stat_of(vampomi_ctx* c, int cls) {
+    return cls == 0 ? &c->stats.ax : cls == 1 ? &c->stats.atx : cls == 3 ? &c->stats.op : &c->stats.loo;
+}
+static vampomi_kernel_stat* stat_k_of(vampomi_ctx* c, int cls, int K) {
+    return cls == 0 ? &c->stats.ax_k[K - 1] : cls == 1 ? &c->stats.atx_k[K - 1] : cls == 3 ? &c->stats.op_k[K - 1]
+                                                                                           : nullptr;
+}
+
+// Every launch is counted exactly (launches, algorithmic bytes and flops);
+// with timing on, one in tperiod launches of each (class, K) also gets HIP
+// events in its dispatch packet.  The per-class time is the sampled average
+// times the exact launch count (vampomi_get_stats), so skipped or dropped
+// samples never inflate it.
+TimedLaunch launch_stat(vampomi_ctx* c, int cls, int K, double bytes, double flops) {
+    for (vampomi_kernel_stat* x : {stat_of(c, cls), stat_k_of(c, cls, K)}) {
+        if (!x) continue;
+        x->launches += 1;
+        x->bytes_total += bytes;
+        x->flops_total += flops;
+    }
     TimedLaunch t{};
     if (!c->timing || c->tcount[cls][K - 1]++ % c->tperiod != 0) return t;
     t.a = ev_get(c);
     t.b = ev_get(c);
-    t.weight = c->tperiod;
+    t.cls = cls;
+    t.K = K;
+    t.bytes = bytes;
+    t.flops = flops;
+    c->pending.push_back(t);
     return t;
 }
 
@@ -82,20 +118,10 @@ void resolve_timing(vampomi_ctx* c) {
     for (auto& t : c->pending) {
         float ms = 0.f;
         if (hipEventSynchronize(t.b) == hipSuccess && hipEventElapsedTime(&ms, t.a, t.b) == hipSuccess) {
-            vampomi_kernel_stat* s = t.cls == 0   ? &c->stats.ax
-                                     : t.cls == 1 ? &c->stats.atx
-                                     : t.cls == 3 ? &c->stats.op
-                                                  : &c->stats.loo;
-            vampomi_kernel_stat* sk = t.cls == 0   ? &c->stats.ax_k[t.K - 1]
-                                      : t.cls == 1 ? &c->stats.atx_k[t.K - 1]
-                                      : t.cls == 3 ? &c->stats.op_k[t.K - 1]
-                                                   : nullptr;
-            for (vampomi_kernel_stat* x : {s, sk}) {  // a sample stands for `weight` launches
+            for (vampomi_kernel_stat* x : {stat_of(c, t.cls), stat_k_of(c, t.cls, t.K)}) {
                 if (!x) continue;
-                x->launches += t.weight;
-                x->ms_total += (double)ms * t.weight;
-                x->bytes_total += t.bytes * t.weight;
-                x->flops_total += t.flops * t.weight;
+                x->timed += 1;
+                x->ms_timed += (double)ms;
             }
         }
         c->ev_pool.push_back(t.a);
@@ -104,13 +130,32 @@ void resolve_timing(vampomi_ctx* c) {
     c->pending.clear();
 }
 
-// algorithmic bytes / flops of one pass with K right-hand sides (SURVEY §8(d)):
-// X once, the K N-vectors, mave/msig and the K M-vectors; (x - mu) once per
-// element and one fma per right-hand side.
-static double pass_bytes(const vampomi_ctx* c, int K) {
-    return 8.0 * (double)c->N * (double)c->M + 8.0 * K * (double)c->N + 8.0 * (2.0 + K) * (double)c->M;
+// the launches of a CG step queued after its solve had stopped did nothing
+// (gated): forget their counts and samples (pcg.cpp)
+void drop_launches(vampomi_ctx* c, size_t pending_mark, const vampomi_stats& before) {
+    for (size_t q = pending_mark; q < c->pending.size(); ++q) {
+        c->ev_pool.push_back(c->pending[q].a);
+        c->ev_pool.push_back(c->pending[q].b);
+    }
+    c->pending.resize(pending_mark);
+    // counts back to `before`; samples (timed, ms_timed) are only resolved
+    // outside a solve, and the dropped ones were removed above
+    auto undo = [](vampomi_kernel_stat& x, const vampomi_kernel_stat& b) {
+        x.launches = b.launches;
+        x.bytes_total = b.bytes_total;
+        x.flops_total = b.flops_total;
+    };
+    undo(c->stats.ax, before.ax);
+    undo(c->stats.atx, before.atx);
+    undo(c->stats.op, before.op);
+    undo(c->stats.loo, before.loo);
+    for (int k = 0; k < 4; ++k) {
+        undo(c->stats.ax_k[k], before.ax_k[k]);
+        undo(c->stats.atx_k[k], before.atx_k[k]);
+        undo(c->stats.op_k[k], before.op_k[k]);
+    }
+    c->stats.a_passes_exec = before.a_passes_exec;
 }
-static double pass_flops(const vampomi_ctx* c, int K) { return (double)c->N * (double)c->M * (1.0 + 2.0 * K); }
 
 // ---------------------------------------------------------------------------
 // reductions
@@ -165,6 +210,14 @@ struct LoopbackComm {
     std::condition_variable cv;
     int P = 0, arrived = 0;
     uint64_t gen = 0;
+    std::string poison;  // non-empty: the job failed (mismatch, abort); every later call fails with it
+    struct Desc {
+        uint64_t seq;      // the rank's collective sequence number
+        size_t n;
+        const char* site;  // the calling function (static string) and line
+        int line;
+    };
+    std::vector<Desc> desc;
     std::vector<std::vector<double>> in;
     std::vector<double> out;
 };
@@ -180,33 +233,62 @@ static std::shared_ptr<LoopbackComm> loopback_join(const void* id, int P) {
         lb = std::make_shared<LoopbackComm>();
         lb->P = P;
         lb->in.resize((size_t)P);
+        lb->desc.resize((size_t)P);
         g_loopback[key] = lb;
     }
     return lb;
 }
 
-static vampomi_status loopback_allreduce(vampomi_ctx* c, double* buf, size_t n) {
+static std::string coll_desc(int r, const LoopbackComm::Desc& d) {
+    return "rank " + std::to_string(r) + ": collective #" + std::to_string(d.seq) + " of " + std::to_string(d.n) +
+           " doubles at " + d.site + ":" + std::to_string(d.line);
+}
+
+// Every rank deposits its buffer with a descriptor (sequence number, size,
+// call site).  The last to arrive checks that all descriptors agree before it
+// sums; a disagreement (ranks that took different branches) poisons the
+// communicator, and every rank fails at once with every rank's descriptor.
+static vampomi_status loopback_allreduce(vampomi_ctx* c, double* buf, size_t n, const char* site, int line) {
     LoopbackComm& lb = *c->loopback;
+    const LoopbackComm::Desc me{++c->coll_seq, n, site, line};
     std::vector<double> mine(n);
     HIPCHK(hipMemcpyAsync(mine.data(), buf, n * 8, hipMemcpyDeviceToHost, c->st));
     HIPCHK(hipStreamSynchronize(c->st));
     {
         std::unique_lock<std::mutex> g(lb.mu);
+        if (!lb.poison.empty()) return fail(VAMPOMI_ERR_STATE, "loopback communicator failed earlier: " + lb.poison);
         const uint64_t my_gen = lb.gen;
         lb.in[(size_t)c->rank] = std::move(mine);
+        lb.desc[(size_t)c->rank] = me;
         if (++lb.arrived == lb.P) {
-            lb.out.assign(n, 0.0);
-            for (int r = 0; r < lb.P; ++r)
-                for (size_t i = 0; i < n; ++i) lb.out[i] += lb.in[(size_t)r][i];
+            bool agree = true;
+            for (int r = 1; r < lb.P; ++r) {
+                const auto& a = lb.desc[0];
+                const auto& b = lb.desc[(size_t)r];
+                agree = agree && a.seq == b.seq && a.n == b.n && a.line == b.line && std::strcmp(a.site, b.site) == 0;
+            }
+            if (!agree) {
+                std::string why = "ranks disagree on the collective:";
+                for (int r = 0; r < lb.P; ++r) why += " [" + coll_desc(r, lb.desc[(size_t)r]) + "]";
+                lb.poison = why;
+            } else {
+                lb.out.assign(n, 0.0);
+                for (int r = 0; r < lb.P; ++r)
+                    for (size_t i = 0; i < n; ++i) lb.out[i] += lb.in[(size_t)r][i];
+            }
             lb.arrived = 0;
             ++lb.gen;
             lb.cv.notify_all();
-        } else if (!lb.cv.wait_for(g, std::chrono::seconds(60), [&] { return lb.gen != my_gen; })) {
-            // a rank that failed (or took another branch) never arrives: end
-            // this rank with an error instead of waiting forever
+        } else if (!lb.cv.wait_for(g, std::chrono::seconds(60),
+                                   [&] { return lb.gen != my_gen || !lb.poison.empty(); })) {
+            // a rank that failed without aborting never arrives: end this rank
+            // with an error instead of waiting forever
             --lb.arrived;
-            return fail(VAMPOMI_ERR_STATE, "loopback all-reduce: not every rank arrived within 60 s");
+            lb.poison = "not every rank arrived within 60 s at " + coll_desc(c->rank, me);
+            lb.cv.notify_all();
+            return fail(VAMPOMI_ERR_STATE, "loopback all-reduce: " + lb.poison);
         }
+        if (!lb.poison.empty()) return fail(VAMPOMI_ERR_STATE, "loopback all-reduce: " + lb.poison);
         mine = lb.out;  // lb.out is only rewritten once every rank has arrived again
     }
     HIPCHK(hipMemcpyAsync(buf, mine.data(), n * 8, hipMemcpyHostToDevice, c->st));
@@ -214,10 +296,78 @@ static vampomi_status loopback_allreduce(vampomi_ctx* c, double* buf, size_t n) 
     return VAMPOMI_OK;
 }
 
-vampomi_status allreduce_dev(vampomi_ctx* c, double* buf, size_t n) {
+// VAMPOMI_COLL_CHECK=1 (RCCL): before every all-reduce, the ranks all-reduce
+// their descriptor (sequence number, size, call-site line) as max and -min and
+// compare on the host: a divergence fails on every rank instead of hanging.
+// Costs a host round trip per collective; a debugging aid.
+static vampomi_status rccl_check(vampomi_ctx* c, size_t n, const char* site, int line) {
+    double* d = c->scal + SL_CHECK;
+    const double v[3] = {(double)c->coll_seq, (double)n, (double)line};
+    double h[6] = {v[0], v[1], v[2], -v[0], -v[1], -v[2]};
+    HIPCHK(hipMemcpyAsync(d, h, sizeof h, hipMemcpyHostToDevice, c->st));
+    NCCLCHK(ncclAllReduce(d, d, 6, ncclDouble, ncclMax, c->comm, c->st));
+    HIPCHK(hipMemcpyAsync(h, d, sizeof h, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    for (int q = 0; q < 3; ++q)
+        if (h[q] != v[q] || -h[3 + q] != v[q])
+            return fail(VAMPOMI_ERR_STATE, "ranks disagree on collective #" + std::to_string(c->coll_seq) + " (this rank: " +
+                                               std::to_string(n) + " doubles at " + site + ":" + std::to_string(line) + ")");
+    return VAMPOMI_OK;
+}
+
+vampomi_status allreduce_dev(vampomi_ctx* c, double* buf, size_t n, const char* site, int line) {
     if (!c->use_comm || n == 0) return VAMPOMI_OK;
-    if (c->loopback) return loopback_allreduce(c, buf, n);
+    if (c->loopback) return loopback_allreduce(c, buf, n, site, line);
+    ++c->coll_seq;
+    static const bool check = std::getenv("VAMPOMI_COLL_CHECK") && std::atoi(std::getenv("VAMPOMI_COLL_CHECK"));
+    if (check) STCHK(rccl_check(c, n, site, line));
     NCCLCHK(ncclAllReduce(buf, buf, n, ncclDouble, ncclSum, c->comm, c->st));
+    return VAMPOMI_OK;
+}
+
+vampomi_status sum_over_ranks(vampomi_ctx* c, double local, double* total, const char* site, int line) {
+    if (!c->use_comm) {
+        *total = local;
+        return VAMPOMI_OK;
+    }
+    double* d = c->scal + SL_AGREE;
+    HIPCHK(vk::set_scalar(d, local, c->st));
+    STCHK(allreduce_dev(c, d, 1, site, line));
+    HIPCHK(hipMemcpyAsync(c->h_scal + SL_AGREE, d, 8, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    *total = c->h_scal[SL_AGREE];
+    return VAMPOMI_OK;
+}
+
+// Ends the job's communicator after a rank-local failure, so that no other
+// rank waits for this one: the loopback communicator is poisoned (every rank's
+// next or pending collective fails at once), RCCL's is aborted.
+void comm_abort(vampomi_ctx* c, const std::string& why) {
+    if (!c || !c->use_comm) return;
+    if (c->loopback) {
+        std::lock_guard<std::mutex> g(c->loopback->mu);
+        if (c->loopback->poison.empty()) c->loopback->poison = "rank " + std::to_string(c->rank) + " aborted: " + why;
+        c->loopback->cv.notify_all();
+    } else if (c->comm) {
+        (void)ncclCommAbort(c->comm);
+        c->comm = nullptr;
+    }
+    c->aborted = true;
+}
+
+extern "C" vampomi_status vampomi_all_ok(vampomi_ctx* c, int local_ok, int* all_ok) {
+    CollScope cs_(c);
+    if (!c || !all_ok) return fail(VAMPOMI_ERR_ARG, "null argument");
+    HIPCHK(hipSetDevice(c->device));
+    double bad = 0.0;
+    STCHK(sum_over_ranks(c, local_ok ? 0.0 : 1.0, &bad));
+    *all_ok = bad == 0.0 ? 1 : 0;
+    return VAMPOMI_OK;
+}
+
+extern "C" vampomi_status vampomi_comm_abort(vampomi_ctx* c) {
+    if (!c) return fail(VAMPOMI_ERR_ARG, "null context");
+    comm_abort(c, "vampomi_comm_abort");
     return VAMPOMI_OK;
 }
 
@@ -302,17 +452,10 @@ vampomi_status ax_dev(vampomi_ctx* c, int K, const double* const* x, double* out
         xs.p[k] = x[k];
         os.p[k] = outbase + (int64_t)k * c->ld;
     }
-    TimedLaunch t = timed_launch(c, 0, K);
+    TimedLaunch t = launch_stat(c, 0, K, pass_bytes(c, K), pass_flops(c, K));
     const vk::AxFuse none{};
     const vk::AxFuse& f = fu ? *fu : none;
     HIPCHK(vk::ax_partial(c->shard(), c->axp, K, xs, c->ax_part, c->st, vk::Timing{t.a, t.b}, f));
-    if (t.a) {
-        t.cls = 0;
-        t.K = K;
-        t.bytes = pass_bytes(c, K);
-        t.flops = pass_flops(c, K);
-        c->pending.push_back(t);
-    }
     c->stats.a_passes_exec++;
     if (!c->use_comm) {
         HIPCHK(vk::ax_reduce(c->axp, K, c->N, c->ld, c->ax_part, os, c->sqrtN, c->st, f.gate));
@@ -345,16 +488,9 @@ vampomi_status atx_dev(vampomi_ctx* c, int K, const double* const* u, double* co
         ps.p[k] = p ? p[k] : nullptr;
         zs.p[k] = zf ? zf[k] : nullptr;
     }
-    TimedLaunch t = timed_launch(c, 1, K);
-    HIPCHK(vk::atx(c->shard(), K, us, os, 1.0 / c->sqrtN, mode, tau, gam2, ps, c->st, vk::Timing{t.a, t.b}, gate, zs,
+    TimedLaunch t = launch_stat(c, 1, K, pass_bytes(c, K), pass_flops(c, K));
+    HIPCHK(vk::atx(c->shard(), K, us, os, 1.0 / c->sqrtN, mode, tau, gam2, ps, c->st, c->atx_variant, vk::Timing{t.a, t.b}, gate, zs,
                    zf ? beta : nullptr, ss));
-    if (t.a) {
-        t.cls = 1;
-        t.K = K;
-        t.bytes = pass_bytes(c, K);
-        t.flops = pass_flops(c, K);
-        c->pending.push_back(t);
-    }
     c->stats.a_passes_exec++;
     if (mode == 1 && dp) {
         // <d_k, p_k> with the fixed-geometry reduction (depends on M only, not on
@@ -383,13 +519,10 @@ vampomi_status op_prepare(vampomi_ctx* c) {
     return VAMPOMI_OK;
 }
 
-// one operator launch: X once, the K q-vectors (as A r and q_old), mave/msig,
-// p, z and d, plus the K A d partials written once per workgroup
-static double op_bytes(const vampomi_ctx* c, int K) {
-    return pass_bytes(c, K) + 8.0 * K * (double)c->N + 8.0 * 2 * K * (double)c->M +
-           8.0 * K * (double)c->N * (double)c->opp.nslots;
-}
-
+// One operator launch is charged SURVEY §8(d)'s bytes of ONE pass
+// (pass_bytes: X once, K N-vectors, mave/msig, K M-vectors), the work it
+// replaces being two such passes; its other traffic (p, z, d, A r, q_old and
+// the per-workgroup A d partials, < 1% at C2) is not counted as algorithmic.
 vampomi_status op_dev(vampomi_ctx* c, int K, const vk::OpArgs& a, const int* gate) {
     if (!c->have_X) return fail(VAMPOMI_ERR_STATE, "A before the methylation data was loaded");
     if (!vk::op_supported(c->N, K)) return fail(VAMPOMI_ERR_ARG, "one-pass operator: K <= 2 and K*N <= 20000");
@@ -401,15 +534,8 @@ vampomi_status op_dev(vampomi_ctx* c, int K, const vk::OpArgs& a, const int* gat
     // <d,p>: one rank into scal[SL_DP+k]; several: behind the A d block, all-reduced with it
     x.ro = vk::RedOut{c->red_part, c->use_comm ? ad + (int64_t)K * c->ld : c->scal + SL_DP, c->ticket, nullptr, 0,
                       gate};
-    TimedLaunch t = timed_launch(c, 3, K);
+    TimedLaunch t = launch_stat(c, 3, K, pass_bytes(c, K), 2.0 * pass_flops(c, K));
     HIPCHK(vk::atax(c->shard(), c->opp, K, x, c->st, vk::Timing{t.a, t.b}, gate));
-    if (t.a) {
-        t.cls = 3;
-        t.K = K;
-        t.bytes = op_bytes(c, K);
-        t.flops = 2.0 * pass_flops(c, K);
-        c->pending.push_back(t);
-    }
     c->stats.a_passes_exec++;
     vk::Ptrs os{};
     for (int k = 0; k < K; ++k) os.p[k] = ad + (int64_t)k * c->ld;
@@ -538,8 +664,9 @@ extern "C" vampomi_status vampomi_open(const vampomi_shard_desc* d, vampomi_ctx*
     STCHK(dev_alloc(&c->mbuf, (size_t)2 * vk::kMaxRhs * Mx));
     HIPCHK(hipMalloc((void**)&c->cgs, sizeof(vk::CgState)));
     HIPCHK(hipMemsetAsync(c->cgs, 0, sizeof(vk::CgState), c->st));
-    HIPCHK(hipHostMalloc((void**)&c->h_cgm, sizeof(vk::CgMirror), hipHostMallocMapped | hipHostMallocCoherent));
-    std::memset(c->h_cgm, 0, sizeof(vk::CgMirror));
+    HIPCHK(hipHostMalloc((void**)&c->h_cgm, vk::kCgMirrorSlots * sizeof(vk::CgMirror),
+                         hipHostMallocMapped | hipHostMallocCoherent));
+    std::memset(c->h_cgm, 0, vk::kCgMirrorSlots * sizeof(vk::CgMirror));
     HIPCHK(hipHostGetDevicePointer((void**)&c->d_cgm, c->h_cgm, 0));
     // VAMPOMI_FORCE_RCCL=1 runs a 1-rank job through the multi-rank code path
     // (RCCL communicator, all-reduces, post-reduce division) so that path can
@@ -579,6 +706,7 @@ extern "C" vampomi_status vampomi_sync(vampomi_ctx* c) {
 }
 
 extern "C" vampomi_status vampomi_barrier(vampomi_ctx* c) {
+    CollScope cs_(c);
     if (!c) return fail(VAMPOMI_ERR_ARG, "null context");
     if (c->use_comm) STCHK(allreduce_dev(c, c->scal + SL_BARRIER, 1));
     HIPCHK(hipStreamSynchronize(c->st));
@@ -766,6 +894,7 @@ extern "C" vampomi_status vampomi_read_markers(vampomi_ctx* c, int64_t i0, int64
 }
 
 extern "C" vampomi_status vampomi_simulate_phen(vampomi_ctx* c, uint64_t seed, double lam, double h2, double* beta_out) {
+    CollScope cs_(c);
     if (!c || !c->have_X) return fail(VAMPOMI_ERR_STATE, "load methylation data first");
     HIPCHK(hipSetDevice(c->device));
     double* beta = c->mbuf;
@@ -819,6 +948,7 @@ static vampomi_status stage_out(vampomi_ctx* c, const double* src, int64_t n, in
 }
 
 extern "C" vampomi_status vampomi_ax(vampomi_ctx* c, const double* x, double* out, int mem) {
+    CollScope cs_(c);
     if (!c || (!x && c->M > 0) || !out) return fail(VAMPOMI_ERR_ARG, "null argument");
     HIPCHK(hipSetDevice(c->device));
     STCHK(stage_in(c, x, c->M, mem, c->mbuf));
@@ -847,20 +977,30 @@ static bool host_all_zero(const double* v, int64_t n) {
     return true;
 }
 
+// Is v zero on EVERY rank?  The reference tests its local slice only
+// (src/vamp.cpp:647-648) and then skips Ax and its MPI_Allreduce: a rank whose
+// slice is zero while another's is not leaves the other ranks waiting.  Here the
+// ranks count their non-zero slices together (COLLECTIVE), so they all take the
+// same branch; on one rank this is the reference's test.
 static vampomi_status is_zero_vec(vampomi_ctx* c, const double* v, int64_t n, int mem, bool* z) {
+    bool local = true;
     if (mem == VAMPOMI_MEM_HOST) {
-        *z = host_all_zero(v, n);
-        return VAMPOMI_OK;
+        local = host_all_zero(v, n);
+    } else {
+        std::vector<double> h((size_t)std::max<int64_t>(n, 1));
+        if (n > 0) HIPCHK(hipMemcpyAsync(h.data(), v, (size_t)n * 8, hipMemcpyDeviceToHost, c->st));
+        HIPCHK(hipStreamSynchronize(c->st));
+        local = host_all_zero(h.data(), n);
     }
-    std::vector<double> h((size_t)std::max<int64_t>(n, 1));
-    if (n > 0) HIPCHK(hipMemcpyAsync(h.data(), v, (size_t)n * 8, hipMemcpyDeviceToHost, c->st));
-    HIPCHK(hipStreamSynchronize(c->st));
-    *z = host_all_zero(h.data(), n);
+    double nonzero = 0.0;
+    STCHK(sum_over_ranks(c, local ? 0.0 : 1.0, &nonzero));
+    *z = nonzero == 0.0;
     return VAMPOMI_OK;
 }
 
 extern "C" vampomi_status vampomi_lmmse_mult(vampomi_ctx* c, const double* v, double tau, double gam2, double* out,
                                              int mem) {
+    CollScope cs_(c);
     if (!c || (c->M > 0 && (!v || !out))) return fail(VAMPOMI_ERR_ARG, "null argument");
     HIPCHK(hipSetDevice(c->device));
     bool zero = false;
@@ -882,6 +1022,7 @@ extern "C" vampomi_status vampomi_lmmse_mult(vampomi_ctx* c, const double* v, do
 
 extern "C" vampomi_status vampomi_pcg(vampomi_ctx* c, const double* v, const double* mu0, double tau, double gam2,
                                       int onsager, int max_iter, double tol, double* mu, int* iters, int mem) {
+    CollScope cs_(c);
     if (!c || (c->M > 0 && (!v || !mu))) return fail(VAMPOMI_ERR_ARG, "null argument");
     HIPCHK(hipSetDevice(c->device));
     const int64_t Mx = std::max<int64_t>(c->M, 1);
@@ -895,8 +1036,8 @@ extern "C" vampomi_status vampomi_pcg(vampomi_ctx* c, const double* v, const dou
     s.d = w + 5 * Mx;
     s.onsager = onsager != 0;
     STCHK(stage_in(c, v, c->M, mem, w));
-    bool zero = true;
-    if (mu0) STCHK(is_zero_vec(c, mu0, c->M, mem, &zero));
+    bool zero = true;  // no mu0 on this rank: zeros (still counted with the others)
+    if (mu0 || c->use_comm) STCHK(is_zero_vec(c, mu0, mu0 ? c->M : 0, mem, &zero));
     s.mu0_nonzero = !zero;
     if (zero)
         HIPCHK(hipMemsetAsync(s.mu, 0, (size_t)Mx * 8, c->st));
@@ -911,6 +1052,7 @@ extern "C" vampomi_status vampomi_pcg(vampomi_ctx* c, const double* v, const dou
 
 extern "C" vampomi_status vampomi_denoise(vampomi_ctx* c, const double* r1, double gam1, const double* probs,
                                           const double* vars, int L, double* x1, double* x1d, double* sum_d, int mem) {
+    CollScope cs_(c);
     if (!c || !probs || !vars || L < 1 || L > VAMPOMI_MAX_L) return fail(VAMPOMI_ERR_ARG, "bad argument");
     HIPCHK(hipSetDevice(c->device));
     const int64_t Mx = std::max<int64_t>(c->M, 1);
@@ -959,6 +1101,7 @@ extern "C" vampomi_status vampomi_denoise_bin(vampomi_ctx* c, const double* p1, 
 // data::pvals_loo src/data.cpp:385-417).  COLLECTIVE (one A.x).
 extern "C" vampomi_status vampomi_assoc_loo(vampomi_ctx* c, const double* est, double* pvals, double* stats,
                                             int mem) {
+    CollScope cs_(c);
     if (!c || (!est && c->M > 0)) return fail(VAMPOMI_ERR_ARG, "null argument");
     if (!c->have_X || !c->have_y) return fail(VAMPOMI_ERR_STATE, "load methylation data and phenotype first");
     HIPCHK(hipSetDevice(c->device));
@@ -975,17 +1118,11 @@ extern "C" vampomi_status vampomi_assoc_loo(vampomi_ctx* c, const double* est, d
     STCHK(ax_dev(c, 1, xs, z1));                                     // :257
     HIPCHK(vk::axpby(N, 1.0, c->y, -1.0, z1, ymod, c->st));          // y_mod = y - z1 (data.cpp:390-391)
     if (ld > N) HIPCHK(hipMemsetAsync(ymod + N, 0, (size_t)(ld - N) * 8, c->st));
-    TimedLaunch t = timed_launch(c, 2, 1);
-    HIPCHK(vk::loo_sums(c->shard(), ymod, x1, std::sqrt((double)N), st, c->st, vk::Timing{t.a, t.b}));  // :393-416
-    if (t.a) {
-        t.cls = 2;
-        t.K = 1;
-        // raw X once, ymod, x1, the five sums; per element 1 div, 2 mul + 1 add
-        // for ym, 5 accumulations (3 of them products)
-        t.bytes = 8.0 * (double)N * (double)M + 8.0 * (double)N + 8.0 * 6.0 * (double)M;
-        t.flops = 11.0 * (double)N * (double)M;
-        c->pending.push_back(t);
-    }
+    // raw X once, ymod, x1, the five sums; per element 1 div, 2 mul + 1 add
+    // for ym, 5 accumulations (3 of them products)
+    TimedLaunch t = launch_stat(c, 2, 1, 8.0 * (double)N * (double)M + 8.0 * (double)N + 8.0 * 6.0 * (double)M,
+                                11.0 * (double)N * (double)M);
+    HIPCHK(vk::loo_sums(c->shard(), ymod, x1, std::sqrt((double)N), st, c->st, c->loo_variant, vk::Timing{t.a, t.b}));  // :393-416
     c->stats.a_passes_exec++;
     HIPCHK(vk::loo_pvals(M, st, (int)N, pv, c->st));
     if (stats) STCHK(stage_out(c, st, 5 * M, mem, stats));
@@ -999,6 +1136,7 @@ extern "C" vampomi_status vampomi_assoc_loo(vampomi_ctx* c, const double* est, d
 // squared correlation on the context's (test) data set.  COLLECTIVE (one A.x).
 extern "C" vampomi_status vampomi_test_metrics(vampomi_ctx* c, const double* est, double* r2, double* corr2,
                                                int mem) {
+    CollScope cs_(c);
     if (!c || (!est && c->M > 0)) return fail(VAMPOMI_ERR_ARG, "null argument");
     if (!c->have_X || !c->have_y) return fail(VAMPOMI_ERR_STATE, "load methylation data and phenotype first");
     HIPCHK(hipSetDevice(c->device));
@@ -1049,6 +1187,13 @@ extern "C" vampomi_status vampomi_get_stats(vampomi_ctx* c, vampomi_stats* out) 
     HIPCHK(hipStreamSynchronize(c->st));
     resolve_timing(c);
     *out = c->stats;
+    // estimated device time of every launch: the sampled average x the exact count
+    auto fill = [](vampomi_kernel_stat& x) {
+        x.ms_total = x.timed > 0 ? x.ms_timed / (double)x.timed * (double)x.launches : 0.0;
+    };
+    for (vampomi_kernel_stat* x : {&out->ax, &out->atx, &out->loo, &out->op}) fill(*x);
+    for (int k = 0; k < 4; ++k)
+        for (vampomi_kernel_stat* x : {&out->ax_k[k], &out->atx_k[k], &out->op_k[k]}) fill(*x);
     return VAMPOMI_OK;
 }
 
@@ -1068,17 +1213,19 @@ extern "C" vampomi_status vampomi_dev_set_variant(vampomi_ctx* c, int which, int
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipStreamSynchronize(c->st));
     if (which == 0) {
-        if (!vk::set_ax_variant(variant)) return fail(VAMPOMI_ERR_ARG, "no such A.x variant");
-        const vk::AxPlan np = vk::ax_plan(c->N, std::max<int64_t>(c->M, 1));
+        if (!vk::ax_variant_ok(variant)) return fail(VAMPOMI_ERR_ARG, "no such A.x variant");
+        const vk::AxPlan np = vk::ax_plan(c->N, std::max<int64_t>(c->M, 1), variant);
         if (np.nslots > c->axp.nslots) {
             dev_free(c->ax_part);
             STCHK(dev_alloc(&c->ax_part, (size_t)np.nslots * vk::kMaxRhs * c->ld));
         }
         c->axp = np;
     } else if (which == 1) {
-        if (!vk::set_atx_variant(variant)) return fail(VAMPOMI_ERR_ARG, "no such A^T.u variant");
+        if (!vk::atx_variant_ok(variant)) return fail(VAMPOMI_ERR_ARG, "no such A^T.u variant");
+        c->atx_variant = variant;
     } else {
-        if (!vk::set_loo_variant(variant)) return fail(VAMPOMI_ERR_ARG, "no such association-pass variant");
+        if (!vk::loo_variant_ok(variant)) return fail(VAMPOMI_ERR_ARG, "no such association-pass variant");
+        c->loo_variant = variant;
     }
     return VAMPOMI_OK;
 }
@@ -1104,7 +1251,7 @@ extern "C" vampomi_status vampomi_dev_time_pass(vampomi_ctx* c, int which, int K
         if (which == 0)
             HIPCHK(vk::ax_partial(c->shard(), c->axp, K, in, c->ax_part, c->st));
         else if (which == 1)
-            HIPCHK(vk::atx(c->shard(), K, in, out, 1.0 / c->sqrtN, 0, 0.0, 0.0, vk::CPtrs{}, c->st));
+            HIPCHK(vk::atx(c->shard(), K, in, out, 1.0 / c->sqrtN, 0, 0.0, 0.0, vk::CPtrs{}, c->st, c->atx_variant));
         else if (which == 3) {  // the operator on q = nbuf/1, p = mbuf slots 0..1, d into slots 2..3
             vk::OpArgs x{};
             for (int k = 0; k < K; ++k) {
@@ -1120,7 +1267,7 @@ extern "C" vampomi_status vampomi_dev_time_pass(vampomi_ctx* c, int which, int K
             HIPCHK(vk::atax(c->shard(), c->opp, K, x, c->st));
         }
         else  // association pass: ymod = nbuf slot 0, x1 = mbuf slot 0, sums in mbuf slots 3..7
-            HIPCHK(vk::loo_sums(c->shard(), c->nbuf, c->mbuf, c->sqrtN, c->mbuf + 3 * Mx, c->st));
+            HIPCHK(vk::loo_sums(c->shard(), c->nbuf, c->mbuf, c->sqrtN, c->mbuf + 3 * Mx, c->st, c->loo_variant));
     }
     HIPCHK(hipEventRecord(b, c->st));
     HIPCHK(hipEventSynchronize(b));
@@ -1132,12 +1279,14 @@ extern "C" vampomi_status vampomi_dev_time_pass(vampomi_ctx* c, int which, int K
     return VAMPOMI_OK;
 }
 
-extern "C" vampomi_status vampomi_dev_kernel_name(int which, int K, int mode, char* out, int cap) {
-    if (!out || cap < 1) return fail(VAMPOMI_ERR_ARG, "bad buffer");
+extern "C" vampomi_status vampomi_dev_kernel_name(const vampomi_ctx* c, int which, int K, int mode, char* out,
+                                                  int cap) {
+    if (!c || !out || cap < 1) return fail(VAMPOMI_ERR_ARG, "bad argument");
     // which = 3: mode carries N (the operator's instantiation depends on it)
-    const std::string n = which == 2   ? vk::loo_kernel_name()
+    const std::string n = which == 2   ? vk::loo_kernel_name(c->loo_variant)
                           : which == 3 ? vk::op_kernel_name(K, mode)
-                                       : vk::kernel_name(which, K, mode);
+                          : which == 0 ? vk::kernel_name(0, K, mode, c->axp.variant)
+                                       : vk::kernel_name(1, K, mode, c->atx_variant);
     std::snprintf(out, (size_t)cap, "%s", n.c_str());
     return VAMPOMI_OK;
 }

@@ -9,7 +9,11 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <chrono>
 #include <fstream>
+#include <thread>
+
+#include <sys/stat.h>
 
 namespace vio {
 
@@ -136,5 +140,56 @@ bool csv_write_row(const std::string& path, int it, const double* vals, int n) {
     ::close(fd);
     return w == (ssize_t)row.size();
 }
+
+static const char kRdzvMagic[] = "VAMPOMI-RDZV1";
+
+std::string rdzv_nonce() {
+    for (const char* v : {"VAMPOMI_RUN_ID", "TORCHELASTIC_RUN_ID"}) {
+        const char* e = std::getenv(v);
+        if (e && *e) return std::string(v) + "=" + e;
+    }
+    const char* a = std::getenv("MASTER_ADDR");
+    const char* p = std::getenv("MASTER_PORT");
+    if (a && p && *a && *p) return std::string("master=") + a + ":" + p;
+    return std::string();
+}
+
+// magic '\n' nonce '\n' id bytes, written to path.tmp and renamed into place
+// (readers never see a partial file); any file already at path is removed first
+bool rdzv_publish(const std::string& path, const std::string& nonce, const void* id, int nbytes) {
+    ::unlink(path.c_str());
+    const std::string tmp = path + ".tmp";
+    {
+        std::ofstream f(tmp, std::ios::binary | std::ios::trunc);
+        if (!f) return false;
+        f << kRdzvMagic << '\n' << nonce << '\n';
+        f.write((const char*)id, nbytes);
+        if (!f.good()) return false;
+    }
+    return std::rename(tmp.c_str(), path.c_str()) == 0;
+}
+
+static bool rdzv_try(const std::string& path, const std::string& nonce, double not_before, void* id, int nbytes) {
+    struct stat st;
+    if (::stat(path.c_str(), &st) != 0) return false;
+    if (nonce.empty() && (double)st.st_mtime < not_before) return false;  // an earlier job's file
+    std::ifstream f(path, std::ios::binary);
+    std::string magic, n;
+    if (!std::getline(f, magic) || magic != kRdzvMagic || !std::getline(f, n) || n != nonce) return false;
+    f.read((char*)id, nbytes);
+    return f.gcount() == nbytes;
+}
+
+bool rdzv_fetch(const std::string& path, const std::string& nonce, double not_before, void* id, int nbytes,
+                int timeout_ms) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        if (rdzv_try(path, nonce, not_before, id, nbytes)) return true;
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(timeout_ms)) return false;
+        std::this_thread::sleep_for(std::chrono::milliseconds(50));
+    }
+}
+
+void rdzv_remove(const std::string& path) { ::unlink(path.c_str()); }
 
 }  // namespace vio

@@ -59,11 +59,15 @@ struct AxPlan {
 };
 // partial slots tile t uses: the workgroups whose share meets it
 inline int64_t ax_slots(const AxPlan& p, int64_t t) { return ((t + 1) * p.sa - 1) / p.sb - (t * p.sa) / p.sb + 1; }
-AxPlan ax_plan(int64_t N, int64_t M);
+// Kernel variants (tuning tables in kernels.hip) are per-context launch
+// settings: the defaults are the measured winners, other values are
+// development hooks (tools/kbench.py, vampomi_dev_set_variant).
+constexpr int kAxDefault = 0, kAtxDefault = -1 /* per-K choice */, kLooDefault = 2;
+AxPlan ax_plan(int64_t N, int64_t M, int variant = kAxDefault);
 int ax_variant_count();
-bool set_ax_variant(int v);   // development hook (tools/kbench.py)
+bool ax_variant_ok(int v);
 int atx_variant_count();
-bool set_atx_variant(int v);
+bool atx_variant_ok(int v);
 // Optional fusion into the A.x pass (the CG direction update of the previous
 // step): with z set, the pass multiplies x_k = z_k + beta[k]*p_k, where
 // p_k is the `x` argument (every consumer of the new direction forms it the
@@ -85,13 +89,13 @@ hipError_t vec_div(int K, int64_t n, int64_t ld, Ptrs v, double div, hipStream_t
 // mode 0: out_k[i] = (msig_i * dot_k(i)) * scale
 // mode 1 (lmmse_mult): out_k[i] = ((msig_i*dot)*scale)*tau + gam2*p_k[i]
 // (<out_k, p_k> is a separate fixed-geometry reduction); gate as in AxFuse
-int atx_blocks(int64_t M, int K);
-std::string kernel_name(int which, int K, int mode);  // as rocprofv3 prints it
+int atx_blocks(int64_t M, int K, int variant);
+std::string kernel_name(int which, int K, int mode, int variant);  // as rocprofv3 prints it
 // zf/beta (mode 1, may be null): the epilogue's p_k is zf_k + beta[k]*p_k;
 // sraw (mode 1, may be null): also stores the raw product (msig_i*dot)*scale
 hipError_t atx(const Shard& s, int K, CPtrs u, Ptrs out, double scale, int mode, double tau,
-               double gam2, CPtrs p, hipStream_t st, const Timing& tm = Timing{}, const int* gate = nullptr,
-               CPtrs zf = CPtrs{}, const double* beta = nullptr, Ptrs sraw = Ptrs{});
+               double gam2, CPtrs p, hipStream_t st, int variant = kAtxDefault, const Timing& tm = Timing{},
+               const int* gate = nullptr, CPtrs zf = CPtrs{}, const double* beta = nullptr, Ptrs sraw = Ptrs{});
 
 // ---- one-pass CG operator: A^T q and A d from ONE read of X ----------------
 // A CG step needs d = tau*A^T(A p) + gam2*p.  With q = A p carried as an
@@ -208,14 +212,16 @@ hipError_t probit_p1(uint64_t seed, int64_t N, double* p1, hipStream_t st);
 // stats[5j + {0..4}] = sum X, sum X^2, sum X*ym, sum ym, sum ym^2 over the
 // samples of marker j (RAW X), ym = ymod + X / sqrtN * x1[j]  (data::pvals_loo)
 hipError_t loo_sums(const Shard& s, const double* ymod, const double* x1, double sqrtN, double* stats,
-                    hipStream_t st, const Timing& tm = Timing{});
-std::string loo_kernel_name();
+                    hipStream_t st, int variant = kLooDefault, const Timing& tm = Timing{});
+std::string loo_kernel_name(int variant);
 int loo_variant_count();
-bool set_loo_variant(int v);  // development hook (tools/kbench.py)
+bool loo_variant_ok(int v);
 // pvals[j] = linear_reg1d_pvals(stats[5j..5j+4], n)  (src/utilities.cpp:269-282)
 hipError_t loo_pvals(int64_t M, const double* stats, int n, double* pvals, hipStream_t st);
 // pvals[j] = P(N(r1_j, 1/(gam1 N)) <= 0), flipped for r1_j <= 0 (src/main_meth.cpp:231-236)
 hipError_t se_pvals(int64_t M, const double* r1, double gam1, int64_t N, double* pvals, hipStream_t st);
+// *p = v (one thread; a host value placed in stream order)
+hipError_t set_scalar(double* p, double v, hipStream_t st);
 // out = x * a
 hipError_t mul_scalar(int64_t n, const double* x, double a, double* out, hipStream_t st);
 
@@ -258,8 +264,11 @@ hipError_t cg_init(int K, int64_t M, const CgVecs& c, double diag, const RedOut&
 // Onsager and residual stops, beta) run on the device from a CgState, so the
 // host can queue the next step before this one's sums are known: every launch
 // of a step is gated on `any` (a step queued after the last system stopped
-// does nothing).  `mirror` (mapped host memory) receives any/iters, then the
-// step's flag.
+// does nothing).  `mirror` (mapped host memory, two slots) receives
+// seq/any/iters of step `it` in slot it & 1, then the step's flag.  Two slots:
+// when the host reads step i-1's decision, step i is already queued and may
+// have decided too (a gated step decides in microseconds); one shared slot let
+// ranks read different steps' decisions and issue different collectives.
 struct CgState {
     double rz[kMaxRhs], vv[kMaxRhs], prev_ons[kMaxRhs], beta[kMaxRhs];
     double gam2, tol;
@@ -267,9 +276,11 @@ struct CgState {
     int K, any;
 };
 struct CgMirror {
+    unsigned long long seq;  // the step's flag value: the slot holds that step's decision
     int any;
     int iters[kMaxRhs];
 };
+constexpr int kCgMirrorSlots = 2;
 // *dst = init (one thread)
 hipError_t cg_start(const CgState& init, CgState* dst, hipStream_t st);
 // *dst = init with rz[k], vv[k] = sums[2k], sums[2k+1] (cg_init's sums, in device memory)

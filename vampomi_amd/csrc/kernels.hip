@@ -380,14 +380,10 @@ static constexpr AxVariant kAxVariants[] = {
     {2, 8, true}, {2, 8, false}, {4, 4, true}, {4, 8, true}, {8, 4, true}, {2, 4, true}, {2, 12, true},
 };
 static constexpr int kNumAxVariants = sizeof(kAxVariants) / sizeof(kAxVariants[0]);
-static int g_ax_variant = 0;  // R=2, U=8, nontemporal (tools/kbench.py)
+// default 0: R=2, U=8, nontemporal (tools/kbench.py)
 
 int ax_variant_count() { return kNumAxVariants; }
-bool set_ax_variant(int v) {
-    if (v < 0 || v >= kNumAxVariants) return false;
-    g_ax_variant = v;
-    return true;
-}
+bool ax_variant_ok(int v) { return v >= 0 && v < kNumAxVariants; }
 
 static int device_cus() {
     int dev = 0, cus = 0;
@@ -397,9 +393,9 @@ static int device_cus() {
     return cus;
 }
 
-AxPlan ax_plan(int64_t N, int64_t M) {
+AxPlan ax_plan(int64_t N, int64_t M, int variant) {
     AxPlan p;
-    p.variant = g_ax_variant;
+    p.variant = ax_variant_ok(variant) ? variant : 0;
     p.rows = (int64_t)kBlock * kAxVariants[p.variant].R;
     p.tiles = cdiv(N, p.rows);
     p.total = p.tiles * M;
@@ -641,33 +637,28 @@ static constexpr AtxVariant kAtxVariants[] = {
     {4, 2, true}, {4, 2, false}, {2, 2, true}, {8, 2, true}, {4, 4, true}, {4, 1, true}, {8, 1, true}, {2, 4, true},
 };
 static constexpr int kNumAtxVariants = sizeof(kAtxVariants) / sizeof(kAtxVariants[0]);
-// -1: per-K choice measured on MI355X at C2 (tools/kbench.py, profiles/r01_kbench.json):
-// K=1 -> G=2,UJ=2 (6.86 TB/s); K>=2 -> G=4,UJ=4 (6.70 TB/s at K=2)
-static int g_atx_variant = -1;
-static int atx_variant_for(int K) { return g_atx_variant >= 0 ? g_atx_variant : (K == 1 ? 2 : 4); }
+// -1 (the default): per-K choice measured on MI355X at C2 (tools/kbench.py,
+// profiles/r01_kbench.json): K=1 -> G=2,UJ=2 (6.86 TB/s); K>=2 -> G=4,UJ=4 (6.70 TB/s at K=2)
+static int atx_variant_for(int variant, int K) { return variant >= 0 ? variant : (K == 1 ? 2 : 4); }
 
 int atx_variant_count() { return kNumAtxVariants; }
-bool set_atx_variant(int v) {
-    if (v < -1 || v >= kNumAtxVariants) return false;
-    g_atx_variant = v;
-    return true;
-}
+bool atx_variant_ok(int v) { return v >= -1 && v < kNumAtxVariants; }
 
 // rocprofv3 kernel name of the launch that ax_partial / atx would make now
-std::string kernel_name(int which, int K, int mode) {
+std::string kernel_name(int which, int K, int mode, int variant) {
     char b[160];
     if (which == 0) {
-        const AxVariant& v = kAxVariants[g_ax_variant];
+        const AxVariant& v = kAxVariants[ax_variant_ok(variant) ? variant : 0];
         std::snprintf(b, sizeof b, "ax_partial_kernel<%d, %d, %d, %s, %s>", K, v.R, v.U, v.NT ? "true" : "false",
                       mode == 1 ? "true" : "false");
     } else {
-        const AtxVariant& v = kAtxVariants[atx_variant_for(K)];
+        const AtxVariant& v = kAtxVariants[atx_variant_for(variant, K)];
         std::snprintf(b, sizeof b, "atx_kernel<%d, %d, %d, %d, %s>", v.G, K, mode, v.UJ, v.NT ? "true" : "false");
     }
     return b;
 }
 
-int atx_blocks(int64_t M, int K) { return (int)cdiv(M, 4 * kAtxVariants[atx_variant_for(K)].G); }
+int atx_blocks(int64_t M, int K, int variant) { return (int)cdiv(M, 4 * kAtxVariants[atx_variant_for(variant, K)].G); }
 
 template <int G, int K, int MODE, int UJ, bool NT>
 static void launch_atx(const Shard& s, CPtrs u, Ptrs out, double scale, double tau, double gam2, CPtrs p,
@@ -697,8 +688,10 @@ static bool launch_atx_v(int v, const Shard& s, CPtrs u, Ptrs out, double scale,
 }
 
 hipError_t atx(const Shard& s, int K, CPtrs u, Ptrs out, double scale, int mode, double tau, double gam2, CPtrs p,
-               hipStream_t st, const Timing& tm, const int* gate, CPtrs zf, const double* beta, Ptrs sraw) {
-    const int v = atx_variant_for(K);
+               hipStream_t st, int variant, const Timing& tm, const int* gate, CPtrs zf, const double* beta,
+               Ptrs sraw) {
+    if (!atx_variant_ok(variant)) return hipErrorInvalidValue;
+    const int v = atx_variant_for(variant, K);
     bool ok = false;
     if (mode == 0) {
         switch (K) {
@@ -1368,6 +1361,15 @@ hipError_t bernoulli(uint64_t seed, int it, int64_t S, int64_t M, double sqrtMt,
     return hipGetLastError();
 }
 
+__global__ void set_scalar_kernel(double* p, double v) {
+    if (threadIdx.x == 0) *p = v;
+}
+
+hipError_t set_scalar(double* p, double v, hipStream_t st) {
+    hipLaunchKernelGGL(set_scalar_kernel, dim3(1), dim3(64), 0, st, p, v);
+    return hipGetLastError();
+}
+
 __global__ void div_scalar_kernel(int64_t n, const double* __restrict__ x, double d, double* __restrict__ out) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i < n) out[i] = x[i] / d;
@@ -1476,8 +1478,10 @@ __device__ void cg_decide_body(CgState* cs, const double* red, int it, CgMirror*
         cs->any = any;
     }
     if (mirror) {
-        mirror->any = cs->any;
-        for (int k = 0; k < kMaxRhs; ++k) mirror->iters[k] = cs->iters[k];
+        CgMirror* m = mirror + (it & 1);
+        m->seq = seq;
+        m->any = cs->any;
+        for (int k = 0; k < kMaxRhs; ++k) m->iters[k] = cs->iters[k];
     }
     if (flag) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -1807,17 +1811,11 @@ static constexpr LooVariant kLooVariants[] = {
 static constexpr int kNumLooVariants = sizeof(kLooVariants) / sizeof(kLooVariants[0]);
 // default: G=2, UJ=2, fma-corrected division: 6.80 TB/s at the c5 shard (N=100,000 x 62,500) on
 // MI355X vs 5.63 TB/s with the IEEE division sequence (tools/kbench.py, profiles/r01_kbench_loo.json)
-static int g_loo_variant = 2;
-
 int loo_variant_count() { return kNumLooVariants; }
-bool set_loo_variant(int v) {
-    if (v < 0 || v >= kNumLooVariants) return false;
-    g_loo_variant = v;
-    return true;
-}
+bool loo_variant_ok(int v) { return v >= 0 && v < kNumLooVariants; }
 
-std::string loo_kernel_name() {
-    const LooVariant& v = kLooVariants[g_loo_variant];
+std::string loo_kernel_name(int variant) {
+    const LooVariant& v = kLooVariants[loo_variant_ok(variant) ? variant : kLooDefault];
     char b[64];
     std::snprintf(b, sizeof b, "loo_kernel<%d, %d, %s>", v.G, v.UJ, v.FD ? "true" : "false");
     return b;
@@ -1834,9 +1832,9 @@ static void launch_loo(const Shard& s, const double* ymod, const double* x1, dou
 }
 
 hipError_t loo_sums(const Shard& s, const double* ymod, const double* x1, double sqrtN, double* stats,
-                    hipStream_t st, const Timing& tm) {
+                    hipStream_t st, int variant, const Timing& tm) {
     if (s.M <= 0) return hipSuccess;
-    switch (g_loo_variant) {
+    switch (variant) {
         case 0: launch_loo<4, 2, true>(s, ymod, x1, sqrtN, stats, st, tm); break;
         case 1: launch_loo<4, 2, false>(s, ymod, x1, sqrtN, stats, st, tm); break;
         case 2: launch_loo<2, 2, true>(s, ymod, x1, sqrtN, stats, st, tm); break;

@@ -31,29 +31,28 @@ static int env_int(const char* a, const char* b, int dflt) {
     return v ? std::atoi(v) : dflt;
 }
 
-static bool exchange_id(const std::string& path, int rank, unsigned char* id) {
-    if (rank == 0) {
-        if (vampomi_comm_unique_id(id) != VAMPOMI_OK) return false;
-        const std::string tmp = path + ".tmp";
-        std::ofstream f(tmp, std::ios::binary);
-        f.write((const char*)id, VAMPOMI_UNIQUE_ID_BYTES);
-        f.close();
-        return std::rename(tmp.c_str(), path.c_str()) == 0;
-    }
-    for (int t = 0; t < 6000; ++t) {  // up to 10 minutes
-        std::ifstream f(path, std::ios::binary);
-        if (f.good()) {
-            f.read((char*)id, VAMPOMI_UNIQUE_ID_BYTES);
-            if (f.gcount() == VAMPOMI_UNIQUE_ID_BYTES) return true;
-        }
-        std::this_thread::sleep_for(std::chrono::milliseconds(100));
-    }
-    return false;
+// rank 0 publishes the RCCL id (removing any file an earlier job left there),
+// the others wait up to 10 minutes for a file of THIS job (vio::rdzv_*)
+static bool exchange_id(const std::string& path, int rank, double not_before, unsigned char* id) {
+    const std::string nonce = vio::rdzv_nonce();
+    if (rank == 0) return vampomi_comm_unique_id(id) == VAMPOMI_OK && vio::rdzv_publish(path, nonce, id, VAMPOMI_UNIQUE_ID_BYTES);
+    return vio::rdzv_fetch(path, nonce, not_before, id, VAMPOMI_UNIQUE_ID_BYTES, 600000);
 }
+
+static vampomi_ctx* g_ctx = nullptr;  // the open context: die() ends the job's communicator
 
 static int die(const char* what) {
     std::cout << "FATAL  : " << what << ": " << vampomi_last_error() << std::endl;
+    if (g_ctx) vampomi_comm_abort(g_ctx);
     return EXIT_FAILURE;
+}
+
+// a rank-local outcome every rank must share before the next collective:
+// false on every rank if it is false on any (src/main_meth.cpp exits rank-locally)
+static bool all_ok(vampomi_ctx* ctx, bool ok) {
+    int all = 0;
+    if (vampomi_all_ok(ctx, ok ? 1 : 0, &all) != VAMPOMI_OK) return false;
+    return all != 0;
 }
 
 // the iteration number of an estimate / r1 file name: the text between the
@@ -109,7 +108,8 @@ static int association_test(vampomi_ctx* ctx, const vopt::Options& opt, int rank
 // --test-iter-range, one _test.csv row each.
 static int test_run(vampomi_ctx* ctx, const vopt::Options& opt, int rank, int64_t M, int64_t S) {
     const std::string csv = opt.out_dir + "/" + opt.out_name + "_test.csv";
-    if (rank == 0 && !vio::csv_create_with_header(csv, {"iteration", "R2 test", "z correlation test"})) {
+    const bool made = rank != 0 || vio::csv_create_with_header(csv, {"iteration", "R2 test", "z correlation test"});
+    if (!all_ok(ctx, made)) {
         std::cout << "FATAL  : cannot create " << csv << std::endl;
         return EXIT_FAILURE;
     }
@@ -128,19 +128,17 @@ static int test_run(vampomi_ctx* ctx, const vopt::Options& opt, int rank, int64_
         const std::string name = est.substr(0, pos_it) + "it_" + std::to_string(it) + "." + ext;
         std::fill(x.begin(), x.end(), 0.0);
         const bool ok = ext == "bin" ? vio::read_vec(name, x.data(), S, M) : vio::read_text_vec(name, x.data(), S, M);
-        if (!ok) {
+        if (!all_ok(ctx, ok)) {
             std::cout << "FATAL  : cannot read estimate file " << name << std::endl;
             return EXIT_FAILURE;
         }
         double row[2];
         if (vampomi_test_metrics(ctx, x.data(), &row[0], &row[1], VAMPOMI_MEM_HOST) != VAMPOMI_OK)
             return die("test metrics");
-        if (rank == 0) {
-            std::cout << row[0] << ", ";
-            if (!vio::csv_write_row(csv, it, row, 2)) {
-                std::cout << "FATAL  : cannot write " << csv << std::endl;
-                return EXIT_FAILURE;
-            }
+        if (rank == 0) std::cout << row[0] << ", ";
+        if (!all_ok(ctx, rank != 0 || vio::csv_write_row(csv, it, row, 2))) {
+            std::cout << "FATAL  : cannot write " << csv << std::endl;
+            return EXIT_FAILURE;
         }
     }
     if (rank == 0) std::cout << std::endl;
@@ -171,10 +169,15 @@ int main(int argc, char** argv) {
     }
 
     unsigned char id[VAMPOMI_UNIQUE_ID_BYTES] = {0};
+    std::string rdzv_path;
+    // launch time (a job without a run nonce accepts only rendezvous files
+    // written after it, minus a margin for ranks that start late)
+    const double t_start = std::chrono::duration<double>(std::chrono::system_clock::now().time_since_epoch()).count();
     if (nranks > 1) {
         const char* rz = std::getenv("VAMPOMI_RDZV");
         const std::string path = rz ? rz : opt.out_dir + "/." + opt.out_name + ".rdzv";
-        if (!exchange_id(path, rank, id)) return die("communicator rendezvous failed");
+        if (!exchange_id(path, rank, t_start - 120.0, id)) return die("communicator rendezvous failed");
+        rdzv_path = path;
     }
     const bool test_mode = opt.run_mode == "test";  // the context holds the TEST data set (:128)
     vampomi_shard_desc d{};
@@ -187,6 +190,10 @@ int main(int argc, char** argv) {
     d.alpha_scale = opt.alpha_scale;
     vampomi_ctx* ctx = nullptr;
     if (vampomi_open(&d, &ctx) != VAMPOMI_OK) return die("cannot open the device context");
+    g_ctx = ctx;
+    // every rank has joined the communicator (its init is collective): the
+    // rendezvous file has served and must not be read by a later job
+    if (rank == 0 && !rdzv_path.empty()) vio::rdzv_remove(rdzv_path);
 
     // data::data: phenotype first (standardised for the linear model, raw 0/1
     // for bin_class, src/data.cpp:40-43), then the shard

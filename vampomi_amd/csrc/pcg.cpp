@@ -19,6 +19,7 @@
 #include <cmath>
 #include <cstddef>
 #include <cstdlib>
+#include <string>
 #include <utility>
 
 #include "ctx.h"
@@ -31,25 +32,26 @@ static T* field(vk::CgState* cs, size_t off) {
 
 // the host loop shared by both forms: queue step i+1, then wait for step i's
 // decision; a step queued after the last system stopped is dropped from the stats
+// Step i-1's decision is read from its own mirror slot ((i-1) & 1), tagged
+// with its flag value: step i, queued before the wait, writes the other slot.
+// *last: the slot of the last decided step (its iteration counts are final).
 template <class Enqueue>
-static vampomi_status cg_loop(vampomi_ctx* c, int max_iter, Enqueue&& enqueue) {
+static vampomi_status cg_loop(vampomi_ctx* c, int max_iter, Enqueue&& enqueue, const vk::CgMirror** last) {
     unsigned long long prev = 0, cur = 0;
     STCHK(enqueue(0, &prev));
     for (int i = 1;; ++i) {
         const size_t mark = c->pending.size();
-        const int64_t passes = c->stats.a_passes_exec;
+        const vampomi_stats before = c->stats;
         if (i < max_iter) STCHK(enqueue(i, &cur));
         c->stats.host_syncs++;
         STCHK(wait_flag(c, prev));  // step i-1 decided
-        if (!c->h_cgm->any || i >= max_iter) {
-            if (i < max_iter) {  // step i was queued in vain: it did nothing
-                for (size_t q = mark; q < c->pending.size(); ++q) {
-                    c->ev_pool.push_back(c->pending[q].a);
-                    c->ev_pool.push_back(c->pending[q].b);
-                }
-                c->pending.resize(mark);
-                c->stats.a_passes_exec = passes;
-            }
+        const vk::CgMirror* m = c->h_cgm + ((i - 1) & 1);
+        if (__atomic_load_n(&m->seq, __ATOMIC_ACQUIRE) != prev)
+            return fail(VAMPOMI_ERR_STATE, "CG step " + std::to_string(i - 1) + ": decision slot holds sequence " +
+                                               std::to_string(m->seq) + ", expected " + std::to_string(prev));
+        *last = m;
+        if (!m->any || i >= max_iter) {
+            if (i < max_iter) drop_launches(c, mark, before);  // step i was queued in vain: it did nothing
             break;
         }
         prev = cur;
@@ -204,9 +206,10 @@ vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double
             }
             return VAMPOMI_OK;
         };
-        STCHK(cg_loop(c, max_iter, enqueue));
+        const vk::CgMirror* last = nullptr;
+        STCHK(cg_loop(c, max_iter, enqueue, &last));
         for (int k = 0; k < K; ++k) {
-            sys[k]->iters = c->h_cgm->iters[k];
+            sys[k]->iters = last->iters[k];
             if (ref_passes) *ref_passes += 2 * (int64_t)sys[k]->iters;
         }
         return VAMPOMI_OK;
@@ -308,9 +311,10 @@ vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double
         }
         return VAMPOMI_OK;
     };
-    STCHK(cg_loop(c, max_iter, enqueue));
+    const vk::CgMirror* last = nullptr;
+    STCHK(cg_loop(c, max_iter, enqueue, &last));
     for (int k = 0; k < K; ++k) {
-        sys[k]->iters = c->h_cgm->iters[k];
+        sys[k]->iters = last->iters[k];
         if (ref_passes) *ref_passes += 2 * (int64_t)sys[k]->iters;
     }
     return VAMPOMI_OK;

@@ -48,8 +48,11 @@ vampomi_status probit_begin(vampomi_ctx* c, VampRun& R) {
         R.p_prior = R.out_dir + "/" + R.out_name + "_prior.csv";
         // setup_io (src/vamp.cpp:854-882); infere_bin_class writes no header
         if (c->rank == 0 &&
-            !(vio::csv_create(R.p_metrics) && vio::csv_create(R.p_params) && vio::csv_create(R.p_prior)))
-            return fail(VAMPOMI_ERR_IO, "cannot create output CSV files in " + R.out_dir);
+            !(vio::csv_create(R.p_metrics) && vio::csv_create(R.p_params) && vio::csv_create(R.p_prior))) {
+            R.io_err = true;
+            R.io_msg = "cannot create output CSV files in " + R.out_dir;
+        }
+        STCHK(agree_io(c, R));
     }
     return VAMPOMI_OK;
 }
@@ -215,9 +218,12 @@ vampomi_status probit_step(vampomi_ctx* c, VampRun& R) {
                                             sizeof prior);
     if (R.write && c->rank == 0) {  // :430-435
         if (!vio::csv_write_row(R.p_params, it, R.params, 8) || !vio::csv_write_row(R.p_metrics, it, R.metrics, 12) ||
-            !vio::csv_write_row(R.p_prior, it, prior, np))
-            return fail(VAMPOMI_ERR_IO, "cannot write CSV rows");
+            !vio::csv_write_row(R.p_prior, it, prior, np)) {
+            R.io_err = true;
+            R.io_msg = "cannot write CSV rows";
+        }
     }
+    if (R.write) STCHK(agree_io(c, R));  // write_bins' and the rows' failures, on every rank at once
     if (R.prm.verbosity >= 1 && c->rank == 0)
         std::printf("it %d: alpha1 %.6g beta1 %.6g gam1 %.6g tau1 %.6g alpha2 %.6g beta2 %.6g L %d cg %d/%d\n", it,
                     R.alpha1, R.beta1, R.gam1, R.tau1, R.alpha2, R.beta2, R.mix.L, sx.iters, so.iters);

@@ -29,6 +29,11 @@ struct VampRun {
     std::string out_dir, out_name, p_params, p_metrics, p_prior;
     int it = 0;
     bool stopped = false;
+    // a file write failed on this rank: reported on every rank by agree_io, so
+    // the ranks leave the collective sequence together (src/vamp.cpp writes
+    // rank-locally; a rank that stopped there would leave the others waiting)
+    bool io_err = false;
+    std::string io_msg;
     Mixture mix, mix_next;
     bool have_next = false;  // x1n, alpha1_next, mix_next, z1 (nb3 slot 2), atx0 valid
     double gam1 = 0, gam2 = 0, gamw = 0;
@@ -73,6 +78,8 @@ vampomi_status denoise_into(vampomi_ctx* c, const Mixture& m, double gam1, const
                             const double* x1_prev, bool damp, double rho, double* x1d, DotBatch& b, double* sum_out);
 vampomi_status upload_or_zero(vampomi_ctx* c, double* dst, const double* host, int64_t n);
 vampomi_status write_bins(vampomi_ctx* c, VampRun& R);
+// a rank-local I/O failure (R.io_err) becomes every rank's ERR_IO. COLLECTIVE
+vampomi_status agree_io(vampomi_ctx* c, VampRun& R);
 // probit.cpp
 vampomi_status probit_begin(vampomi_ctx* c, VampRun& R);
 vampomi_status probit_step(vampomi_ctx* c, VampRun& R);

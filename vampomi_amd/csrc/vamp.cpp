@@ -196,6 +196,7 @@ static vampomi_status vamp_alloc(vampomi_ctx* c, VampRun& R) {
 }
 
 extern "C" vampomi_status vampomi_vamp_begin(vampomi_ctx* c, const vampomi_params* p, vampomi_result* r) {
+    CollScope cs_(c);
     if (!c || !p) return fail(VAMPOMI_ERR_ARG, "null argument");
     if (!c->have_X || !c->have_y) return fail(VAMPOMI_ERR_STATE, "load methylation data and phenotype first");
     const bool probit = p->model && std::strcmp(p->model, "bin_class") == 0;
@@ -260,8 +261,12 @@ extern "C" vampomi_status vampomi_vamp_begin(vampomi_ctx* c, const vampomi_param
                                                           "z2 correlation LMMSE"}) &&
                 vio::csv_create_with_header(R.p_params, {"iteration", "alpha1", "gam1", "alpha2", "gam2", "gamw"}) &&
                 vio::csv_create_with_header(R.p_prior, prior_h);
-            if (!ok) return fail(VAMPOMI_ERR_IO, "cannot create output CSV files in " + R.out_dir);
+            if (!ok) {
+                R.io_err = true;
+                R.io_msg = "cannot create output CSV files in " + R.out_dir;
+            }
         }
+        STCHK(agree_io(c, R));
     }
     if (r) {
         r->iterations_run = 0;
@@ -290,14 +295,26 @@ vampomi_status write_bins(vampomi_ctx* c, VampRun& R) {
     if (R.write) {
         const std::string base = R.out_dir + "/" + R.out_name;
         if (!vio::store_vec(base + "_it_" + std::to_string(R.it) + ".bin", hx.data(), c->S, M) ||
-            !vio::store_vec(base + "_r1_it_" + std::to_string(R.it) + ".bin", hr.data(), c->S, M))
-            return fail(VAMPOMI_ERR_IO, "cannot write iteration vectors to " + R.out_dir);
+            !vio::store_vec(base + "_r1_it_" + std::to_string(R.it) + ".bin", hr.data(), c->S, M)) {
+            R.io_err = true;  // reported by agree_io at the end of the iteration
+            R.io_msg = "cannot write iteration vectors to " + R.out_dir;
+        }
     }
+    return VAMPOMI_OK;
+}
+
+vampomi_status agree_io(vampomi_ctx* c, VampRun& R) {
+    double bad = 0.0;
+    STCHK(sum_over_ranks(c, R.io_err ? 1.0 : 0.0, &bad));
+    if (bad > 0)
+        return fail(VAMPOMI_ERR_IO, R.io_err ? R.io_msg
+                                             : "output file write failed on " + std::to_string((int)bad) + " other rank(s)");
     return VAMPOMI_OK;
 }
 
 // one VAMP iteration (src/vamp.cpp:148-428)
 extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
+    CollScope cs_(c);
     if (!c || !c->run) return fail(VAMPOMI_ERR_STATE, "vampomi_vamp_begin not called");
     VampRun& R = *c->run;
     if (R.stopped || R.it >= R.prm.max_iter) {
@@ -467,9 +484,12 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
     if (res && res->params) std::memcpy(res->params + (int64_t)(it - 1) * 5, R.params, 5 * sizeof(double));
     if (res && res->metrics) std::memcpy(res->metrics + (int64_t)(it - 1) * 6, R.metrics, 6 * sizeof(double));
     if (R.write && c->rank == 0) {  // :388-393
-        if (!vio::csv_write_row(R.p_params, it, R.params, 5) || !vio::csv_write_row(R.p_metrics, it, R.metrics, 6))
-            return fail(VAMPOMI_ERR_IO, "cannot write CSV rows");
+        if (!vio::csv_write_row(R.p_params, it, R.params, 5) || !vio::csv_write_row(R.p_metrics, it, R.metrics, 6)) {
+            R.io_err = true;
+            R.io_msg = "cannot write CSV rows";
+        }
     }
+    if (R.write) STCHK(agree_io(c, R));  // write_bins' and the rows' failures, on every rank at once
     if (R.prm.verbosity >= 1 && c->rank == 0)
         std::printf("it %d: alpha1 %.6g gam1 %.6g alpha2 %.6g gam2 %.6g gamw %.6g L %d cg %d/%d\n", it, R.alpha1,
                     R.gam1, R.alpha2, R.gam2, R.gamw, R.mix.L, sx.iters, so.iters);
@@ -515,6 +535,7 @@ extern "C" vampomi_status vampomi_vamp_end(vampomi_ctx* c) {
 }
 
 extern "C" vampomi_status vampomi_infere(vampomi_ctx* c, const vampomi_params* p, vampomi_result* r) {
+    CollScope cs_(c);
     STCHK(vampomi_vamp_begin(c, p, r));
     int stopped = 0;
     while (!stopped) {
@@ -562,6 +583,7 @@ extern "C" void vampomi_params_default(vampomi_params* p) {
 extern "C" vampomi_status vampomi_update_prior(vampomi_ctx* c, const double* r1, double gam1, int* L, double* probs,
                                                double* vars, int EM_max_iter, double EM_err_thr, int learn_vars,
                                                double merge_vars_thr, int mem) {
+    CollScope cs_(c);
     if (!c || !L || !probs || !vars || (!r1 && c->M > 0)) return fail(VAMPOMI_ERR_ARG, "null argument");
     if (*L < 1 || *L > VAMPOMI_MAX_L) return fail(VAMPOMI_ERR_ARG, "number of mixture components out of range");
     HIPCHK(hipSetDevice(c->device));

@@ -16,6 +16,10 @@ c4full: configs[3] whole (N=50,000 x Mt=200,000, 80 GB) on any number of
 c5: LOO association test (configs[4], --run-mode association_test
     --pval-method loo): N=100,000 with 62,500 methylation-like markers per
     GPU; n=8 is exactly N=100,000 x Mt=500,000.
+c3full: configs[2] itself, N=100,000 x Mt=500,000 methylation-like (400 GB),
+    fixed, markers sharded over n >= 2 GPUs (strong scaling: 200 GB per GPU at
+    n = 2, 50 GB at n = 8).  It does not fit one MI355X (288 GB).
+auto: the bench default, c2 at n = 1 and c3full at n > 1.
 c3big: configs[2]'s samples with 300,000 methylation-like markers per GPU,
     i.e. 240 GB of the 288 GB HBM3E resident on one MI355X (the
     1-GPU row at a reduced Mt); n=2 covers Mt=600,000 > configs[2]'s 500,000.
@@ -26,6 +30,13 @@ GEN_GAUSS, GEN_METH = 0, 1
 
 
 def workload(cfg: str, n: int) -> dict:
+    if cfg == "auto":
+        cfg = "c2" if n == 1 else "c3full"
+    if cfg == "c3full":
+        if n < 2:
+            raise ValueError("c3full (400 GB) needs n >= 2 GPUs; at n = 1 use c2 or c3big")
+        return {"workload": "c3full", "N": 100000, "Mt": 500000, "kind": GEN_METH, "model": "linear",
+                "scaling": "strong"}
     if cfg == "c3":
         return {"workload": "c3-shard", "N": 100000, "Mt": 62500 * n, "kind": GEN_METH, "model": "linear"}
     if cfg == "c4":
