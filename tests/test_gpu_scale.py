@@ -1,0 +1,198 @@
+"""GPU parity at the BASELINE configs' own sizes (VERDICT r01 "configs
+untested"), plus the CLI on files the reference itself wrote.
+
+* C3's samples, N = 100,000 methylation-like (configs[2]/[4]):
+  - against the oracle at a reduced Mt (the oracle finishes in seconds):
+    x1_hat / r1 within 1e-10 norm-relative per iteration, iteration / CG /
+    Onsager / mixture counts exact;
+  - the full 62,500-marker per-GPU shard (50 GB): the production schedule and
+    batch_rhs 3 against batch_rhs 1 (bitwise the reference's sequential
+    order, tests/test_gpu_parity.py) within 1e-11, counts equal;
+  - the same shard split over two ranks (loopback communicator) against the
+    one-rank run.
+* C2 (configs[1], N = 10,000 x Mt = 50,000) whole, with the production
+  one-pass CG operator (batch_rhs 4), against the oracle for 6 iterations.
+* main_meth.exe on tests/golden/datasim.* (written by the reference's
+  simulation/data_sim.py) against tests/golden/oracle_datasim.npz.
+"""
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import relerr
+from _data import make_problem
+from test_gpu_sharded import run_ranks
+
+pytestmark = pytest.mark.gpu
+
+va = pytest.importorskip("vampomi_amd")
+from oracle import pyoracle as O  # noqa: E402  (checker)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+G = os.path.join(HERE, "golden")
+
+
+def _run(d, y=None, beta=None, **kw):
+    if y is not None:
+        d.set_phen(y, standardize=False)
+    v = va.Vamp(d, va.VampOptions(**kw), true_signal=beta)
+    v.infere(keep_hist=True)
+    s = v.summary()
+    n = s["iterations"]
+    s["x1_hist"], s["r1_hist"] = v.x1_hist[:n, :d.M].copy(), v.r1_hist[:n, :d.M].copy()
+    return s
+
+
+def _counts_equal(a, b):
+    assert a["iterations"] == b["iterations"]
+    assert list(a["cg_iters"]) == list(b["cg_iters"]), (a["cg_iters"], b["cg_iters"])
+    assert list(a["ons_iters"]) == list(b["ons_iters"]), (a["ons_iters"], b["ons_iters"])
+    assert list(a["L"]) == list(b["L"])
+
+
+def test_c3_samples_reduced_markers_vs_oracle():
+    N, Mt, its = 100000, 2000, 8
+    X, y, beta = make_problem(N, Mt, seed=7, kind=1)
+    kw = dict(max_iter=its, stop_criteria_thr=0.0)
+    ref = O.vamp_infere(X, y, Mt, true_signal=beta, **kw)
+    with va.Data(N, Mt) as d:
+        d.load_meth(X)
+        s = _run(d, y, beta, **kw)
+    _counts_equal(s, ref)
+    for k in range(its):
+        assert relerr(s["x1_hist"][k], ref["x1_hist"][k]) <= 1e-10, k
+        assert relerr(s["r1_hist"][k], ref["r1_hist"][k]) <= 1e-10, k
+    assert np.allclose(np.array(s["params"]), ref["params"], rtol=1e-9, atol=0)
+
+
+C3_SHARD = dict(N=100000, Mt=62500, its=6, seed=20250711)
+
+
+@pytest.fixture(scope="module")
+def c3_shard_runs():
+    """The full per-GPU C3 shard on one rank, for batch_rhs 1, 3 and the default."""
+    c = C3_SHARD
+    out = {}
+    with va.Data(c["N"], c["Mt"]) as d:
+        d.generate(c["seed"], va.GEN_METH)
+        beta = d.simulate_phen(c["seed"] + 1, lam=0.1, h2=0.8)
+        for b in (1, 3, va.VampOptions().batch_rhs):
+            out[b] = _run(d, None, beta, max_iter=c["its"], stop_criteria_thr=0.0, batch_rhs=b)
+    out["beta"] = beta
+    return out
+
+
+def test_c3_full_shard_schedules_agree(c3_shard_runs):
+    base = c3_shard_runs[1]  # the reference's sequential order, bit for bit (batch_rhs 0 == 1)
+    for b in sorted(k for k in c3_shard_runs if k not in (1, "beta")):
+        s = c3_shard_runs[b]
+        _counts_equal(s, base)
+        for k in range(s["iterations"]):
+            assert relerr(s["x1_hist"][k], base["x1_hist"][k]) <= 1e-11, (b, k)
+            assert relerr(s["r1_hist"][k], base["r1_hist"][k]) <= 1e-11, (b, k)
+    assert all(c >= 1 for c in base["cg_iters"])
+
+
+def test_c3_full_shard_two_ranks(monkeypatch, c3_shard_runs):
+    c = C3_SHARD
+    one = c3_shard_runs[va.VampOptions().batch_rhs]
+
+    def fn(r, d):
+        d.generate(c["seed"], va.GEN_METH)  # index-keyed: each rank generates its own columns
+        beta = d.simulate_phen(c["seed"] + 1, lam=0.1, h2=0.8)
+        return _run(d, None, beta, max_iter=c["its"], stop_criteria_thr=0.0)
+
+    parts = run_ranks(monkeypatch, 2, c["N"], c["Mt"], fn, timeout=400)
+    for p in parts:
+        _counts_equal(p, one)
+    for k in range(one["iterations"]):
+        assert relerr(np.concatenate([p["x1_hist"][k] for p in parts]), one["x1_hist"][k]) <= 1e-12, k
+        assert relerr(np.concatenate([p["r1_hist"][k] for p in parts]), one["r1_hist"][k]) <= 1e-12, k
+
+
+def test_c2_whole_production_schedule_vs_oracle():
+    N, Mt, its = 10000, 50000, 6
+    X, y, beta = make_problem(N, Mt, seed=11)
+    kw = dict(max_iter=its, stop_criteria_thr=0.0)
+    ref = O.vamp_infere(X, y, Mt, true_signal=beta, **kw)
+    with va.Data(N, Mt) as d:
+        d.load_meth(X)
+        del X
+        s = _run(d, y, beta, **kw)  # batch_rhs default: the one-pass CG operator at this shape
+        st = d.stats()
+    assert va.VampOptions().batch_rhs == 4 and st.op.launches > 0, "the one-pass operator did not run"
+    _counts_equal(s, ref)
+    for k in range(its):
+        assert relerr(s["x1_hist"][k], ref["x1_hist"][k]) <= 1e-10, k
+        assert relerr(s["r1_hist"][k], ref["r1_hist"][k]) <= 1e-10, k
+
+
+def test_cli_on_reference_written_files(tmp_path):
+    """main_meth.exe reads the files data_sim.py wrote (marker-major .bin, PLINK
+    .phen, _ts.bin) through the device readers and reproduces the oracle's run
+    on them: _it_K.bin / _r1_it_K.bin within 1e-10, CSV rows within 1e-9, the
+    per-iteration CG / Onsager counts exact."""
+    z = np.load(os.path.join(G, "oracle_datasim.npz"))
+    its = int(z["its"])
+    vars_ = ",".join(repr(v) for v in O.DEFAULT_VARS)
+    probs = ",".join(repr(v) for v in O.DEFAULT_PROBS)
+    r = subprocess.run([va.CLI_PATH, "--meth-file", os.path.join(G, "datasim.bin"),
+                        "--phen-file", os.path.join(G, "datasim.phen"),
+                        "--true-signal-file", os.path.join(G, "datasim_ts.bin"), "--N", "100", "--Mt", "200",
+                        "--iterations", str(its), "--stop-criteria-thr", str(float(z["thr"])), "--vars", vars_,
+                        "--probs", probs, "--seed", str(0x5EED5EED), "--out-dir", str(tmp_path), "--out-name", "g"],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+    counts = [tuple(map(int, m)) for m in re.findall(r"it \d+: CG iterations (\d+), onsager CG iterations (\d+)",
+                                                     r.stdout)]
+    assert [c[0] for c in counts] == z["cg_iters"].tolist()
+    assert [c[1] for c in counts] == z["ons_iters"].tolist()
+    for q, k in enumerate(z["keep_its"]):
+        x1 = np.fromfile(tmp_path / f"g_it_{k}.bin", dtype="<f8")
+        r1 = np.fromfile(tmp_path / f"g_r1_it_{k}.bin", dtype="<f8")
+        assert relerr(x1, z["x1"][q]) <= 1e-10, k
+        assert relerr(r1, z["r1"][q]) <= 1e-10, k
+
+    def rows(b):
+        lines = bytes(b).decode().replace("\0", "").splitlines()[1:]
+        return np.array([[float(t) for t in ln.split(",")] for ln in lines if ln.strip()])
+
+    for name in ("params", "metrics"):
+        got = rows(open(tmp_path / f"g_{name}.csv", "rb").read())
+        want = rows(z[f"csv_{name}"])
+        assert got.shape == want.shape
+        assert np.allclose(got, want, rtol=1e-9, atol=1e-12, equal_nan=True), name
+
+
+@pytest.mark.parametrize("name", ["datasim", "gen"])
+def test_device_operators_vs_reference_outputs(name):
+    """Device marker statistics, A.x and A^T.u against the REFERENCE's own
+    src/data.cpp outputs (tests/golden/ref_data_pin.npz, tests/test_ref_pin.py):
+    1e-13 relative (fixed-order device reductions vs the reference's OpenMP ones)."""
+    import sys
+
+    sys.path.insert(0, G)
+    from make_ref_golden import case_matrix, probe_vectors
+
+    pin = np.load(os.path.join(G, "ref_data_pin.npz"))
+    X = case_matrix(name)
+    M, N = X.shape
+    x, u = probe_vectors(N, M)
+    for a, tag in ((1.0, ""), (0.7, "_a07")):
+        with va.Data(N, M, alpha_scale=a) as d:
+            if name == "datasim":
+                d.read_methylation_data(os.path.join(G, "datasim.bin"))  # the device reader on the reference's file
+            else:
+                d.load_meth(X)
+            assert relerr(d.get_mave(), pin[f"{name}_mave{tag}"]) <= 1e-13
+            assert relerr(d.get_msig(), pin[f"{name}_msig{tag}"]) <= 1e-13
+            if a == 1.0:
+                assert relerr(d.Ax(x), pin[f"{name}_ax"]) <= 1e-13
+                assert relerr(d.ATx(u), pin[f"{name}_atx"]) <= 1e-13
+                if name == "datasim":
+                    for s in (0, 1):
+                        d.read_phen(os.path.join(G, "datasim.phen"), standardize=bool(s))
+                        assert np.array_equal(d.get_phen(), pin[f"datasim_phen_std{s}"]), s

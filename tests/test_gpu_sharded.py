@@ -143,3 +143,65 @@ def test_sharded_association_and_test_mode(monkeypatch):
     for r in res:
         assert abs(r[2][0] - ro) <= 1e-12 * abs(ro) and abs(r[2][1] - co) <= 1e-12 * abs(co)
     assert np.allclose(np.concatenate([r[3] for r in res]), O.assoc_se(est, 2.0, N), rtol=1e-14, atol=1e-16)
+
+
+def _run_ranks_collect(monkeypatch, P, N, Mt, fn, timeout=60):
+    """Like run_ranks, but returns each rank's exception (or None) instead of asserting."""
+    monkeypatch.setenv("VAMPOMI_COMM", "loopback")
+    cid = os.urandom(va.UNIQUE_ID_BYTES)
+    errs = [None] * P
+
+    def work(r):
+        try:
+            with va.Data(N, Mt, rank=r, nranks=P, comm_id=cid, device=0) as d:
+                fn(r, d)
+        except BaseException as e:  # noqa: BLE001 - returned
+            errs[r] = e
+
+    th = [threading.Thread(target=work, args=(r,), daemon=True) for r in range(P)]
+    [t.start() for t in th]
+    deadline = time.monotonic() + timeout
+    [t.join(max(0.0, deadline - time.monotonic())) for t in th]
+    assert not [r for r, t in enumerate(th) if t.is_alive()], "a rank is still waiting"
+    return errs
+
+
+def test_rank_local_failure_releases_the_other_ranks(monkeypatch):
+    """A collective entry point that fails on one rank (here an argument error
+    in updatePrior) poisons the communicator: the rank waiting in its own
+    collective fails at once with the cause, instead of after a timeout."""
+    N, Mt = 300, 500
+    X, _, _ = make_problem(N, Mt)
+
+    def fn(r, d):
+        d.load_meth(X[d.S:d.S + d.M])
+        if r == 1:
+            time.sleep(0.5)  # rank 0 is inside its all-reduce by now
+            d.update_prior(np.zeros(d.M), 1.0, [], [])  # L = 0: ERR_ARG on this rank only
+        else:
+            d.Ax(np.ones(d.M))
+
+    t0 = time.monotonic()
+    errs = _run_ranks_collect(monkeypatch, 2, N, Mt, fn)
+    assert time.monotonic() - t0 < 30
+    assert isinstance(errs[1], va.VampomiError) and "mixture components" in str(errs[1])
+    assert isinstance(errs[0], va.VampomiError) and "rank 1 aborted" in str(errs[0]), errs[0]
+
+
+def test_divergent_collectives_fail_on_every_rank(monkeypatch):
+    """Ranks that issue different collectives (sequence, size or call site)
+    fail together, each naming every rank's collective."""
+    N, Mt = 300, 500
+    X, _, _ = make_problem(N, Mt)
+
+    def fn(r, d):
+        d.load_meth(X[d.S:d.S + d.M])
+        if r == 0:
+            d.Ax(np.ones(d.M))  # the A.x all-reduce (N doubles)
+        else:
+            d.barrier()  # a 1-double all-reduce
+
+    errs = _run_ranks_collect(monkeypatch, 2, N, Mt, fn)
+    for e in errs:
+        assert isinstance(e, va.VampomiError) and "ranks disagree on the collective" in str(e), e
+        assert "rank 0:" in str(e) and "rank 1:" in str(e)

@@ -22,10 +22,18 @@ def _make(path: str, clean: bool = False) -> None:
     subprocess.run(["make", "-C", path, "-j", jobs], check=True)
 
 
+REF_SRC = "/root/reference/src/data.cpp"
+
+
 def build(clean: bool = False, oracle: bool = True) -> None:
     _make(os.path.join(HERE, "csrc"), clean)
     if oracle:
         _make(os.path.join(ROOT, "oracle"), clean)
+        # the reference's own data-class operators (oracle/ref_data_harness.cpp),
+        # where the reference exists (the build container; the GPU box uses the
+        # prebuilt oracle/_ref or skips); a checker, never the product
+        if os.path.exists(REF_SRC):
+            subprocess.run(["make", "-C", os.path.join(ROOT, "oracle"), "ref"], check=True)
 
 
 if __name__ == "__main__":

@@ -254,42 +254,51 @@ static vampomi_status loopback_allreduce(vampomi_ctx* c, double* buf, size_t n, 
     std::vector<double> mine(n);
     HIPCHK(hipMemcpyAsync(mine.data(), buf, n * 8, hipMemcpyDeviceToHost, c->st));
     HIPCHK(hipStreamSynchronize(c->st));
+    std::string err;  // reported after the lock is released (fail() may abort the communicator)
     {
         std::unique_lock<std::mutex> g(lb.mu);
-        if (!lb.poison.empty()) return fail(VAMPOMI_ERR_STATE, "loopback communicator failed earlier: " + lb.poison);
-        const uint64_t my_gen = lb.gen;
-        lb.in[(size_t)c->rank] = std::move(mine);
-        lb.desc[(size_t)c->rank] = me;
-        if (++lb.arrived == lb.P) {
-            bool agree = true;
-            for (int r = 1; r < lb.P; ++r) {
-                const auto& a = lb.desc[0];
-                const auto& b = lb.desc[(size_t)r];
-                agree = agree && a.seq == b.seq && a.n == b.n && a.line == b.line && std::strcmp(a.site, b.site) == 0;
+        if (!lb.poison.empty()) {
+            err = "loopback communicator failed earlier: " + lb.poison;
+        } else {
+            const uint64_t my_gen = lb.gen;
+            lb.in[(size_t)c->rank] = std::move(mine);
+            lb.desc[(size_t)c->rank] = me;
+            if (++lb.arrived == lb.P) {
+                bool agree = true;
+                for (int r = 1; r < lb.P; ++r) {
+                    const auto& a = lb.desc[0];
+                    const auto& b = lb.desc[(size_t)r];
+                    agree = agree && a.seq == b.seq && a.n == b.n && a.line == b.line && std::strcmp(a.site, b.site) == 0;
+                }
+                if (!agree) {
+                    std::string why = "ranks disagree on the collective:";
+                    for (int r = 0; r < lb.P; ++r) why += " [" + coll_desc(r, lb.desc[(size_t)r]) + "]";
+                    lb.poison = why;
+                } else {
+                    lb.out.assign(n, 0.0);
+                    for (int r = 0; r < lb.P; ++r)
+                        for (size_t i = 0; i < n; ++i) lb.out[i] += lb.in[(size_t)r][i];
+                }
+                lb.arrived = 0;
+                ++lb.gen;
+                lb.cv.notify_all();
+            } else if (!lb.cv.wait_for(g, std::chrono::seconds(60),
+                                       [&] { return lb.gen != my_gen || !lb.poison.empty(); })) {
+                // a rank that failed without aborting never arrives: end this
+                // rank with an error instead of waiting forever
+                --lb.arrived;
+                lb.poison = "not every rank arrived within 60 s at " + coll_desc(c->rank, me);
+                lb.cv.notify_all();
             }
-            if (!agree) {
-                std::string why = "ranks disagree on the collective:";
-                for (int r = 0; r < lb.P; ++r) why += " [" + coll_desc(r, lb.desc[(size_t)r]) + "]";
-                lb.poison = why;
-            } else {
-                lb.out.assign(n, 0.0);
-                for (int r = 0; r < lb.P; ++r)
-                    for (size_t i = 0; i < n; ++i) lb.out[i] += lb.in[(size_t)r][i];
-            }
-            lb.arrived = 0;
-            ++lb.gen;
-            lb.cv.notify_all();
-        } else if (!lb.cv.wait_for(g, std::chrono::seconds(60),
-                                   [&] { return lb.gen != my_gen || !lb.poison.empty(); })) {
-            // a rank that failed without aborting never arrives: end this rank
-            // with an error instead of waiting forever
-            --lb.arrived;
-            lb.poison = "not every rank arrived within 60 s at " + coll_desc(c->rank, me);
-            lb.cv.notify_all();
-            return fail(VAMPOMI_ERR_STATE, "loopback all-reduce: " + lb.poison);
+            if (!lb.poison.empty())
+                err = "loopback all-reduce: " + lb.poison;
+            else
+                mine = lb.out;  // lb.out is only rewritten once every rank has arrived again
         }
-        if (!lb.poison.empty()) return fail(VAMPOMI_ERR_STATE, "loopback all-reduce: " + lb.poison);
-        mine = lb.out;  // lb.out is only rewritten once every rank has arrived again
+    }
+    if (!err.empty()) {
+        c->aborted = true;  // the communicator is poisoned already
+        return fail(VAMPOMI_ERR_STATE, err);
     }
     HIPCHK(hipMemcpyAsync(buf, mine.data(), n * 8, hipMemcpyHostToDevice, c->st));
     HIPCHK(hipStreamSynchronize(c->st));
