@@ -292,8 +292,11 @@ vampomi_status vampomi_reset_stats(vampomi_ctx* ctx);
  * which: 0 = A.x partial-sum kernel, 1 = A^T.u kernel, 2 = association-test pass
  * (K = 1), 3 = one-pass CG operator (K = 1, 2).  Variants index the
  * tuning tables in vampomi_amd/csrc/kernels.hip and are settings of this
- * context only; the defaults are 0 (A.x), -1 (A^T.u: the per-K choice) and 2
- * (association pass). */
+ * context only; the defaults are 0 (A.x), -1 (A^T.u: the per-K choice), 2
+ * (association pass) and -1 (operator: whole columns per workgroup while
+ * K*N fits the LDS, else teams of workgroups; 0 forces the whole-column
+ * kernel, T*10 + c the team kernel with team size T and configuration c,
+ * vampomi_amd/csrc/atax_team.hip). */
 vampomi_status vampomi_dev_set_variant(vampomi_ctx* ctx, int which, int variant);
 /* average device time (HIP events) of `reps` back-to-back launches, K RHS */
 vampomi_status vampomi_dev_time_pass(vampomi_ctx* ctx, int which, int K, int reps, double* avg_ms);
@@ -302,6 +305,16 @@ vampomi_status vampomi_dev_time_pass(vampomi_ctx* ctx, int which, int K, int rep
  * fused direction update; which = 2: the association-test pass of
  * vampomi_assoc_loo) */
 vampomi_status vampomi_dev_kernel_name(const vampomi_ctx* ctx, int which, int K, int mode, char* out, int cap);
+/* One application of the one-pass CG operator (K <= 2 systems, one rank),
+ * host buffers: q_k = ar_k/diag [+ beta_k*qo_k], p_k [= z_k + beta_k*p_k]
+ * when z is not null (then qo and beta are required), and
+ *   d_k = tau * A^T q_k + gam2 * p_k   (M doubles each, k-major),
+ *   ad_k = A d_k                      (N doubles each),
+ *   dp_k = <d_k, p_k>.
+ * ar, qo: K x N; p, z: K x M. */
+vampomi_status vampomi_dev_op_apply(vampomi_ctx* ctx, int K, const double* ar, const double* qo, const double* p,
+                                    const double* z, const double* beta, double diag, double tau, double gam2,
+                                    double* d, double* ad, double* dp);
 
 #ifdef __cplusplus
 }

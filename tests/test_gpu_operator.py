@@ -1,0 +1,105 @@
+"""The one-pass CG operator (kernels.h: atax) on its own, every plan.
+
+One application computes, for K <= 2 systems, q = A r/diag [+ beta q_old]
+and p [= z + beta p] (the fused CG direction update), then from ONE read of X
+
+    d = tau * A^T q + gam2 * p        (lmmse_mult, src/vamp.cpp:645-662)
+    A d                                (data::Ax, src/data.cpp:340-373)
+    <d, p>
+
+with A = (X - mave) * msig / sqrt(N) (data::ATx src/data.cpp:294-333).
+Checked against numpy on the explicit matrix (norm-relative 1e-12), for the
+whole-column kernel and every team plan (team sizes 1..32, each hand-off
+configuration) that exists for the shape, including odd N (the zero pad row)
+and shapes where the last team member holds a short tile.  Team results
+are also bitwise repeatable.
+"""
+import numpy as np
+import pytest
+
+from conftest import relerr
+
+pytestmark = pytest.mark.gpu
+
+va = pytest.importorskip("vampomi_amd")
+from oracle import pyoracle as O  # noqa: E402  (checker: the generator and marker statistics)
+
+SHAPES = [(1000, 3000, 0), (10000, 4000, 0), (50001, 1500, 1), (100000, 600, 1)]
+CANDIDATES = [0] + [T * 10 + c for T in (1, 2, 4, 8, 16, 32) for c in range(5)]
+
+
+def _ref(X, mave, msig, ar, qo, p, z, beta, diag, tau, gam2):
+    N = X.shape[1]
+    Xc = X - mave[:, None]
+    q = ar / diag
+    pp = p.copy()
+    if z is not None:
+        q = q + beta[:, None] * qo
+        pp = z + beta[:, None] * p
+    t = (Xc @ q.T).T * msig[None, :] / np.sqrt(N)
+    d = tau * t + gam2 * pp
+    ad = (Xc.T @ (msig[None, :] * d).T).T / np.sqrt(N)
+    return d, ad, np.sum(d * pp, axis=1)
+
+
+@pytest.fixture(scope="module", params=SHAPES, ids=lambda s: "N%d_M%d" % s[:2])
+def problem(request):
+    N, Mt, kind = request.param
+    X = O.generate_markers(11, kind, N, 0, Mt)
+    mave, msig = O.marker_stats(X)
+    d = va.Data(N, Mt)
+    d.load_meth(X)
+    yield N, Mt, X, mave, msig, d
+    d.close()
+
+
+def _plans(d):
+    ok = []
+    for v in CANDIDATES:
+        try:
+            d.set_variant(3, v)
+        except va.VampomiError:
+            continue
+        ok.append(v)
+    d.set_variant(3, -1)
+    return ok
+
+
+def test_operator_every_plan_vs_numpy(problem):
+    N, Mt, X, mave, msig, d = problem
+    plans = _plans(d)
+    assert plans, "no operator plan for N=%d" % N
+    if N > 20000:
+        assert all(v >= 10 for v in plans), plans  # whole columns cannot hold these N
+        assert any(v >= 20 for v in plans), plans  # teams with a hand-off do
+    rng = np.random.default_rng(N)
+    diag, tau, gam2 = 1.7, 0.9, 0.35
+    for K in (1, 2):
+        ar, qo = rng.normal(size=(K, N)), rng.normal(size=(K, N))
+        p, z = rng.normal(size=(K, Mt)), rng.normal(size=(K, Mt))
+        beta = rng.uniform(0.1, 0.9, size=K)
+        for fused in (False, True):
+            zz, qq, bb = (z, qo, beta) if fused else (None, None, None)
+            rd, rad, rdp = _ref(X, mave, msig, ar, qq, p, zz, bb, diag, tau, gam2)
+            for v in plans:
+                d.set_variant(3, v)
+                gd, gad, gdp = d.op_apply(ar, p, diag, tau, gam2, z=zz, qo=qq, beta=bb)
+                what = "plan %d (%s) K=%d fused=%d" % (v, d.kernel_name(3, K), K, fused)
+                assert relerr(gd, rd) < 1e-12, (what, relerr(gd, rd))
+                assert relerr(gad, rad) < 1e-12, (what, relerr(gad, rad))
+                assert np.allclose(gdp, rdp, rtol=1e-12, atol=0), (what, gdp, rdp)
+    d.set_variant(3, -1)
+
+
+def test_operator_team_plans_bitwise_repeatable(problem):
+    N, Mt, X, mave, msig, d = problem
+    plans = [v for v in _plans(d) if v >= 20] or _plans(d)
+    rng = np.random.default_rng(1)
+    ar, p = rng.normal(size=(2, N)), rng.normal(size=(2, Mt))
+    for v in plans[:3]:
+        d.set_variant(3, v)
+        a = d.op_apply(ar, p, 1.0, 1.0, 0.5)
+        b = d.op_apply(ar, p, 1.0, 1.0, 0.5)
+        for x, y in zip(a, b):
+            assert np.array_equal(x, y), v
+    d.set_variant(3, -1)

@@ -1,6 +1,6 @@
 """Kernel tuning sweep for the A.x / A^T.u passes (run on the GPU box).
 
-    python tools/kbench.py [N] [Mt] [reps] [which: ax,atx,loo]
+    python tools/kbench.py [N] [Mt] [reps] [which: ax,atx,loo,op]   (OP_PLANS=v1,v2: operator plans)
 
 Prints, per variant and batch width K, the average launch time and the
 algorithmic HBM rate 8*N*M + 8*K*N + 8*(2+K)*M bytes per launch.
@@ -52,10 +52,17 @@ for which, name, Ks, nvar in ((0, "ax", (1, 2, 3), 7), (1, "atx", (1, 2), 8)):
         res[name][v] = row
         print(name, v, json.dumps(row), flush=True)
     _lib.check(lib.vampomi_dev_set_variant(d.ctx, which, 0))
-if "op" in only:  # the one-pass CG operator (A^T q and A d from one read of X)
+if "op" in only:  # the one-pass CG operator (A^T q and A d from one read of X), every plan for this N
     res["op"] = {}
-    for v in range(1):
-        row = {"kernel": d.kernel_name(3, 2, N)}
+    plans = os.environ.get("OP_PLANS")
+    cands = [int(v) for v in plans.split(",")] if plans else \
+        [-1, 0] + [T * 10 + c for T in (1, 2, 4, 8, 16, 32) for c in range(5)]
+    for v in cands:
+        try:
+            d.set_variant(3, v)
+        except va.VampomiError:
+            continue
+        row = {"kernel": d.kernel_name(3, 2)}
         for K in (1, 2):
             ms = C.c_double()
             _lib.check(lib.vampomi_dev_time_pass(d.ctx, 3, K, 2, C.byref(ms)))
@@ -64,6 +71,7 @@ if "op" in only:  # the one-pass CG operator (A^T q and A d from one read of X)
             row[f"K{K}"] = {"us": round(ms.value * 1e3, 1), "GBs": round(b / (ms.value * 1e-3) / 1e9, 1)}
         res["op"][v] = row
         print("op", v, json.dumps(row), flush=True)
+    d.set_variant(3, -1)
 if "loo" in only:
     d.set_phen(rng.normal(size=N), standardize=False)
     est = rng.normal(size=Mt) * 1e-3

@@ -253,11 +253,34 @@ class Data:
     # -- measurement --
     def kernel_name(self, which: int, K: int, mode: int = 0) -> str:
         """rocprofv3 name of the kernel this context launches for pass ``which``
-        (0 A.x, 1 A^T.u, 2 association test, 3 one-pass CG operator with mode = N)
+        (0 A.x, 1 A^T.u, 2 association test, 3 one-pass CG operator under the
+        context's plan)
         with K right-hand sides, under its current variant settings."""
         buf = C.create_string_buffer(256)
         check(self._lib.vampomi_dev_kernel_name(self.ctx, which, K, mode, buf, 256))
         return buf.value.decode()
+
+    def op_apply(self, ar, p, diag: float, tau: float, gam2: float, z=None, qo=None, beta=None):
+        """Development hook: one application of the one-pass CG operator on K <= 2
+        systems (vampomi_dev_op_apply): returns (d, A d, <d, p>) for
+        q = ar/diag [+ beta*qo] and p [= z + beta*p]."""
+        ar = np.ascontiguousarray(np.atleast_2d(ar), dtype=np.float64)
+        p = np.ascontiguousarray(np.atleast_2d(p), dtype=np.float64)
+        K = ar.shape[0]
+        if ar.shape != (K, self.N) or p.shape != (K, self.M):
+            raise ValueError("ar must be K x N and p K x M")
+        fz = z is not None
+        if fz:
+            z = np.ascontiguousarray(np.atleast_2d(z), dtype=np.float64)
+            qo = np.ascontiguousarray(np.atleast_2d(qo), dtype=np.float64)
+            beta = np.ascontiguousarray(beta, dtype=np.float64)
+        d = np.zeros((K, max(self.M, 1)))
+        ad = np.zeros((K, self.N))
+        dp = np.zeros(K)
+        check(self._lib.vampomi_dev_op_apply(self.ctx, K, _dp(ar), _dp(qo) if fz else None, _dp(p),
+                                             _dp(z) if fz else None, _dp(beta) if fz else None, diag, tau, gam2,
+                                             _dp(d), _dp(ad), _dp(dp)))
+        return d[:, : self.M], ad, dp
 
     def set_variant(self, which: int, variant: int):
         """Development hook: this context's kernel variant for pass ``which``."""

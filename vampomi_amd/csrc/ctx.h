@@ -98,9 +98,16 @@ struct vampomi_ctx {
     vk::CgMirror* d_cgm = nullptr;
     // one-pass CG operator (batch_rhs 4; allocated on first use, pcg.cpp)
     vk::OpPlan opp{};
+    int op_variant = vk::kOpDefault;  // plan choice (dev hook: vampomi_dev_set_variant(c, 3, v))
+    bool op_ready = false;            // opp planned and its buffers allocated
+    bool op_ok = false;               // a plan exists for this N
     int cus = 0;                // compute units of the device (the operator's grid)
     double* op_part = nullptr;  // opp.nslots x kMaxRhs x ld partial A d
+    int64_t op_part_slots = 0;
     double* op_nvec = nullptr;  // 3 x kMaxRhs x ld: A r, q = A p, A d (+ <d,p> tail)
+    unsigned long long* op_xg = nullptr;  // team hand-off granules (M x kOpMaxK x T x 2), zeroed once
+    size_t op_xg_words = 0;
+    unsigned op_tag = 0;        // the last team launch's tag
     double* nbuf = nullptr;     // kMaxRhs * ld scratch N-vectors (API calls)
     double* mbuf = nullptr;     // (2*kMaxRhs) * M scratch M-vectors (API calls)
 
@@ -221,8 +228,12 @@ struct CgSystem {
 vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double tau, double gam2, int max_iter,
                        double tol, double* nscratch, int64_t* ref_passes, DotBatch* init,
                        const double* extra_x = nullptr, double* ex_out = nullptr, bool onepass = false);
-// allocates the one-pass operator's buffers (idempotent)
+// plans the one-pass operator (c->opp, c->op_ok) and allocates its buffers
+// (idempotent until the variant changes)
 vampomi_status op_prepare(vampomi_ctx* c);
+// the device word a team launch sets when a hand-off timed out, and its host view
+unsigned* op_err_dev(vampomi_ctx* c);
+vampomi_status op_check_err(vampomi_ctx* c);
 // d_k = tau*A^T q_k + gam2*p_k and A d_k (into op_nvec's A d block, /sqrt(N),
 // summed over ranks with <d_k,p_k> at its tail; one rank: <d_k,p_k> in
 // scal[SL_DP+k]) from one pass over X.  COLLECTIVE

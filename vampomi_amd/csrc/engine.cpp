@@ -519,27 +519,69 @@ vampomi_status atx_dev(vampomi_ctx* c, int K, const double* const* u, double* co
 // one-pass CG operator (batch_rhs 4)
 // ---------------------------------------------------------------------------
 vampomi_status op_prepare(vampomi_ctx* c) {
-    if (c->op_nvec) return VAMPOMI_OK;
+    if (c->op_ready) return VAMPOMI_OK;
     if (c->cus <= 0) HIPCHK(hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, c->device));
-    c->opp = vk::op_plan(c->N, c->M, c->cus);
-    STCHK(dev_alloc(&c->op_part, (size_t)c->opp.nslots * vk::kMaxRhs * c->ld));
-    STCHK(dev_alloc(&c->op_nvec, (size_t)3 * vk::kMaxRhs * c->ld));
-    HIPCHK(hipMemsetAsync(c->op_nvec, 0, (size_t)3 * vk::kMaxRhs * c->ld * 8, c->st));
+    const int64_t M = std::max<int64_t>(c->M, 1);
+    c->op_ok = vk::op_plan(c->N, M, c->cus, c->op_variant, &c->opp);
+    if (!c->op_nvec) {
+        STCHK(dev_alloc(&c->op_nvec, (size_t)3 * vk::kMaxRhs * c->ld));
+        HIPCHK(hipMemsetAsync(c->op_nvec, 0, (size_t)3 * vk::kMaxRhs * c->ld * 8, c->st));
+    }
+    if (c->op_ok) {
+        if (c->opp.nslots > c->op_part_slots) {
+            dev_free(c->op_part);
+            STCHK(dev_alloc(&c->op_part, (size_t)c->opp.nslots * vk::kMaxRhs * c->ld));
+            c->op_part_slots = c->opp.nslots;
+        }
+        if (c->opp.T > 1) {
+            // M columns x K x T granule pairs, then a dummy pair per workgroup and K
+            const size_t words =
+                (size_t)M * vk::kOpMaxK * (size_t)c->opp.T * 2 + (size_t)c->opp.grid * (2 * vk::kOpMaxK + 1);
+            if (words > c->op_xg_words) {
+                if (c->op_xg) (void)hipFree(c->op_xg);
+                c->op_xg = nullptr;
+                c->op_xg_words = 0;
+                HIPCHK(hipMalloc((void**)&c->op_xg, words * 8));
+                HIPCHK(hipMemsetAsync(c->op_xg, 0, words * 8, c->st));  // tags start below every launch's
+                c->op_xg_words = words;
+            }
+        }
+    }
+    c->op_ready = true;
+    return VAMPOMI_OK;
+}
+
+// word 4 of the mapped flag block (zeroed at open)
+unsigned* op_err_dev(vampomi_ctx* c) { return reinterpret_cast<unsigned*>(c->d_flag + 4); }
+
+vampomi_status op_check_err(vampomi_ctx* c) {
+    if (c->h_flag && __atomic_load_n(reinterpret_cast<unsigned*>(c->h_flag + 4), __ATOMIC_ACQUIRE))
+        return fail(VAMPOMI_ERR_HIP, "one-pass operator: a team hand-off timed out (a workgroup of the team never "
+                                     "ran: fewer compute units than planned?)");
     return VAMPOMI_OK;
 }
 
 // One operator launch is charged SURVEY §8(d)'s bytes of ONE pass
 // (pass_bytes: X once, K N-vectors, mave/msig, K M-vectors), the work it
 // replaces being two such passes; its other traffic (p, z, d, A r, q_old and
-// the per-workgroup A d partials, < 1% at C2) is not counted as algorithmic.
+// the per-slot A d partials, < 1% at C2) is not counted as algorithmic.
 vampomi_status op_dev(vampomi_ctx* c, int K, const vk::OpArgs& a, const int* gate) {
     if (!c->have_X) return fail(VAMPOMI_ERR_STATE, "A before the methylation data was loaded");
-    if (!vk::op_supported(c->N, K)) return fail(VAMPOMI_ERR_ARG, "one-pass operator: K <= 2 and K*N <= 20000");
     STCHK(op_prepare(c));
+    if (!c->op_ok || K < 1 || K > vk::kOpMaxK)
+        return fail(VAMPOMI_ERR_ARG, "one-pass operator: K <= 2 and a plan for N = " + std::to_string(c->N));
     double* ad = c->op_nvec + (int64_t)2 * vk::kMaxRhs * c->ld;
     vk::OpArgs x = a;
     x.part = c->op_part;
     x.scale = 1.0 / c->sqrtN;
+    if (c->opp.T > 1) {
+        x.xg = c->op_xg;
+        if (++c->op_tag == 0) ++c->op_tag;
+        x.tag = c->op_tag;
+        x.err = op_err_dev(c);
+    }
+    static const int dbg = std::getenv("VAMPOMI_OP_DBG") ? std::atoi(std::getenv("VAMPOMI_OP_DBG")) : 0;
+    x.dbg = dbg;
     // <d,p>: one rank into scal[SL_DP+k]; several: behind the A d block, all-reduced with it
     x.ro = vk::RedOut{c->red_part, c->use_comm ? ad + (int64_t)K * c->ld : c->scal + SL_DP, c->ticket, nullptr, 0,
                       gate};
@@ -609,6 +651,11 @@ void release_ctx_resources(vampomi_ctx* c) {
     for (double** p : {&c->X, &c->mave, &c->msig, &c->y, &c->ax_part, &c->red_part, &c->scal, &c->nbuf, &c->mbuf,
                        &c->op_part, &c->op_nvec})
         dev_free(*p);
+    if (c->op_xg) (void)hipFree(c->op_xg);
+    c->op_xg = nullptr;
+    c->op_xg_words = 0;
+    c->op_part_slots = 0;
+    c->op_ready = false;
     if (c->h_scal) (void)hipHostFree(c->h_scal);
     c->h_scal = nullptr;
     if (c->ticket) (void)hipFree(c->ticket);
@@ -664,7 +711,7 @@ extern "C" vampomi_status vampomi_open(const vampomi_shard_desc* d, vampomi_ctx*
     HIPCHK(hipHostMalloc((void**)&c->h_scal, SL_TOTAL * sizeof(double), hipHostMallocMapped | hipHostMallocCoherent));
     HIPCHK(hipHostGetDevicePointer((void**)&c->d_hscal, c->h_scal, 0));
     HIPCHK(hipHostMalloc((void**)&c->h_flag, 64, hipHostMallocMapped | hipHostMallocCoherent));
-    *c->h_flag = 0;
+    std::memset(c->h_flag, 0, 64);  // word 0: stream sync sequence; word 4: operator hand-off error
     HIPCHK(hipHostGetDevicePointer((void**)&c->d_flag, c->h_flag, 0));
     HIPCHK(hipMalloc((void**)&c->ticket, 64 * sizeof(unsigned)));
     HIPCHK(hipMemsetAsync(c->ticket, 0, 64 * sizeof(unsigned), c->st));
@@ -1232,6 +1279,12 @@ extern "C" vampomi_status vampomi_dev_set_variant(vampomi_ctx* c, int which, int
     } else if (which == 1) {
         if (!vk::atx_variant_ok(variant)) return fail(VAMPOMI_ERR_ARG, "no such A^T.u variant");
         c->atx_variant = variant;
+    } else if (which == 3) {
+        vk::OpPlan p{};
+        if (!vk::op_plan(c->N, std::max<int64_t>(c->M, 1), c->cus > 0 ? c->cus : 256, variant, &p))
+            return fail(VAMPOMI_ERR_ARG, "no such one-pass operator plan for this N");
+        c->op_variant = variant;
+        c->op_ready = false;
     } else {
         if (!vk::loo_variant_ok(variant)) return fail(VAMPOMI_ERR_ARG, "no such association-pass variant");
         c->loo_variant = variant;
@@ -1244,7 +1297,10 @@ extern "C" vampomi_status vampomi_dev_time_pass(vampomi_ctx* c, int which, int K
         return fail(VAMPOMI_ERR_ARG, "bad argument");
     if (!c->have_X) return fail(VAMPOMI_ERR_STATE, "no methylation data loaded");
     HIPCHK(hipSetDevice(c->device));
-    if (which == 3) STCHK(op_prepare(c));
+    if (which == 3) {
+        STCHK(op_prepare(c));
+        if (!c->op_ok) return fail(VAMPOMI_ERR_ARG, "no one-pass operator plan for this N");
+    }
     const int64_t Mx = std::max<int64_t>(c->M, 1);
     vk::CPtrs in{};
     vk::Ptrs out{};
@@ -1273,6 +1329,14 @@ extern "C" vampomi_status vampomi_dev_time_pass(vampomi_ctx* c, int which, int K
             x.tau = 1.0;
             x.part = c->op_part;
             x.ro = vk::RedOut{c->red_part, c->scal + SL_DP, c->ticket, nullptr, 0, nullptr};
+            if (c->opp.T > 1) {
+                x.xg = c->op_xg;
+                if (++c->op_tag == 0) ++c->op_tag;
+                x.tag = c->op_tag;
+                x.err = op_err_dev(c);
+            }
+            x.dbg = std::getenv("VAMPOMI_OP_DBG") ? std::atoi(std::getenv("VAMPOMI_OP_DBG")) : 0;
+            if (c->opp.T > 1) x.err = op_err_dev(c);
             HIPCHK(vk::atax(c->shard(), c->opp, K, x, c->st));
         }
         else  // association pass: ymod = nbuf slot 0, x1 = mbuf slot 0, sums in mbuf slots 3..7
@@ -1280,6 +1344,12 @@ extern "C" vampomi_status vampomi_dev_time_pass(vampomi_ctx* c, int which, int K
     }
     HIPCHK(hipEventRecord(b, c->st));
     HIPCHK(hipEventSynchronize(b));
+    if (which == 3 && std::getenv("VAMPOMI_OP_DBG") && (std::atoi(std::getenv("VAMPOMI_OP_DBG")) & 64)) {
+        unsigned* w = reinterpret_cast<unsigned*>(c->h_flag + 4);
+        std::fprintf(stderr, "op dbg: slow polls %u, spins %u, columns polled %u (over %d launches)\n", w[1], w[2], w[3],
+                     reps);
+        w[1] = w[2] = w[3] = 0;
+    }
     float ms = 0.f;
     HIPCHK(hipEventElapsedTime(&ms, a, b));
     (void)hipEventDestroy(a);
@@ -1288,12 +1358,68 @@ extern "C" vampomi_status vampomi_dev_time_pass(vampomi_ctx* c, int which, int K
     return VAMPOMI_OK;
 }
 
+extern "C" vampomi_status vampomi_dev_op_apply(vampomi_ctx* c, int K, const double* ar, const double* qo,
+                                               const double* p, const double* z, const double* beta, double diag,
+                                               double tau, double gam2, double* d, double* ad, double* dp) {
+    if (!c || K < 1 || K > vk::kOpMaxK || !ar || !p || !d || !ad || !dp || (z && (!qo || !beta)))
+        return fail(VAMPOMI_ERR_ARG, "bad argument");
+    if (c->use_comm) return fail(VAMPOMI_ERR_ARG, "vampomi_dev_op_apply: one rank only");
+    HIPCHK(hipSetDevice(c->device));
+    STCHK(op_prepare(c));
+    if (!c->op_ok) return fail(VAMPOMI_ERR_ARG, "no one-pass operator plan for this N");
+    const int64_t Mx = std::max<int64_t>(c->M, 1);
+    double* AR = c->op_nvec;
+    double* Q = c->op_nvec + (int64_t)vk::kMaxRhs * c->ld;
+    vk::OpArgs a{};
+    for (int k = 0; k < K; ++k) {
+        STCHK(stage_in(c, ar + k * c->N, c->N, VAMPOMI_MEM_HOST, AR + k * c->ld));
+        STCHK(stage_in(c, p + k * c->M, c->M, VAMPOMI_MEM_HOST, c->mbuf + k * Mx));
+        a.ar.p[k] = AR + k * c->ld;
+        a.p.p[k] = c->mbuf + k * Mx;
+        a.d.p[k] = c->mbuf + (2 + k) * Mx;
+        if (z) {
+            STCHK(stage_in(c, qo + k * c->N, c->N, VAMPOMI_MEM_HOST, Q + k * c->ld));
+            STCHK(stage_in(c, z + k * c->M, c->M, VAMPOMI_MEM_HOST, c->mbuf + (4 + k) * Mx));
+            a.qo.p[k] = Q + k * c->ld;
+            a.z.p[k] = c->mbuf + (4 + k) * Mx;
+        }
+    }
+    double* dbeta = c->mbuf + 6 * Mx;  // K <= 2 <= M... at least K doubles: mbuf slot 6 (Mx >= 1)
+    if (z) {
+        if (Mx < K) return fail(VAMPOMI_ERR_ARG, "vampomi_dev_op_apply: fused form needs M >= K");
+        STCHK(stage_in(c, beta, K, VAMPOMI_MEM_HOST, dbeta));
+        a.beta = dbeta;
+        a.fuse = 1;
+    }
+    a.diag = diag;
+    a.tau = tau;
+    a.gam2 = gam2;
+    STCHK(op_dev(c, K, a, nullptr));
+    const double* AD = c->op_nvec + (int64_t)2 * vk::kMaxRhs * c->ld;
+    for (int k = 0; k < K; ++k) {
+        STCHK(stage_out(c, c->mbuf + (2 + k) * Mx, c->M, VAMPOMI_MEM_HOST, d + k * c->M));
+        STCHK(stage_out(c, AD + k * c->ld, c->N, VAMPOMI_MEM_HOST, ad + k * c->N));
+    }
+    HIPCHK(hipMemcpyAsync(dp, c->scal + SL_DP, (size_t)K * 8, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    return op_check_err(c);
+}
+
+// the operator's kernel as rocprofv3 prints it, for the context's plan
+static std::string op_name(const vampomi_ctx* c, int K) {
+    vk::OpPlan p{};
+    int cus = c->cus;
+    if (cus <= 0 && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess) cus = 256;
+    if (!vk::op_plan(c->N, std::max<int64_t>(c->M, 1), cus, c->op_variant, &p)) return "(no one-pass plan)";
+    return vk::op_kernel_name(K, p);
+}
+
 extern "C" vampomi_status vampomi_dev_kernel_name(const vampomi_ctx* c, int which, int K, int mode, char* out,
                                                   int cap) {
     if (!c || !out || cap < 1) return fail(VAMPOMI_ERR_ARG, "bad argument");
     // which = 3: mode carries N (the operator's instantiation depends on it)
     const std::string n = which == 2   ? vk::loo_kernel_name(c->loo_variant)
-                          : which == 3 ? vk::op_kernel_name(K, mode)
+                          : which == 3 ? op_name(c, K)
                           : which == 0 ? vk::kernel_name(0, K, mode, c->axp.variant)
                                        : vk::kernel_name(1, K, mode, c->atx_variant);
     std::snprintf(out, (size_t)cap, "%s", n.c_str());

@@ -103,15 +103,27 @@ hipError_t atx(const Shard& s, int K, CPtrs u, Ptrs out, double scale, int mode,
 // over X computes, per marker i, t_i = (msig_i*sum_j (X_ij - mave_i) q_j)/sqrt(N)
 // and d_i = tau*t_i + gam2*p_i, and while the column is still in registers
 // accumulates (A d)_j += (X_ij - mave_i)*(msig_i*d_i): A^T and A in one read.
-// One workgroup per CU owns whole columns; q lives in LDS, so K*N <= 20,000
-// (op_supported); larger problems keep the two-pass CG step.
+// Two kernels:
+//  * T = 0 (atax_kernel, kernels.hip): one workgroup per CU owns whole
+//    columns, q in LDS, so K*N <= 20,000;
+//  * T >= 1 (atax_team_kernel, atax_team.hip): teams of T workgroups split
+//    the rows of each column and hand the column dots over inside the launch
+//    (T = 1: no hand-off), for N up to 32 x 8 x 896 rows.
+constexpr int kOpMaxK = 2;
 struct OpPlan {
-    int grid;       // workgroups (one per CU, at most M)
-    int S;          // 16-byte loads per lane per column: ceil(N / 1024)
-    int64_t nslots; // partial A d slots (grid x kMaxRhs x ld)
+    int grid;       // workgroups (at most one per CU)
+    int S;          // 16-byte loads per lane per column
+    int64_t nslots; // partial A d slots (nslots x kMaxRhs x ld): workgroups (T = 0) or teams
+    int T = 0;      // team size (0: the whole-column kernel)
+    int TR = 0;     // rows per team member (T >= 1)
+    int cfg = 0;    // team kernel configuration (prefetch, lag, polls in flight)
 };
+// variant: -1 the default choice for N; 0 the whole-column kernel; T*10 + cfg
+// a team plan (development hook, tools/kbench.py)
+constexpr int kOpDefault = -1;
+bool op_plan(int64_t N, int64_t M, int cus, int variant, OpPlan* out);
 bool op_supported(int64_t N, int K);
-OpPlan op_plan(int64_t N, int64_t M, int cus);
+bool team_plan(int64_t N, int64_t M, int cus, int T, int cfg, OpPlan* out);
 struct OpArgs {
     CPtrs ar, qo;       // q_k = ar_k/diag [+ beta_k*qo_k when fuse] (N-space, replicated)
     CPtrs p, z;         // p_k [= z_k + beta_k*p_k when fuse] (M-space)
@@ -119,13 +131,27 @@ struct OpArgs {
     int fuse;
     double diag, scale, tau, gam2;
     Ptrs d, sraw;       // d_k (M); sraw_k = t_k (may be null)
-    double* part;       // grid x kMaxRhs x ld partial A d (before the sum over workgroups)
+    double* part;       // nslots x kMaxRhs x ld partial A d (before the sum over slots)
     RedOut ro;          // <d_k, p_k> summed over the shard (K values)
+    // team kernel with T > 1: hand-off granules (M x kOpMaxK x T x 2 words,
+    // then 2 x kOpMaxK dummy words per workgroup, then one XCD word per
+    // workgroup; zeroed once), this launch's
+    // tag (never 0, new every launch) and a mapped host word set when a
+    // hand-off timed out
+    unsigned long long* xg;
+    unsigned tag;
+    unsigned* err;
+    int dbg;  // timing experiments only (VAMPOMI_OP_DBG; results are wrong when set, except bit 5):
+              // bit 0 no poll waits, 1 no publishes, 2 no butterfly, 3 no A d accumulation,
+              // 5 write-through hand-off even when the team shares an XCD
 };
-std::string op_kernel_name(int K, int64_t N);
+std::string op_kernel_name(int K, const OpPlan& pl);
+std::string team_kernel_name(int K, const OpPlan& pl);
 hipError_t atax(const Shard& s, const OpPlan& pl, int K, const OpArgs& a, hipStream_t st, const Timing& tm = Timing{},
                 const int* gate = nullptr);
-// out_k[j] = sum_b part[b][k][j] (workgroups in order); if div > 0 then /= div
+hipError_t atax_team(const Shard& s, const OpPlan& pl, int K, const OpArgs& a, hipStream_t st, const Timing& tm,
+                     const int* gate);
+// out_k[j] = sum_b part[b][k][j] (slots in order); if div > 0 then /= div
 hipError_t op_reduce(const OpPlan& pl, int K, int64_t N, int64_t ld, const double* part, Ptrs out, double div,
                      hipStream_t st, const int* gate = nullptr);
 

@@ -8,6 +8,7 @@
 // and fixed summation order, so every result is bitwise reproducible run to
 // run and independent of the rank count's effect on scheduling.
 #include "kernels.h"
+#include "kdev.h"
 
 #include <algorithm>
 #include <cstdlib>
@@ -17,23 +18,16 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <mutex>
 #include <string>
 
 namespace vk {
-
-typedef double v2d __attribute__((ext_vector_type(2)));
 
 static constexpr int kBlock = 256;   // 4 waves of 64
 
 // ---------------------------------------------------------------------------
 // small helpers
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;  // butterfly: every lane holds the same value
-}
-
 // sum over a 256-thread block; every thread gets the result
 __device__ __forceinline__ double block_sum(double v, double* lds4) {
     v = wave_sum(v);
@@ -44,19 +38,8 @@ __device__ __forceinline__ double block_sum(double v, double* lds4) {
     return ((lds4[0] + lds4[1]) + lds4[2]) + lds4[3];
 }
 
-// Fused finish of a two-stage reduction.  Thread 0 of every block publishes
-// its per-block partials with red_put (agent-coherent, write-through stores);
-// red_finish drains them (s_waitcnt) and takes a ticket; the LAST block to
-// arrive sums the partials in block order, exactly as a separate one-block
-// sum kernel would (so results are bitwise those of the two-launch form),
-// writes out[0..nq) (device memory or mapped host memory) and re-arms the
-// ticket.  No __threadfence: an agent-scope fence writes back the XCD's whole
-// L2 (every dirty line of the vectors the kernel just updated), which made
-// the fused kernels slower than the two launches (MI355X_MICROARCH.md,
-// handoff-flag: drained sc1 payload, then the flag).
-__device__ __forceinline__ void red_put(const RedOut& ro, int64_t idx, double v) {
-    __hip_atomic_store(ro.part + idx, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
+// red_put (kdev.h) publishes a block's partials; red_finish (below) takes the
+// ticket and sums them in block order (the protocol is described in kdev.h).
 
 // Block sums of nq <= NQ values at once, published with red_put at
 // part[base + q]: every wave reduces all values in registers, ONE barrier,
@@ -737,16 +720,37 @@ static constexpr int kOpRows = 128 * kOpWaves;   // rows per load step of the wo
 static constexpr int kOpMaxS = 10;               // rows per workgroup <= kOpRows*kOpMaxS = 10,240
 static constexpr int64_t kOpLdsDoubles = 20480 - 2 - 2 * kOpWaves * 2;  // the CU's 160 KiB of LDS
 
-bool op_supported(int64_t N, int K) {
-    return K >= 1 && K <= 2 && N >= 1 && K * (N + 2) <= kOpLdsDoubles && (N + kOpRows - 1) / kOpRows <= kOpMaxS;
+static bool whole_column_ok(int64_t N) {
+    return N >= 1 && kOpMaxK * (N + 2) <= kOpLdsDoubles && (N + kOpRows - 1) / kOpRows <= kOpMaxS;
 }
 
-OpPlan op_plan(int64_t N, int64_t M, int cus) {
+// The default: whole columns per workgroup while K*N fits the LDS, else the
+// smallest team whose members' rows fit the registers (configuration 2).
+bool op_plan(int64_t N, int64_t M, int cus, int variant, OpPlan* out) {
+    if (N < 1 || cus < 1) return false;
+    if (variant == 0 || (variant == kOpDefault && whole_column_ok(N))) {
+        if (!whole_column_ok(N)) return false;
+        OpPlan p{};
+        p.S = (int)std::max<int64_t>(1, (N + kOpRows - 1) / kOpRows);
+        p.grid = (int)std::max<int64_t>(1, std::min<int64_t>(cus, M));
+        p.nslots = p.grid;
+        p.T = 0;
+        *out = p;
+        return true;
+    }
+    if (variant > 0) return team_plan(N, M, cus, variant / 10, variant % 10, out);
+    for (int T = 2; T <= 32; T *= 2) {
+        OpPlan p{};
+        if (!team_plan(N, M, cus, T, 2, &p)) continue;
+        *out = p;
+        return true;
+    }
+    return false;
+}
+
+bool op_supported(int64_t N, int K) {
     OpPlan p{};
-    p.S = (int)std::max<int64_t>(1, (N + kOpRows - 1) / kOpRows);
-    p.grid = (int)std::max<int64_t>(1, std::min<int64_t>(cus, M));
-    p.nslots = p.grid;
-    return p;
+    return K >= 1 && K <= kOpMaxK && op_plan(N, 1 << 20, 256, kOpDefault, &p);
 }
 
 // one column in registers: its X rows and the marker's mean
@@ -935,27 +939,13 @@ __global__ __launch_bounds__(kOpThreads) void atax_kernel(const double* __restri
 #pragma unroll
         for (int k = 0; k < K; ++k) red_put(ro, (int64_t)blockIdx.x * K + k, dpacc[k]);
     }
-    if (wave != 0) return;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    unsigned old = 0;
-    if (lane == 0) old = __hip_atomic_fetch_add(ro.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    old = __shfl(old, 0, 64);
-    if (old != gridDim.x - 1) return;
-    const int nblk = (int)gridDim.x;
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-        double t = 0.0;
-        for (int b = lane; b < nblk; b += 64)
-            t += __hip_atomic_load(ro.part + (int64_t)b * K + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        t = wave_sum(t);
-        if (lane == 0) ro.out[k] = t;
-    }
-    if (lane == 0) __hip_atomic_store(ro.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (wave == 0) ticket_sum_blocks<K>(ro);
 }
 
-std::string op_kernel_name(int K, int64_t N) {
+std::string op_kernel_name(int K, const OpPlan& pl) {
+    if (pl.T > 0) return team_kernel_name(K, pl);
     char b[96];
-    std::snprintf(b, sizeof b, "atax_kernel<%d, %d>", K, (int)std::max<int64_t>(1, (N + kOpRows - 1) / kOpRows));
+    std::snprintf(b, sizeof b, "atax_kernel<%d, %d>", K, pl.S);
     return b;
 }
 
@@ -963,12 +953,11 @@ template <int K, int S>
 static void launch_op(const Shard& s, const OpPlan& pl, const OpArgs& a, hipStream_t st, const Timing& tm,
                       const int* gate) {
     const size_t lds = ((size_t)K * (s.N + 1 + (s.N & 1)) + 2 + 2 * kOpWaves * K) * sizeof(double);
-    static bool attr = false;
-    if (!attr) {  // more than 64 KiB of dynamic LDS must be allowed explicitly
+    static std::once_flag once;  // more than 64 KiB of dynamic LDS must be allowed explicitly
+    std::call_once(once, [] {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&atax_kernel<K, S>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        attr = true;
-    }
+    });
     hipExtLaunchKernelGGL((atax_kernel<K, S>), dim3(pl.grid), dim3(kOpThreads), lds, st, tm.start, tm.stop, 0, s.X,
                           s.ld, s.N, s.M, s.mave, s.msig, a, gate);
 }
@@ -993,7 +982,10 @@ static bool launch_op_s(int S, const Shard& s, const OpPlan& pl, const OpArgs& a
 
 hipError_t atax(const Shard& s, const OpPlan& pl, int K, const OpArgs& a, hipStream_t st, const Timing& tm,
                 const int* gate) {
-    if (!op_supported(s.N, K) || pl.S != (int)std::max<int64_t>(1, (s.N + kOpRows - 1) / kOpRows)) return hipErrorInvalidValue;
+    if (pl.T > 0) return atax_team(s, pl, K, a, st, tm, gate);
+    if (K < 1 || K > kOpMaxK || !whole_column_ok(s.N) ||
+        pl.S != (int)std::max<int64_t>(1, (s.N + kOpRows - 1) / kOpRows))
+        return hipErrorInvalidValue;
     if (s.M <= 0) return hipSuccess;
     bool ok = false;
     switch (K) {

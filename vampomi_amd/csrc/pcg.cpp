@@ -134,12 +134,12 @@ vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double
     }
     const int* gate = field<int>(c->cgs, offsetof(vk::CgState, any));
     const double* beta = field<double>(c->cgs, offsetof(vk::CgState, beta));
-    if (onepass && vk::op_supported(N, K) && c->have_X) {
+    if (onepass && K <= vk::kOpMaxK && c->have_X) STCHK(op_prepare(c));
+    if (onepass && K <= vk::kOpMaxK && c->have_X && c->op_ok) {
         // ---- one pass over X per CG step (vk::atax) ----
         // A r0 for every system (and A extra_x) by one A.x pass; then each step
         // forms q = A p = A r/diag + beta*q_old on the fly, streams X once for
         // d = tau*A^T q + gam2*p and A d, and cg_update carries A r -= alpha*A d
-        STCHK(op_prepare(c));
         double* AR = c->op_nvec;
         double* Q = c->op_nvec + (int64_t)vk::kMaxRhs * c->ld;
         const double* AD = c->op_nvec + (int64_t)2 * vk::kMaxRhs * c->ld;
@@ -208,6 +208,7 @@ vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double
         };
         const vk::CgMirror* last = nullptr;
         STCHK(cg_loop(c, max_iter, enqueue, &last));
+        STCHK(op_check_err(c));
         for (int k = 0; k < K; ++k) {
             sys[k]->iters = last->iters[k];
             if (ref_passes) *ref_passes += 2 * (int64_t)sys[k]->iters;
