@@ -43,6 +43,7 @@
 namespace vk {
 
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+typedef unsigned int v2u __attribute__((ext_vector_type(2)));
 
 #ifndef TM_FMA
 #define TM_FMA 0  // experiment switch: fused multiply-adds in the dot and the A d accumulation
@@ -65,10 +66,10 @@ static constexpr TmCfg kTmCfg[] = {
     {3, 5, 2, true, 4},    // 2
     {2, 4, 2, true, 5},    // 3
     {3, 6, 3, true, 4},    // 4
-    {2, 5, 3, true, 4},    // 5
-    {3, 5, 3, true, 4},    // 6
-    {2, 6, 4, true, 4},    // 7
-    {2, 4, 3, true, 5},    // 8
+    {3, 6, 2, true, 4},    // 5
+    {4, 5, 2, true, 4},    // 6
+    {4, 6, 2, true, 4},    // 7
+    {3, 4, 2, true, 4},    // 8
 };
 static constexpr int kTmNCfg = sizeof(kTmCfg) / sizeof(kTmCfg[0]);
 
@@ -97,6 +98,13 @@ __device__ __forceinline__ void tm_poll(v4u& dst, const unsigned long long* p) {
 template <int N>
 __device__ __forceinline__ void tm_wait(v4u& r) {
     asm volatile("s_waitcnt vmcnt(%1)" : "+v"(r) : "n"(N) : "memory");
+}
+__device__ __forceinline__ void tm_load8(v2u& dst, const double* p) {
+    asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(dst) : "v"(p) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void tm_wait2(v4u& r, v2u& q) {
+    asm volatile("s_waitcnt vmcnt(%2)" : "+v"(r), "+v"(q) : "n"(N) : "memory");
 }
 __device__ __forceinline__ void tm_publish(unsigned long long* p, const v4u& v) {
     asm volatile("s_nop 4\n\tglobal_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
@@ -137,109 +145,163 @@ __global__ __launch_bounds__(kTmThreads) void atax_team_kernel(const double* __r
     const int nbytes = ((nrows + 1) & ~1) * 8;            // the tile of a column (+ the zero pad row for odd N)
 
     if (COMM && wave == CW) {
-        // ---------------- the hand-off wave: polls, sums, publishes ----------------
-        // Its memory operations are inline asm the compiler does not track:
-        // exactly two per step (one 16-byte poll of a column's granules, one
-        // 16-byte publish, to a dummy slot outside the team's columns when
-        // there is nothing to publish), so the poll of step m - P is waited
-        // for with vmcnt(2P) while the P younger polls stay in flight.  Every
-        // poll register passes through such a wait before it is read or
-        // reused (the compiler sees the wait as the writer).
+        // ---------------- the hand-off wave ----------------
+        // Per step: polls the granules of the column finished P steps later
+        // together with that column's scalars (msig, p_k, z_k), sums the T
+        // member partials of the column finished now, forms its d (the
+        // lmmse_mult epilogue, stored by the member that owns the column,
+        // which also adds <d,p>) and hands c_k = msig*d_k to the streaming
+        // waves through LDS; after the barrier it publishes this member's
+        // dot of the step's column.  Its polls and publishes are inline asm
+        // the compiler does not track: exactly three per step (the scalars,
+        // the 16-byte poll, the 16-byte publish, to a dummy slot when there
+        // is nothing to publish), so the poll of step m - P is waited for
+        // with vmcnt(3P) while the younger ones stay in flight (the d stores
+        // and the compiler's own loads only add younger operations: the wait
+        // stays sufficient).  Every poll register passes through such a wait
+        // before it is read or reused (the compiler sees the wait as its writer).
         const int nq = K * T;
         unsigned long long* xg = a.xg + mb * nq * 2;  // the team's first column
         unsigned long long* dummy = a.xg + M * kOpMaxK * T * 2 + (int64_t)blockIdx.x * 2 * K;
         const int ql = lane < nq ? lane : 0;  // lanes past nq re-read lane 0's granules (no divergence)
         const unsigned tag = a.tag;
+        // per-lane source of a column's scalars: lane 0 msig, 1.. p_k, 1+K.. z_k
+        const double* scp = msig;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            if (lane == 1 + k) scp = a.p.p[k];
+            if (lane == 1 + K + k && a.fuse) scp = a.z.p[k];
+        }
+        scp += mb;
+        double bk[K], dpacc[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            bk[k] = a.fuse ? a.beta[k] : 0.0;
+            dpacc[k] = 0.0;
+        }
         v4u pl[RING];
+        v2u ps[RING];
         bool dead = false;
         unsigned nslow = 0, nspin = 0;
-        if (n <= 0) return;  // (the streaming waves skip their loop too: barriers match)
-        // Are all members on this CU's XCD?  Then the granules go to the
-        // shared L2 (plain stores; the polls read L2), a round trip that does
-        // not queue behind the HBM stream; otherwise write-through (sc1).
-        // Each member posts {XCC id, tag} write-through, then reads all T.
-        bool l2 = false;
-        {
-            unsigned long long* hdr = a.xg + M * kOpMaxK * T * 2 + (int64_t)gridDim.x * 2 * K + (int64_t)team * T;
-            unsigned xcc;
-            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-            xcc &= 0xf;
-            if (lane == 0)
-                __hip_atomic_store(hdr + member, ((unsigned long long)tag << 32) | xcc, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-            unsigned long long h = 0;
-            for (unsigned spins = 0;; ++spins) {
-                h = lane < T ? __hip_atomic_load(hdr + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                             : ((unsigned long long)tag << 32) | xcc;
-                if (__all((unsigned)(h >> 32) == tag)) break;
-                if (spins >= kTmMaxSpins) {
-                    dead = true;
-                    if (lane == 0) __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(2);
-            }
-            l2 = !dead && __all((unsigned)h == xcc);
-            if (a.dbg & 32) l2 = false;
-        }
-        // the streaming waves' step numbering (m from -F, column c in slot
-        // (c + F) % RING, whole rounds of RING steps, a barrier in every step)
-        for (int base = -F; base < n + L; base += RING) {
-#pragma unroll
-            for (int i = 0; i < RING; ++i) {
-                const int m = base + i;  // columns relative to mb (32-bit: scalar compares)
-                // the poll issued now (for the column finished P steps later), the column finished now
-                const int ci = m - L + P, cf = m - L;
-                const int cic = ci < 0 ? 0 : ci < n ? ci : n - 1;
-                tm_poll(pl[(i + RING - L + P) % RING], xg + ((int64_t)cic * nq + ql) * 2);
-                v4u& g = pl[(i + RING - L) % RING];
-                if (!(a.dbg & 1)) tm_wait<2 * P>(g);  // the poll of step m - P; 2P younger operations stay in flight
-                if (cf >= 0 && cf < n) {
-                    for (unsigned spins = 0;; ++spins) {
-                        const bool ok = g.y == tag && g.w == tag;  // {lo, tag} {hi, tag}
-                        if (__all(ok) || dead || (a.dbg & 1)) break;
-                        if (a.dbg & 64) {
-                            nslow += spins == 0;
-                            nspin++;
-                        }
-                        if (spins >= kTmMaxSpins) {  // a member never published: give up this launch (err)
-                            dead = true;
-                            if (lane == 0) __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                            break;
-                        }
-                        __builtin_amdgcn_s_sleep(2);
-                        tm_poll(g, xg + ((int64_t)cf * nq + ql) * 2);
-                        tm_wait<0>(g);
+        if (n > 0) {
+            // Are all members on this CU's XCD?  Then the granules go to the
+            // shared L2 (plain stores; the polls read L2), a round trip that
+            // does not queue behind the HBM stream; otherwise write-through
+            // (sc1).  Each member posts {XCC id, tag} write-through, then reads all T.
+            bool l2 = false;
+            {
+                unsigned long long* hdr = a.xg + M * kOpMaxK * T * 2 + (int64_t)gridDim.x * 2 * K + (int64_t)team * T;
+                unsigned xcc;
+                asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+                xcc &= 0xf;
+                if (lane == 0)
+                    __hip_atomic_store(hdr + member, ((unsigned long long)tag << 32) | xcc, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                unsigned long long h = 0;
+                for (unsigned spins = 0;; ++spins) {
+                    h = lane < T ? __hip_atomic_load(hdr + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                 : ((unsigned long long)tag << 32) | xcc;
+                    if (__all((unsigned)(h >> 32) == tag)) break;
+                    if (spins >= kTmMaxSpins) {
+                        dead = true;
+                        if (lane == 0) __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                        break;
                     }
-                    double v = lane < nq ? __builtin_bit_cast(double, ((unsigned long long)g.z << 32) | g.x) : 0.0;
-                    for (int o = T >> 1; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);  // fixed order within each k group
-                    if (lane < nq && (lane & (T - 1)) == 0) s_tot[(cf & 1) * K + lane / T] = v;
+                    __builtin_amdgcn_s_sleep(2);
                 }
-                __syncthreads();
-                if (lane < K && !(a.dbg & 2) ) {  // this member's dot of column m: the streaming waves' partials in order
-                    const bool real = m >= 0 && m < n;
-                    double v = 0.0;
-                    if (real) {
+                l2 = !dead && __all((unsigned)h == xcc);
+                if (a.dbg & 32) l2 = false;
+            }
+            // the streaming waves' step numbering (m from -F, column c in slot
+            // (c + F) % RING, whole rounds of RING steps, a barrier in every step)
+            for (int base = -F; base < n + L; base += RING) {
 #pragma unroll
-                        for (int w = 0; w < CW; ++w) v += s_part[((m & 1) * CW + w) * K + lane];
+                for (int i = 0; i < RING; ++i) {
+                    const int m = base + i;  // columns relative to mb (32-bit: scalar compares)
+                    // the column polled now (finished P steps later), the column finished now
+                    const int ci = m - L + P, cf = m - L;
+                    const int cic = ci < 0 ? 0 : ci < n ? ci : n - 1;
+                    tm_load8(ps[(i + RING - L + P) % RING], scp + cic);
+                    tm_poll(pl[(i + RING - L + P) % RING], xg + ((int64_t)cic * nq + ql) * 2);
+                    v4u& g = pl[(i + RING - L) % RING];
+                    v2u& sc = ps[(i + RING - L) % RING];
+                    if (!(a.dbg & 1)) tm_wait2<3 * P>(g, sc);  // step m - P's poll; 3P younger operations in flight
+                    if (cf >= 0 && cf < n) {
+                        for (unsigned spins = 0;; ++spins) {
+                            const bool ok = g.y == tag && g.w == tag;  // {lo, tag} {hi, tag}
+                            if (__all(ok) || dead || (a.dbg & 1)) break;
+                            if (a.dbg & 64) {
+                                nslow += spins == 0;
+                                nspin++;
+                            }
+                            if (spins >= kTmMaxSpins) {  // a member never published: give up this launch (err)
+                                dead = true;
+                                if (lane == 0) __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                                break;
+                            }
+                            __builtin_amdgcn_s_sleep(2);
+                            tm_poll(g, xg + ((int64_t)cf * nq + ql) * 2);
+                            tm_wait<0>(g);
+                        }
+                        double v = lane < nq ? __builtin_bit_cast(double, ((unsigned long long)g.z << 32) | g.x) : 0.0;
+                        for (int o = T >> 1; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);  // fixed order per k group
+                        // d of column cf (src/vamp.cpp:656-659, data::ATx's scaling src/data.cpp:327-330)
+                        const double scv = __builtin_bit_cast(double, ((unsigned long long)sc.y << 32) | sc.x);
+                        const double sg = readlane_d(scv, 0);
+                        const bool own = (cf % T) == member;
+                        const int64_t mg = mb + cf;  // the shard's column index
+#pragma unroll
+                        for (int k = 0; k < K; ++k) {
+                            double t = sg * readlane_d(v, k * T);  // sigma_inv * dpa
+                            t *= a.scale;                          // ATx[mloc] *= 1/sqrt(N)
+                            double p = readlane_d(scv, 1 + k);
+                            if (a.fuse) p = readlane_d(scv, 1 + K + k) + bk[k] * p;  // p = z + beta p
+                            double val = t * a.tau;  // res[i] *= tau
+                            val += a.gam2 * p;       // res[i] += gam2 * v[i]
+                            if (own) {
+                                if (lane == 0) {
+                                    if (a.sraw.p[0]) a.sraw.p[k][mg] = t;
+                                    a.d.p[k][mg] = val;
+                                }
+                                dpacc[k] += val * p;
+                            }
+                            if (lane == 0) s_tot[(cf & 1) * K + k] = sg * val;  // c_k: Ax's (x - mave)*(msig*d)
+                        }
                     }
-                    const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
-                    const v4u gr = {(unsigned)u, tag, (unsigned)(u >> 32), tag};
-                    unsigned long long* dst = real ? xg + ((int64_t)m * nq + lane * T + member) * 2 : dummy + 2 * lane;
-                    if (l2)
-                        tm_publish_l2(dst, gr);
-                    else
-                        tm_publish(dst, gr);
+                    __syncthreads();
+                    if (lane < K && !(a.dbg & 2)) {  // this member's dot of column m: the streaming waves' partials in order
+                        const bool real = m >= 0 && m < n;
+                        double v = 0.0;
+                        if (real) {
+#pragma unroll
+                            for (int w = 0; w < CW; ++w) v += s_part[((m & 1) * CW + w) * K + lane];
+                        }
+                        const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+                        const v4u gr = {(unsigned)u, tag, (unsigned)(u >> 32), tag};
+                        unsigned long long* dst = real ? xg + ((int64_t)m * nq + lane * T + member) * 2 : dummy + 2 * lane;
+                        if (l2)
+                            tm_publish_l2(dst, gr);
+                        else
+                            tm_publish(dst, gr);
+                    }
                 }
             }
-        }
 #pragma unroll
-        for (int s = 0; s < RING; ++s) tm_wait<0>(pl[s]);  // nothing of ours lands after the wave ends
-        if ((a.dbg & 64) && lane == 0) {  // timing experiments: slow-path counts into the flag block
-            __hip_atomic_fetch_add(a.err + 1, nslow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_fetch_add(a.err + 2, nspin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_fetch_add(a.err + 3, (unsigned)n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            for (int s = 0; s < RING; ++s) tm_wait2<0>(pl[s], ps[s]);  // nothing of ours lands after the loop
+            if ((a.dbg & 64) && lane == 0) {  // timing experiments: slow-path counts into the flag block
+                __hip_atomic_fetch_add(a.err + 1, nslow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_fetch_add(a.err + 2, nspin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_fetch_add(a.err + 3, (unsigned)n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
         }
+        // <d_k, p_k> over the columns this member owns, in order; drained
+        // before the barrier after which wave 0 takes the ticket
+        if (lane == 0) {
+#pragma unroll
+            for (int k = 0; k < K; ++k) red_put(a.ro, (int64_t)blockIdx.x * K + k, dpacc[k]);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
         return;
     }
 
@@ -348,11 +410,16 @@ __global__ __launch_bounds__(kTmThreads) void atax_team_kernel(const double* __r
         }
     };
     // d of column m from its total dot, and acc += (x - mave) * msig * d
+    // tot: the column's total dots, or (COMM) the c_k the hand-off wave formed
     auto finish = [&](int slot, int m, const double (&tot)[K]) {
+        double cc[K];
+        if constexpr (COMM) {
+#pragma unroll
+            for (int k = 0; k < K; ++k) cc[k] = tot[k];
+        } else {
         const double sg = readlane_d(pk[slot], 1);
         const bool own = (m % T) == member;
         const int64_t mg = mb + m;  // the shard's column index
-        double cc[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             double t = sg * tot[k];  // sigma_inv * dpa
@@ -369,6 +436,7 @@ __global__ __launch_bounds__(kTmThreads) void atax_team_kernel(const double* __r
                 dpacc[k] += val * p;
             }
             cc[k] = sg * val;  // Ax: (x - mave) * (msig * x_i)
+        }
         }
 #pragma unroll
         for (int s = 0; s < S; ++s) {
@@ -432,9 +500,12 @@ __global__ __launch_bounds__(kTmThreads) void atax_team_kernel(const double* __r
             if (jl + 1 < nrows) dst[(int64_t)k * ld + jl + 1] = acc[k][s].y;
         }
     }
-    // <d_k, p_k>: each workgroup's sums over the columns it owns, in order;
-    // the last workgroup adds them in block order
-    if (threadIdx.x == 0) {
+    // <d_k, p_k>: each workgroup's sums over the columns it owns, in order
+    // (COMM: the hand-off wave's, put before the barrier below); the last
+    // workgroup adds them in block order
+    if constexpr (COMM) {
+        __syncthreads();
+    } else if (threadIdx.x == 0) {
 #pragma unroll
         for (int k = 0; k < K; ++k) red_put(a.ro, (int64_t)blockIdx.x * K + k, dpacc[k]);
     }

@@ -724,11 +724,24 @@ static bool whole_column_ok(int64_t N) {
     return N >= 1 && kOpMaxK * (N + 2) <= kOpLdsDoubles && (N + kOpRows - 1) / kOpRows <= kOpMaxS;
 }
 
-// The default: whole columns per workgroup while K*N fits the LDS, else the
-// smallest team whose members' rows fit the registers (configuration 2).
+// The default: whole columns per workgroup (team size 1, the team kernel
+// without a hand-off: 585 us against 646 us for atax_kernel at C2, K = 2,
+// profiles/r02c_op_sweep.txt) while the rows fit one workgroup, else the
+// smallest team whose members' rows fit the registers (configuration 6:
+// 4 columns prefetched, a lag of 5 steps, polls 2 steps ahead; measured best
+// at N = 50,000 and 100,000, profiles/r02c_op_sweep.txt).
 bool op_plan(int64_t N, int64_t M, int cus, int variant, OpPlan* out) {
     if (N < 1 || cus < 1) return false;
-    if (variant == 0 || (variant == kOpDefault && whole_column_ok(N))) {
+    if (variant == kOpDefault) {
+        // one workgroup per column range (team size 1): two columns prefetched
+        // where they fit the registers (S <= 8), else one
+        OpPlan p{};
+        if (team_plan(N, M, cus, 1, 1, &p) || team_plan(N, M, cus, 1, 0, &p)) {
+            *out = p;
+            return true;
+        }
+    }
+    if (variant == 0) {
         if (!whole_column_ok(N)) return false;
         OpPlan p{};
         p.S = (int)std::max<int64_t>(1, (N + kOpRows - 1) / kOpRows);
@@ -741,7 +754,7 @@ bool op_plan(int64_t N, int64_t M, int cus, int variant, OpPlan* out) {
     if (variant > 0) return team_plan(N, M, cus, variant / 10, variant % 10, out);
     for (int T = 2; T <= 32; T *= 2) {
         OpPlan p{};
-        if (!team_plan(N, M, cus, T, 2, &p)) continue;
+        if (!team_plan(N, M, cus, T, 6, &p)) continue;
         *out = p;
         return true;
     }
