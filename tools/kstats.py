@@ -23,7 +23,7 @@ w = csv.writer(sys.stdout)
 w.writerow(["Name", "Calls", "GatedCalls", "TotalDurationNs", "AverageNs", "MinNs", "MaxNs"])
 for n, d in sorted(dur.items(), key=lambda kv: -sum(kv[1])):
     gated = []
-    if any(k in n for k in ("ax_partial_kernel", "atx_kernel", "atax_kernel", "loo_kernel")):
+    if any(k in n for k in ("ax_partial_kernel", "atx_kernel", "atax_kernel", "atax_team_kernel", "loo_kernel")):
         cut = 0.05 * max(d)
         gated = [x for x in d if x < cut]
         d = [x for x in d if x >= cut]

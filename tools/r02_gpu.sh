@@ -32,6 +32,7 @@ for s in "$@"; do
         prof) step "rocprof_$a" 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$a" -o run --output-format csv -- \
                   python bench.py --config "$a" --steps "${b:-10}" --warmup 2 --no-cpu-baseline ;;
         pmc) step "pmc_$a" 500 bash tools/pmc.sh "$a" ;;
+        pmcsq) step "pmcsq_$a" 300 bash tools/pmc_sq.sh "$a" ;;
         kbench) step "kbench_$a" 600 python tools/kbench.py $a ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac
