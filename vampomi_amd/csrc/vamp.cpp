@@ -17,14 +17,17 @@
 //      (:681) up to the tau / gam2 epilogue applied when those are known.
 // err_measures' A.x2_hat (:826) is the product of (2); A^T y (:303) is
 // computed once.  Scalar reductions are batched per dependency level.
-// batch_rhs=2 (default) replaces the A^T pass of (3) by recurrences: the CG
+// batch_rhs=2 replaces the A^T pass of (3) by recurrences: the CG
 // keeps W += alpha*A^T(A p) beside mu += alpha*p for both systems, so the
 // pass count per iteration is 1 + 2*max(k1, k2) instead of 2 + 2*max(k1, k2);
 // the vectors are the same up to rounding (parity within 1e-10, counts exact).
-// batch_rhs=3 (default) also carries A x2 as A x2 += alpha * A p through the
-// CG steps (from the previous iteration's A x2) and computes z1 = A x1_hat as
-// one more right-hand side of the first CG pass, so no pass over X is left
-// outside the CG: 2*max(k1, k2) passes per iteration.
+// batch_rhs=3 also carries A x2 as A x2 += alpha * A p through the CG steps
+// (from the previous iteration's A x2) and computes z1 = A x1_hat as one more
+// right-hand side of the first CG pass, so no pass over X is left outside the
+// CG: 2*max(k1, k2) passes per iteration.
+// batch_rhs=4 (the default) reads X once per CG step: A p is carried as an
+// N-vector recurrence and the one-pass operator (atax_team.hip) forms A^T q
+// and A d from the same column read: 1 + max(k1, k2) passes per iteration.
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
