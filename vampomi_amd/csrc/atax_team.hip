@@ -46,7 +46,7 @@ typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 typedef unsigned int v2u __attribute__((ext_vector_type(2)));
 
 #ifndef TM_FMA
-#define TM_FMA 0  // experiment switch: fused multiply-adds in the dot and the A d accumulation
+#define TM_FMA 1  // fused multiply-adds in the dot and the A d accumulation
 #endif
 static constexpr int kTmThreads = 512;        // 8 waves, 2 per SIMD: <= 256 VGPRs per lane
 static constexpr int kTmMaxT = 32;            // members per team (one XCD under round-robin dealing)

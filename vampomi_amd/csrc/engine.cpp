@@ -554,6 +554,33 @@ vampomi_status op_prepare(vampomi_ctx* c) {
 // word 4 of the mapped flag block (zeroed at open)
 unsigned* op_err_dev(vampomi_ctx* c) { return reinterpret_cast<unsigned*>(c->d_flag + 4); }
 
+// A team launch needs every workgroup of its grid resident at once (one per
+// CU).  Two of them running together on one device (contexts of one process
+// on the same GPU, e.g. ranks as threads) could each hold part of the CUs and
+// wait for members that never start, until the hand-off times out.  So the
+// team launches of all contexts of this process on a device are ordered by an
+// event chain: each waits (on the device, no host sync) for the previous one.
+struct TeamGate {
+    std::mutex mu;
+    hipEvent_t last = nullptr;
+};
+static TeamGate g_team_gate[64];
+
+template <class Launch>
+static vampomi_status team_launch(vampomi_ctx* c, Launch&& launch) {
+    if (c->opp.T <= 1 || c->device < 0 || c->device >= 64) {
+        HIPCHK(launch());
+        return VAMPOMI_OK;
+    }
+    TeamGate& g = g_team_gate[c->device];
+    std::lock_guard<std::mutex> lk(g.mu);
+    if (g.last) HIPCHK(hipStreamWaitEvent(c->st, g.last, 0));
+    HIPCHK(launch());
+    if (!g.last) HIPCHK(hipEventCreateWithFlags(&g.last, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(g.last, c->st));
+    return VAMPOMI_OK;
+}
+
 vampomi_status op_check_err(vampomi_ctx* c) {
     if (c->h_flag && __atomic_load_n(reinterpret_cast<unsigned*>(c->h_flag + 4), __ATOMIC_ACQUIRE))
         return fail(VAMPOMI_ERR_HIP, "one-pass operator: a team hand-off timed out (a workgroup of the team never "
@@ -586,7 +613,7 @@ vampomi_status op_dev(vampomi_ctx* c, int K, const vk::OpArgs& a, const int* gat
     x.ro = vk::RedOut{c->red_part, c->use_comm ? ad + (int64_t)K * c->ld : c->scal + SL_DP, c->ticket, nullptr, 0,
                       gate};
     TimedLaunch t = launch_stat(c, 3, K, pass_bytes(c, K), 2.0 * pass_flops(c, K));
-    HIPCHK(vk::atax(c->shard(), c->opp, K, x, c->st, vk::Timing{t.a, t.b}, gate));
+    STCHK(team_launch(c, [&] { return vk::atax(c->shard(), c->opp, K, x, c->st, vk::Timing{t.a, t.b}, gate); }));
     c->stats.a_passes_exec++;
     vk::Ptrs os{};
     for (int k = 0; k < K; ++k) os.p[k] = ad + (int64_t)k * c->ld;
@@ -1337,7 +1364,7 @@ extern "C" vampomi_status vampomi_dev_time_pass(vampomi_ctx* c, int which, int K
             }
             x.dbg = std::getenv("VAMPOMI_OP_DBG") ? std::atoi(std::getenv("VAMPOMI_OP_DBG")) : 0;
             if (c->opp.T > 1) x.err = op_err_dev(c);
-            HIPCHK(vk::atax(c->shard(), c->opp, K, x, c->st));
+            STCHK(team_launch(c, [&] { return vk::atax(c->shard(), c->opp, K, x, c->st); }));
         }
         else  // association pass: ymod = nbuf slot 0, x1 = mbuf slot 0, sums in mbuf slots 3..7
             HIPCHK(vk::loo_sums(c->shard(), c->nbuf, c->mbuf, c->sqrtN, c->mbuf + 3 * Mx, c->st, c->loo_variant));
