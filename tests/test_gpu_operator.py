@@ -103,3 +103,41 @@ def test_operator_team_plans_bitwise_repeatable(problem):
         for x, y in zip(a, b):
             assert np.array_equal(x, y), v
     d.set_variant(3, -1)
+
+
+def test_team_launches_from_two_contexts_on_one_gpu():
+    """Two contexts of one process on the same GPU (ranks as threads, as the
+    loopback tests run them) launching team grids at the same time: each
+    grid needs every CU, so the launches are ordered on the device
+    (engine.cpp team_launch); without that the two grids can each hold part
+    of the CUs and time out."""
+    import threading
+
+    N, Mt = 50001, 1500
+    X = O.generate_markers(5, 1, N, 0, Mt)
+    mave, msig = O.marker_stats(X)
+    rng = np.random.default_rng(3)
+    ar, p = rng.normal(size=(2, N)), rng.normal(size=(2, Mt))
+    ref = _ref(X, mave, msig, ar, None, p, None, None, 1.3, 0.8, 0.4)
+    errs, outs = [], []
+
+    def work():
+        try:
+            with va.Data(N, Mt) as d:
+                d.load_meth(X)
+                for _ in range(6):
+                    outs.append(d.op_apply(ar, p, 1.3, 0.8, 0.4))
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+
+    ts = [threading.Thread(target=work) for _ in range(2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=120)
+    assert not any(t.is_alive() for t in ts), "a context is stuck"
+    assert not errs, errs
+    assert len(outs) == 12
+    for gd, gad, gdp in outs:
+        assert relerr(gd, ref[0]) < 1e-12 and relerr(gad, ref[1]) < 1e-12
+        assert np.array_equal(gd, outs[0][0]) and np.array_equal(gad, outs[0][1])
