@@ -305,6 +305,14 @@ vampomi_status vampomi_dev_time_pass(vampomi_ctx* ctx, int which, int K, int rep
  * fused direction update; which = 2: the association-test pass of
  * vampomi_assoc_loo) */
 vampomi_status vampomi_dev_kernel_name(const vampomi_ctx* ctx, int which, int K, int mode, char* out, int cap);
+/* The one-pass operator's plan for N samples, M markers and `cus` compute
+ * units under `variant` (as vampomi_dev_set_variant(ctx, 3, variant)), no
+ * device needed: team size T (0: the whole-column kernel), loads per lane per
+ * column S, rows per team member TR, workgroups grid, partial-sum slots
+ * nslots, and the kernel name for K right-hand sides.  VAMPOMI_ERR_ARG if
+ * no such plan exists. */
+vampomi_status vampomi_dev_op_plan(int64_t N, int64_t M, int cus, int variant, int K, int* T, int* S, int* TR,
+                                   int* grid, int64_t* nslots, char* name, int cap);
 /* One application of the one-pass CG operator (K <= 2 systems, one rank),
  * host buffers: q_k = ar_k/diag [+ beta_k*qo_k], p_k [= z_k + beta_k*p_k]
  * when z is not null (then qo and beta are required), and

@@ -1,0 +1,68 @@
+"""Host logic of the one-pass operator's plans (kernels.hip op_plan,
+atax_team.hip team_plan) through the C ABI, no device: which kernel runs
+for which N, and the invariants every team plan must keep (every team member
+holds rows, teams fill the grid, one workgroup per CU at most, the member's
+rows fit its loads)."""
+import ctypes as C
+
+import pytest
+
+from vampomi_amd import _lib
+
+lib = _lib.load()
+
+
+def plan(N, M=62500, cus=256, variant=-1, K=2):
+    T, S, TR, grid = C.c_int(), C.c_int(), C.c_int(), C.c_int()
+    ns = C.c_int64()
+    name = C.create_string_buffer(128)
+    st = lib.vampomi_dev_op_plan(N, M, cus, variant, K, C.byref(T), C.byref(S), C.byref(TR), C.byref(grid),
+                                 C.byref(ns), name, 128)
+    if st != 0:
+        return None
+    return dict(T=T.value, S=S.value, TR=TR.value, grid=grid.value, nslots=ns.value, name=name.value.decode())
+
+
+def test_default_plans_of_the_baseline_shapes():
+    c2, c3, c4 = plan(10000), plan(100000), plan(50000)
+    assert c2["T"] == 1 and c2["name"] == "atax_team_kernel<2, 10, 1, 0, 0, false, 2>"
+    assert c3["T"] == 32 and c3["S"] == 4 and c3["TR"] == 3200 and c3["nslots"] == 8
+    assert c3["name"] == "atax_team_kernel<2, 4, 4, 5, 2, true, 2>"
+    assert c4["T"] == 16 and c4["S"] == 4 and c4["nslots"] == 16
+    assert plan(10000, variant=0)["name"] == "atax_kernel<2, 10>"
+
+
+@pytest.mark.parametrize("N", [1, 2, 7, 128, 1023, 1025, 4097, 8192, 10239, 10240, 10241, 20000, 33333, 50001,
+                               65536, 99999, 100000, 114688, 120000, 143360])
+def test_team_plan_invariants(N):
+    p = plan(N)
+    assert p is not None, N
+    T, S, TR, grid = p["T"], p["S"], p["TR"], p["grid"]
+    assert 1 <= T <= 32 and T & (T - 1) == 0
+    assert grid <= 256 and grid % T == 0 and (T == 1 or grid % (8 * T) == 0)
+    assert p["nslots"] == grid // T
+    if T > 1:
+        assert (T - 1) * TR < N <= T * TR  # every member holds rows, the team covers N
+        rows_per_step = 7 * 128
+    else:
+        rows_per_step = 8 * 128
+    assert S * rows_per_step >= min(TR, N) and (S - 1) * rows_per_step < min(TR, N)
+
+
+def test_no_plan_beyond_the_largest_team():
+    # 32 members x 5 loads x 896 rows: beyond it the CG step keeps two passes
+    assert plan(143360) is not None and plan(143361) is None
+    assert plan(100000, K=3) is None
+    assert plan(0) is None
+
+
+def test_every_variant_plan_is_valid_or_refused():
+    for v in [0] + [T * 10 + c for T in (1, 2, 4, 8, 16, 32) for c in range(9)]:
+        for N in (1000, 10000, 50001, 100000):
+            p = plan(N, variant=v)
+            if p is None:
+                continue
+            if v == 0:
+                assert p["T"] == 0
+            else:
+                assert p["T"] == v // 10

@@ -53,35 +53,39 @@ static constexpr int kTmMaxT = 32;            // members per team (one XCD under
 static constexpr unsigned kTmMaxSpins = 1u << 21;  // ~2 s of polling, then the launch gives up (err)
 
 // configurations: F columns prefetched, L steps of lag, P polls in flight,
-// hand-off (T > 1), and the most 16-byte loads per lane per column that fit
-// 256 VGPRs at K = 2 without spilling (gfx950, ROCm 7.2 compiler)
+// hand-off (T > 1), the most loads per lane per column that fit 256 VGPRs at
+// K = 2 without spilling (gfx950, ROCm 7.2 compiler), and E doubles per lane
+// per load (2: 16-byte loads, rows in steps of 128 per wave; 1: 8-byte
+// loads, steps of 64, for tiles that 16-byte steps would pad by up to 14 %)
 struct TmCfg {
     int F, L, P;
     bool comm;
     int maxS;
+    int E;
+    bool ilv;  // team t takes columns t, t + nteams, ... (else a contiguous range)
 };
 static constexpr TmCfg kTmCfg[] = {
-    {1, 0, 0, false, 10},  // 0: T = 1, one column prefetched
-    {2, 0, 0, false, 8},   // 1: T = 1, two
-    {3, 5, 2, true, 4},    // 2
-    {2, 4, 2, true, 5},    // 3
-    {3, 6, 3, true, 4},    // 4
-    {3, 6, 2, true, 4},    // 5
-    {4, 5, 2, true, 4},    // 6
-    {4, 6, 2, true, 4},    // 7
-    {3, 4, 2, true, 4},    // 8
+    {1, 0, 0, false, 10, 2, false},  // 0: T = 1, one column prefetched
+    {2, 0, 0, false, 8, 2, false},   // 1: T = 1, two
+    {3, 5, 2, true, 4, 2, false},    // 2
+    {2, 4, 2, true, 5, 2, false},    // 3
+    {3, 6, 3, true, 4, 2, false},    // 4
+    {3, 6, 2, true, 4, 2, false},    // 5
+    {4, 5, 2, true, 4, 2, false},    // 6
+    {4, 5, 2, true, 4, 2, true},     // 7
+    {3, 5, 2, true, 4, 2, true},     // 8
 };
 static constexpr int kTmNCfg = sizeof(kTmCfg) / sizeof(kTmCfg[0]);
 
-__host__ __device__ constexpr int tm_rows_per_step(bool comm) { return 128 * (comm ? 7 : 8); }
+__host__ __device__ constexpr int tm_rows_per_step(bool comm, int E) { return 64 * E * (comm ? 7 : 8); }
 // q in LDS: every lane row of the S steps (zeros past the tile, so those
 // rows need no mask) when that fits beside the partials, else the tile only
 // (rows past it masked)
-__host__ __device__ constexpr bool tm_qfull(int K, int S, bool comm) {
-    return (K * S * tm_rows_per_step(comm) + 4 * 8 * K) * 8 <= 160 * 1024;
+__host__ __device__ constexpr bool tm_qfull(int K, int S, bool comm, int E) {
+    return (K * S * tm_rows_per_step(comm, E) + 4 * 8 * K) * 8 <= 160 * 1024;
 }
-__host__ __device__ constexpr int64_t tm_qstride(int K, int S, bool comm, int64_t tile_rows) {
-    return tm_qfull(K, S, comm) ? (int64_t)S * tm_rows_per_step(comm) : (tile_rows + 1) & ~(int64_t)1;
+__host__ __device__ constexpr int64_t tm_qstride(int K, int S, bool comm, int E, int64_t tile_rows) {
+    return tm_qfull(K, S, comm, E) ? (int64_t)S * tm_rows_per_step(comm, E) : (tile_rows + 1) & ~(int64_t)1;
 }
 
 __device__ __forceinline__ double readlane_d(double v, int l) {
@@ -89,6 +93,63 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
     const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)u, l);
     const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), l);
     return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+
+// Cross-lane sums without the LDS (DPP moves and the gfx950 permlane swaps are
+// VALU; ds_bpermute shuffles queue behind the streaming waves' LDS reads).
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+    const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_mov_dpp((int)(unsigned)u, CTRL, 0xf, 0xf, false);
+    const unsigned hi = (unsigned)__builtin_amdgcn_mov_dpp((int)(unsigned)(u >> 32), CTRL, 0xf, 0xf, false);
+    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+__device__ __forceinline__ double pack_d(unsigned lo, unsigned hi) {
+    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+// v_permlane16_swap(x, x): the first result holds rows {0,0,2,2}, the second
+// {1,1,3,3} of x (16-lane rows), so their sum is row 0+1 / 2+3 in every lane
+__device__ __forceinline__ double swap16_sum(double v) {
+    const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+    const auto l = __builtin_amdgcn_permlane16_swap((unsigned)u, (unsigned)u, false, false);
+    const auto h = __builtin_amdgcn_permlane16_swap((unsigned)(u >> 32), (unsigned)(u >> 32), false, false);
+    return pack_d(l[0], h[0]) + pack_d(l[1], h[1]);
+}
+// v_permlane32_swap(a, b): the first result is {a lanes 0-31, b lanes 0-31},
+// the second {a lanes 32-63, b lanes 32-63}
+__device__ __forceinline__ void swap32(double a, double b, double& r0, double& r1) {
+    const unsigned long long ua = __builtin_bit_cast(unsigned long long, a), ub = __builtin_bit_cast(unsigned long long, b);
+    const auto l = __builtin_amdgcn_permlane32_swap((unsigned)ua, (unsigned)ub, false, false);
+    const auto h = __builtin_amdgcn_permlane32_swap((unsigned)(ua >> 32), (unsigned)(ub >> 32), false, false);
+    r0 = pack_d(l[0], h[0]);
+    r1 = pack_d(l[1], h[1]);
+}
+// the sum over each aligned group of G lanes, in every lane of the group; the
+// pairs are added in the same order in every lane (a + b = b + a), so every
+// lane of a group holds the same bits
+template <int G>
+__device__ __forceinline__ double group_sum(double v) {
+    if constexpr (G >= 2) v = v + dpp_d<0xb1>(v);   // quad_perm [1,0,3,2]: lane ^ 1
+    if constexpr (G >= 4) v = v + dpp_d<0x4e>(v);   // quad_perm [2,3,0,1]: lane ^ 2
+    if constexpr (G >= 8) v = v + dpp_d<0x141>(v);  // row_half_mirror: the other quad of 8
+    if constexpr (G >= 16) v = v + dpp_d<0x140>(v); // row_mirror: the other half of the row
+    if constexpr (G >= 32) v = swap16_sum(v);       // the other row of 32
+    if constexpr (G >= 64) {
+        double a, b;
+        swap32(v, v, a, b);
+        v = a + b;
+    }
+    return v;
+}
+__device__ __forceinline__ double group_sum_rt(double v, int G) {  // G a power of two <= 32, wave-uniform
+    switch (G) {
+        case 2: return group_sum<2>(v);
+        case 4: return group_sum<4>(v);
+        case 8: return group_sum<8>(v);
+        case 16: return group_sum<16>(v);
+        case 32: return group_sum<32>(v);
+        default: return v;
+    }
 }
 
 // Untracked 16-byte granule traffic of the hand-off wave (see there).
@@ -114,14 +175,15 @@ __device__ __forceinline__ void tm_publish_l2(unsigned long long* p, const v4u& 
     asm volatile("s_nop 4\n\tglobal_store_dwordx4 %0, %1, off\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
 }
 
-template <int K, int S, int F, int L, int P, bool COMM>
+template <int K, int S, int F, int L, int P, bool COMM, int E>
 __global__ __launch_bounds__(kTmThreads) void atax_team_kernel(const double* __restrict__ X, int64_t ld, int64_t N,
                                                                int64_t M, const double* __restrict__ mave,
                                                                const double* __restrict__ msig, OpArgs a, int T,
-                                                               int TR, const int* __restrict__ gate) {
+                                                               int TR, int ilv, const int* __restrict__ gate) {
     if (gate && !*gate) return;
     constexpr int CW = COMM ? 7 : 8;  // streaming waves
-    constexpr int RS = tm_rows_per_step(COMM);
+    constexpr int RS = tm_rows_per_step(COMM, E);
+    static_assert(E == 1 || E == 2, "doubles per lane per load");
     constexpr int RING = F + L + 1;
     static_assert(COMM || L == 0, "without a hand-off the column is finished in its own step");
     static_assert(!COMM || (P >= 1 && P <= L), "polls in flight");
@@ -132,17 +194,22 @@ __global__ __launch_bounds__(kTmThreads) void atax_team_kernel(const double* __r
     const int member = g % T;
     const int team = (blockIdx.x & 7) + 8 * (g / T);  // members share blockIdx % 8: one XCD (speed only)
     const int nteams = gridDim.x / T;
-    const int64_t mb = (int64_t)team * M / nteams, me = (int64_t)(team + 1) * M / nteams;
-    const int n = (int)(me - mb);  // the team's columns
+    // the team's columns: mb + cs*m, m < n (a contiguous range, or every nteams-th)
+    const int64_t cs = ilv ? nteams : 1;
+    const int64_t mb = ilv ? team : (int64_t)team * M / nteams;
+    const int n = (int)(ilv ? (M - team + nteams - 1) / nteams : (int64_t)(team + 1) * M / nteams - mb);
+    const int64_t nmax = (M + nteams - 1) / nteams;  // granule rows per team
+    const int64_t gwords = (M + gridDim.x) * kOpMaxK * T * 2;  // the granule block (OpArgs.xg)
     const int64_t r0 = (int64_t)member * TR;
     const int nrows = (int)(N - r0 < TR ? N - r0 : TR);  // >= 1 (op_plan)
-    constexpr bool QFULL = tm_qfull(K, S, COMM);
-    const int QS = (int)tm_qstride(K, S, COMM, TR < N ? TR : N);  // q stride
+    constexpr bool QFULL = tm_qfull(K, S, COMM, E);
+    const int QS = (int)tm_qstride(K, S, COMM, E, TR < N ? TR : N);  // q stride
     double* q_lds = lds;                                  // K x QS
     double* s_part = lds + K * QS;                        // [2][CW][K] wave partials of a column's dot
     double* s_tot = s_part + 2 * CW * K;                  // [2][K] team totals (hand-off)
-    const int jb = 128 * wave + 2 * lane;                 // row of this lane in step s: RS*s + jb
-    const int nbytes = ((nrows + 1) & ~1) * 8;            // the tile of a column (+ the zero pad row for odd N)
+    const int jb = 64 * E * wave + E * lane;              // row of this lane in step s: RS*s + jb
+    // the tile of a column (E = 2: + the zero pad row for odd N)
+    const int nbytes = (E == 2 ? (nrows + 1) & ~1 : nrows) * 8;
 
     if (COMM && wave == CW) {
         // ---------------- the hand-off wave ----------------
@@ -161,8 +228,8 @@ __global__ __launch_bounds__(kTmThreads) void atax_team_kernel(const double* __r
         // stays sufficient).  Every poll register passes through such a wait
         // before it is read or reused (the compiler sees the wait as its writer).
         const int nq = K * T;
-        unsigned long long* xg = a.xg + mb * nq * 2;  // the team's first column
-        unsigned long long* dummy = a.xg + M * kOpMaxK * T * 2 + (int64_t)blockIdx.x * 2 * K;
+        unsigned long long* xg = a.xg + (int64_t)team * nmax * nq * 2;  // the team's first column
+        unsigned long long* dummy = a.xg + gwords + (int64_t)blockIdx.x * 2 * K;
         const int ql = lane < nq ? lane : 0;  // lanes past nq re-read lane 0's granules (no divergence)
         const unsigned tag = a.tag;
         // per-lane source of a column's scalars: lane 0 msig, 1.. p_k, 1+K.. z_k
@@ -172,7 +239,7 @@ __global__ __launch_bounds__(kTmThreads) void atax_team_kernel(const double* __r
             if (lane == 1 + k) scp = a.p.p[k];
             if (lane == 1 + K + k && a.fuse) scp = a.z.p[k];
         }
-        scp += mb;
+        scp += mb;  // column m (relative) is scp[m * cs]
         double bk[K], dpacc[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) {
@@ -190,7 +257,7 @@ __global__ __launch_bounds__(kTmThreads) void atax_team_kernel(const double* __r
             // (sc1).  Each member posts {XCC id, tag} write-through, then reads all T.
             bool l2 = false;
             {
-                unsigned long long* hdr = a.xg + M * kOpMaxK * T * 2 + (int64_t)gridDim.x * 2 * K + (int64_t)team * T;
+                unsigned long long* hdr = a.xg + gwords + (int64_t)gridDim.x * 2 * kOpMaxK + (int64_t)team * T;
                 unsigned xcc;
                 asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
                 xcc &= 0xf;
@@ -221,7 +288,7 @@ __global__ __launch_bounds__(kTmThreads) void atax_team_kernel(const double* __r
                     // the column polled now (finished P steps later), the column finished now
                     const int ci = m - L + P, cf = m - L;
                     const int cic = ci < 0 ? 0 : ci < n ? ci : n - 1;
-                    tm_load8(ps[(i + RING - L + P) % RING], scp + cic);
+                    tm_load8(ps[(i + RING - L + P) % RING], scp + cic * cs);
                     tm_poll(pl[(i + RING - L + P) % RING], xg + ((int64_t)cic * nq + ql) * 2);
                     v4u& g = pl[(i + RING - L) % RING];
                     v2u& sc = ps[(i + RING - L) % RING];
@@ -244,14 +311,22 @@ __global__ __launch_bounds__(kTmThreads) void atax_team_kernel(const double* __r
                             tm_wait<0>(g);
                         }
                         double v = lane < nq ? __builtin_bit_cast(double, ((unsigned long long)g.z << 32) | g.x) : 0.0;
-                        for (int o = T >> 1; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);  // fixed order per k group
+                        if (a.dbg & 512) {  // timing experiment: the ds_bpermute butterfly
+                            for (int o = T >> 1; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+                        } else if (!(a.dbg & 256)) {
+                            v = group_sum_rt(v, T);  // the T members, fixed order per k group
+                        }
                         // d of column cf (src/vamp.cpp:656-659, data::ATx's scaling src/data.cpp:327-330)
                         const double scv = __builtin_bit_cast(double, ((unsigned long long)sc.y << 32) | sc.x);
                         const double sg = readlane_d(scv, 0);
                         const bool own = (cf % T) == member;
-                        const int64_t mg = mb + cf;  // the shard's column index
+                        const int64_t mg = mb + cf * cs;  // the shard's column index
 #pragma unroll
                         for (int k = 0; k < K; ++k) {
+                            if (a.dbg & 128) {
+                                if (lane == 0) s_tot[(cf & 1) * K + k] = 0.0;
+                                continue;
+                            }
                             double t = sg * readlane_d(v, k * T);  // sigma_inv * dpa
                             t *= a.scale;                          // ATx[mloc] *= 1/sqrt(N)
                             double p = readlane_d(scv, 1 + k);
@@ -314,7 +389,7 @@ __global__ __launch_bounds__(kTmThreads) void atax_team_kernel(const double* __r
 #pragma unroll
         for (int k = 0; k < K; ++k) {
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
+            for (int h = 0; h < E; ++h) {
                 double q = 0.0;
                 if (jl + h < nrows) {
                     const int64_t j = r0 + jl + h;
@@ -336,31 +411,39 @@ __global__ __launch_bounds__(kTmThreads) void atax_team_kernel(const double* __r
         if (lane == 2 + k) pkp = a.p.p[k];
         if (lane == 2 + K + k && a.fuse) pkp = a.z.p[k];
     }
-    pkp += mb;  // column m (relative) is pkp[m]
+    pkp += mb;  // column m (relative) is pkp[m * cs]
     bool valid[S];
 #pragma unroll
     for (int s = 0; s < S; ++s) valid[s] = RS * s + jb < nrows;
-    v2d acc[K][S];
+    double acc[K][S][E];
 #pragma unroll
     for (int k = 0; k < K; ++k)
 #pragma unroll
-        for (int s = 0; s < S; ++s) acc[k][s] = v2d{0.0, 0.0};
+        for (int s = 0; s < S; ++s)
+#pragma unroll
+            for (int e = 0; e < E; ++e) acc[k][s][e] = 0.0;
     double dpacc[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) dpacc[k] = 0.0;
 
-    v2d xr[RING][S];
+    double xr[RING][S][E];
     double pk[RING];
     const char* xtile = reinterpret_cast<const char*>(X + mb * ld + r0);
     auto load = [&](int slot, int m) {
-        pk[slot] = pkp[m];  // older than the column's X loads: it lands first
+        pk[slot] = pkp[m * cs];  // older than the column's X loads: it lands first
         const __amdgpu_buffer_rsrc_t rs =
-            __builtin_amdgcn_make_buffer_rsrc((void*)(xtile + (int64_t)m * ld * 8), (short)0, nbytes, 0x00020000);
+            __builtin_amdgcn_make_buffer_rsrc((void*)(xtile + m * cs * ld * 8), (short)0, nbytes, 0x00020000);
 #pragma unroll
-        for (int s = 0; s < S; ++s)
-            xr[slot][s] = __builtin_bit_cast(v2d, __builtin_amdgcn_raw_buffer_load_b128(rs, (RS * s + jb) * 8, 0, 2));
+        for (int s = 0; s < S; ++s) {
+            if constexpr (E == 2) {
+                const v2d x = __builtin_bit_cast(v2d, __builtin_amdgcn_raw_buffer_load_b128(rs, (RS * s + jb) * 8, 0, 2));
+                xr[slot][s][0] = x.x;
+                xr[slot][s][E - 1] = x.y;
+            } else {
+                xr[slot][s][0] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, (RS * s + jb) * 8, 0, 2));
+            }
+        }
     };
-    // this wave's partial dots of the column in `slot` -> s_part[par]
     // this wave's partial dots of the column in `slot` -> s_part[par]; the
     // slot is centred in place (x - mave), the form finish() uses
     auto dot = [&](int slot, int par) {
@@ -372,40 +455,46 @@ __global__ __launch_bounds__(kTmThreads) void atax_team_kernel(const double* __r
         for (int s = 0; s < S; ++s) {
             // rows past the tile load 0; with QFULL their q is 0, else mave is masked
             const double me_ = QFULL || valid[s] ? mu : 0.0;
-            const double dx = xr[slot][s].x - me_, dy = xr[slot][s].y - me_;
-            xr[slot][s] = v2d{dx, dy};
-            const int jq = QFULL || RS * s + jb < QS ? RS * s + jb : QS - 2;
+            const int jq = QFULL || RS * s + jb < QS ? RS * s + jb : QS - E;
+            double dx[E], q[K][E];
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                dx[e] = xr[slot][s][e] - me_;
+                xr[slot][s][e] = dx[e];
+            }
 #pragma unroll
             for (int k = 0; k < K; ++k) {
-                const v2d q = *reinterpret_cast<const v2d*>(q_lds + k * QS + jq);
+                if constexpr (E == 2) {
+                    const v2d qq = *reinterpret_cast<const v2d*>(q_lds + k * QS + jq);
+                    q[k][0] = qq.x;
+                    q[k][E - 1] = qq.y;
+                } else {
+                    q[k][0] = q_lds[k * QS + jq];
+                }
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
 #if TM_FMA
-                v[k] = __builtin_fma(dx, q.x, v[k]);
-                v[k] = __builtin_fma(dy, q.y, v[k]);
+                    v[k] = __builtin_fma(dx[e], q[k][e], v[k]);
 #else
-                v[k] += dx * q.x;
-                v[k] += dy * q.y;
+                    v[k] += dx[e] * q[k][e];
 #endif
+                }
             }
         }
         if (K == 2) {
-            // reduce-scatter: the xor-32 exchange leaves k = 0 in lanes 0-31 and
-            // k = 1 in lanes 32-63 (one exchange instead of two), then 5 steps
-            const bool hi = lane >= 32;
-            const double send = hi ? v[0] : v[K - 1];
-            double keep = hi ? v[K - 1] : v[0];
-            keep += __shfl_xor(send, 32, 64);
-#pragma unroll
-            for (int o = 16; o > 0; o >>= 1) {
-                if (a.dbg & 4) break;
-                keep += __shfl_xor(keep, o, 64);
+            // reduce-scatter: one permlane32 swap leaves k = 0 in lanes 0-31
+            // and k = 1 in lanes 32-63, then sums within each half
+            double r0, r1;
+            swap32(v[0], v[K - 1], r0, r1);
+            double keep = r0 + r1;
+            if (a.dbg & 512) {  // timing experiment: the ds_bpermute butterfly
+                for (int o = 16; o > 0; o >>= 1) keep += __shfl_xor(keep, o, 64);
+            } else if (!(a.dbg & 4)) {
+                keep = group_sum<32>(keep);
             }
             if ((lane & 31) == 0) s_part[(par * CW + wave) * K + (lane >> 5)] = keep;
         } else {
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) {
-                if (a.dbg & 4) break;
-                v[0] += __shfl_xor(v[0], o, 64);
-            }
+            if (!(a.dbg & 4)) v[0] = group_sum<64>(v[0]);
             if (lane == 0) s_part[(par * CW + wave) * K] = v[0];
         }
     };
@@ -417,41 +506,40 @@ __global__ __launch_bounds__(kTmThreads) void atax_team_kernel(const double* __r
 #pragma unroll
             for (int k = 0; k < K; ++k) cc[k] = tot[k];
         } else {
-        const double sg = readlane_d(pk[slot], 1);
-        const bool own = (m % T) == member;
-        const int64_t mg = mb + m;  // the shard's column index
+            const double sg = readlane_d(pk[slot], 1);
+            const bool own = (m % T) == member;
+            const int64_t mg = mb + m * cs;  // the shard's column index
 #pragma unroll
-        for (int k = 0; k < K; ++k) {
-            double t = sg * tot[k];  // sigma_inv * dpa
-            t *= a.scale;            // ATx[mloc] *= 1/sqrt(N)
-            double p = readlane_d(pk[slot], 2 + k);
-            if (a.fuse) p = readlane_d(pk[slot], 2 + K + k) + bk[k] * p;  // p = z + beta p
-            double val = t * a.tau;  // res[i] *= tau
-            val += a.gam2 * p;       // res[i] += gam2 * v[i]
-            if (own) {
-                if (threadIdx.x == 0) {
-                    if (a.sraw.p[0]) a.sraw.p[k][mg] = t;
-                    a.d.p[k][mg] = val;
+            for (int k = 0; k < K; ++k) {
+                double t = sg * tot[k];  // sigma_inv * dpa
+                t *= a.scale;            // ATx[mloc] *= 1/sqrt(N)
+                double p = readlane_d(pk[slot], 2 + k);
+                if (a.fuse) p = readlane_d(pk[slot], 2 + K + k) + bk[k] * p;  // p = z + beta p
+                double val = t * a.tau;  // res[i] *= tau
+                val += a.gam2 * p;       // res[i] += gam2 * v[i]
+                if (own) {
+                    if (threadIdx.x == 0) {
+                        if (a.sraw.p[0]) a.sraw.p[k][mg] = t;
+                        a.d.p[k][mg] = val;
+                    }
+                    dpacc[k] += val * p;
                 }
-                dpacc[k] += val * p;
+                cc[k] = sg * val;  // Ax: (x - mave) * (msig * x_i)
             }
-            cc[k] = sg * val;  // Ax: (x - mave) * (msig * x_i)
-        }
         }
 #pragma unroll
         for (int s = 0; s < S; ++s) {
             if (a.dbg & 8) break;
-            const double dx = xr[slot][s].x, dy = xr[slot][s].y;  // centred by dot()
 #pragma unroll
-            for (int k = 0; k < K; ++k) {
+            for (int k = 0; k < K; ++k)
+#pragma unroll
+                for (int e = 0; e < E; ++e) {  // xr is centred by dot()
 #if TM_FMA
-                acc[k][s].x = __builtin_fma(dx, cc[k], acc[k][s].x);
-                acc[k][s].y = __builtin_fma(dy, cc[k], acc[k][s].y);
+                    acc[k][s][e] = __builtin_fma(xr[slot][s][e], cc[k], acc[k][s][e]);
 #else
-                acc[k][s].x += dx * cc[k];
-                acc[k][s].y += dy * cc[k];
+                    acc[k][s][e] += xr[slot][s][e] * cc[k];
 #endif
-            }
+                }
         }
     };
     if (n > 0) {
@@ -495,10 +583,10 @@ __global__ __launch_bounds__(kTmThreads) void atax_team_kernel(const double* __r
         const int jl = RS * s + jb;
         if (jl >= nrows) continue;
 #pragma unroll
-        for (int k = 0; k < K; ++k) {
-            dst[(int64_t)k * ld + jl] = acc[k][s].x;
-            if (jl + 1 < nrows) dst[(int64_t)k * ld + jl + 1] = acc[k][s].y;
-        }
+        for (int k = 0; k < K; ++k)
+#pragma unroll
+            for (int e = 0; e < E; ++e)
+                if (jl + e < nrows) dst[(int64_t)k * ld + jl + e] = acc[k][s][e];
     }
     // <d_k, p_k>: each workgroup's sums over the columns it owns, in order
     // (COMM: the hand-off wave's, put before the barrier below); the last
@@ -515,8 +603,8 @@ __global__ __launch_bounds__(kTmThreads) void atax_team_kernel(const double* __r
 // ---------------------------------------------------------------------------
 // host side: plans, instantiations, launch
 // ---------------------------------------------------------------------------
-static int tm_S(int64_t rows, bool comm) {
-    const int rs = tm_rows_per_step(comm);
+static int tm_S(int64_t rows, bool comm, int E) {
+    const int rs = tm_rows_per_step(comm, E);
     return (int)((rows + rs - 1) / rs);
 }
 
@@ -530,12 +618,13 @@ bool team_plan(int64_t N, int64_t M, int cus, int T, int cfg, OpPlan* out) {
     if (grid < T) return false;
     int64_t TR = N;
     if (T > 1) {
-        TR = ((N + T - 1) / T + 127) / 128 * 128;
+        // E = 2: tiles on 128-row (1 KiB) boundaries; E = 1: tiles of ceil(N/T) rows
+        TR = c.E == 2 ? ((N + T - 1) / T + 127) / 128 * 128 : (N + T - 1) / T;
         if ((int64_t)(T - 1) * TR >= N) return false;  // every member holds rows
     }
-    const int S = tm_S(TR, c.comm);
+    const int S = tm_S(TR, c.comm, c.E);
     if (S > c.maxS) return false;
-    const int64_t QS = tm_qfull(kOpMaxK, S, c.comm) ? (int64_t)S * tm_rows_per_step(c.comm) : (std::min<int64_t>(TR, N) + 1) & ~1;
+    const int64_t QS = tm_qstride(kOpMaxK, S, c.comm, c.E, std::min<int64_t>(TR, N));
     const int64_t lds = (QS * kOpMaxK + 2 * 8 * kOpMaxK + 2 * kOpMaxK) * 8;
     if (lds > 160 * 1024) return false;
     OpPlan p{};
@@ -555,8 +644,8 @@ static void launch_tm(const Shard& s, const OpPlan& pl, const OpArgs& a, hipStre
                       const int* gate) {
     constexpr TmCfg c = kTmCfg[C];
     constexpr int CW = c.comm ? 7 : 8;
-    auto kern = atax_team_kernel<K, S, c.F, c.L, c.P, c.comm>;
-    const int64_t QS = tm_qstride(K, S, c.comm, std::min<int64_t>(pl.TR, s.N));
+    auto kern = atax_team_kernel<K, S, c.F, c.L, c.P, c.comm, c.E>;
+    const int64_t QS = tm_qstride(K, S, c.comm, c.E, std::min<int64_t>(pl.TR, s.N));
     const size_t lds = (size_t)(K * QS + 2 * CW * K + 2 * K) * sizeof(double);
     static std::once_flag once;  // more than 64 KiB of dynamic LDS must be allowed explicitly
     std::call_once(once, [&] {
@@ -564,7 +653,7 @@ static void launch_tm(const Shard& s, const OpPlan& pl, const OpArgs& a, hipStre
                                   160 * 1024);
     });
     hipExtLaunchKernelGGL(kern, dim3(pl.grid), dim3(kTmThreads), lds, st, tm.start, tm.stop, 0, s.X, s.ld, s.N, s.M,
-                          s.mave, s.msig, a, pl.T, pl.TR, gate);
+                          s.mave, s.msig, a, pl.T, pl.TR, c.ilv ? 1 : 0, gate);
 }
 
 template <int K, int C, int S>
@@ -630,8 +719,8 @@ hipError_t atax_team(const Shard& s, const OpPlan& pl, int K, const OpArgs& a, h
 std::string team_kernel_name(int K, const OpPlan& pl) {
     const TmCfg& c = kTmCfg[pl.cfg];
     char b[128];
-    std::snprintf(b, sizeof b, "atax_team_kernel<%d, %d, %d, %d, %d, %s>", K, pl.S, c.F, c.L, c.P,
-                  c.comm ? "true" : "false");
+    std::snprintf(b, sizeof b, "atax_team_kernel<%d, %d, %d, %d, %d, %s, %d>", K, pl.S, c.F, c.L, c.P,
+                  c.comm ? "true" : "false", c.E);
     return b;
 }
 

@@ -535,8 +535,8 @@ vampomi_status op_prepare(vampomi_ctx* c) {
         }
         if (c->opp.T > 1) {
             // M columns x K x T granule pairs, then a dummy pair per workgroup and K
-            const size_t words =
-                (size_t)M * vk::kOpMaxK * (size_t)c->opp.T * 2 + (size_t)c->opp.grid * (2 * vk::kOpMaxK + 1);
+            const size_t words = (size_t)(M + c->opp.grid) * vk::kOpMaxK * (size_t)c->opp.T * 2 +
+                                 (size_t)c->opp.grid * (2 * vk::kOpMaxK + 1);
             if (words > c->op_xg_words) {
                 if (c->op_xg) (void)hipFree(c->op_xg);
                 c->op_xg = nullptr;
@@ -1430,6 +1430,20 @@ extern "C" vampomi_status vampomi_dev_op_apply(vampomi_ctx* c, int K, const doub
     HIPCHK(hipMemcpyAsync(dp, c->scal + SL_DP, (size_t)K * 8, hipMemcpyDeviceToHost, c->st));
     HIPCHK(hipStreamSynchronize(c->st));
     return op_check_err(c);
+}
+
+extern "C" vampomi_status vampomi_dev_op_plan(int64_t N, int64_t M, int cus, int variant, int K, int* T, int* S,
+                                              int* TR, int* grid, int64_t* nslots, char* name, int cap) {
+    vk::OpPlan p{};
+    if (K < 1 || K > vk::kOpMaxK || !vk::op_plan(N, std::max<int64_t>(M, 1), cus, variant, &p))
+        return fail(VAMPOMI_ERR_ARG, "no one-pass operator plan");
+    if (T) *T = p.T;
+    if (S) *S = p.S;
+    if (TR) *TR = p.TR;
+    if (grid) *grid = p.grid;
+    if (nslots) *nslots = p.nslots;
+    if (name && cap > 0) std::snprintf(name, (size_t)cap, "%s", vk::op_kernel_name(K, p).c_str());
+    return VAMPOMI_OK;
 }
 
 // the operator's kernel as rocprofv3 prints it, for the context's plan

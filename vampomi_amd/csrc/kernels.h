@@ -133,8 +133,8 @@ struct OpArgs {
     Ptrs d, sraw;       // d_k (M); sraw_k = t_k (may be null)
     double* part;       // nslots x kMaxRhs x ld partial A d (before the sum over slots)
     RedOut ro;          // <d_k, p_k> summed over the shard (K values)
-    // team kernel with T > 1: hand-off granules (M x kOpMaxK x T x 2 words,
-    // then 2 x kOpMaxK dummy words per workgroup, then one XCD word per
+    // team kernel with T > 1: hand-off granules ((M + grid) x kOpMaxK x T x 2
+    // words, then 2 x kOpMaxK dummy words per workgroup, then one XCD word per
     // workgroup; zeroed once), this launch's
     // tag (never 0, new every launch) and a mapped host word set when a
     // hand-off timed out

@@ -752,13 +752,15 @@ bool op_plan(int64_t N, int64_t M, int cus, int variant, OpPlan* out) {
         return true;
     }
     if (variant > 0) return team_plan(N, M, cus, variant / 10, variant % 10, out);
-    for (int T = 2; T <= 32; T *= 2) {
-        OpPlan p{};
-        if (!team_plan(N, M, cus, T, 6, &p)) continue;
-        *out = p;
-        return true;
+    for (int cfg : {6, 3}) {  // then fewer columns in flight for one more load per lane (S <= 5)
+        for (int T = 2; T <= 32; T *= 2) {
+            OpPlan p{};
+            if (!team_plan(N, M, cus, T, cfg, &p)) continue;
+            *out = p;
+            return true;
+        }
     }
-    return false;
+    return false;  // N beyond 32 x 5 x 896 rows: the CG step keeps two passes (pcg.cpp)
 }
 
 bool op_supported(int64_t N, int K) {
