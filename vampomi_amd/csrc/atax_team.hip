@@ -46,7 +46,8 @@ typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 typedef unsigned int v2u __attribute__((ext_vector_type(2)));
 
 #ifndef TM_FMA
-#define TM_FMA 1  // fused multiply-adds in the dot and the A d accumulation
+#define TM_FMA 1  // fused multiply-adds in the dot and the A d accumulation (DESIGN.md §3;
+                  // A/B in one gpurun call: C3 shard K=2 7207 vs 7332 us, C2 587 vs 600 us)
 #endif
 static constexpr int kTmThreads = 512;        // 8 waves, 2 per SIMD: <= 256 VGPRs per lane
 static constexpr int kTmMaxT = 32;            // members per team (one XCD under round-robin dealing)
@@ -175,7 +176,7 @@ __device__ __forceinline__ void tm_publish_l2(unsigned long long* p, const v4u& 
     asm volatile("s_nop 4\n\tglobal_store_dwordx4 %0, %1, off\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
 }
 
-template <int K, int S, int F, int L, int P, bool COMM, int E>
+template <int K, int S, int F, int L, int P, bool COMM, int E, bool FMA>
 __global__ __launch_bounds__(kTmThreads) void atax_team_kernel(const double* __restrict__ X, int64_t ld, int64_t N,
                                                                int64_t M, const double* __restrict__ mave,
                                                                const double* __restrict__ msig, OpArgs a, int T,
@@ -473,11 +474,10 @@ __global__ __launch_bounds__(kTmThreads) void atax_team_kernel(const double* __r
                 }
 #pragma unroll
                 for (int e = 0; e < E; ++e) {
-#if TM_FMA
-                    v[k] = __builtin_fma(dx[e], q[k][e], v[k]);
-#else
-                    v[k] += dx[e] * q[k][e];
-#endif
+                    if constexpr (FMA)
+                        v[k] = __builtin_fma(dx[e], q[k][e], v[k]);
+                    else
+                        v[k] += dx[e] * q[k][e];
                 }
             }
         }
@@ -534,11 +534,10 @@ __global__ __launch_bounds__(kTmThreads) void atax_team_kernel(const double* __r
             for (int k = 0; k < K; ++k)
 #pragma unroll
                 for (int e = 0; e < E; ++e) {  // xr is centred by dot()
-#if TM_FMA
-                    acc[k][s][e] = __builtin_fma(xr[slot][s][e], cc[k], acc[k][s][e]);
-#else
-                    acc[k][s][e] += xr[slot][s][e] * cc[k];
-#endif
+                    if constexpr (FMA)
+                        acc[k][s][e] = __builtin_fma(xr[slot][s][e], cc[k], acc[k][s][e]);
+                    else
+                        acc[k][s][e] += xr[slot][s][e] * cc[k];
                 }
         }
     };
@@ -644,7 +643,7 @@ static void launch_tm(const Shard& s, const OpPlan& pl, const OpArgs& a, hipStre
                       const int* gate) {
     constexpr TmCfg c = kTmCfg[C];
     constexpr int CW = c.comm ? 7 : 8;
-    auto kern = atax_team_kernel<K, S, c.F, c.L, c.P, c.comm, c.E>;
+    auto kern = atax_team_kernel<K, S, c.F, c.L, c.P, c.comm, c.E, (bool)TM_FMA>;
     const int64_t QS = tm_qstride(K, S, c.comm, c.E, std::min<int64_t>(pl.TR, s.N));
     const size_t lds = (size_t)(K * QS + 2 * CW * K + 2 * K) * sizeof(double);
     static std::once_flag once;  // more than 64 KiB of dynamic LDS must be allowed explicitly
