@@ -236,5 +236,6 @@ unsigned* op_err_dev(vampomi_ctx* c);
 vampomi_status op_check_err(vampomi_ctx* c);
 // d_k = tau*A^T q_k + gam2*p_k and A d_k (into op_nvec's A d block, /sqrt(N),
 // summed over ranks with <d_k,p_k> at its tail; one rank: <d_k,p_k> in
-// scal[SL_DP+k]) from one pass over X.  COLLECTIVE
-vampomi_status op_dev(vampomi_ctx* c, int K, const vk::OpArgs& a, const int* gate);
+// scal[SL_DP+k]) from one pass over X.  COLLECTIVE.  reduce = false (one
+// rank only): the per-slot A d partials stay in op_part for cg_update to sum
+vampomi_status op_dev(vampomi_ctx* c, int K, const vk::OpArgs& a, const int* gate, bool reduce = true);

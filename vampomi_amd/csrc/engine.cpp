@@ -592,7 +592,7 @@ vampomi_status op_check_err(vampomi_ctx* c) {
 // (pass_bytes: X once, K N-vectors, mave/msig, K M-vectors), the work it
 // replaces being two such passes; its other traffic (p, z, d, A r, q_old and
 // the per-slot A d partials, < 1% at C2) is not counted as algorithmic.
-vampomi_status op_dev(vampomi_ctx* c, int K, const vk::OpArgs& a, const int* gate) {
+vampomi_status op_dev(vampomi_ctx* c, int K, const vk::OpArgs& a, const int* gate, bool reduce) {
     if (!c->have_X) return fail(VAMPOMI_ERR_STATE, "A before the methylation data was loaded");
     STCHK(op_prepare(c));
     if (!c->op_ok || K < 1 || K > vk::kOpMaxK)
@@ -618,7 +618,7 @@ vampomi_status op_dev(vampomi_ctx* c, int K, const vk::OpArgs& a, const int* gat
     vk::Ptrs os{};
     for (int k = 0; k < K; ++k) os.p[k] = ad + (int64_t)k * c->ld;
     if (!c->use_comm) {
-        HIPCHK(vk::op_reduce(c->opp, K, c->N, c->ld, c->op_part, os, c->sqrtN, c->st, gate));
+        if (reduce) HIPCHK(vk::op_reduce(c->opp, K, c->N, c->ld, c->op_part, os, c->sqrtN, c->st, gate));
     } else {
         HIPCHK(vk::op_reduce(c->opp, K, c->N, c->ld, c->op_part, os, 0.0, c->st, gate));
         STCHK(allreduce_dev(c, ad, (size_t)K * c->ld + K));  // src/data.cpp:367

@@ -282,6 +282,14 @@ struct CgVecs {
     double* Q[kMaxRhs];
     double* AR[kMaxRhs];
     const double* AD[kMaxRhs];
+    // one rank, one-pass operator (may be null): AD is not read; A d of
+    // sample i is summed here from the operator's per-slot partials
+    // adpart[(t*kMaxRhs + k)*adld + i], t < adslots, in op_reduce's order, and
+    // divided by addiv (the separate op_reduce launch folded into this one)
+    const double* adpart;
+    int64_t adld;
+    int adslots;
+    double addiv;
 };
 // r = v - d (or v, or v - (atx0*tau + gam2*mu)), z = r/diag, p = z;
 // <r,z>, <v,v> per system in ro.out (2K values)

@@ -1012,40 +1012,52 @@ hipError_t atax(const Shard& s, const OpPlan& pl, int K, const OpArgs& a, hipStr
     return hipGetLastError();
 }
 
-// 64 samples per workgroup; its 8 waves sum contiguous eighths of the slots
-// (in slot order) and wave 0 adds the eighths in order: a fixed order, and
-// 64x more loads in flight than one thread per sample
-static constexpr int kOpRedWaves = 8;
-__global__ __launch_bounds__(64 * kOpRedWaves) void op_reduce_kernel(int K, int64_t N, int64_t ld, int nslots,
-                                                                     const double* __restrict__ part, Ptrs out,
-                                                                     double div, const int* __restrict__ gate) {
+// The per-slot A d partials summed over the slots: a workgroup takes 128
+// samples of one system (two per lane, 16-byte loads); wave w sums the slots
+// [w*ns/4, (w+1)*ns/4) in order with eight loads in flight, wave 0 adds the
+// four wave sums in order.  cg_update's one-rank form (cg_update_kernel,
+// c.adpart) sums in exactly this order, so the two paths agree bit for bit.
+__device__ __forceinline__ v2d slot_sum(const double* src, int64_t ss, int t0, int t1) {
+    v2d acc = {0.0, 0.0};
+    int t = t0;
+    for (; t + 8 <= t1; t += 8) {
+        v2d x[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) x[u] = *reinterpret_cast<const v2d*>(src + (t + u) * ss);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc += x[u];
+    }
+    for (; t < t1; ++t) acc += *reinterpret_cast<const v2d*>(src + t * ss);
+    return acc;
+}
+
+__global__ __launch_bounds__(256) void op_reduce_kernel(int64_t N, int64_t ld, int nslots,
+                                                        const double* __restrict__ part, Ptrs out, double div,
+                                                        const int* __restrict__ gate) {
     if (gate && !*gate) return;
-    __shared__ double lds[kOpRedWaves][64];
+    __shared__ v2d wsum[4][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int64_t e = (int64_t)blockIdx.x * 64 + lane;
-    const bool ok = e < (int64_t)K * N;
-    const int k = ok ? (int)(e / N) : 0;
-    const int64_t j = ok ? e - (int64_t)k * N : 0;
-    const int t0 = w * nslots / kOpRedWaves, t1 = (w + 1) * nslots / kOpRedWaves;
-    double s = 0.0;
-    if (ok)
-        for (int t = t0; t < t1; ++t) s += part[((int64_t)t * kMaxRhs + k) * ld + j];
-    lds[w][lane] = s;
+    const int64_t tpk = (N + 127) / 128;
+    const int k = (int)(blockIdx.x / tpk);
+    const int64_t i = (blockIdx.x - k * tpk) * 128 + 2 * lane;  // < ld (a multiple of 16)
+    const bool ok = i < N;
+    wsum[w][lane] = ok ? slot_sum(part + (int64_t)k * ld + i, (int64_t)kMaxRhs * ld, w * nslots / 4,
+                                  (w + 1) * nslots / 4)
+                       : v2d{0.0, 0.0};
     __syncthreads();
     if (w != 0 || !ok) return;
-    double r = lds[0][lane];
-#pragma unroll
-    for (int q = 1; q < kOpRedWaves; ++q) r += lds[q][lane];
+    v2d r = ((wsum[0][lane] + wsum[1][lane]) + wsum[2][lane]) + wsum[3][lane];
     if (div > 0) r /= div;
-    out.p[k][j] = r;
+    out.p[k][i] = r.x;
+    if (i + 1 < N) out.p[k][i + 1] = r.y;
 }
 
 hipError_t op_reduce(const OpPlan& pl, int K, int64_t N, int64_t ld, const double* part, Ptrs out, double div,
                      hipStream_t st, const int* gate) {
     const int64_t n = (int64_t)K * N;
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(op_reduce_kernel, dim3((unsigned)cdiv(n, 64)), dim3(64 * kOpRedWaves), 0, st, K, N, ld,
-                       (int)pl.nslots, part, out, div, gate);
+    hipLaunchKernelGGL(op_reduce_kernel, dim3((unsigned)(K * cdiv(N, 128))), dim3(256), 0, st, N, ld, (int)pl.nslots,
+                       part, out, div, gate);
     return hipGetLastError();
 }
 
@@ -1501,9 +1513,12 @@ __global__ void cg_decide_kernel(CgState* cs, const double* __restrict__ red, in
 __global__ __launch_bounds__(kBlock) void cg_update_kernel(int K, int64_t M, CgVecs c, double diag,
                                                            CgState* cs, const double* __restrict__ dp_dev,
                                                            const double* __restrict__ pp_dev, int fuse, RedOut ro,
-                                                           CgDecide dc) {
+                                                           CgDecide dc, int mblocks) {
     if (!cs->any) return;
     __shared__ double lds[4];
+    // blocks [0, mblocks) stream the M-vectors; with c.adpart the blocks past
+    // them sum the operator's A d partials and update the N-vectors
+    const bool mpart = (int)blockIdx.x < mblocks;
     double alpha[kMaxRhs];
     bool on[kMaxRhs];
 #pragma unroll
@@ -1518,7 +1533,7 @@ __global__ __launch_bounds__(kBlock) void cg_update_kernel(int K, int64_t M, CgV
     double beta[kMaxRhs];
 #pragma unroll
     for (int k = 0; k < kMaxRhs; ++k) beta[k] = fuse && on[k] ? cs->beta[k] : 0.0;
-    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < M; i += (int64_t)gridDim.x * kBlock) {
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; mpart && i < M; i += (int64_t)mblocks * kBlock) {
         // every load of the element first (the vectors may alias as far as the
         // compiler knows: loads after a store would wait for it)
         double pv[kMaxRhs], zv[kMaxRhs], muv[kMaxRhs], rv[kMaxRhs], dv[kMaxRhs], vv[kMaxRhs], wv[kMaxRhs],
@@ -1558,7 +1573,46 @@ __global__ __launch_bounds__(kBlock) void cg_update_kernel(int K, int64_t M, CgV
         }
     }
     // A mu alongside mu (replicated N-vectors, the same on every rank)
-    if (c.Q[0]) {  // one-pass operator: q (the step's A p) from A r, then A r -= A d * alpha
+    if (c.adpart) {
+        // one rank, one-pass operator: A d from the operator's slots, in
+        // op_reduce's order (tiles of 128 samples of one system)
+        __shared__ v2d wsum[4][64];
+        const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, ns = c.adslots;
+        const int nb = (int)gridDim.x - mblocks;
+        const int64_t tpk = (c.nA + 127) / 128;  // tiles per system
+        for (int64_t tile = (int)blockIdx.x - mblocks; !mpart && tile < K * tpk; tile += nb) {
+            const int k = (int)(tile / tpk);
+            const int64_t i = (tile - k * tpk) * 128 + 2 * lane;  // < adld (a multiple of 16)
+            const bool ok = i < c.nA;
+            wsum[w][lane] = ok ? slot_sum(c.adpart + (int64_t)k * c.adld + i, (int64_t)kMaxRhs * c.adld, w * ns / 4,
+                                          (w + 1) * ns / 4)
+                               : v2d{0.0, 0.0};
+            __syncthreads();
+            bool onk = false;  // on[k], alpha[k], beta[k] without indexing registers at run time
+            double alk = 0.0, bek = 0.0;
+#pragma unroll
+            for (int kk = 0; kk < kOpMaxK; ++kk)
+                if (kk == k) {
+                    onk = on[kk];
+                    alk = alpha[kk];
+                    bek = beta[kk];
+                }
+            if (w == 0 && ok && onk) {
+                const v2d ad = (((wsum[0][lane] + wsum[1][lane]) + wsum[2][lane]) + wsum[3][lane]) / c.addiv;
+#pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                    const int64_t j = i + e;
+                    if (j >= c.nA) break;
+                    double q = c.AR[k][j] / diag;
+                    if (fuse) q = q + bek * c.Q[k][j];
+                    c.Q[k][j] = q;
+                    if (c.AW[k]) c.AW[k][j] = c.AW[k][j] + alk * q;
+                    c.AR[k][j] = c.AR[k][j] - ad[e] * alk;
+                }
+            }
+            __syncthreads();
+        }
+    } else if (c.Q[0]) {  // one-pass operator: q (the step's A p) from A r, then A r -= A d * alpha
         for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < c.nA; i += (int64_t)gridDim.x * kBlock) {
             double ar[kMaxRhs], qo[kMaxRhs], ad[kMaxRhs], aw[kMaxRhs];
 #pragma unroll
@@ -1600,8 +1654,17 @@ __global__ __launch_bounds__(kBlock) void cg_update_kernel(int K, int64_t M, CgV
 
 hipError_t cg_update(int K, int64_t M, const CgVecs& c, double diag, CgState* cs, const double* dp_dev,
                      const double* pp_dev, int fuse, const RedOut& ro, const CgDecide& dc, hipStream_t st) {
-    hipLaunchKernelGGL(cg_update_kernel, dim3(red_blocks(M)), dim3(kBlock), 0, st, K, M, c, diag, cs, dp_dev, pp_dev,
-                       fuse, ro, dc);
+    // VAMPOMI_CG_EPT: M elements per thread (tuning experiments; default 2, red_blocks)
+    static const int ept = std::getenv("VAMPOMI_CG_EPT") ? std::max(1, std::atoi(std::getenv("VAMPOMI_CG_EPT"))) : 2;
+    const int mb = (int)std::min<int64_t>(std::max<int64_t>(cdiv(M, (int64_t)kBlock * ept), 1), kRedBlocks / 2);
+    int nb = 0;
+    if (c.adpart) {
+        if (K > kOpMaxK || c.adslots < 1 || !c.Q[0]) return hipErrorInvalidValue;
+        nb = (int)std::min<int64_t>(K * cdiv(c.nA, 128), kRedBlocks - mb);
+        nb = std::max(nb, 1);
+    }
+    hipLaunchKernelGGL(cg_update_kernel, dim3(mb + nb), dim3(kBlock), 0, st, K, M, c, diag, cs, dp_dev, pp_dev,
+                       fuse, ro, dc, mb);
     return hipGetLastError();
 }
 

@@ -166,6 +166,12 @@ vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double
             cu.AR[k] = AR + (int64_t)k * c->ld;
             cu.AD[k] = AD + (int64_t)k * c->ld;
         }
+        if (!c->use_comm) {  // one rank: cg_update sums the operator's A d slots itself
+            cu.adpart = c->op_part;
+            cu.adld = c->ld;
+            cu.adslots = c->opp.nslots;
+            cu.addiv = c->sqrtN;
+        }
         bool rec = false;
         for (int k = 0; k < K; ++k) rec = rec || sys[k]->W;
         if (rec)
@@ -187,7 +193,7 @@ vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double
             a.diag = diag;
             a.tau = tau;
             a.gam2 = gam2;
-            STCHK(op_dev(c, K, a, gate));
+            STCHK(op_dev(c, K, a, gate, c->use_comm));
             const double* dp = c->use_comm ? AD + (int64_t)K * c->ld : c->scal + SL_DP;
             const vk::RedOut ro{c->red_part, c->scal + SL_CG, c->ticket, nullptr, 0, gate};
             *seq = ++c->sync_seq;
