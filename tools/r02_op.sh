@@ -21,7 +21,8 @@ for s in "$@"; do
         optest) run optest 600 python -u -m pytest tests/test_gpu_operator.py -x -v -rf --timeout 300 --timeout-method thread ;;
         tests1) run "pytest_$a" 900 python -u -m pytest tests -m gpu -x -v -rf --timeout 300 --timeout-method thread -k "$a" ;;
         kb) run "kbench_op_${a}_${b}" 600 python tools/kbench.py "$a" "$b" "${c:-10}" op ;;
-        kbdbg) for dbg in ${DBGS:-0 1 2 3 4 8 15}; do VAMPOMI_OP_DBG=$dbg OP_PLANS=$c run "kbench_dbg${dbg}_${a}_${b}" 300 python tools/kbench.py "$a" "$b" 5 op; done ;;
+        # team plans honour VAMPOMI_OP_DBG only in a TM_DBG=1 build: DBGLIB=<that .so> (vampomi_amd/csrc/Makefile)
+        kbdbg) [ -n "${DBGLIB:-}" ] && export VAMPOMI_LIB="$DBGLIB"; for dbg in ${DBGS:-0 1 2 3 4 8 15}; do VAMPOMI_OP_DBG=$dbg OP_PLANS=$c run "kbench_dbg${dbg}_${a}_${b}" 300 python tools/kbench.py "$a" "$b" 5 op; done ;;
         bench) run "bench_$a" 900 python bench.py --config "$a" --steps "${b:-20}" --warmup 5 --no-cpu-baseline ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac

@@ -19,7 +19,8 @@ except Exception:  # pragma: no cover - torch is optional for the library itself
     torch = None
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libvampomi.so")
+# VAMPOMI_LIB: another in-tree build of the same library (timing experiments, tools/)
+LIB_PATH = os.environ.get("VAMPOMI_LIB") or os.path.join(HERE, "lib", "libvampomi.so")
 CLI_PATH = os.path.join(HERE, "bin", "main_meth.exe")
 
 MAX_L = 64

@@ -49,6 +49,9 @@ typedef unsigned int v2u __attribute__((ext_vector_type(2)));
 #define TM_FMA 1  // fused multiply-adds in the dot and the A d accumulation (DESIGN.md §3;
                   // A/B in one gpurun call: C3 shard K=2 7207 vs 7332 us, C2 587 vs 600 us)
 #endif
+#ifndef TM_DBG
+#define TM_DBG 0  // 1: honour OpArgs.dbg (timing experiments); 0: its branches compile out
+#endif
 static constexpr int kTmThreads = 512;        // 8 waves, 2 per SIMD: <= 256 VGPRs per lane
 static constexpr int kTmMaxT = 32;            // members per team (one XCD under round-robin dealing)
 static constexpr unsigned kTmMaxSpins = 1u << 21;  // ~2 s of polling, then the launch gives up (err)
@@ -182,6 +185,11 @@ __global__ __launch_bounds__(kTmThreads) void atax_team_kernel(const double* __r
                                                                const double* __restrict__ msig, OpArgs a, int T,
                                                                int TR, int ilv, const int* __restrict__ gate) {
     if (gate && !*gate) return;
+    // timing experiments (VAMPOMI_OP_DBG): with a hand-off only in a TM_DBG
+    // build (the branches cost the hand-off wave's chain 2 % at the C3 shard);
+    // T = 1 keeps them: at 252-256 VGPRs its schedule without them waits more
+    // (C2 K = 2: 613 against 591 us, profiles/r02f_op_experiments.txt)
+    const int dbg = (TM_DBG || !COMM) ? a.dbg : 0;
     constexpr int CW = COMM ? 7 : 8;  // streaming waves
     constexpr int RS = tm_rows_per_step(COMM, E);
     static_assert(E == 1 || E == 2, "doubles per lane per load");
@@ -278,7 +286,7 @@ __global__ __launch_bounds__(kTmThreads) void atax_team_kernel(const double* __r
                     __builtin_amdgcn_s_sleep(2);
                 }
                 l2 = !dead && __all((unsigned)h == xcc);
-                if (a.dbg & 32) l2 = false;
+                if (dbg & 32) l2 = false;
             }
             // the streaming waves' step numbering (m from -F, column c in slot
             // (c + F) % RING, whole rounds of RING steps, a barrier in every step)
@@ -293,12 +301,12 @@ __global__ __launch_bounds__(kTmThreads) void atax_team_kernel(const double* __r
                     tm_poll(pl[(i + RING - L + P) % RING], xg + ((int64_t)cic * nq + ql) * 2);
                     v4u& g = pl[(i + RING - L) % RING];
                     v2u& sc = ps[(i + RING - L) % RING];
-                    if (!(a.dbg & 1)) tm_wait2<3 * P>(g, sc);  // step m - P's poll; 3P younger operations in flight
+                    if (!(dbg & 1)) tm_wait2<3 * P>(g, sc);  // step m - P's poll; 3P younger operations in flight
                     if (cf >= 0 && cf < n) {
                         for (unsigned spins = 0;; ++spins) {
                             const bool ok = g.y == tag && g.w == tag;  // {lo, tag} {hi, tag}
-                            if (__all(ok) || dead || (a.dbg & 1)) break;
-                            if (a.dbg & 64) {
+                            if (__all(ok) || dead || (dbg & 1)) break;
+                            if (dbg & 64) {
                                 nslow += spins == 0;
                                 nspin++;
                             }
@@ -312,9 +320,9 @@ __global__ __launch_bounds__(kTmThreads) void atax_team_kernel(const double* __r
                             tm_wait<0>(g);
                         }
                         double v = lane < nq ? __builtin_bit_cast(double, ((unsigned long long)g.z << 32) | g.x) : 0.0;
-                        if (a.dbg & 512) {  // timing experiment: the ds_bpermute butterfly
+                        if (dbg & 512) {  // timing experiment: the ds_bpermute butterfly
                             for (int o = T >> 1; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-                        } else if (!(a.dbg & 256)) {
+                        } else if (!(dbg & 256)) {
                             v = group_sum_rt(v, T);  // the T members, fixed order per k group
                         }
                         // d of column cf (src/vamp.cpp:656-659, data::ATx's scaling src/data.cpp:327-330)
@@ -324,7 +332,7 @@ __global__ __launch_bounds__(kTmThreads) void atax_team_kernel(const double* __r
                         const int64_t mg = mb + cf * cs;  // the shard's column index
 #pragma unroll
                         for (int k = 0; k < K; ++k) {
-                            if (a.dbg & 128) {
+                            if (dbg & 128) {
                                 if (lane == 0) s_tot[(cf & 1) * K + k] = 0.0;
                                 continue;
                             }
@@ -345,7 +353,7 @@ __global__ __launch_bounds__(kTmThreads) void atax_team_kernel(const double* __r
                         }
                     }
                     __syncthreads();
-                    if (lane < K && !(a.dbg & 2)) {  // this member's dot of column m: the streaming waves' partials in order
+                    if (lane < K && !(dbg & 2)) {  // this member's dot of column m: the streaming waves' partials in order
                         const bool real = m >= 0 && m < n;
                         double v = 0.0;
                         if (real) {
@@ -364,7 +372,7 @@ __global__ __launch_bounds__(kTmThreads) void atax_team_kernel(const double* __r
             }
 #pragma unroll
             for (int s = 0; s < RING; ++s) tm_wait2<0>(pl[s], ps[s]);  // nothing of ours lands after the loop
-            if ((a.dbg & 64) && lane == 0) {  // timing experiments: slow-path counts into the flag block
+            if ((dbg & 64) && lane == 0) {  // timing experiments: slow-path counts into the flag block
                 __hip_atomic_fetch_add(a.err + 1, nslow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 __hip_atomic_fetch_add(a.err + 2, nspin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 __hip_atomic_fetch_add(a.err + 3, (unsigned)n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -487,14 +495,14 @@ __global__ __launch_bounds__(kTmThreads) void atax_team_kernel(const double* __r
             double r0, r1;
             swap32(v[0], v[K - 1], r0, r1);
             double keep = r0 + r1;
-            if (a.dbg & 512) {  // timing experiment: the ds_bpermute butterfly
+            if (dbg & 512) {  // timing experiment: the ds_bpermute butterfly
                 for (int o = 16; o > 0; o >>= 1) keep += __shfl_xor(keep, o, 64);
-            } else if (!(a.dbg & 4)) {
+            } else if (!(dbg & 4)) {
                 keep = group_sum<32>(keep);
             }
             if ((lane & 31) == 0) s_part[(par * CW + wave) * K + (lane >> 5)] = keep;
         } else {
-            if (!(a.dbg & 4)) v[0] = group_sum<64>(v[0]);
+            if (!(dbg & 4)) v[0] = group_sum<64>(v[0]);
             if (lane == 0) s_part[(par * CW + wave) * K] = v[0];
         }
     };
@@ -529,7 +537,7 @@ __global__ __launch_bounds__(kTmThreads) void atax_team_kernel(const double* __r
         }
 #pragma unroll
         for (int s = 0; s < S; ++s) {
-            if (a.dbg & 8) break;
+            if (dbg & 8) break;
 #pragma unroll
             for (int k = 0; k < K; ++k)
 #pragma unroll
