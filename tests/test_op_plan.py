@@ -25,7 +25,8 @@ def plan(N, M=62500, cus=256, variant=-1, K=2):
 
 def test_default_plans_of_the_baseline_shapes():
     c2, c3, c4 = plan(10000), plan(100000), plan(50000)
-    assert c2["T"] == 1 and c2["name"] == "atax_team_kernel<2, 10, 1, 0, 0, false, 2>"
+    assert c2["T"] == 4 and c2["S"] == 3 and c2["name"] == "atax_team_kernel<2, 3, 4, 5, 2, true, 2>"
+    assert plan(9216)["T"] == 1 and plan(9216)["name"] == "atax_team_kernel<2, 9, 1, 0, 0, false, 2>"
     assert c3["T"] == 32 and c3["S"] == 4 and c3["TR"] == 3200 and c3["nslots"] == 8
     assert c3["name"] == "atax_team_kernel<2, 4, 4, 5, 2, true, 2>"
     assert c4["T"] == 16 and c4["S"] == 4 and c4["nslots"] == 16

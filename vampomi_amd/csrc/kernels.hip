@@ -734,9 +734,12 @@ bool op_plan(int64_t N, int64_t M, int cus, int variant, OpPlan* out) {
     if (N < 1 || cus < 1) return false;
     if (variant == kOpDefault) {
         // one workgroup per column range (team size 1): two columns prefetched
-        // where they fit the registers (S <= 8), else one
+        // where they fit the registers (S <= 8), else one, up to S = 9; at
+        // S = 10 (252-256 VGPRs) a team of 4 is faster (C2, N = 10,000, K = 2:
+        // 585-588 against 597 us; N = 9,216, S = 9: 543 against 560 us for the
+        // team; profiles/r02g_op_plans_by_N.txt)
         OpPlan p{};
-        if (team_plan(N, M, cus, 1, 1, &p) || team_plan(N, M, cus, 1, 0, &p)) {
+        if ((team_plan(N, M, cus, 1, 1, &p) || team_plan(N, M, cus, 1, 0, &p)) && p.S <= 9) {
             *out = p;
             return true;
         }
