@@ -145,16 +145,6 @@ __device__ __forceinline__ double group_sum(double v) {
     }
     return v;
 }
-__device__ __forceinline__ double group_sum_rt(double v, int G) {  // G a power of two <= 32, wave-uniform
-    switch (G) {
-        case 2: return group_sum<2>(v);
-        case 4: return group_sum<4>(v);
-        case 8: return group_sum<8>(v);
-        case 16: return group_sum<16>(v);
-        case 32: return group_sum<32>(v);
-        default: return v;
-    }
-}
 
 // Untracked 16-byte granule traffic of the hand-off wave (see there).
 __device__ __forceinline__ void tm_poll(v4u& dst, const unsigned long long* p) {
@@ -239,7 +229,11 @@ __global__ __launch_bounds__(kTmThreads) void atax_team_kernel(const double* __r
         const int nq = K * T;
         unsigned long long* xg = a.xg + (int64_t)team * nmax * nq * 2;  // the team's first column
         unsigned long long* dummy = a.xg + gwords + (int64_t)blockIdx.x * 2 * K;
-        const int ql = lane < nq ? lane : 0;  // lanes past nq re-read lane 0's granules (no divergence)
+        // lane 32k + j reads member j's granule of system k (j < T), so one
+        // fixed 32-lane butterfly sums every team size (the zeros of lanes
+        // j >= T leave the sums' bits unchanged); other lanes re-read granule 0
+        const bool qv = (lane >> 5) < K && (lane & 31) < T;
+        const int ql = qv ? (lane >> 5) * T + (lane & 31) : 0;
         const unsigned tag = a.tag;
         // per-lane source of a column's scalars: lane 0 msig, 1.. p_k, 1+K.. z_k
         const double* scp = msig;
@@ -319,37 +313,44 @@ __global__ __launch_bounds__(kTmThreads) void atax_team_kernel(const double* __r
                             tm_poll(g, xg + ((int64_t)cf * nq + ql) * 2);
                             tm_wait<0>(g);
                         }
-                        double v = lane < nq ? __builtin_bit_cast(double, ((unsigned long long)g.z << 32) | g.x) : 0.0;
+                        double v = qv ? __builtin_bit_cast(double, ((unsigned long long)g.z << 32) | g.x) : 0.0;
                         if (dbg & 512) {  // timing experiment: the ds_bpermute butterfly
                             for (int o = T >> 1; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
                         } else if (!(dbg & 256)) {
-                            v = group_sum_rt(v, T);  // the T members, fixed order per k group
+                            v = group_sum<32>(v);  // the T members of system k in lanes 32k.., fixed order
                         }
                         // d of column cf (src/vamp.cpp:656-659, data::ATx's scaling src/data.cpp:327-330)
                         const double scv = __builtin_bit_cast(double, ((unsigned long long)sc.y << 32) | sc.x);
                         const double sg = readlane_d(scv, 0);
-                        const bool own = (cf % T) == member;
+                        const bool own = (cf & (T - 1)) == member;  // T: a power of two
                         const int64_t mg = mb + cf * cs;  // the shard's column index
+                        // both systems' chains first (independent: interleaved), then the
+                        // LDS hand-over, then the owner's stores and <d,p>
+                        double tsc[K], dval[K], pdir[K];
 #pragma unroll
                         for (int k = 0; k < K; ++k) {
-                            if (dbg & 128) {
-                                if (lane == 0) s_tot[(cf & 1) * K + k] = 0.0;
-                                continue;
-                            }
-                            double t = sg * readlane_d(v, k * T);  // sigma_inv * dpa
-                            t *= a.scale;                          // ATx[mloc] *= 1/sqrt(N)
+                            double t = sg * readlane_d(v, 32 * k);  // sigma_inv * dpa
+                            t *= a.scale;                           // ATx[mloc] *= 1/sqrt(N)
                             double p = readlane_d(scv, 1 + k);
                             if (a.fuse) p = readlane_d(scv, 1 + K + k) + bk[k] * p;  // p = z + beta p
                             double val = t * a.tau;  // res[i] *= tau
                             val += a.gam2 * p;       // res[i] += gam2 * v[i]
-                            if (own) {
+                            tsc[k] = t;
+                            dval[k] = val;
+                            pdir[k] = p;
+                        }
+#pragma unroll
+                        for (int k = 0; k < K; ++k)  // c_k: Ax's (x - mave)*(msig*d)
+                            if (lane == 0) s_tot[(cf & 1) * K + k] = (dbg & 128) ? 0.0 : sg * dval[k];
+                        if (own) {
+#pragma unroll
+                            for (int k = 0; k < K; ++k) {
                                 if (lane == 0) {
-                                    if (a.sraw.p[0]) a.sraw.p[k][mg] = t;
-                                    a.d.p[k][mg] = val;
+                                    if (a.sraw.p[0]) a.sraw.p[k][mg] = tsc[k];
+                                    a.d.p[k][mg] = dval[k];
                                 }
-                                dpacc[k] += val * p;
+                                dpacc[k] += dval[k] * pdir[k];
                             }
-                            if (lane == 0) s_tot[(cf & 1) * K + k] = sg * val;  // c_k: Ax's (x - mave)*(msig*d)
                         }
                     }
                     __syncthreads();
