@@ -146,6 +146,18 @@ __device__ __forceinline__ double group_sum(double v) {
     return v;
 }
 
+// x[0] + x[s] + ... + x[(N-1)s] as a fixed pairwise tree (halves, the odd
+// one last): log2 N dependent adds instead of N - 1
+template <int N>
+__device__ __forceinline__ double tree_sum(const double* x, int s) {
+    if constexpr (N == 1) {
+        return x[0];
+    } else {
+        constexpr int H = N / 2;
+        return tree_sum<H>(x, s) + tree_sum<N - H>(x + H * s, s);
+    }
+}
+
 // Untracked 16-byte granule traffic of the hand-off wave (see there).
 __device__ __forceinline__ void tm_poll(v4u& dst, const unsigned long long* p) {
     asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(dst) : "v"(p) : "memory");
@@ -233,7 +245,9 @@ __global__ __launch_bounds__(kTmThreads) void atax_team_kernel(const double* __r
         // fixed 32-lane butterfly sums every team size (the zeros of lanes
         // j >= T leave the sums' bits unchanged); other lanes re-read granule 0
         const bool qv = (lane >> 5) < K && (lane & 31) < T;
-        const int ql = qv ? (lane >> 5) * T + (lane & 31) : 0;
+        const int ql2 = qv ? 2 * ((lane >> 5) * T + (lane & 31)) : 0;
+        const int nq2 = 2 * nq;          // words per column of the granule block
+        const int csi = (int)cs;         // column stride (1 or nteams)
         const unsigned tag = a.tag;
         // per-lane source of a column's scalars: lane 0 msig, 1.. p_k, 1+K.. z_k
         const double* scp = msig;
@@ -291,27 +305,30 @@ __global__ __launch_bounds__(kTmThreads) void atax_team_kernel(const double* __r
                     // the column polled now (finished P steps later), the column finished now
                     const int ci = m - L + P, cf = m - L;
                     const int cic = ci < 0 ? 0 : ci < n ? ci : n - 1;
-                    tm_load8(ps[(i + RING - L + P) % RING], scp + cic * cs);
-                    tm_poll(pl[(i + RING - L + P) % RING], xg + ((int64_t)cic * nq + ql) * 2);
+                    tm_load8(ps[(i + RING - L + P) % RING], scp + cic * csi);  // offsets < 2^31: 32-bit math
+                    tm_poll(pl[(i + RING - L + P) % RING], xg + (cic * nq2 + ql2));
                     v4u& g = pl[(i + RING - L) % RING];
                     v2u& sc = ps[(i + RING - L) % RING];
                     if (!(dbg & 1)) tm_wait2<3 * P>(g, sc);  // step m - P's poll; 3P younger operations in flight
                     if (cf >= 0 && cf < n) {
-                        for (unsigned spins = 0;; ++spins) {
-                            const bool ok = g.y == tag && g.w == tag;  // {lo, tag} {hi, tag}
-                            if (__all(ok) || dead || (dbg & 1)) break;
-                            if (dbg & 64) {
-                                nslow += spins == 0;
-                                nspin++;
+                        // every granule of column cf carries this launch's tag {lo, tag} {hi, tag}
+                        if (!(__all(g.y == tag && g.w == tag) || dead || (dbg & 1))) {
+#pragma unroll 1
+                            for (unsigned spins = 0;; ++spins) {  // slow path: poll again until it does
+                                if (dbg & 64) {
+                                    nslow += spins == 0;
+                                    nspin++;
+                                }
+                                if (spins >= kTmMaxSpins) {  // a member never published: give up this launch (err)
+                                    dead = true;
+                                    if (lane == 0) __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                                    break;
+                                }
+                                __builtin_amdgcn_s_sleep(2);
+                                tm_poll(g, xg + (cf * nq2 + ql2));
+                                tm_wait<0>(g);
+                                if (__all(g.y == tag && g.w == tag)) break;
                             }
-                            if (spins >= kTmMaxSpins) {  // a member never published: give up this launch (err)
-                                dead = true;
-                                if (lane == 0) __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                                break;
-                            }
-                            __builtin_amdgcn_s_sleep(2);
-                            tm_poll(g, xg + ((int64_t)cf * nq + ql) * 2);
-                            tm_wait<0>(g);
                         }
                         double v = qv ? __builtin_bit_cast(double, ((unsigned long long)g.z << 32) | g.x) : 0.0;
                         if (dbg & 512) {  // timing experiment: the ds_bpermute butterfly
@@ -323,7 +340,7 @@ __global__ __launch_bounds__(kTmThreads) void atax_team_kernel(const double* __r
                         const double scv = __builtin_bit_cast(double, ((unsigned long long)sc.y << 32) | sc.x);
                         const double sg = readlane_d(scv, 0);
                         const bool own = (cf & (T - 1)) == member;  // T: a power of two
-                        const int64_t mg = mb + cf * cs;  // the shard's column index
+                        const int64_t mg = mb + cf * csi;  // the shard's column index
                         // both systems' chains first (independent: interleaved), then the
                         // LDS hand-over, then the owner's stores and <d,p>
                         double tsc[K], dval[K], pdir[K];
@@ -357,13 +374,10 @@ __global__ __launch_bounds__(kTmThreads) void atax_team_kernel(const double* __r
                     if (lane < K && !(dbg & 2)) {  // this member's dot of column m: the streaming waves' partials in order
                         const bool real = m >= 0 && m < n;
                         double v = 0.0;
-                        if (real) {
-#pragma unroll
-                            for (int w = 0; w < CW; ++w) v += s_part[((m & 1) * CW + w) * K + lane];
-                        }
+                        if (real) v = tree_sum<CW>(s_part + (m & 1) * CW * K + lane, K);  // fixed pairwise order
                         const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
                         const v4u gr = {(unsigned)u, tag, (unsigned)(u >> 32), tag};
-                        unsigned long long* dst = real ? xg + ((int64_t)m * nq + lane * T + member) * 2 : dummy + 2 * lane;
+                        unsigned long long* dst = real ? xg + (m * nq2 + (lane * T + member) * 2) : dummy + 2 * lane;
                         if (l2)
                             tm_publish_l2(dst, gr);
                         else
