@@ -46,8 +46,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-PMC_FILE = os.path.join(ROOT, "profiles", "r01_pmc_traffic_{}.json")
-PMC_FILES = [os.path.join(ROOT, "profiles", f) for f in ("r02_pmc_traffic_{}.json", "r01_pmc_traffic_{}.json")]
+PMC_FILES = [os.path.join(ROOT, "profiles", f)
+             for f in ("r02h_pmc_traffic_{}.json", "r02_pmc_traffic_{}.json", "r01_pmc_traffic_{}.json")]
 
 
 def parse_args(argv=None):
@@ -114,8 +114,10 @@ def pmc_traffic(kernel: str, workload: str):
     for pat in PMC_FILES:
         f = pat.format(workload)
         try:
-            for name, d in json.load(open(f)).items():
-                if kernel in name:
+            base = kernel[:-1] if kernel.endswith(">") else kernel  # the profile's name may carry more
+            for name, d in json.load(open(f)).items():                # template arguments after these
+                at = name.find(base)
+                if at >= 0 and name[at + len(base):at + len(base) + 1] in (">", ","):
                     return d.get("traffic_bytes_per_launch"), os.path.relpath(f, ROOT)
         except Exception:
             continue
