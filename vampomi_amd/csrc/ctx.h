@@ -68,6 +68,8 @@ struct vampomi_ctx {
     double alpha_scale = 1.0;
     double sqrtN = 1.0;
     hipStream_t st = nullptr;
+    bool team_reg = false;           // registered with its device's team gate (engine.cpp)
+    hipEvent_t team_ev = nullptr;    // recorded on st when another context must order behind it
     ncclComm_t comm = nullptr;
     bool use_comm = false;  // nranks > 1 (or VAMPOMI_FORCE_RCCL): all-reduces through RCCL
     std::shared_ptr<LoopbackComm> loopback;  // VAMPOMI_COMM=loopback: ranks are threads of one process
