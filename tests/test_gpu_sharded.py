@@ -205,3 +205,30 @@ def test_divergent_collectives_fail_on_every_rank(monkeypatch):
     for e in errs:
         assert isinstance(e, va.VampomiError) and "ranks disagree on the collective" in str(e), e
         assert "rank 0:" in str(e) and "rank 1:" in str(e)
+
+
+@pytest.mark.parametrize("P", [1, 2])
+@pytest.mark.parametrize("em", [dict(), dict(EM_max_iter=3, EM_err_thr=1e-9), dict(learn_prior_delay=4)])
+def test_side_stream_bitwise(monkeypatch, P, em):
+    """north_star's second HIP stream: the prefetched EM sums and denoiser of
+    iteration it+1 on the side stream beside iteration it's reductions give
+    bitwise the one-stream results (same fixed-order kernels), on one rank and
+    on two loopback ranks, with one EM round, several, and none (delay)."""
+    N, Mt = 1001, 2003
+    X, y, beta = make_problem(N, Mt)
+    out = {}
+    for side in (0, 1):
+        def fn(r, d, side=side):
+            d.set_variant(4, side)
+            return _vamp(d, X, y, beta, max_iter=12, stop_criteria_thr=0.0, **em)
+
+        if P == 1:
+            with va.Data(N, Mt) as d:
+                out[side] = [fn(0, d)]
+        else:
+            out[side] = run_ranks(monkeypatch, P, N, Mt, fn)
+    for a, b in zip(out[0], out[1]):
+        for k in ("iterations", "cg_iters", "ons_iters", "L"):
+            assert a[k] == b[k], k
+        for k in ("x1_hist", "r1_hist", "params", "metrics"):
+            np.testing.assert_array_equal(np.asarray(a[k]), np.asarray(b[k]), err_msg=k)

@@ -68,6 +68,16 @@ struct vampomi_ctx {
     double alpha_scale = 1.0;
     double sqrtN = 1.0;
     hipStream_t st = nullptr;
+    // side stream: the prefetched denoiser/EM of iteration it+1 runs on it
+    // beside iteration it's updateNoisePrec / err_measures / NMSE reductions
+    // on st (north_star's second HIP stream). Collectives stay on st. Its
+    // reductions have their own partials and ticket; st waits on ev_join
+    // before it reads their results (DotBatch::side, flush)
+    hipStream_t st2 = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    double* red_part2 = nullptr;
+    unsigned* ticket2 = nullptr;
+    bool side_on = true;  // VAMPOMI_SIDE_STREAM=0 or vampomi_dev_set_variant(c, 4, 0): one stream
     bool team_reg = false;           // registered with its device's team gate (engine.cpp)
     hipEvent_t team_ev = nullptr;    // recorded on st when another context must order behind it
     ncclComm_t comm = nullptr;
@@ -94,7 +104,7 @@ struct vampomi_ctx {
     unsigned* ticket = nullptr; // arrival counter of the fused reductions (zero between launches)
     unsigned long long* h_flag = nullptr;  // mapped host word the stream stores sync sequence numbers into
     unsigned long long* d_flag = nullptr;
-    unsigned long long sync_seq = 0;
+    unsigned long long sync_seq = 0, side_seq = 0;
     vk::CgState* cgs = nullptr;     // device-side CG control (pcg.cpp)
     vk::CgMirror* h_cgm = nullptr;  // its mapped host mirror, and the mirror's device address
     vk::CgMirror* d_cgm = nullptr;
@@ -131,7 +141,8 @@ vampomi_status dev_alloc(double** p, size_t n);
 void dev_free(double*& p);
 vampomi_status host_sync(vampomi_ctx* c);
 // spins until the context's host flag reaches seq (stores from the stream)
-vampomi_status wait_flag(vampomi_ctx* c, unsigned long long seq);
+// (word 1: the side stream's sequence, stored by its one-rank reductions)
+vampomi_status wait_flag(vampomi_ctx* c, unsigned long long seq, int word = 0);
 // SUM all-reduce of n doubles over the ranks (nothing on one rank). COLLECTIVE:
 // every rank must make the same calls in the same order; site/line identify
 // the call for the divergence checks (loopback always, RCCL with
@@ -187,6 +198,15 @@ class DotBatch {
     vampomi_status sink(int nq, bool sync, double* out, vk::RedOut* ro);
     vampomi_status flush();
     bool empty() const { return sinks_.empty(); }
+    // on = true: the following sinks/adds run on the context's side stream
+    // (ordered after everything queued on st so far); flush() joins it back.
+    // No effect (one stream) when the context's side stream is off
+    vampomi_status side(bool on);
+    // the side stream's work starts from st's state NOW (launches queued on st
+    // after this call may overlap it); side(true) forks here if not yet done
+    vampomi_status fork();
+    // the stream the next launch of this batch goes to
+    hipStream_t stream() const;
 
    private:
     struct Sink {
@@ -195,7 +215,9 @@ class DotBatch {
     };
     vampomi_ctx* c_;
     int nsync_ = 0, nlocal_ = 0;
+    bool on_side_ = false, forked_ = false;
     unsigned long long last_seq_ = 0;  // one rank: flag value the last reduction kernel stores
+    unsigned long long side_seq_ = 0;  // ... and the last side-stream reduction (flag word 1)
     std::vector<Sink> sinks_;
 };
 

@@ -167,16 +167,17 @@ void drop_launches(vampomi_ctx* c, size_t pending_mark, const vampomi_stats& bef
 // (a 1-thread kernel stores the flag); a one-rank DotBatch waits for its last
 // reduction kernel, whose last block stores the flag itself.  Faults are
 // still reported: the spin polls hipStreamQuery, and gives up after 10 min.
-vampomi_status wait_flag(vampomi_ctx* c, unsigned long long seq) {
+vampomi_status wait_flag(vampomi_ctx* c, unsigned long long seq, int word) {
     const auto t0 = std::chrono::steady_clock::now();
+    hipStream_t st = word == 1 ? c->st2 : c->st;  // word 1: the side stream's sequence
     for (uint64_t spin = 1;; ++spin) {
-        if (__atomic_load_n(c->h_flag, __ATOMIC_ACQUIRE) >= seq) return VAMPOMI_OK;
+        if (__atomic_load_n(c->h_flag + word, __ATOMIC_ACQUIRE) >= seq) return VAMPOMI_OK;
         if ((spin & 4095) == 0) {
-            const hipError_t e = hipStreamQuery(c->st);
+            const hipError_t e = hipStreamQuery(st);
             if (e != hipSuccess && e != hipErrorNotReady)
                 return fail(VAMPOMI_ERR_HIP, std::string("stream failed: ") + hipGetErrorString(e));
             if (e == hipSuccess) {  // finished, flag not seen yet: complete through the runtime
-                HIPCHK(hipStreamSynchronize(c->st));
+                HIPCHK(hipStreamSynchronize(st));
                 return VAMPOMI_OK;
             }
             if (std::chrono::steady_clock::now() - t0 > std::chrono::minutes(10))
@@ -384,14 +385,21 @@ vampomi_status DotBatch::sink(int nq, bool sync, double* out, vk::RedOut* ro) {
     int& used = sync ? nsync_ : nlocal_;
     const int base = sync ? SL_SYNC : SL_LOCAL, cap = sync ? SL_NSYNC : SL_NLOCAL;
     if (used + nq > cap) return fail(VAMPOMI_ERR_STATE, "DotBatch overflow");
-    ro->part = c_->red_part;
+    ro->part = on_side_ ? c_->red_part2 : c_->red_part;
     ro->out = (c_->use_comm ? c_->scal : c_->d_hscal) + base + used;
-    ro->ticket = c_->ticket;
+    ro->ticket = on_side_ ? c_->ticket2 : c_->ticket;
     ro->flag = nullptr;
     ro->seq = 0;
-    if (!c_->use_comm && c_->h_flag) {  // results land in host memory: the kernel flags their arrival
-        ro->flag = c_->d_flag;
-        ro->seq = last_seq_ = ++c_->sync_seq;
+    // results land in host memory: the kernel flags their arrival (word 0
+    // counts along st, word 1 along the side stream: each is monotone)
+    if (!c_->use_comm && c_->h_flag) {
+        if (on_side_) {
+            ro->flag = c_->d_flag + 1;
+            ro->seq = side_seq_ = ++c_->side_seq;
+        } else {
+            ro->flag = c_->d_flag;
+            ro->seq = last_seq_ = ++c_->sync_seq;
+        }
     }
     sinks_.push_back(Sink{base + used, nq, out});
     used += nq;
@@ -410,11 +418,39 @@ vampomi_status DotBatch::add(std::initializer_list<vk::DotTerm> terms, int64_t n
     }
     vk::RedOut ro{};
     STCHK(sink(a.nt, sync, out, &ro));
-    HIPCHK(vk::dots(a, n, ro, c_->st));
+    HIPCHK(vk::dots(a, n, ro, stream()));
+    return VAMPOMI_OK;
+}
+
+hipStream_t DotBatch::stream() const { return on_side_ ? c_->st2 : c_->st; }
+
+vampomi_status DotBatch::fork() {
+    if (forked_ || !c_->side_on || !c_->st2) return VAMPOMI_OK;
+    HIPCHK(hipEventRecord(c_->ev_fork, c_->st));
+    HIPCHK(hipStreamWaitEvent(c_->st2, c_->ev_fork, 0));
+    forked_ = true;
+    return VAMPOMI_OK;
+}
+
+vampomi_status DotBatch::side(bool on) {
+    on_side_ = on && c_->side_on && c_->st2;
+    if (on_side_) STCHK(fork());  // the side stream starts after everything queued on st so far
     return VAMPOMI_OK;
 }
 
 vampomi_status DotBatch::flush() {
+    on_side_ = false;
+    const bool had_side = side_seq_ != 0;
+    if (forked_) {  // join: st continues after the side stream's work
+        HIPCHK(hipEventRecord(c_->ev_join, c_->st2));
+        HIPCHK(hipStreamWaitEvent(c_->st, c_->ev_join, 0));
+        forked_ = false;
+    }
+    if (side_seq_) {  // one rank: the host reads the side results when their own kernel flags them
+        c_->stats.host_syncs++;
+        STCHK(wait_flag(c_, side_seq_, 1));
+        side_seq_ = 0;
+    }
     if (sinks_.empty()) return VAMPOMI_OK;
     if (c_->use_comm) {  // slots in device memory: all-reduce the synced ones, then publish both ranges
         if (nsync_ > 0) STCHK(allreduce_dev(c_, c_->scal + SL_SYNC, (size_t)nsync_));
@@ -436,7 +472,7 @@ vampomi_status DotBatch::flush() {
     } else if (last_seq_) {
         c_->stats.host_syncs++;
         STCHK(wait_flag(c_, last_seq_));
-    } else {
+    } else if (!had_side) {
         STCHK(host_sync(c_));
     }
     for (const Sink& k : sinks_)
@@ -713,11 +749,12 @@ extern "C" vampomi_status vampomi_comm_unique_id(void* out) {
 void release_ctx_resources(vampomi_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->st) (void)hipStreamSynchronize(c->st);
+    if (c->st2) (void)hipStreamSynchronize(c->st2);
     team_gate_leave(c);
     resolve_timing(c);
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
     c->ev_pool.clear();
-    for (double** p : {&c->X, &c->mave, &c->msig, &c->y, &c->ax_part, &c->red_part, &c->scal, &c->nbuf, &c->mbuf,
+    for (double** p : {&c->X, &c->mave, &c->msig, &c->y, &c->ax_part, &c->red_part, &c->red_part2, &c->scal, &c->nbuf, &c->mbuf,
                        &c->op_part, &c->op_nvec})
         dev_free(*p);
     if (c->op_xg) (void)hipFree(c->op_xg);
@@ -729,6 +766,8 @@ void release_ctx_resources(vampomi_ctx* c) {
     c->h_scal = nullptr;
     if (c->ticket) (void)hipFree(c->ticket);
     c->ticket = nullptr;
+    if (c->ticket2) (void)hipFree(c->ticket2);
+    c->ticket2 = nullptr;
     if (c->h_flag) (void)hipHostFree(c->h_flag);
     c->h_flag = nullptr;
     if (c->h_cgm) (void)hipHostFree(c->h_cgm);
@@ -737,6 +776,10 @@ void release_ctx_resources(vampomi_ctx* c) {
     c->cgs = nullptr;
     if (c->comm) (void)ncclCommDestroy(c->comm);
     c->comm = nullptr;
+    for (hipEvent_t* e : {&c->ev_fork, &c->ev_join})
+        if (*e) (void)hipEventDestroy(*e), *e = nullptr;
+    if (c->st2) (void)hipStreamDestroy(c->st2);
+    c->st2 = nullptr;
     if (c->st) (void)hipStreamDestroy(c->st);
     c->st = nullptr;
 }
@@ -777,6 +820,11 @@ extern "C" vampomi_status vampomi_open(const vampomi_shard_desc* d, vampomi_ctx*
                                    (size_t)((Mx + 255) / 256) * (1 + 2 * (vk::kMaxL - 1)),
                                    (size_t)(Mx / 8 + 1) * vk::kMaxRhs, (size_t)4096});  // ATx partials at G >= 2
     STCHK(dev_alloc(&c->red_part, c->red_cap));
+    STCHK(dev_alloc(&c->red_part2, c->red_cap));
+    HIPCHK(hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
+    if (const char* sv = std::getenv("VAMPOMI_SIDE_STREAM")) c->side_on = std::atoi(sv) != 0;
     STCHK(dev_alloc(&c->scal, SL_TOTAL));
     HIPCHK(hipHostMalloc((void**)&c->h_scal, SL_TOTAL * sizeof(double), hipHostMallocMapped | hipHostMallocCoherent));
     HIPCHK(hipHostGetDevicePointer((void**)&c->d_hscal, c->h_scal, 0));
@@ -785,6 +833,8 @@ extern "C" vampomi_status vampomi_open(const vampomi_shard_desc* d, vampomi_ctx*
     HIPCHK(hipHostGetDevicePointer((void**)&c->d_flag, c->h_flag, 0));
     HIPCHK(hipMalloc((void**)&c->ticket, 64 * sizeof(unsigned)));
     HIPCHK(hipMemsetAsync(c->ticket, 0, 64 * sizeof(unsigned), c->st));
+    HIPCHK(hipMalloc((void**)&c->ticket2, 64 * sizeof(unsigned)));
+    HIPCHK(hipMemsetAsync(c->ticket2, 0, 64 * sizeof(unsigned), c->st));
     STCHK(dev_alloc(&c->nbuf, (size_t)vk::kMaxRhs * c->ld));
     HIPCHK(hipMemsetAsync(c->nbuf, 0, (size_t)vk::kMaxRhs * c->ld * 8, c->st));
     STCHK(dev_alloc(&c->mbuf, (size_t)2 * vk::kMaxRhs * Mx));
@@ -1355,6 +1405,9 @@ extern "C" vampomi_status vampomi_dev_set_variant(vampomi_ctx* c, int which, int
             return fail(VAMPOMI_ERR_ARG, "no such one-pass operator plan for this N");
         c->op_variant = variant;
         c->op_ready = false;
+    } else if (which == 4) {  // side stream for the prefetched denoiser/EM: 0 off, 1 on
+        if (variant != 0 && variant != 1) return fail(VAMPOMI_ERR_ARG, "side stream: 0 or 1");
+        c->side_on = variant == 1;
     } else {
         if (!vk::loo_variant_ok(variant)) return fail(VAMPOMI_ERR_ARG, "no such association-pass variant");
         c->loo_variant = variant;

@@ -72,8 +72,21 @@ struct EmParams {
     double merge_vars_thr;
     int verbosity;
 };
+EmParams em_params(const VampRun& R);
 vampomi_status update_prior(vampomi_ctx* c, const EmParams& P, Mixture& m, double gam1, const double* r1);
 vampomi_status update_prior(vampomi_ctx* c, const VampRun& R, Mixture& m, double gam1, const double* r1);
+// updatePrior in two halves (vamp.cpp): em_begin queues the first EM round's
+// sums into b; after b.flush(), em_finish completes the update
+struct EmState {
+    int emit = 0;
+    double lambda = 0;
+    double omegas[VAMPOMI_MAX_L] = {};
+    double sums[2 * VAMPOMI_MAX_L] = {};
+};
+vampomi_status em_begin(vampomi_ctx* c, const EmParams& P, const Mixture& m, double gam1, const double* r1,
+                        DotBatch& b, EmState& s);
+vampomi_status em_queue(vampomi_ctx* c, const Mixture& m, double gam1, const double* r1, DotBatch& b, EmState& s);
+vampomi_status em_finish(vampomi_ctx* c, const EmParams& P, Mixture& m, double gam1, const double* r1, EmState& s);
 vampomi_status denoise_into(vampomi_ctx* c, const Mixture& m, double gam1, const double* r1, double* x1,
                             const double* x1_prev, bool damp, double rho, double* x1d, DotBatch& b, double* sum_out);
 vampomi_status upload_or_zero(vampomi_ctx* c, double* dst, const double* host, int64_t n);

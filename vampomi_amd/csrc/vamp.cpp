@@ -51,54 +51,67 @@ vampomi_ctx::~vampomi_ctx() {
     release_ctx_resources(this);
 }
 
-// updatePrior (src/vamp.cpp:531-643) on mixture m, from r1 and gam1
-vampomi_status update_prior(vampomi_ctx* c, const VampRun& R, Mixture& m, double gam1, const double* r1) {
-    const EmParams ep{R.prm.EM_max_iter, R.prm.EM_err_thr, R.prm.learn_vars, R.prm.merge_vars_thr, R.prm.verbosity};
-    return update_prior(c, ep, m, gam1, r1);
+// updatePrior (src/vamp.cpp:531-643) on mixture m, from r1 and gam1, split in
+// two so that a caller can queue the first EM round's sums early (on the side
+// stream) and resolve them with other reductions: em_begin queues round 0
+// into b; after b.flush(), em_finish does its host part, the further rounds
+// (each with its own batch) and the merge.  update_prior runs both.
+vampomi_status em_begin(vampomi_ctx* c, const EmParams& P, const Mixture& m, double gam1, const double* r1,
+                        DotBatch& b, EmState& s) {
+    s.emit = 0;
+    s.lambda = 1 - m.probs[0];
+    for (int j = 0; j < m.L; ++j) s.omegas[j] = m.probs[j];
+    for (int j = 1; j < m.L; ++j) s.omegas[j] /= s.lambda;
+    if (P.EM_max_iter < 1) return VAMPOMI_OK;
+    return em_queue(c, m, gam1, r1, b, s);
 }
 
-vampomi_status update_prior(vampomi_ctx* c, const EmParams& P, Mixture& m, double gam1, const double* r1) {
-    const double noise_var = 1 / gam1;
-    double lambda = 1 - m.probs[0];
-    double omegas[VAMPOMI_MAX_L];
-    for (int j = 0; j < m.L; ++j) omegas[j] = m.probs[j];
-    for (int j = 1; j < m.L; ++j) omegas[j] /= lambda;
-    std::vector<double> sums(2 * VAMPOMI_MAX_L);
-    for (int emit = 0; emit < P.EM_max_iter; ++emit) {
+// one EM round's per-slab sums (:555-597) into b, on b's current stream
+vampomi_status em_queue(vampomi_ctx* c, const Mixture& m, double gam1, const double* r1, DotBatch& b,
+                        EmState& s) {
+    const int L = m.L;
+    double max_sigma = m.vars[0];
+    for (int j = 1; j < L; ++j) max_sigma = smax(max_sigma, m.vars[j]);  // std::max_element
+    vk::EmArgs a{};
+    for (int j = 0; j < L; ++j) {
+        a.omegas[j] = s.omegas[j];
+        a.vars[j] = m.vars[j];
+    }
+    for (int j = 1; j < L; ++j) a.v[j - 1] = 1.0 / (1.0 / m.vars[j] + gam1);
+    a.lambda = s.lambda;
+    a.noise_var = 1 / gam1;
+    a.gam1 = gam1;
+    a.max_sigma = max_sigma;
+    a.L = L;
+    vk::RedOut ro{};
+    STCHK(b.sink(1 + 2 * (L - 1), true, s.sums, &ro));  // :578, :596-597
+    HIPCHK(vk::em_sums(c->M, r1, a, ro, b.stream()));
+    return VAMPOMI_OK;
+}
+
+vampomi_status em_finish(vampomi_ctx* c, const EmParams& P, Mixture& m, double gam1, const double* r1,
+                         EmState& s) {
+    for (; s.emit < P.EM_max_iter; ++s.emit) {
+        if (s.emit > 0) {  // round 0 was queued by em_begin and resolved by its batch
+            DotBatch b(c);
+            STCHK(em_queue(c, m, gam1, r1, b, s));
+            STCHK(b.flush());
+        }
         const int L = m.L;
-        double max_sigma = m.vars[0];
-        for (int j = 1; j < L; ++j) max_sigma = smax(max_sigma, m.vars[j]);  // std::max_element
         double probs_prev[VAMPOMI_MAX_L], vars_prev[VAMPOMI_MAX_L];
         std::memcpy(probs_prev, m.probs, sizeof probs_prev);
         std::memcpy(vars_prev, m.vars, sizeof vars_prev);
-        vk::EmArgs a{};
-        for (int j = 0; j < L; ++j) {
-            a.omegas[j] = omegas[j];
-            a.vars[j] = m.vars[j];
-        }
-        for (int j = 1; j < L; ++j) a.v[j - 1] = 1.0 / (1.0 / m.vars[j] + gam1);
-        a.lambda = lambda;
-        a.noise_var = noise_var;
-        a.gam1 = gam1;
-        a.max_sigma = max_sigma;
-        a.L = L;
-        const int Q = 1 + 2 * (L - 1);
-        DotBatch b(c);
-        vk::RedOut ro{};
-        STCHK(b.sink(Q, true, sums.data(), &ro));  // :578, :596-597
-        HIPCHK(vk::em_sums(c->M, r1, a, ro, c->st));
-        STCHK(b.flush());
-        const double lambda_total = sums[0];
-        lambda = lambda_total / (double)c->Mt;
+        const double lambda_total = s.sums[0];
+        s.lambda = lambda_total / (double)c->Mt;
         const double sum_of_pin = lambda_total;
         for (int j = 0; j < L - 1; ++j) {
-            const double res_total = sums[1 + j];
-            const double res_gammas_total = sums[L + j];
+            const double res_total = s.sums[1 + j];
+            const double res_gammas_total = s.sums[L + j];
             if (P.learn_vars == 1) m.vars[j + 1] = res_gammas_total / res_total;
-            omegas[j + 1] = res_total / sum_of_pin;
-            m.probs[j + 1] = lambda * omegas[j + 1];
+            s.omegas[j + 1] = res_total / sum_of_pin;
+            m.probs[j + 1] = s.lambda * s.omegas[j + 1];
         }
-        m.probs[0] = 1 - lambda;
+        m.probs[0] = 1 - s.lambda;
         double dprob = 0, nprob = 0, dvar = 0, nvar = 0;
         for (int j = 0; j < L; ++j) {
             dprob += (m.probs[j] - probs_prev[j]) * (m.probs[j] - probs_prev[j]);
@@ -108,7 +121,7 @@ vampomi_status update_prior(vampomi_ctx* c, const EmParams& P, Mixture& m, doubl
         }
         const double dist_probs = std::sqrt(dprob / nprob), dist_vars = std::sqrt(dvar / nvar);
         if (P.verbosity == 1 && c->rank == 0)
-            std::printf("it = %d: dist_probs = %g & dist_vars = %g\n", emit, dist_probs, dist_vars);
+            std::printf("it = %d: dist_probs = %g & dist_vars = %g\n", s.emit, dist_probs, dist_vars);
         if (dist_probs < P.EM_err_thr && dist_vars < P.EM_err_thr) break;
     }
     // merging close variances (:626-642)
@@ -130,6 +143,22 @@ vampomi_status update_prior(vampomi_ctx* c, const EmParams& P, Mixture& m, doubl
     return VAMPOMI_OK;
 }
 
+vampomi_status update_prior(vampomi_ctx* c, const EmParams& P, Mixture& m, double gam1, const double* r1) {
+    EmState s;
+    DotBatch b(c);
+    STCHK(em_begin(c, P, m, gam1, r1, b, s));
+    STCHK(b.flush());
+    return em_finish(c, P, m, gam1, r1, s);
+}
+
+EmParams em_params(const VampRun& R) {
+    return EmParams{R.prm.EM_max_iter, R.prm.EM_err_thr, R.prm.learn_vars, R.prm.merge_vars_thr, R.prm.verbosity};
+}
+
+vampomi_status update_prior(vampomi_ctx* c, const VampRun& R, Mixture& m, double gam1, const double* r1) {
+    return update_prior(c, em_params(R), m, gam1, r1);
+}
+
 // x1 = g1(r1) [damped], x1d = g1d(r1); sum of x1d over ranks queued in b
 vampomi_status denoise_into(vampomi_ctx* c, const Mixture& m, double gam1, const double* r1, double* x1,
                                    const double* x1_prev, bool damp, double rho, double* x1d, DotBatch& b,
@@ -142,7 +171,7 @@ vampomi_status denoise_into(vampomi_ctx* c, const Mixture& m, double gam1, const
     }
     vk::RedOut ro{};
     STCHK(b.sink(1, true, sum_out, &ro));  // :214-222
-    HIPCHK(vk::denoise(c->M, r1, gam1, mix, x1, x1_prev, damp ? 1 : 0, rho, x1d, ro, c->st));
+    HIPCHK(vk::denoise(c->M, r1, gam1, mix, x1, x1_prev, damp ? 1 : 0, rho, x1d, ro, b.stream()));
     return VAMPOMI_OK;
 }
 
@@ -437,11 +466,22 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
     HIPCHK(vk::lincomb_div(M, R.eta2, R.x2, R.gam2, R.r2, R.gam1, R.r1, c->st));  // r1 (:348-350)
 
     // ---- prefetch: denoising of iteration it+1 (discarded if the stop fires) ----
+    // (batch_rhs >= 3: on the side stream, beside the reductions below)
     const bool next = R.fuse && it < R.prm.max_iter;
+    const bool em_next = next && it + 1 > R.prm.learn_prior_delay;
     DotBatch fin(c);
-    if (next) {
-        R.mix_next = R.mix;
-        if (it + 1 > R.prm.learn_prior_delay) STCHK(update_prior(c, R, R.mix_next, R.gam1, R.r1));
+    EmState em;
+    if (next) R.mix_next = R.mix;
+    if (next && arec) {  // the side stream starts from r1 and x1; its EM sums are queued before these reductions
+        STCHK(fin.fork());
+        if (em_next) {
+            STCHK(fin.side(true));
+            STCHK(em_begin(c, em_params(R), R.mix_next, R.gam1, R.r1, fin, em));
+            STCHK(fin.side(false));
+        }
+    }
+    if (next && !arec) {  // the pass below carries the next z1 = A x1_hat: denoise first
+        if (em_next) STCHK(update_prior(c, R, R.mix_next, R.gam1, R.r1));
         STCHK(denoise_into(c, R.mix_next, R.gam1, R.r1, R.x1n, R.x1, true, R.prm.rho, R.x1d, fin, &R.sum_d));
     }
 
@@ -474,6 +514,21 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
     }
     STCHK(err_queue(c, R, R.x2, ax2, fin, R.e2m, R.e2n, R.e2s));  // :365 (A.x2_hat of :826)
     R.passes_ref += 1;
+    // Second stream (batch_rhs >= 3, north_star): iteration it+1's EM sums run
+    // on the side stream beside these reductions and share their all-reduce
+    // and host wait; then its denoiser (g1, g1d, sum of g1d) runs there beside
+    // the NMSE sums, again one all-reduce and one wait. Every reduction is the
+    // same fixed-order kernel as on one stream, so the values are bitwise the
+    // same (tests/test_gpu_sharded.py::test_side_stream_bitwise)
+    if (next && arec && em_next) {
+        STCHK(fin.flush());
+        STCHK(em_finish(c, em_params(R), R.mix_next, R.gam1, R.r1, em));
+    }
+    if (next && arec) {
+        STCHK(fin.side(true));  // forks again after an EM flush
+        STCHK(denoise_into(c, R.mix_next, R.gam1, R.r1, R.x1n, R.x1, true, R.prm.rho, R.x1d, fin, &R.sum_d));
+        STCHK(fin.side(false));
+    }
     STCHK(fin.add({T(R.x1p, R.x1, vk::DIFF2), T(R.x1p, R.x1p)}, M, true, R.nm));  // NMSE (:409-413)
     STCHK(fin.flush());
     const double trace_corr = R.tc * (double)Mt;  // :521
