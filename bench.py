@@ -179,6 +179,31 @@ def cpu_baseline(d, w: dict, beta, seed: int, warmup: int, steps: int, gpu_ref_p
                        f"{gpu_ref_passes:.2f} passes per iteration (W + k iterations exceed the {budget_s:.0f} s budget)")
 
 
+def cpu_reference_ops(w: dict, seed: int, threads: int, k_cg: float):
+    """The reference's OWN Ax / ATx (src/data.cpp:294-373, compiled from its
+    sources into oracle/_ref/ref_data in the build container) timed on a
+    generated matrix of the workload's shape, on the same host threads; the
+    projected reference iteration rate uses its own call counts per
+    iteration (it > 1): 5 + k Ax and 3 + k ATx with k = k1 + k2 CG steps
+    (src/vamp.cpp:232,303,508,518-519,653-654,681,826), k from
+    the GPU window.  The denoiser/EM (< 1 % of its CPU time) is left out."""
+    exe = os.path.join(ROOT, "oracle", "_ref", "ref_data")
+    if not os.path.exists(exe):
+        return {"skipped": "oracle/_ref/ref_data not built (needs /root/reference in the build container)"}
+    env = dict(os.environ, OMP_NUM_THREADS=str(threads))
+    out = subprocess.run([exe, "time", str(w["N"]), str(w["Mt"]), "2", str(seed)], env=env, capture_output=True,
+                         text=True, timeout=300)
+    if out.returncode != 0:
+        return {"error": f"ref_data exit {out.returncode}: {out.stderr[-300:]}"}
+    r = json.loads(out.stdout.strip().splitlines()[-1])
+    t_it = ((5 + k_cg) * r["ax_ms"] + (3 + k_cg) * r["atx_ms"]) * 1e-3
+    return {"value": 1.0 / t_it, "unit": "VAMP iterations/s", "kind": "reference", "projected": True,
+            "cores": r["threads"], "ax_ms": r["ax_ms"], "atx_ms": r["atx_ms"],
+            "sample": f"Ax and ATx (mean of 2 calls each) of the reference's src/data.cpp (oracle/_ref) on a generated "
+                      f"{w['N']} x {w['Mt']} matrix, {r['threads']} OpenMP threads; iteration = (5 + k) Ax + (3 + k) "
+                      f"ATx, k = {k_cg:.2f} (the GPU window's mean CG + Onsager steps)"}
+
+
 def cpu_baseline_assoc(d, w: dict, est, seed: int) -> dict:
     """The oracle's LOO test (OpenMP) on the first Ms markers of the same workload."""
     from oracle import pyoracle as O
@@ -440,6 +465,13 @@ def main():
                                                 args.cpu_budget)
         except Exception as e:  # reported, never fatal for the GPU number
             line["cpu_baseline"] = {"error": repr(e)}
+        if model == "linear":
+            try:
+                k_cg = (sum(line["cg_iters"]) + sum(line["ons_iters"])) / max(len(line["cg_iters"]), 1)
+                threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+                line["cpu_reference_ops"] = cpu_reference_ops(w, args.seed, threads, k_cg)
+            except Exception as e:
+                line["cpu_reference_ops"] = {"error": repr(e)}
     d.close()
     if R.rank == 0:
         print(json.dumps(line), flush=True)

@@ -18,7 +18,13 @@
 //   ref_data ax    <X.bin> <N> <M> <x.bin> <out.bin>     (statistics first, as data::data does)
 //   ref_data atx   <X.bin> <N> <M> <u.bin> <out.bin>
 //   ref_data phen  <phen> <N> <standardize 0|1> <out.bin>
+//   ref_data time  <N> <M> <reps> <seed>   (bench.py's CPU leg: the reference's own Ax / ATx
+//                  on a generated N x M matrix, OpenMP threads as set; prints one JSON line)
 #include <mpi.h>
+#include <omp.h>
+
+#include <chrono>
+#include <cstdint>
 
 #include <cstdio>
 #include <cstdlib>
@@ -73,12 +79,57 @@ struct Obj {
     }
 };
 
+static uint64_t splitmix(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+// times the reference's Ax and ATx (src/data.cpp:294-373) on an N x M
+// marker-major matrix of uniform values (timing only; the values do not matter)
+static int time_ops(int N, int M, int reps, uint64_t seed) {
+    const size_t n = size_t(N) * size_t(M);
+    double* X = (double*)_mm_malloc(n * sizeof(double), 64);  // as data::read_methylation_data (:129)
+    if (!X) return 5;
+#pragma omp parallel for schedule(static)
+    for (long long m = 0; m < M; ++m)
+        for (int j = 0; j < N; ++j)
+            X[size_t(m) * N + j] = double(splitmix(seed ^ (size_t(m) * N + j)) >> 11) * 0x1.0p-53 * 3.4 - 1.7;
+    Obj o(N, M, 1.0);
+    o.d->meth_data = X;
+    o.d->compute_markers_statistics();
+    std::vector<double> x(M), u(N);
+    for (int i = 0; i < M; ++i) x[i] = double(splitmix(seed + 1 + i) >> 11) * 0x1.0p-53 - 0.5;
+    for (int j = 0; j < N; ++j) u[j] = double(splitmix(seed + 7 + j) >> 11) * 0x1.0p-53 - 0.5;
+    using clk = std::chrono::steady_clock;
+    double ax = 0, atx = 0, chk = 0;
+    for (int r = 0; r < reps; ++r) {
+        auto t0 = clk::now();
+        std::vector<double> a = o.d->Ax(x.data());
+        auto t1 = clk::now();
+        std::vector<double> b = o.d->ATx(u.data());
+        auto t2 = clk::now();
+        ax += std::chrono::duration<double>(t1 - t0).count();
+        atx += std::chrono::duration<double>(t2 - t1).count();
+        chk += a[0] + b[0];
+    }
+    std::printf("{\"N\": %d, \"M\": %d, \"reps\": %d, \"threads\": %d, \"ax_ms\": %.3f, \"atx_ms\": %.3f, "
+                "\"check\": %.6g}\n",
+                N, M, reps, omp_get_max_threads(), ax / reps * 1e3, atx / reps * 1e3, chk);
+    _mm_free(X);
+    return 0;
+}
+
 int main(int argc, char** argv) {
     MPI_Init(&argc, &argv);
     if (argc < 3) return 2;
     const std::string cmd = argv[1];
     int rc = 0;
-    if (cmd == "phen") {
+    if (cmd == "time") {
+        if (argc < 6) return 2;
+        rc = time_ops(std::atoi(argv[2]), std::atoi(argv[3]), std::atoi(argv[4]), std::strtoull(argv[5], nullptr, 10));
+    } else if (cmd == "phen") {
         const int N = std::atoi(argv[3]);
         Obj o(N, 1, 1.0);
         o.d->phenfp = argv[2];
