@@ -46,3 +46,18 @@ def test_workload_selection():
     with pytest.raises(ValueError):
         workload("c3full", 1)
     assert workload("c2", 4)["Mt"] == 200000 and workload("c3", 8)["Mt"] == 500000
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(ROOT, "oracle", "_ref", "ref_data")),
+                    reason="oracle/_ref not built (needs /root/reference)")
+def test_cpu_reference_ops_leg():
+    """bench.py's kind-"reference" CPU leg: the reference's own Ax / ATx
+    (src/data.cpp via oracle/_ref) timed on a small generated matrix, and the
+    projection from its call counts per iteration."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    r = bench.cpu_reference_ops({"N": 300, "Mt": 500, "workload": "tiny"}, 3, 2, 10.0)
+    assert r["kind"] == "reference" and r["cores"] == 2 and r["ax_ms"] > 0 and r["atx_ms"] > 0
+    want = 1.0 / ((15 * r["ax_ms"] + 13 * r["atx_ms"]) * 1e-3)
+    assert abs(r["value"] - want) <= 1e-9 * want
