@@ -25,7 +25,7 @@ va = pytest.importorskip("vampomi_amd")
 from oracle import pyoracle as O  # noqa: E402  (checker: the generator and marker statistics)
 
 SHAPES = [(1000, 3000, 0), (10000, 4000, 0), (50001, 1500, 1), (100000, 600, 1)]
-CANDIDATES = [0] + [T * 10 + c for T in (1, 2, 4, 8, 16, 32) for c in range(5)]
+CANDIDATES = [0] + [T * 10 + c for T in (1, 2, 4, 8, 16, 32) for c in range(10)]
 
 
 def _ref(X, mave, msig, ar, qo, p, z, beta, diag, tau, gam2):

@@ -78,6 +78,7 @@ static constexpr TmCfg kTmCfg[] = {
     {4, 5, 2, true, 4, 2, false},    // 6
     {4, 5, 2, true, 4, 2, true},     // 7
     {3, 5, 2, true, 4, 2, true},     // 8
+    {2, 4, 2, true, 5, 2, true},     // 9: 3, interleaved
 };
 static constexpr int kTmNCfg = sizeof(kTmCfg) / sizeof(kTmCfg[0]);
 
@@ -719,6 +720,7 @@ static bool launch_tm_c(const Shard& s, const OpPlan& pl, const OpArgs& a, hipSt
         case 6: return launch_tm_s<K, 6>(pl.S, s, pl, a, st, tm, gate);
         case 7: return launch_tm_s<K, 7>(pl.S, s, pl, a, st, tm, gate);
         case 8: return launch_tm_s<K, 8>(pl.S, s, pl, a, st, tm, gate);
+        case 9: return launch_tm_s<K, 9>(pl.S, s, pl, a, st, tm, gate);
         default: return false;
     }
 }

@@ -727,9 +727,13 @@ static bool whole_column_ok(int64_t N) {
 // The default: whole columns per workgroup (team size 1, the team kernel
 // without a hand-off: 585 us against 646 us for atax_kernel at C2, K = 2,
 // profiles/r02c_op_sweep.txt) while the rows fit one workgroup, else the
-// smallest team whose members' rows fit the registers (configuration 6:
-// 4 columns prefetched, a lag of 5 steps, polls 2 steps ahead; measured best
-// at N = 50,000 and 100,000, profiles/r02c_op_sweep.txt).
+// smallest team whose members' rows fit the registers (configuration 7:
+// 4 columns prefetched, a lag of 5 steps, polls 2 steps ahead, measured best
+// at N = 50,000 and 100,000, profiles/r02c_op_sweep.txt; with the teams'
+// columns interleaved, team t taking columns t, t + nteams, ..., so that all
+// teams stream neighbouring columns instead of 8-16 ranges gigabytes apart:
+// 10-13 % faster at the C3 shard, config 4 whole and 240 GB,
+// profiles/r02i_op_interleave.txt).
 bool op_plan(int64_t N, int64_t M, int cus, int variant, OpPlan* out) {
     if (N < 1 || cus < 1) return false;
     if (variant == kOpDefault) {
@@ -755,7 +759,7 @@ bool op_plan(int64_t N, int64_t M, int cus, int variant, OpPlan* out) {
         return true;
     }
     if (variant > 0) return team_plan(N, M, cus, variant / 10, variant % 10, out);
-    for (int cfg : {6, 3}) {  // then fewer columns in flight for one more load per lane (S <= 5)
+    for (int cfg : {7, 9}) {  // then fewer columns in flight for one more load per lane (S <= 5)
         for (int T = 2; T <= 32; T *= 2) {
             OpPlan p{};
             if (!team_plan(N, M, cus, T, cfg, &p)) continue;
