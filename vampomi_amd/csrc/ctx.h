@@ -249,9 +249,13 @@ struct CgSystem {
 // step runs).  nscratch holds kMaxRhs*ld + kMaxRhs doubles.
 // onepass (K <= 2): every CG step reads X once (vk::atax; A r0 by one A.x pass
 // per solve, which also carries extra_x); otherwise two passes per step.
+// ar0 (may be null; onepass only): ar0[k] (device, ld, may be null) already
+// holds A r0 of system k (its start is zero, so r0 = v), and the first A.x
+// pass covers only the systems without it (no pass if none).
 vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double tau, double gam2, int max_iter,
                        double tol, double* nscratch, int64_t* ref_passes, DotBatch* init,
-                       const double* extra_x = nullptr, double* ex_out = nullptr, bool onepass = false);
+                       const double* extra_x = nullptr, double* ex_out = nullptr, bool onepass = false,
+                       const double* const* ar0 = nullptr);
 // plans the one-pass operator (c->opp, c->op_ok) and allocates its buffers
 // (idempotent until the variant changes)
 vampomi_status op_prepare(vampomi_ctx* c);

@@ -61,7 +61,7 @@ static vampomi_status cg_loop(vampomi_ctx* c, int max_iter, Enqueue&& enqueue, c
 
 vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double tau, double gam2, int max_iter,
                        double tol, double* nscratch, int64_t* ref_passes, DotBatch* init, const double* extra_x,
-                       double* ex_out, bool onepass) {
+                       double* ex_out, bool onepass, const double* const* ar0) {
     const int64_t M = c->M, N = c->N;
     const double diag = tau * (double)(N - 1) / (double)N + gam2;  // :676-677
     const int K = (int)sys.size();
@@ -143,11 +143,41 @@ vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double
         double* AR = c->op_nvec;
         double* Q = c->op_nvec + (int64_t)vk::kMaxRhs * c->ld;
         const double* AD = c->op_nvec + (int64_t)2 * vk::kMaxRhs * c->ld;
-        const double* px[vk::kMaxRhs];
-        for (int k = 0; k < K; ++k) px[k] = sys[k]->r;
-        if (extra_x) px[K] = extra_x;
-        STCHK(ax_dev(c, extra_x ? K + 1 : K, px, AR));
-        if (extra_x) HIPCHK(hipMemcpyAsync(ex_out, AR + (int64_t)K * c->ld, (size_t)N * 8, hipMemcpyDeviceToDevice, c->st));
+        bool given = false;
+        for (int k = 0; k < K; ++k) given = given || (ar0 && ar0[k]);
+        if (!given) {
+            const double* px[vk::kMaxRhs];
+            for (int k = 0; k < K; ++k) px[k] = sys[k]->r;
+            if (extra_x) px[K] = extra_x;
+            STCHK(ax_dev(c, extra_x ? K + 1 : K, px, AR));
+            if (extra_x)
+                HIPCHK(hipMemcpyAsync(ex_out, AR + (int64_t)K * c->ld, (size_t)N * 8, hipMemcpyDeviceToDevice, c->st));
+        } else {  // A r0 given for some systems (zero starts, r0 = v): one pass for the others, if any
+            const double* px[vk::kMaxRhs];
+            int slot[vk::kMaxRhs], n = 0;
+            for (int k = 0; k < K; ++k) {
+                if (ar0[k]) {
+                    if (sys[k]->mu0_nonzero) return fail(VAMPOMI_ERR_ARG, "pcg: A r0 given for a nonzero start");
+                    HIPCHK(hipMemcpyAsync(AR + (int64_t)k * c->ld, ar0[k], (size_t)N * 8, hipMemcpyDeviceToDevice,
+                                          c->st));
+                } else {
+                    slot[n] = k;
+                    px[n++] = sys[k]->r;
+                }
+            }
+            if (extra_x) {
+                slot[n] = K;
+                px[n++] = extra_x;
+            }
+            if (n > 0) {
+                STCHK(ax_dev(c, n, px, nscratch));
+                for (int j = 0; j < n; ++j) {
+                    double* dst = slot[j] < K ? AR + (int64_t)slot[j] * c->ld : ex_out;
+                    HIPCHK(hipMemcpyAsync(dst, nscratch + (int64_t)j * c->ld, (size_t)N * 8, hipMemcpyDeviceToDevice,
+                                          c->st));
+                }
+            }
+        }
         vk::CgVecs cu{};
         cu.tau = tau;
         cu.gam2 = gam2;

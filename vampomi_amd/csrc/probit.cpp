@@ -129,8 +129,34 @@ vampomi_status probit_step(vampomi_ctx* c, VampRun& R) {
     R.metrics[5] = xc1[0] / std::sqrt(xc1[1] * xc1[2]);
 
     // ---------------- LMMSE (:297-385) ----------------
-    HIPCHK(vk::bernoulli(R.prm.seed, it, c->S, M, std::sqrt((double)Mt), R.bern, c->st));  // :297-298 (P2)
-    {
+    if (R.bern_it != it)  // (drawn at the end of iteration it-1 when its A.x pass carried A.bern)
+        HIPCHK(vk::bernoulli(R.prm.seed, it, c->S, M, std::sqrt((double)Mt), R.bern, c->st));  // :297-298 (P2)
+    R.bern_it = it;
+    // v = tau2*A^T p2 + gam2*r2 (:300-303).  Both CG solves start from zero, so
+    // r0 = v and the x2 solve's first A.x pass needs A v: with the one-pass
+    // operator ONE launch forms v (as d = tau*A^T q + gam2*p with q = p2/1,
+    // p = r2) and A v from one read of X; the Onsager solve's A r0 = A.bern
+    // came with the previous iteration's last A.x pass.  2 + max(k1, k2) reads
+    // of X per iteration instead of 3 + max(k1, k2)
+    const double* ar0[2] = {nullptr, nullptr};
+    bool merged = R.onepass && R.fuse && c->have_X;
+    if (merged) {
+        STCHK(op_prepare(c));
+        merged = c->op_ok;
+    }
+    if (merged) {
+        vk::OpArgs a{};
+        a.ar.p[0] = R.p2;  // ld-padded, zero pads
+        a.p.p[0] = R.r2;
+        a.d.p[0] = R.v;
+        a.diag = 1.0;
+        a.tau = R.tau2;
+        a.gam2 = R.gam2;
+        STCHK(op_dev(c, 1, a, nullptr));  // COLLECTIVE (the A v all-reduce)
+        R.passes_ref += 1;
+        ar0[0] = c->op_nvec + (int64_t)2 * vk::kMaxRhs * ld;  // A v, read by pcg_run before any other launch
+        if (R.abern_it == it) ar0[1] = R.nb3 + 3 * ld;
+    } else {
         const double* u[1] = {R.p2};
         double* o[1] = {R.tmpM};
         STCHK(atx_dev(c, 1, u, o, 0, 0.0, 0.0, nullptr));  // :300
@@ -156,7 +182,7 @@ vampomi_status probit_step(vampomi_ctx* c, VampRun& R) {
     HIPCHK(hipMemsetAsync(R.invQ, 0, Mb, c->st));
     if (R.fuse) {
         STCHK(pcg_run(c, {&sx, &so}, R.tau2, R.gam2, R.prm.CG_max_iter, R.prm.CG_err_tol, R.nsc, &R.passes_ref,
-                      nullptr, nullptr, nullptr, R.onepass));
+                      nullptr, nullptr, nullptr, R.onepass, merged ? ar0 : nullptr));
     } else {
         STCHK(pcg_run(c, {&sx}, R.tau2, R.gam2, R.prm.CG_max_iter, R.prm.CG_err_tol, R.nsc, &R.passes_ref, nullptr));
         STCHK(pcg_run(c, {&so}, R.tau2, R.gam2, R.prm.CG_max_iter, R.prm.CG_err_tol, R.nsc, &R.passes_ref, nullptr));
@@ -183,10 +209,17 @@ vampomi_status probit_step(vampomi_ctx* c, VampRun& R) {
         STCHK(denoise_into(c, R.mix, R.gam1, R.r1, R.x1n, R.x1, true, rho, R.x1d, fin, &R.sum_d));
         HIPCHK(vk::div_scalar(M, R.x1n, sqrtN, R.x1sn, c->st));
     }
-    // ---- A.x2 (:352), A.x2_hat_s (:403) [+ the next A.(x1/sqrtN)]: one pass ----
+    // ---- A.x2 (:352), A.x2_hat_s (:403) [+ the next A.(x1/sqrtN) and, with the
+    // merged launch, the next iteration's probe and its A.bern]: one pass ----
     {
-        const double* xs[3] = {R.x2, R.x2s, R.x1sn};
-        STCHK(ax_dev(c, next ? 3 : 2, xs, R.nb3));
+        const bool carry = next && merged;
+        if (carry) {  // bern (of this iteration) was last read by the a2 batch above
+            HIPCHK(vk::bernoulli(R.prm.seed, it + 1, c->S, M, std::sqrt((double)Mt), R.bern, c->st));
+            R.bern_it = it + 1;
+            R.abern_it = it + 1;
+        }
+        const double* xs[4] = {R.x2, R.x2s, R.x1sn, R.bern};
+        STCHK(ax_dev(c, carry ? 4 : next ? 3 : 2, xs, R.nb3));
         R.passes_ref += 2;
     }
     R.beta2 = (double)Mt / N * (1 - R.alpha2);                                            // :354

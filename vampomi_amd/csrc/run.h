@@ -26,6 +26,8 @@ struct VampRun {
     bool arec = false;   // batch_rhs >= 3: also A x2 by a CG recurrence, z1 in the first CG pass
     bool onepass = false;  // batch_rhs >= 4: each CG step reads X once (vk::atax)
     int z1n_slot = 2;    // nb3 slot of the prefetched z1
+    int bern_it = 0;     // probit: the iteration whose probe bern holds (drawn one iteration early)
+    int abern_it = 0;    // probit: the iteration whose A.bern is in nb3 slot 3
     std::string out_dir, out_name, p_params, p_metrics, p_prior;
     int it = 0;
     bool stopped = false;

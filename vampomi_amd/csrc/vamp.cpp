@@ -217,12 +217,12 @@ static vampomi_status vamp_alloc(vampomi_ctx* c, VampRun& R) {
         STCHK(dev_alloc(p, M));
     for (auto& p : R.cgw) STCHK(dev_alloc(&p, M));
     STCHK(dev_alloc(&R.z1buf, ld));
-    STCHK(dev_alloc(&R.nb3, 3 * ld));
+    STCHK(dev_alloc(&R.nb3, vk::kMaxRhs * ld));  // probit: slot 3 carries the next A.bern_vec
     STCHK(dev_alloc(&R.nsc, vk::kMaxRhs * ld));
     STCHK(dev_alloc(&R.ax2, ld));
     HIPCHK(hipMemsetAsync(R.ax2, 0, ld * 8, c->st));
     HIPCHK(hipMemsetAsync(R.z1buf, 0, ld * 8, c->st));
-    HIPCHK(hipMemsetAsync(R.nb3, 0, 3 * ld * 8, c->st));
+    HIPCHK(hipMemsetAsync(R.nb3, 0, vk::kMaxRhs * ld * 8, c->st));
     HIPCHK(hipMemsetAsync(R.nsc, 0, vk::kMaxRhs * ld * 8, c->st));
     return VAMPOMI_OK;
 }
