@@ -77,7 +77,7 @@ struct vampomi_ctx {
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     double* red_part2 = nullptr;
     unsigned* ticket2 = nullptr;
-    bool side_on = true;  // VAMPOMI_SIDE_STREAM=0 or vampomi_dev_set_variant(c, 4, 0): one stream
+    bool side_on = false;  // default: several ranks; VAMPOMI_SIDE_STREAM=0/1 or vampomi_dev_set_variant(c, 4, 0/1)
     bool team_reg = false;           // registered with its device's team gate (engine.cpp)
     hipEvent_t team_ev = nullptr;    // recorded on st when another context must order behind it
     ncclComm_t comm = nullptr;

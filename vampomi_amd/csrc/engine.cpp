@@ -824,7 +824,6 @@ extern "C" vampomi_status vampomi_open(const vampomi_shard_desc* d, vampomi_ctx*
     HIPCHK(hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking));
     HIPCHK(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
-    if (const char* sv = std::getenv("VAMPOMI_SIDE_STREAM")) c->side_on = std::atoi(sv) != 0;
     STCHK(dev_alloc(&c->scal, SL_TOTAL));
     HIPCHK(hipHostMalloc((void**)&c->h_scal, SL_TOTAL * sizeof(double), hipHostMallocMapped | hipHostMallocCoherent));
     HIPCHK(hipHostGetDevicePointer((void**)&c->d_hscal, c->h_scal, 0));
@@ -849,6 +848,12 @@ extern "C" vampomi_status vampomi_open(const vampomi_shard_desc* d, vampomi_ctx*
     // be exercised on a single GPU
     const char* force = std::getenv("VAMPOMI_FORCE_RCCL");
     c->use_comm = c->nranks > 1 || (force && std::atoi(force) != 0);
+    // the side stream overlaps the EM/denoiser with the reductions and their
+    // all-reduces: on where collectives exist (several ranks); one rank runs
+    // one stream, 0.5 % faster at C2 (profiles/r02j_side_ab_c2.txt: the
+    // cross-queue events cost more than the 5-17 us kernels they overlap)
+    c->side_on = c->use_comm;
+    if (const char* sv = std::getenv("VAMPOMI_SIDE_STREAM")) c->side_on = std::atoi(sv) != 0;
     const char* mode = std::getenv("VAMPOMI_COMM");
     if (c->use_comm && mode && std::strcmp(mode, "loopback") == 0) {
         if (!d->comm_id) return fail(VAMPOMI_ERR_ARG, "the loopback communicator needs a communicator id");
