@@ -454,6 +454,19 @@ def main():
         "setup_s": round(t_setup, 2),
         "cpu_baseline": None,
     }
+    if strong and n > 1:
+        # the problem does not fit one GPU: the 1-GPU point of the strong-scaling
+        # curve is the committed c3big line (same N and design, 300,000 markers
+        # resident on one MI355X) scaled to this problem's markers per iteration
+        try:
+            ref = json.load(open(os.path.join(ROOT, "profiles", "r02j_bench_c3big.json")))
+            one = ref["value"] * ref["config"]["Mt"] / Mt
+            line["one_gpu_equivalent"] = {
+                "value": round(one, 4), "unit": "iterations/s",
+                "source": "profiles/r02j_bench_c3big.json (N=100,000 x 300,000 on 1 GPU) x 300,000 / Mt",
+                "strong_scaling_efficiency": round(it_s / (n * one), 4)}
+        except Exception as e:
+            line["one_gpu_equivalent"] = {"error": repr(e)}
     if model == "bin_class":
         line["parity_note"] = ("probit: x1_hat/r1 parity bar is max(1e-10, 10x the oracle's own rank-count spread), "
                                "integers exact (DESIGN.md §3)")
