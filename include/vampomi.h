@@ -296,7 +296,8 @@ vampomi_status vampomi_reset_stats(vampomi_ctx* ctx);
  * (association pass) and -1 (operator: whole columns per workgroup while
  * K*N fits the LDS, else teams of workgroups; 0 forces the whole-column
  * kernel, T*10 + c the team kernel with team size T and configuration c,
- * vampomi_amd/csrc/atax_team.hip). */
+ * vampomi_amd/csrc/atax_team.hip).  which = 4: the side stream of the
+ * prefetched EM/denoiser, 0 off, 1 on (default: on with several ranks). */
 vampomi_status vampomi_dev_set_variant(vampomi_ctx* ctx, int which, int variant);
 /* average device time (HIP events) of `reps` back-to-back launches, K RHS */
 vampomi_status vampomi_dev_time_pass(vampomi_ctx* ctx, int which, int K, int reps, double* avg_ms);
