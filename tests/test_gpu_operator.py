@@ -24,7 +24,8 @@ pytestmark = pytest.mark.gpu
 va = pytest.importorskip("vampomi_amd")
 from oracle import pyoracle as O  # noqa: E402  (checker: the generator and marker statistics)
 
-SHAPES = [(1000, 3000, 0), (10000, 4000, 0), (50001, 1500, 1), (100000, 600, 1)]
+SHAPES = [(1000, 3000, 0), (10000, 4000, 0), (50001, 1500, 1), (100000, 600, 1),
+          (50001, 7, 0)]  # fewer markers than teams: empty teams
 CANDIDATES = [0] + [T * 10 + c for T in (1, 2, 4, 8, 16, 32) for c in range(10)]
 
 

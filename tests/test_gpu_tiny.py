@@ -28,7 +28,7 @@ def test_operators_tiny(N, Mt):
         assert relerr(d.ATx(u), O.atx(X, mave, msig, u)) < 1e-13
 
 
-@pytest.mark.parametrize("N,Mt", [(17, 1), (33, 3), (40, 2)])
+@pytest.mark.parametrize("N,Mt", [(17, 1), (33, 3), (40, 2), (12000, 3)])  # 12000: a team plan, 61 empty teams
 def test_vamp_tiny(N, Mt):
     X = O.generate_markers(4, 0, N, 0, Mt)
     beta = np.zeros(Mt)
