@@ -187,3 +187,14 @@ def test_c4_shape_properties():
         m = a.metrics
         assert np.all(m[:, 0:4].sum(axis=1) == N) and np.all(m[:, 6:10].sum(axis=1) == N)
         assert m[3, 10] > 0.75 and m[3, 11] > 0.3
+
+
+def test_probit_parity_team_operator():
+    """N > 9,216: the one-pass operator runs as teams (T = 4), including the
+    merged first launch of every iteration (v = tau2 A^T p2 + gam2 r2 and A v
+    from one read of X, A.bern carried by the previous iteration's last pass)."""
+    N, Mt = 12000, 1500
+    X, y, beta = _binary_problem(N, Mt)
+    ref, spread = oracle_with_spread(X, y, beta, Mt, max_iter=8, stop_criteria_thr=0.0, model="bin_class")
+    s = _gpu_probit(X, y, beta, Mt, max_iter=8, stop_criteria_thr=0.0)
+    _assert_probit_parity(s, ref, spread)
