@@ -83,9 +83,11 @@ def oracle_with_spread(X, y, beta, Mt, ranks=(2, 3, 4), **kw):
             num = np.linalg.norm(h - ref[f"{key}_hist"], axis=1)
             den = np.maximum(np.linalg.norm(ref[f"{key}_hist"], axis=1), 1e-300)
             sp[key] = np.maximum(sp[key], num / den)
-        for key in ("params", "metrics"):
+        for key in ("params", "metrics", "prior"):
+            if key not in ref:
+                continue
             a, b = res[0][key], ref[key]
             with np.errstate(invalid="ignore", divide="ignore"):
                 e = np.where(np.isnan(a) & np.isnan(b), 0.0, np.abs(a - b) / np.maximum(np.abs(b), 1e-300))
-            sp[key] = np.maximum(sp[key], e)
+            sp[key] = np.maximum(sp.get(key, np.zeros_like(e)), e)
     return ref, sp
