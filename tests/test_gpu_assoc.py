@@ -155,11 +155,30 @@ def test_cli_association_files(tmp_path):
     assert r.returncode == 1 and "cannot parse the iteration" in r.stdout
 
 
-def test_c5_shape_properties():
-    """BASELINE config 5 per-GPU sample dimension (N = 100,000) with a 16k-marker
-    shard: the device sums equal a float64 restatement on sampled markers and
-    the causal markers stand out."""
-    N, Mt = 100000, 16000
+def test_c5_samples_whole_vector_vs_oracle():
+    """configs[4]'s sample count, N = 100,000 methylation-like, at a reduced
+    Mt: the WHOLE p-value and sums vectors against the oracle's assoc_loo
+    (src/data.cpp:385-417, src/main_meth.cpp:245-264) with the bars above."""
+    N, Mt = 100000, 2000
+    X, y, beta = make_problem(N, Mt, seed=9, kind=1, lam=0.05, h2=0.5)
+    est = _estimate(beta, N)
+    po, sto = O.assoc_loo(X, y, est)
+    with va.Data(N, Mt) as d:
+        d.load_meth(X)
+        d.set_phen(y, standardize=False)
+        p, st = d.assoc_loo(est)
+    _check_pfun(p, st, N)
+    _check_loo(p, st, po, sto, _order_spread(X, y, est, po))
+    assert np.median(p[beta != 0]) < np.median(p[beta == 0])
+
+
+def test_c5_full_shard_properties():
+    """The whole per-GPU C5 shard (N = 100,000 x 62,500 methylation-like
+    markers, 50 GB; eight of them are configs[4]): the device sums equal a
+    float64 restatement on 16 markers spread over the shard (first, last,
+    power-of-two boundaries, random), the p-values equal the oracle's p-value
+    function of those sums, and the causal markers stand out."""
+    N, Mt = 100000, 62500
     with va.Data(N, Mt) as d:
         d.generate(9, va.GEN_METH)
         beta = d.simulate_phen(10, lam=0.05, h2=0.5)
@@ -168,12 +187,17 @@ def test_c5_shape_properties():
         p, st = d.assoc_loo(est)
         z1 = d.Ax(est * np.sqrt(N))
         ymod = y - z1
-        for j in (0, 1, 7777, Mt - 1):
+        rng = np.random.default_rng(5)
+        picks = sorted({0, 1, Mt - 2, Mt - 1, 8191, 8192, 32767, 32768, 61439, 61440,
+                        *rng.integers(0, Mt, 6).tolist()})
+        for j in picks:
             x = d.get_meth_data(j, 1)[0]
             ym = ymod + x / np.sqrt(N) * (est[j] * np.sqrt(N))
             ref = [x.sum(), x @ x, x @ ym, ym.sum(), ym @ ym]
             assert np.allclose(st[j], ref, rtol=1e-11), j
             q = O.reg1d_pval(*ref, N)
             assert abs(p[j] - q) <= 1e-8 * q
-        assert np.all((p >= 0) & (p <= 1))
+        _check_pfun(p[picks], st[picks], N)
+        assert np.all((p >= 0) & (p <= 1)) and np.all(np.isfinite(st))
+        assert np.all(st[:, 0] > 0) and np.all(st[:, 1] > 0)  # methylation values in (0, 1)
         assert np.median(p[beta != 0]) < 1e-3 < np.median(p[beta == 0])

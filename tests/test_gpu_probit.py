@@ -26,6 +26,7 @@ from oracle import pyoracle as O  # noqa: E402  (checker)
 
 
 def _binary_problem(N, Mt, seed=3, kind=0):
+    """make_problem's liability thresholded at 0 (raw 0/1 phenotype)."""
     X, y, beta = make_problem(N, Mt, seed=seed, kind=kind)
     return X, (y > 0).astype(np.float64), beta
 
@@ -192,6 +193,91 @@ def test_c4_shape_properties():
         m = a.metrics
         assert np.all(m[:, 0:4].sum(axis=1) == N) and np.all(m[:, 6:10].sum(axis=1) == N)
         assert m[3, 10] > 0.75 and m[3, 11] > 0.3
+
+
+def _team_plan(N):
+    import ctypes as C
+
+    T, S, TR, grid = C.c_int(), C.c_int(), C.c_int(), C.c_int()
+    ns = C.c_int64()
+    name = C.create_string_buffer(128)
+    assert va.load().vampomi_dev_op_plan(N, 1000, 256, -1, 2, C.byref(T), C.byref(S), C.byref(TR), C.byref(grid),
+                                         C.byref(ns), name, 128) == 0
+    return T.value
+
+
+def test_c4_samples_production_schedule_vs_oracle():
+    """configs[3]'s sample count, N = 50,000, on the production schedule
+    (batch_rhs 4: the team operator with T = 16 and the merged first launch of
+    every iteration) against the oracle at a reduced Mt, with the probit bar
+    (max(1e-10, 10 x the oracle's own rank-count spread)) and every integer
+    exact.  src/vamp_probit.cpp:19-467."""
+    N, Mt, its = 50000, 1800, 8
+    assert _team_plan(N) == 16
+    X, y, beta = _binary_problem(N, Mt, seed=5)
+    ref, spread = oracle_with_spread(X, y, beta, Mt, max_iter=its, stop_criteria_thr=0.0, model="bin_class")
+    with va.Data(N, Mt) as d:
+        d.load_meth(X)
+        d.set_phen(y, standardize=False)
+        v = va.Vamp(d, va.VampOptions(model="bin_class", max_iter=its, stop_criteria_thr=0.0), true_signal=beta)
+        x1 = v.infere(keep_hist=True)
+        s = v.summary()
+        s["x1_hist"], s["r1_hist"], s["x1_final"] = v.x1_hist[:its, :d.M].copy(), v.r1_hist[:its, :d.M].copy(), x1
+        st = d.stats()
+    assert va.VampOptions().batch_rhs == 4 and st.op.launches > 0, "the one-pass operator did not run"
+    _assert_probit_parity(s, ref, spread)
+
+
+C4_SHARD = dict(N=50000, Mt=50000, its=8, seed=20250711)
+
+
+def test_c4_full_shard_production_vs_sequential(monkeypatch):
+    """The whole per-GPU C4 shard (N = 50,000 x 50,000 markers, 20 GB) on the
+    production schedule against batch_rhs 1 (bitwise the reference's
+    sequential order, test_probit_batched_bitwise_equal_to_sequential): counts
+    exact, x1_hat / r1 / params within the probit bar, measured here on the
+    device itself as 10 x the change of the sequential run when the same
+    problem runs on 2 or 3 ranks (loopback), i.e. the reference's own
+    sensitivity to the all-reduce order."""
+    from test_gpu_sharded import run_ranks
+
+    c = C4_SHARD
+
+    def run(d, b):
+        d.generate(c["seed"], va.GEN_GAUSS)  # index-keyed: each rank generates its own columns
+        beta = d.simulate_phen_binary(c["seed"] + 1, lam=0.1, h2=0.8)
+        v = va.Vamp(d, va.VampOptions(model="bin_class", max_iter=c["its"], stop_criteria_thr=0.0, batch_rhs=b),
+                    true_signal=beta)
+        v.infere(keep_hist=True)
+        s = v.summary()
+        s["x1_hist"], s["r1_hist"] = v.x1_hist[:c["its"], :d.M].copy(), v.r1_hist[:c["its"], :d.M].copy()
+        return s
+
+    with va.Data(c["N"], c["Mt"]) as d:
+        prod, seq = run(d, 4), run(d, 1)
+    its = seq["iterations"]
+    spread = {"x1": np.zeros(its), "r1": np.zeros(its), "params": np.zeros_like(np.array(seq["params"]))}
+    for P in (2, 3):
+        parts = run_ranks(monkeypatch, P, c["N"], c["Mt"], lambda r, d: run(d, 1), timeout=300)
+        for key in ("x1", "r1"):
+            h = np.concatenate([p[f"{key}_hist"] for p in parts], axis=1)
+            spread[key] = np.maximum(spread[key], [relerr(h[k], seq[f"{key}_hist"][k]) for k in range(its)])
+        a, b = np.array(parts[0]["params"]), np.array(seq["params"])
+        spread["params"] = np.maximum(spread["params"], np.abs(a - b) / np.maximum(np.abs(b), 1e-300))
+    for key in ("iterations", "cg_iters", "ons_iters", "L"):
+        assert prod[key] == seq[key], key
+    for k in range(its):
+        for key in ("x1", "r1"):
+            e = relerr(prod[f"{key}_hist"][k], seq[f"{key}_hist"][k])
+            assert e <= max(1e-10, 10 * spread[key][k]), f"{key} it {k + 1}: {e:.2e} vs spread {spread[key][k]:.2e}"
+    p, ps = np.array(prod["params"]), np.array(seq["params"])
+    assert np.all(np.abs(p - ps) <= np.maximum(1e-9, 10 * spread["params"]) * np.abs(ps))
+    m, ms = np.array(prod["metrics"]), np.array(seq["metrics"])
+    for o in (0, 6):
+        assert np.all(m[:, o:o + 4].sum(axis=1) == c["N"])
+        assert np.array_equal(m[:, o:o + 4], ms[:, o:o + 4]), "confusion counts"
+    assert m[-1, 10] > 0.75
+    assert prod["a_passes_exec"] < seq["a_passes_exec"]
 
 
 def test_probit_parity_team_operator():

@@ -113,14 +113,18 @@ def test_c3_full_shard_two_ranks(monkeypatch, c3_shard_runs):
         assert relerr(np.concatenate([p["r1_hist"][k] for p in parts]), one["r1_hist"][k]) <= 1e-12, k
 
 
-def test_c2_whole_production_schedule_vs_oracle():
+@pytest.fixture(scope="module")
+def c2_problem():
+    return make_problem(10000, 50000, seed=11)
+
+
+def test_c2_whole_production_schedule_vs_oracle(c2_problem):
     N, Mt, its = 10000, 50000, 6
-    X, y, beta = make_problem(N, Mt, seed=11)
+    X, y, beta = c2_problem
     kw = dict(max_iter=its, stop_criteria_thr=0.0)
     ref = O.vamp_infere(X, y, Mt, true_signal=beta, **kw)
     with va.Data(N, Mt) as d:
         d.load_meth(X)
-        del X
         s = _run(d, y, beta, **kw)  # batch_rhs default: the one-pass CG operator at this shape
         st = d.stats()
     assert va.VampOptions().batch_rhs == 4 and st.op.launches > 0, "the one-pass operator did not run"
@@ -128,6 +132,41 @@ def test_c2_whole_production_schedule_vs_oracle():
     for k in range(its):
         assert relerr(s["x1_hist"][k], ref["x1_hist"][k]) <= 1e-10, k
         assert relerr(s["r1_hist"][k], ref["r1_hist"][k]) <= 1e-10, k
+
+
+def test_c2_bench_window_vs_oracle_fixture(c2_problem):
+    """Iterations 1-25 of C2 on the production schedule (the driver's bench
+    times 6-25) against the oracle's run committed in
+    tests/golden/oracle_c2_window.npz (made by make_c2_window.py in the build
+    container): every iteration's CG / Onsager / mixture counts exact, params
+    within 1e-9, the norms and four +-1 projections of x1_hat / r1 within the
+    1e-10 norm bar (a projection moves by at most sqrt(M) * ||delta||), and
+    the whole x1_hat / r1 vectors at iterations 6, 15 and 25 within 1e-10."""
+    import sys
+
+    sys.path.insert(0, G)
+    from make_c2_window import probes
+
+    z = np.load(os.path.join(G, "oracle_c2_window.npz"))
+    N, Mt, its = int(z["N"]), int(z["Mt"]), int(z["its"])
+    X, y, beta = c2_problem
+    assert X.shape == (Mt, N)
+    with va.Data(N, Mt) as d:
+        d.load_meth(X)
+        s = _run(d, y, beta, max_iter=its, stop_criteria_thr=0.0)
+    assert s["iterations"] == its
+    assert s["cg_iters"] == z["cg_iters"].tolist() and s["ons_iters"] == z["ons_iters"].tolist()
+    assert s["L"] == z["L"].tolist()
+    assert np.allclose(np.array(s["params"]), z["params"], rtol=1e-9, atol=0)
+    P = probes(Mt)
+    for key in ("x1", "r1"):
+        h = s[f"{key}_hist"]
+        nrm = z[f"{key}_norm"]
+        assert np.all(np.abs(np.linalg.norm(h, axis=1) - nrm) <= 1e-10 * nrm), key
+        bound = 1e-10 * np.sqrt(Mt) * nrm[:, None]
+        assert np.all(np.abs(h @ P.T - z[f"{key}_proj"]) <= bound), key
+        for q, k in enumerate(z["keep_its"]):
+            assert relerr(h[k - 1], z[key][q]) <= 1e-10, (key, k)
 
 
 def test_cli_on_reference_written_files(tmp_path):
