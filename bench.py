@@ -62,9 +62,12 @@ def parse_args(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=45.0, help="seconds of host time for the CPU baseline")
     ap.add_argument("--no-timing", action="store_true", help="skip the HIP-event kernel timing")
-    ap.add_argument("--timing-period", type=int, default=4,
+    ap.add_argument("--timing-period", type=int, default=1,
                     help="time one A/A^T launch in this many of each (kernel, K) with HIP events")
     ap.add_argument("--batch-rhs", type=int, default=4)
+    ap.add_argument("--write", nargs="?", const=os.environ.get("TMPDIR", "/tmp"), default=None, metavar="DIR",
+                    help="also time the same window with the per-iteration output files on (the main_meth.exe "
+                         "drop-in rate: _it_K.bin, _r1_it_K.bin and CSV rows into a fresh directory under DIR)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher / rendezvous / max-over-ranks path only: no GPU work (CPU tests)")
     return ap.parse_args(argv)
@@ -203,6 +206,69 @@ def cpu_reference_ops(w: dict, seed: int, threads: int, k_cg: float):
             "sample": f"Ax and ATx (mean of 2 calls each) of the reference's src/data.cpp (oracle/_ref) on a generated "
                       f"{w['N']} x {w['Mt']} matrix, {r['threads']} OpenMP threads; iteration = (5 + k) Ax + (3 + k) "
                       f"ATx, k = {k_cg:.2f} (the GPU window's mean CG + Onsager steps)"}
+
+
+def write_rate(args, d, R, opts, beta, barrier, el_nowrite: float) -> dict:
+    """The same W + K iterations again with the reference's per-iteration
+    output on (src/vamp.cpp:235-249 _it_K.bin / _r1_it_K.bin, :388-393 CSV
+    rows) into a fresh directory under args.write: what a main_meth.exe user
+    gets per iteration.  Timing off, so both windows time the same work."""
+    import dataclasses
+    import shutil
+    import tempfile
+
+    import vampomi_amd as va
+
+    out = tempfile.mkdtemp(prefix="vampomi_bench_", dir=args.write) if R.rank == 0 else None
+    if R.world > 1:
+        obj = [out]
+        R.dist.broadcast_object_list(obj, src=0)
+        out = obj[0]
+    try:
+        d.set_timing(False)
+        v = va.Vamp(d, dataclasses.replace(opts, out_dir=out, out_name="bench"), true_signal=beta)
+        v.begin()
+        for _ in range(args.warmup):
+            v.step()
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            v.step()
+        barrier()
+        el = R.max(time.perf_counter() - t0)
+        v.end()
+        files = sorted(os.listdir(out))
+        nbytes = sum(os.path.getsize(os.path.join(out, f)) for f in files)
+    finally:
+        R.barrier()
+        if R.rank == 0:
+            shutil.rmtree(out, ignore_errors=True)
+    return {"elapsed_s": el, "ms_per_step": round(el / args.steps * 1e3, 3),
+            "rate_vs_no_write": round(el_nowrite / el, 4), "files": len(files), "bytes_written": int(nbytes),
+            "out_dir": args.write,
+            "what": "the same iterations with _it_K.bin, _r1_it_K.bin (every iteration, every rank) and the CSV rows "
+                    "written (async writer thread, writer.h); HIP-event timing off in this window"}
+
+
+def per_rank_times(R, st, el: float) -> list:
+    """Per-rank device time of the A-kernels / the one-pass operator and the
+    wall time of the window, gathered on rank 0 (a multi-GPU run's straggler
+    shows up here)."""
+    mine = {"rank": R.rank, "wall_s": round(el, 4),
+            "op_ms_avg": round(st.op.ms_timed / st.op.timed, 4) if st.op.timed else None,
+            "op_launches": int(st.op.launches),
+            "a_kernels_ms": round(st.ax.ms_total + st.atx.ms_total + st.op.ms_total, 3),
+            # RCCL all-reduces: HIP events on the stream around each (the wait
+            # for the slowest rank included), count and bytes
+            "allreduce_launches": int(st.coll.launches),
+            "allreduce_ms_total": round(st.coll.ms_total, 3),
+            "allreduce_us_avg": round(st.coll.ms_timed / st.coll.timed * 1e3, 2) if st.coll.timed else None,
+            "allreduce_bytes": int(st.coll.bytes_total)}
+    if R.world == 1:
+        return [mine]
+    out = [None] * R.world
+    R.dist.all_gather_object(out, mine)
+    return out
 
 
 def cpu_baseline_assoc(d, w: dict, est, seed: int) -> dict:
@@ -411,9 +477,11 @@ def main():
     barrier()
     el = R.max(time.perf_counter() - t0)
     st = d.stats()
+    rank_times = per_rank_times(R, st, el)
     ref1, _ = v.a_passes
     summ = v.summary()
     v.end()
+    with_writes = write_rate(args, d, R, opts, beta, barrier, el) if args.write else None
 
     it_s = args.steps / el
     strong = w.get("scaling") == "strong"
@@ -449,25 +517,41 @@ def main():
         "hbm_gbs_all_A_kernels": round(all_bytes / (all_ms * 1e-3) / 1e9, 1) if all_ms > 0 else None,
         "passes_exec_per_step": round(st.a_passes_exec / args.steps, 2),  # stats reset at the timed region
         "passes_ref_per_step": round(ref_passes, 2),
-        # device time of the A-kernels (sampled average x exact launch count)
-        # over the wall time; sampling noise can push the ratio past 1 when
-        # they fill the step, so it is capped there
-        "a_kernel_frac_of_step": round(min(1.0, all_ms * 1e-3 / el), 3) if el > 0 else None,
+        # device time of the A-kernels over the wall time (with --timing-period 1,
+        # the default, every launch is timed: a measured sum, not an extrapolation)
+        "a_kernel_frac_of_step": round(all_ms * 1e-3 / el, 4) if el > 0 else None,
+        "a_kernel_timing": {"timed_launches": int(st.ax.timed + st.atx.timed + st.op.timed),
+                            "launches": int(st.ax.launches + st.atx.launches + st.op.launches),
+                            "period": args.timing_period},
+        "per_rank": rank_times,
         "cg_iters": summ["cg_iters"][args.warmup:], "ons_iters": summ["ons_iters"][args.warmup:],
         "setup_s": round(t_setup, 2),
         "cpu_baseline": None,
     }
+    line["config"]["output_files"] = ("not written in the timed window (BASELINE.md: the metric excludes output-file "
+                                      "writes); see with_writes" if args.write else
+                                      "not written in the timed window (BASELINE.md: the metric excludes output-file "
+                                      "writes; bench.py --write times them)")
+    if with_writes:
+        ws = with_writes.pop("elapsed_s")
+        with_writes["value"] = round(args.steps / ws if strong else n * args.steps / ws, 4)
+        line["with_writes"] = with_writes
     if strong and n > 1:
-        # the problem does not fit one GPU: the 1-GPU point of the strong-scaling
-        # curve is the committed c3big line (same N and design, 300,000 markers
-        # resident on one MI355X) scaled to this problem's markers per iteration
+        # the problem does not fit one GPU.  ESTIMATE of its 1-GPU rate from the
+        # committed c3big line (same N and design, 300,000 markers resident on
+        # one MI355X, another run and build): its time per executed pass per
+        # marker, times this run's markers and executed passes per iteration
+        src = "profiles/r02j_bench_c3big.json"
         try:
-            ref = json.load(open(os.path.join(ROOT, "profiles", "r02j_bench_c3big.json")))
-            one = ref["value"] * ref["config"]["Mt"] / Mt
+            ref = json.load(open(os.path.join(ROOT, src)))
+            per_pass_marker = ref["ms_per_step"] / (ref["passes_exec_per_step"] * ref["config"]["Mt"])
+            one = 1e3 / (per_pass_marker * Mt * (st.a_passes_exec / args.steps))
             line["one_gpu_equivalent"] = {
-                "value": round(one, 4), "unit": "iterations/s",
-                "source": "profiles/r02j_bench_c3big.json (N=100,000 x 300,000 on 1 GPU) x 300,000 / Mt",
-                "strong_scaling_efficiency": round(it_s / (n * one), 4)}
+                "estimate": True, "value": round(one, 4), "unit": "iterations/s",
+                "source": f"{src} (N=100,000 x 300,000 on 1 GPU, {ref['ms_per_step']} ms per iteration at "
+                          f"{ref['passes_exec_per_step']} passes): ms per pass per marker x Mt x this run's "
+                          "passes per iteration; not a measurement of this problem on one GPU (it does not fit)",
+                "strong_scaling_efficiency_estimate": round(it_s / (n * one), 4)}
         except Exception as e:
             line["one_gpu_equivalent"] = {"error": repr(e)}
     if model == "bin_class":

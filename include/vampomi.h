@@ -278,6 +278,9 @@ typedef struct {
     vampomi_kernel_stat loo;      /* association-test pass (vampomi_assoc_loo) */
     vampomi_kernel_stat op;       /* one-pass CG operator (A^T q and A d, batch_rhs 4) */
     vampomi_kernel_stat op_k[4];
+    vampomi_kernel_stat coll;     /* RCCL all-reduces (several ranks): launches, bytes; with timing
+                                     on, HIP events on the stream around each (its time on the
+                                     stream, waits for the slowest rank included) */
 } vampomi_stats;
 
 /* HIP-event timing of the A/A^T kernels: on = 0 off, 1 every launch, n > 1 one

@@ -46,9 +46,35 @@ def _order_spread(X, y, est, po):
     return np.abs(pp - po) / np.maximum(po, 1e-300)
 
 
-def _check_loo(p, st, po, sto, spread):
+def _sums_extended(X, y, est, chunk=64):
+    """The five per-marker sums of the float64 terms (raw x, y_mark = y_mod +
+    x/sqrt(N)*x1_hat, their float64 products) accumulated in x87 extended
+    precision: the reference value of each sum to ~1e-18, against which both
+    the device's tree sums and the oracle's sequential sums are rounding."""
+    N = X.shape[1]
+    mave, msig = O.marker_stats(X)
+    x1 = est * np.sqrt(N)
+    ymod = y - O.ax(X, mave, msig, x1)
+    out = np.zeros((X.shape[0], 5))
+    L = np.longdouble
+    for a in range(0, X.shape[0], chunk):
+        Xc = X[a:a + chunk]
+        ym = ymod[None, :] + Xc / np.sqrt(N) * x1[a:a + chunk, None]
+        out[a:a + chunk] = np.stack([Xc.sum(1, dtype=L), (Xc * Xc).sum(1, dtype=L), (Xc * ym).sum(1, dtype=L),
+                                     ym.sum(1, dtype=L), (ym * ym).sum(1, dtype=L)], axis=1)
+    return out
+
+
+def _check_loo(p, st, po, sto, spread, exact=None):
     for q in range(5):
-        assert relerr(st[:, q], sto[:, q]) < 1e-13, q
+        if exact is None:
+            assert relerr(st[:, q], sto[:, q]) < 1e-13, q
+        else:
+            # at large N the oracle's SEQUENTIAL sums carry ~sqrt(N)*eps of their
+            # own: the device is held to 1e-13 of the extended-precision sums,
+            # and to the oracle within twice the oracle's own rounding
+            assert relerr(st[:, q], exact[:, q]) < 1e-13, q
+            assert relerr(st[:, q], sto[:, q]) < max(1e-13, 2 * relerr(sto[:, q], exact[:, q])), q
     tol = np.maximum(1e-10, 10 * spread)
     ok = np.abs(p - po) <= tol * po + 1e-300
     assert ok.all(), (p[~ok][:5], po[~ok][:5], spread[~ok][:5])
@@ -168,7 +194,7 @@ def test_c5_samples_whole_vector_vs_oracle():
         d.set_phen(y, standardize=False)
         p, st = d.assoc_loo(est)
     _check_pfun(p, st, N)
-    _check_loo(p, st, po, sto, _order_spread(X, y, est, po))
+    _check_loo(p, st, po, sto, _order_spread(X, y, est, po), _sums_extended(X, y, est))
     assert np.median(p[beta != 0]) < np.median(p[beta == 0])
 
 

@@ -145,6 +145,31 @@ def test_sharded_association_and_test_mode(monkeypatch):
     assert np.allclose(np.concatenate([r[3] for r in res]), O.assoc_se(est, 2.0, N), rtol=1e-14, atol=1e-16)
 
 
+def test_pcg_warm_start_on_some_ranks_only(monkeypatch):
+    """vampomi_pcg with mu0 on rank 0 and NULL on rank 1: the zero-vector test
+    is collective (both ranks run the warm-start pass), rank 1 starts from a
+    zero slice; equals the one-rank solve from [mu0_0, 0]."""
+    N, Mt = 700, 1301
+    X, _, _ = make_problem(N, Mt, seed=9)
+    rng = np.random.default_rng(4)
+    v = rng.normal(size=Mt)
+    mu0 = rng.normal(size=Mt) * 0.1
+    M0, S1, _ = O.divide_work(Mt, 2, 0)
+    mu0_full = np.concatenate([mu0[:M0], np.zeros(Mt - M0)])
+    tau, gam2 = 1.7, 0.4
+    with va.Data(N, Mt) as d:
+        d.load_meth(X)
+        one, it1 = d.pcg(v, tau, gam2, mu0=mu0_full, tol=1e-9, max_iter=200)
+
+    def fn(r, d):
+        d.load_meth(X[d.S:d.S + d.M])
+        return d.pcg(v[d.S:d.S + d.M], tau, gam2, mu0=mu0[:M0] if r == 0 else None, tol=1e-9, max_iter=200)
+
+    parts = run_ranks(monkeypatch, 2, N, Mt, fn)
+    assert [p[1] for p in parts] == [it1, it1]
+    assert relerr(np.concatenate([p[0] for p in parts]), one) < 1e-12
+
+
 def _run_ranks_collect(monkeypatch, P, N, Mt, fn, timeout=60):
     """Like run_ranks, but returns each rank's exception (or None) instead of asserting."""
     monkeypatch.setenv("VAMPOMI_COMM", "loopback")

@@ -87,7 +87,7 @@ class KernelStat(C.Structure):
 class Stats(C.Structure):
     _fields_ = [("ax", KernelStat), ("atx", KernelStat), ("ax_k", KernelStat * 4), ("atx_k", KernelStat * 4),
                 ("a_passes_exec", C.c_int64), ("host_syncs", C.c_int64), ("loo", KernelStat),
-                ("op", KernelStat), ("op_k", KernelStat * 4)]
+                ("op", KernelStat), ("op_k", KernelStat * 4), ("coll", KernelStat)]
 
 
 # exported symbol -> (restype, argtypes); also the list the ABI test checks

@@ -662,9 +662,11 @@ bool team_plan(int64_t N, int64_t M, int cus, int T, int cfg, OpPlan* out) {
     return true;
 }
 
+// occ != null: no launch, *occ = the workgroups of this instantiation one CU
+// holds at once (hipOccupancyMaxActiveBlocksPerMultiprocessor)
 template <int K, int S, int C>
 static void launch_tm(const Shard& s, const OpPlan& pl, const OpArgs& a, hipStream_t st, const Timing& tm,
-                      const int* gate) {
+                      const int* gate, int* occ) {
     constexpr TmCfg c = kTmCfg[C];
     constexpr int CW = c.comm ? 7 : 8;
     auto kern = atax_team_kernel<K, S, c.F, c.L, c.P, c.comm, c.E, (bool)TM_FMA>;
@@ -675,15 +677,19 @@ static void launch_tm(const Shard& s, const OpPlan& pl, const OpArgs& a, hipStre
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                   160 * 1024);
     });
+    if (occ) {
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, kern, kTmThreads, lds) != hipSuccess) *occ = 0;
+        return;
+    }
     hipExtLaunchKernelGGL(kern, dim3(pl.grid), dim3(kTmThreads), lds, st, tm.start, tm.stop, 0, s.X, s.ld, s.N, s.M,
                           s.mave, s.msig, a, pl.T, pl.TR, c.ilv ? 1 : 0, gate);
 }
 
 template <int K, int C, int S>
 static bool launch_tm_if(const Shard& s, const OpPlan& pl, const OpArgs& a, hipStream_t st, const Timing& tm,
-                         const int* gate) {
+                         const int* gate, int* occ) {
     if constexpr (S <= kTmCfg[C].maxS) {
-        launch_tm<K, S, C>(s, pl, a, st, tm, gate);
+        launch_tm<K, S, C>(s, pl, a, st, tm, gate, occ);
         return true;
     }
     return false;
@@ -691,36 +697,36 @@ static bool launch_tm_if(const Shard& s, const OpPlan& pl, const OpArgs& a, hipS
 
 template <int K, int C>
 static bool launch_tm_s(int S, const Shard& s, const OpPlan& pl, const OpArgs& a, hipStream_t st,
-                        const Timing& tm, const int* gate) {
+                        const Timing& tm, const int* gate, int* occ) {
     switch (S) {
-        case 1: return launch_tm_if<K, C, 1>(s, pl, a, st, tm, gate);
-        case 2: return launch_tm_if<K, C, 2>(s, pl, a, st, tm, gate);
-        case 3: return launch_tm_if<K, C, 3>(s, pl, a, st, tm, gate);
-        case 4: return launch_tm_if<K, C, 4>(s, pl, a, st, tm, gate);
-        case 5: return launch_tm_if<K, C, 5>(s, pl, a, st, tm, gate);
-        case 6: return launch_tm_if<K, C, 6>(s, pl, a, st, tm, gate);
-        case 7: return launch_tm_if<K, C, 7>(s, pl, a, st, tm, gate);
-        case 8: return launch_tm_if<K, C, 8>(s, pl, a, st, tm, gate);
-        case 9: return launch_tm_if<K, C, 9>(s, pl, a, st, tm, gate);
-        case 10: return launch_tm_if<K, C, 10>(s, pl, a, st, tm, gate);
+        case 1: return launch_tm_if<K, C, 1>(s, pl, a, st, tm, gate, occ);
+        case 2: return launch_tm_if<K, C, 2>(s, pl, a, st, tm, gate, occ);
+        case 3: return launch_tm_if<K, C, 3>(s, pl, a, st, tm, gate, occ);
+        case 4: return launch_tm_if<K, C, 4>(s, pl, a, st, tm, gate, occ);
+        case 5: return launch_tm_if<K, C, 5>(s, pl, a, st, tm, gate, occ);
+        case 6: return launch_tm_if<K, C, 6>(s, pl, a, st, tm, gate, occ);
+        case 7: return launch_tm_if<K, C, 7>(s, pl, a, st, tm, gate, occ);
+        case 8: return launch_tm_if<K, C, 8>(s, pl, a, st, tm, gate, occ);
+        case 9: return launch_tm_if<K, C, 9>(s, pl, a, st, tm, gate, occ);
+        case 10: return launch_tm_if<K, C, 10>(s, pl, a, st, tm, gate, occ);
         default: return false;
     }
 }
 
 template <int K>
 static bool launch_tm_c(const Shard& s, const OpPlan& pl, const OpArgs& a, hipStream_t st, const Timing& tm,
-                        const int* gate) {
+                        const int* gate, int* occ = nullptr) {
     switch (pl.cfg) {
-        case 0: return launch_tm_s<K, 0>(pl.S, s, pl, a, st, tm, gate);
-        case 1: return launch_tm_s<K, 1>(pl.S, s, pl, a, st, tm, gate);
-        case 2: return launch_tm_s<K, 2>(pl.S, s, pl, a, st, tm, gate);
-        case 3: return launch_tm_s<K, 3>(pl.S, s, pl, a, st, tm, gate);
-        case 4: return launch_tm_s<K, 4>(pl.S, s, pl, a, st, tm, gate);
-        case 5: return launch_tm_s<K, 5>(pl.S, s, pl, a, st, tm, gate);
-        case 6: return launch_tm_s<K, 6>(pl.S, s, pl, a, st, tm, gate);
-        case 7: return launch_tm_s<K, 7>(pl.S, s, pl, a, st, tm, gate);
-        case 8: return launch_tm_s<K, 8>(pl.S, s, pl, a, st, tm, gate);
-        case 9: return launch_tm_s<K, 9>(pl.S, s, pl, a, st, tm, gate);
+        case 0: return launch_tm_s<K, 0>(pl.S, s, pl, a, st, tm, gate, occ);
+        case 1: return launch_tm_s<K, 1>(pl.S, s, pl, a, st, tm, gate, occ);
+        case 2: return launch_tm_s<K, 2>(pl.S, s, pl, a, st, tm, gate, occ);
+        case 3: return launch_tm_s<K, 3>(pl.S, s, pl, a, st, tm, gate, occ);
+        case 4: return launch_tm_s<K, 4>(pl.S, s, pl, a, st, tm, gate, occ);
+        case 5: return launch_tm_s<K, 5>(pl.S, s, pl, a, st, tm, gate, occ);
+        case 6: return launch_tm_s<K, 6>(pl.S, s, pl, a, st, tm, gate, occ);
+        case 7: return launch_tm_s<K, 7>(pl.S, s, pl, a, st, tm, gate, occ);
+        case 8: return launch_tm_s<K, 8>(pl.S, s, pl, a, st, tm, gate, occ);
+        case 9: return launch_tm_s<K, 9>(pl.S, s, pl, a, st, tm, gate, occ);
         default: return false;
     }
 }
@@ -738,6 +744,19 @@ hipError_t atax_team(const Shard& s, const OpPlan& pl, int K, const OpArgs& a, h
     }
     if (!ok) return hipErrorInvalidValue;
     return hipGetLastError();
+}
+
+int team_occupancy(const OpPlan& pl, int K) {
+    int occ = 0;
+    const Shard s{nullptr, 0, (int64_t)pl.TR * pl.T, 1, nullptr, nullptr};  // the LDS size needs TR and N only
+    const OpArgs a{};
+    bool ok = false;
+    switch (K) {
+        case 1: ok = launch_tm_c<1>(s, pl, a, nullptr, Timing{}, nullptr, &occ); break;
+        case 2: ok = launch_tm_c<2>(s, pl, a, nullptr, Timing{}, nullptr, &occ); break;
+        default: break;
+    }
+    return ok ? occ : 0;
 }
 
 std::string team_kernel_name(int K, const OpPlan& pl) {

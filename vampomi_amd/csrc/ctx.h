@@ -50,7 +50,7 @@ struct LoopbackComm;  // engine.cpp: test-only in-process communicator
 
 struct TimedLaunch {
     hipEvent_t a, b;
-    int cls;  // 0 ax, 1 atx, 2 loo, 3 one-pass operator
+    int cls;  // 0 ax, 1 atx, 2 loo, 3 one-pass operator, 4 all-reduce
     int K;
     double bytes, flops;
 };
@@ -77,6 +77,7 @@ struct vampomi_ctx {
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     double* red_part2 = nullptr;
     unsigned* ticket2 = nullptr;
+    bool side_open = false;  // the side stream has work st has not joined (DotBatch fork .. flush)
     bool side_on = false;  // default: several ranks; VAMPOMI_SIDE_STREAM=0/1 or vampomi_dev_set_variant(c, 4, 0/1)
     bool team_reg = false;           // registered with its device's team gate (engine.cpp)
     hipEvent_t team_ev = nullptr;    // recorded on st when another context must order behind it
@@ -125,7 +126,7 @@ struct vampomi_ctx {
 
     bool timing = false;
     int tperiod = 1;            // time 1 in tperiod launches of each (class, K)
-    int64_t tcount[4][vk::kMaxRhs] = {};
+    int64_t tcount[5][vk::kMaxRhs] = {};
     std::vector<TimedLaunch> pending;
     std::vector<hipEvent_t> ev_pool;
     vampomi_stats stats{};
@@ -143,6 +144,10 @@ vampomi_status host_sync(vampomi_ctx* c);
 // spins until the context's host flag reaches seq (stores from the stream)
 // (word 1: the side stream's sequence, stored by its one-rank reductions)
 vampomi_status wait_flag(vampomi_ctx* c, unsigned long long seq, int word = 0);
+// hipStreamSynchronize, except with an RCCL communicator: polls the stream and
+// the communicator, and aborts / fails on a broken job or after
+// VAMPOMI_COLL_TIMEOUT_S (engine.cpp) instead of blocking forever
+vampomi_status sync_stream(vampomi_ctx* c, hipStream_t st);
 // SUM all-reduce of n doubles over the ranks (nothing on one rank). COLLECTIVE:
 // every rank must make the same calls in the same order; site/line identify
 // the call for the divergence checks (loopback always, RCCL with

@@ -83,7 +83,8 @@ static double pass_bytes(const vampomi_ctx* c, int K) {
 static double pass_flops(const vampomi_ctx* c, int K) { return (double)c->N * (double)c->M * (1.0 + 2.0 * K); }
 
 static vampomi_kernel_stat* stat_of(vampomi_ctx* c, int cls) {
-    return cls == 0 ? &c->stats.ax : cls == 1 ? &c->stats.atx : cls == 3 ? &c->stats.op : &c->stats.loo;
+    return cls == 0 ? &c->stats.ax : cls == 1 ? &c->stats.atx : cls == 3 ? &c->stats.op : cls == 4 ? &c->stats.coll
+                                                                                                : &c->stats.loo;
 }
 static vampomi_kernel_stat* stat_k_of(vampomi_ctx* c, int cls, int K) {
     return cls == 0 ? &c->stats.ax_k[K - 1] : cls == 1 ? &c->stats.atx_k[K - 1] : cls == 3 ? &c->stats.op_k[K - 1]
@@ -149,6 +150,7 @@ void drop_launches(vampomi_ctx* c, size_t pending_mark, const vampomi_stats& bef
     undo(c->stats.atx, before.atx);
     undo(c->stats.op, before.op);
     undo(c->stats.loo, before.loo);
+    undo(c->stats.coll, before.coll);
     for (int k = 0; k < 4; ++k) {
         undo(c->stats.ax_k[k], before.ax_k[k]);
         undo(c->stats.atx_k[k], before.atx_k[k]);
@@ -167,6 +169,41 @@ void drop_launches(vampomi_ctx* c, size_t pending_mark, const vampomi_stats& bef
 // (a 1-thread kernel stores the flag); a one-rank DotBatch waits for its last
 // reduction kernel, whose last block stores the flag itself.  Faults are
 // still reported: the spin polls hipStreamQuery, and gives up after 10 min.
+//
+// With an RCCL communicator the waits also watch the job: a peer that died or
+// a communicator RCCL reports broken (ncclCommGetAsyncError) or a wait longer
+// than VAMPOMI_COLL_TIMEOUT_S (default 600 s; the queued all-reduce waits for
+// a peer that never comes) aborts this rank's communicator (ncclCommAbort)
+// and fails, instead of blocking forever in a collective.
+static double coll_timeout_s() {
+    static const double t = [] {
+        const char* e = std::getenv("VAMPOMI_COLL_TIMEOUT_S");
+        const double v = e ? std::atof(e) : 0.0;
+        return v > 0 ? v : 600.0;
+    }();
+    return t;
+}
+
+// nullptr while the job is healthy, else why it is not
+static const char* job_broken(vampomi_ctx* c, std::chrono::steady_clock::time_point t0) {
+    if (c->comm && !c->loopback) {
+        ncclResult_t r = ncclSuccess;
+        if (ncclCommGetAsyncError(c->comm, &r) == ncclSuccess && r != ncclSuccess && r != ncclInProgress)
+            return "RCCL communicator error";
+    }
+    const double lim = c->use_comm ? coll_timeout_s() : 600.0;
+    if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > lim)
+        return c->use_comm ? "no completion within VAMPOMI_COLL_TIMEOUT_S (a peer rank stopped?)"
+                           : "device did not signal completion within 10 minutes";
+    return nullptr;
+}
+
+static vampomi_status job_failed(vampomi_ctx* c, const char* why) {
+    const std::string msg = std::string(why) + " (rank " + std::to_string(c->rank) + ")";
+    comm_abort(c, msg);  // ncclCommAbort: this rank's queued collectives are released
+    return fail(c->use_comm ? VAMPOMI_ERR_RCCL : VAMPOMI_ERR_HIP, msg);
+}
+
 vampomi_status wait_flag(vampomi_ctx* c, unsigned long long seq, int word) {
     const auto t0 = std::chrono::steady_clock::now();
     hipStream_t st = word == 1 ? c->st2 : c->st;  // word 1: the side stream's sequence
@@ -180,9 +217,24 @@ vampomi_status wait_flag(vampomi_ctx* c, unsigned long long seq, int word) {
                 HIPCHK(hipStreamSynchronize(st));
                 return VAMPOMI_OK;
             }
-            if (std::chrono::steady_clock::now() - t0 > std::chrono::minutes(10))
-                return fail(VAMPOMI_ERR_HIP, "device did not signal completion within 10 minutes");
+            if (const char* why = job_broken(c, t0)) return job_failed(c, why);
         }
+        __builtin_ia32_pause();
+    }
+}
+
+vampomi_status sync_stream(vampomi_ctx* c, hipStream_t st) {
+    if (!c->comm || c->loopback) {
+        HIPCHK(hipStreamSynchronize(st));
+        return VAMPOMI_OK;
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint64_t spin = 1;; ++spin) {
+        const hipError_t e = hipStreamQuery(st);
+        if (e == hipSuccess) return VAMPOMI_OK;
+        if (e != hipErrorNotReady) return fail(VAMPOMI_ERR_HIP, std::string("stream failed: ") + hipGetErrorString(e));
+        if ((spin & 255) == 0)
+            if (const char* why = job_broken(c, t0)) return job_failed(c, why);
         __builtin_ia32_pause();
     }
 }
@@ -190,7 +242,7 @@ vampomi_status wait_flag(vampomi_ctx* c, unsigned long long seq, int word) {
 vampomi_status host_sync(vampomi_ctx* c) {
     c->stats.host_syncs++;
     if (!c->h_flag) {
-        HIPCHK(hipStreamSynchronize(c->st));
+        STCHK(sync_stream(c, c->st));
         return VAMPOMI_OK;
     }
     const unsigned long long seq = ++c->sync_seq;
@@ -254,7 +306,7 @@ static vampomi_status loopback_allreduce(vampomi_ctx* c, double* buf, size_t n, 
     const LoopbackComm::Desc me{++c->coll_seq, n, site, line};
     std::vector<double> mine(n);
     HIPCHK(hipMemcpyAsync(mine.data(), buf, n * 8, hipMemcpyDeviceToHost, c->st));
-    HIPCHK(hipStreamSynchronize(c->st));
+    STCHK(sync_stream(c, c->st));
     std::string err;  // reported after the lock is released (fail() may abort the communicator)
     {
         std::unique_lock<std::mutex> g(lb.mu);
@@ -302,7 +354,7 @@ static vampomi_status loopback_allreduce(vampomi_ctx* c, double* buf, size_t n, 
         return fail(VAMPOMI_ERR_STATE, err);
     }
     HIPCHK(hipMemcpyAsync(buf, mine.data(), n * 8, hipMemcpyHostToDevice, c->st));
-    HIPCHK(hipStreamSynchronize(c->st));
+    STCHK(sync_stream(c, c->st));
     return VAMPOMI_OK;
 }
 
@@ -317,7 +369,7 @@ static vampomi_status rccl_check(vampomi_ctx* c, size_t n, const char* site, int
     HIPCHK(hipMemcpyAsync(d, h, sizeof h, hipMemcpyHostToDevice, c->st));
     NCCLCHK(ncclAllReduce(d, d, 6, ncclDouble, ncclMax, c->comm, c->st));
     HIPCHK(hipMemcpyAsync(h, d, sizeof h, hipMemcpyDeviceToHost, c->st));
-    HIPCHK(hipStreamSynchronize(c->st));
+    STCHK(sync_stream(c, c->st));
     for (int q = 0; q < 3; ++q)
         if (h[q] != v[q] || -h[3 + q] != v[q])
             return fail(VAMPOMI_ERR_STATE, "ranks disagree on collective #" + std::to_string(c->coll_seq) + " (this rank: " +
@@ -331,7 +383,10 @@ vampomi_status allreduce_dev(vampomi_ctx* c, double* buf, size_t n, const char* 
     ++c->coll_seq;
     static const bool check = std::getenv("VAMPOMI_COLL_CHECK") && std::atoi(std::getenv("VAMPOMI_COLL_CHECK"));
     if (check) STCHK(rccl_check(c, n, site, line));
+    const TimedLaunch t = launch_stat(c, 4, 1, 8.0 * (double)n, 0.0);
+    if (t.a) HIPCHK(hipEventRecord(t.a, c->st));
     NCCLCHK(ncclAllReduce(buf, buf, n, ncclDouble, ncclSum, c->comm, c->st));
+    if (t.b) HIPCHK(hipEventRecord(t.b, c->st));
     return VAMPOMI_OK;
 }
 
@@ -344,7 +399,7 @@ vampomi_status sum_over_ranks(vampomi_ctx* c, double local, double* total, const
     HIPCHK(vk::set_scalar(d, local, c->st));
     STCHK(allreduce_dev(c, d, 1, site, line));
     HIPCHK(hipMemcpyAsync(c->h_scal + SL_AGREE, d, 8, hipMemcpyDeviceToHost, c->st));
-    HIPCHK(hipStreamSynchronize(c->st));
+    STCHK(sync_stream(c, c->st));
     *total = c->h_scal[SL_AGREE];
     return VAMPOMI_OK;
 }
@@ -429,6 +484,7 @@ vampomi_status DotBatch::fork() {
     HIPCHK(hipEventRecord(c_->ev_fork, c_->st));
     HIPCHK(hipStreamWaitEvent(c_->st2, c_->ev_fork, 0));
     forked_ = true;
+    c_->side_open = true;
     return VAMPOMI_OK;
 }
 
@@ -445,6 +501,7 @@ vampomi_status DotBatch::flush() {
         HIPCHK(hipEventRecord(c_->ev_join, c_->st2));
         HIPCHK(hipStreamWaitEvent(c_->st, c_->ev_join, 0));
         forked_ = false;
+        c_->side_open = false;
     }
     if (side_seq_) {  // one rank: the host reads the side results when their own kernel flags them
         c_->stats.host_syncs++;
@@ -559,6 +616,18 @@ vampomi_status op_prepare(vampomi_ctx* c) {
     if (c->cus <= 0) HIPCHK(hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, c->device));
     const int64_t M = std::max<int64_t>(c->M, 1);
     c->op_ok = vk::op_plan(c->N, M, c->cus, c->op_variant, &c->opp);
+    if (c->op_ok && c->opp.T >= 1) {
+        // a team launch waits for members that must all be resident at once:
+        // the device must hold the whole grid (one workgroup per CU) for every K
+        for (int K = 1; K <= vk::kOpMaxK; ++K) {
+            const int occ = vk::team_occupancy(c->opp, K);
+            if ((int64_t)occ * c->cus < c->opp.grid)
+                return fail(VAMPOMI_ERR_HIP, "one-pass operator: " + vk::team_kernel_name(K, c->opp) + " fits " +
+                                                 std::to_string(occ) + " workgroup(s) per CU; the plan needs " +
+                                                 std::to_string(c->opp.grid) + " resident on " +
+                                                 std::to_string(c->cus) + " CUs");
+        }
+    }
     if (!c->op_nvec) {
         STCHK(dev_alloc(&c->op_nvec, (size_t)3 * vk::kMaxRhs * c->ld));
         HIPCHK(hipMemsetAsync(c->op_nvec, 0, (size_t)3 * vk::kMaxRhs * c->ld * 8, c->st));
@@ -631,6 +700,11 @@ static void team_gate_leave(vampomi_ctx* c) {  // after the context's stream has
 
 template <class Launch>
 static vampomi_status team_launch(vampomi_ctx* c, Launch&& launch) {
+    if (c->side_open && c->st2) {  // never beside the context's own side-stream work (not reached: batches join first)
+        HIPCHK(hipEventRecord(c->ev_join, c->st2));
+        HIPCHK(hipStreamWaitEvent(c->st, c->ev_join, 0));
+        c->side_open = false;
+    }
     if (c->opp.T <= 1 || !c->team_reg) {
         HIPCHK(launch());
         return VAMPOMI_OK;
@@ -658,8 +732,10 @@ static vampomi_status team_launch(vampomi_ctx* c, Launch&& launch) {
     return VAMPOMI_OK;
 }
 
+// reads and clears the word: each check reports the launches since the last
+// one, so one timed-out launch does not fail every later solve of the context
 vampomi_status op_check_err(vampomi_ctx* c) {
-    if (c->h_flag && __atomic_load_n(reinterpret_cast<unsigned*>(c->h_flag + 4), __ATOMIC_ACQUIRE))
+    if (c->h_flag && __atomic_exchange_n(reinterpret_cast<unsigned*>(c->h_flag + 4), 0u, __ATOMIC_ACQ_REL))
         return fail(VAMPOMI_ERR_HIP, "one-pass operator: a team hand-off timed out (a workgroup of the team never "
                                      "ran: fewer compute units than planned?)");
     return VAMPOMI_OK;
@@ -866,7 +942,7 @@ extern "C" vampomi_status vampomi_open(const vampomi_shard_desc* d, vampomi_ctx*
             NCCLCHK(ncclGetUniqueId(&id));
         NCCLCHK(ncclCommInitRank(&c->comm, c->nranks, id, c->rank));
     }
-    HIPCHK(hipStreamSynchronize(c->st));
+    STCHK(sync_stream(c.get(), c->st));
     *out = c.release();
     return VAMPOMI_OK;
 }
@@ -882,7 +958,7 @@ extern "C" vampomi_status vampomi_shard_info(const vampomi_ctx* c, int64_t* M, i
 extern "C" vampomi_status vampomi_sync(vampomi_ctx* c) {
     if (!c) return fail(VAMPOMI_ERR_ARG, "null context");
     HIPCHK(hipSetDevice(c->device));
-    HIPCHK(hipStreamSynchronize(c->st));
+    STCHK(sync_stream(c, c->st));
     return VAMPOMI_OK;
 }
 
@@ -890,7 +966,7 @@ extern "C" vampomi_status vampomi_barrier(vampomi_ctx* c) {
     CollScope cs_(c);
     if (!c) return fail(VAMPOMI_ERR_ARG, "null context");
     if (c->use_comm) STCHK(allreduce_dev(c, c->scal + SL_BARRIER, 1));
-    HIPCHK(hipStreamSynchronize(c->st));
+    STCHK(sync_stream(c, c->st));
     return VAMPOMI_OK;
 }
 
@@ -907,7 +983,7 @@ static vampomi_status finish_X(vampomi_ctx* c) {
         HIPCHK(hipMemset2DAsync(c->X + c->N, (size_t)c->ld * 8, 0, (size_t)(c->ld - c->N) * 8, (size_t)c->M, c->st));
     // compute_markers_statistics with nonas = N (read_phen asserts N rows, src/data.cpp:85)
     HIPCHK(vk::marker_stats(c->X, c->ld, c->N, c->M, (double)c->N, c->alpha_scale, c->mave, c->msig, c->st));
-    HIPCHK(hipStreamSynchronize(c->st));
+    STCHK(sync_stream(c, c->st));
     c->have_X = true;
     return VAMPOMI_OK;
 }
@@ -1019,7 +1095,7 @@ extern "C" vampomi_status vampomi_generate_meth(vampomi_ctx* c, uint64_t seed, i
 
 static vampomi_status upload_phen(vampomi_ctx* c) {
     HIPCHK(hipMemcpyAsync(c->y, c->y_host.data(), (size_t)c->N * 8, hipMemcpyHostToDevice, c->st));
-    HIPCHK(hipStreamSynchronize(c->st));
+    STCHK(sync_stream(c, c->st));
     c->have_y = true;
     return VAMPOMI_OK;
 }
@@ -1059,7 +1135,7 @@ extern "C" vampomi_status vampomi_get_marker_stats(vampomi_ctx* c, double* mave,
     HIPCHK(hipSetDevice(c->device));
     if (mave && c->M > 0) HIPCHK(hipMemcpyAsync(mave, c->mave, (size_t)c->M * 8, hipMemcpyDeviceToHost, c->st));
     if (msig && c->M > 0) HIPCHK(hipMemcpyAsync(msig, c->msig, (size_t)c->M * 8, hipMemcpyDeviceToHost, c->st));
-    HIPCHK(hipStreamSynchronize(c->st));
+    STCHK(sync_stream(c, c->st));
     return VAMPOMI_OK;
 }
 
@@ -1070,7 +1146,7 @@ extern "C" vampomi_status vampomi_read_markers(vampomi_ctx* c, int64_t i0, int64
     if (count > 0)
         HIPCHK(hipMemcpy2DAsync(out, (size_t)c->N * 8, c->X + i0 * c->ld, (size_t)c->ld * 8, (size_t)c->N * 8,
                                 (size_t)count, hipMemcpyDeviceToHost, c->st));
-    HIPCHK(hipStreamSynchronize(c->st));
+    STCHK(sync_stream(c, c->st));
     return VAMPOMI_OK;
 }
 
@@ -1124,7 +1200,7 @@ static vampomi_status stage_out(vampomi_ctx* c, const double* src, int64_t n, in
     if (n > 0)
         HIPCHK(hipMemcpyAsync(dst, src, (size_t)n * 8, mem == VAMPOMI_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost,
                               c->st));
-    HIPCHK(hipStreamSynchronize(c->st));
+    STCHK(sync_stream(c, c->st));
     return VAMPOMI_OK;
 }
 
@@ -1170,7 +1246,7 @@ static vampomi_status is_zero_vec(vampomi_ctx* c, const double* v, int64_t n, in
     } else {
         std::vector<double> h((size_t)std::max<int64_t>(n, 1));
         if (n > 0) HIPCHK(hipMemcpyAsync(h.data(), v, (size_t)n * 8, hipMemcpyDeviceToHost, c->st));
-        HIPCHK(hipStreamSynchronize(c->st));
+        STCHK(sync_stream(c, c->st));
         local = host_all_zero(h.data(), n);
     }
     double nonzero = 0.0;
@@ -1219,8 +1295,10 @@ extern "C" vampomi_status vampomi_pcg(vampomi_ctx* c, const double* v, const dou
     STCHK(stage_in(c, v, c->M, mem, w));
     bool zero = true;  // no mu0 on this rank: zeros (still counted with the others)
     if (mu0 || c->use_comm) STCHK(is_zero_vec(c, mu0, mu0 ? c->M : 0, mem, &zero));
+    // zero is collective (every rank runs the same lmmse pass), but only a rank
+    // that holds mu0 stages it in: the others start from a zero local slice
     s.mu0_nonzero = !zero;
-    if (zero)
+    if (zero || !mu0)
         HIPCHK(hipMemsetAsync(s.mu, 0, (size_t)Mx * 8, c->st));
     else
         STCHK(stage_in(c, mu0, c->M, mem, s.mu));
@@ -1308,7 +1386,7 @@ extern "C" vampomi_status vampomi_assoc_loo(vampomi_ctx* c, const double* est, d
     HIPCHK(vk::loo_pvals(M, st, (int)N, pv, c->st));
     if (stats) STCHK(stage_out(c, st, 5 * M, mem, stats));
     if (pvals) STCHK(stage_out(c, pv, M, mem, pvals));
-    HIPCHK(hipStreamSynchronize(c->st));
+    STCHK(sync_stream(c, c->st));
     if (c->timing) resolve_timing(c);
     return VAMPOMI_OK;
 }
@@ -1365,14 +1443,14 @@ extern "C" vampomi_status vampomi_set_timing(vampomi_ctx* c, int on) {
 
 extern "C" vampomi_status vampomi_get_stats(vampomi_ctx* c, vampomi_stats* out) {
     if (!c || !out) return fail(VAMPOMI_ERR_ARG, "null argument");
-    HIPCHK(hipStreamSynchronize(c->st));
+    STCHK(sync_stream(c, c->st));
     resolve_timing(c);
     *out = c->stats;
     // estimated device time of every launch: the sampled average x the exact count
     auto fill = [](vampomi_kernel_stat& x) {
         x.ms_total = x.timed > 0 ? x.ms_timed / (double)x.timed * (double)x.launches : 0.0;
     };
-    for (vampomi_kernel_stat* x : {&out->ax, &out->atx, &out->loo, &out->op}) fill(*x);
+    for (vampomi_kernel_stat* x : {&out->ax, &out->atx, &out->loo, &out->op, &out->coll}) fill(*x);
     for (int k = 0; k < 4; ++k)
         for (vampomi_kernel_stat* x : {&out->ax_k[k], &out->atx_k[k], &out->op_k[k]}) fill(*x);
     return VAMPOMI_OK;
@@ -1380,7 +1458,7 @@ extern "C" vampomi_status vampomi_get_stats(vampomi_ctx* c, vampomi_stats* out) 
 
 extern "C" vampomi_status vampomi_reset_stats(vampomi_ctx* c) {
     if (!c) return fail(VAMPOMI_ERR_ARG, "null context");
-    HIPCHK(hipStreamSynchronize(c->st));
+    STCHK(sync_stream(c, c->st));
     resolve_timing(c);
     c->stats = vampomi_stats{};
     return VAMPOMI_OK;
@@ -1392,7 +1470,7 @@ extern "C" vampomi_status vampomi_reset_stats(vampomi_ctx* c) {
 extern "C" vampomi_status vampomi_dev_set_variant(vampomi_ctx* c, int which, int variant) {
     if (!c) return fail(VAMPOMI_ERR_ARG, "null context");
     HIPCHK(hipSetDevice(c->device));
-    HIPCHK(hipStreamSynchronize(c->st));
+    STCHK(sync_stream(c, c->st));
     if (which == 0) {
         if (!vk::ax_variant_ok(variant)) return fail(VAMPOMI_ERR_ARG, "no such A.x variant");
         const vk::AxPlan np = vk::ax_plan(c->N, std::max<int64_t>(c->M, 1), variant);
@@ -1529,7 +1607,7 @@ extern "C" vampomi_status vampomi_dev_op_apply(vampomi_ctx* c, int K, const doub
         STCHK(stage_out(c, AD + k * c->ld, c->N, VAMPOMI_MEM_HOST, ad + k * c->N));
     }
     HIPCHK(hipMemcpyAsync(dp, c->scal + SL_DP, (size_t)K * 8, hipMemcpyDeviceToHost, c->st));
-    HIPCHK(hipStreamSynchronize(c->st));
+    STCHK(sync_stream(c, c->st));
     return op_check_err(c);
 }
 

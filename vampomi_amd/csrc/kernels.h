@@ -147,6 +147,10 @@ struct OpArgs {
 };
 std::string op_kernel_name(int K, const OpPlan& pl);
 std::string team_kernel_name(int K, const OpPlan& pl);
+// workgroups of the team kernel of plan pl (T >= 1) with K right-hand sides one
+// CU holds at once (0: it cannot run); a plan needs grid <= this x CUs, since
+// a team launch needs all its workgroups resident together
+int team_occupancy(const OpPlan& pl, int K);
 hipError_t atax(const Shard& s, const OpPlan& pl, int K, const OpArgs& a, hipStream_t st, const Timing& tm = Timing{},
                 const int* gate = nullptr);
 hipError_t atax_team(const Shard& s, const OpPlan& pl, int K, const OpArgs& a, hipStream_t st, const Timing& tm,
@@ -221,6 +225,8 @@ hipError_t bernoulli(uint64_t seed, int it, int64_t S, int64_t M, double sqrtMt,
                      hipStream_t st);
 // out = x / d
 hipError_t div_scalar(int64_t n, const double* x, double d, double* out, hipStream_t st);
+// out[0, n) = x / d and out[n, 2n) = r / d in one launch (the iteration writer)
+hipError_t div2_scalar(int64_t n, const double* x, const double* r, double d, double* out, hipStream_t st);
 
 // ---- probit model (src/vamp_probit.cpp) -------------------------------------
 // z1[i] = g1_bin_class(p1[i], tau1, y[i]); the sum of g1d_bin_class in ro.out[0]

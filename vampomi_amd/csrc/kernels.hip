@@ -1407,6 +1407,22 @@ hipError_t div_scalar(int64_t n, const double* x, double d, double* out, hipStre
     return hipGetLastError();
 }
 
+// out[0, n) = x / d, out[n, 2n) = r / d (IEEE division, as the host's x / sqrt(N))
+__global__ void div2_scalar_kernel(int64_t n, const double* __restrict__ x, const double* __restrict__ r, double d,
+                                   double* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) {
+        out[i] = x[i] / d;
+        out[n + i] = r[i] / d;
+    }
+}
+
+hipError_t div2_scalar(int64_t n, const double* x, const double* r, double d, double* out, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(div2_scalar_kernel, dim3((unsigned)cdiv(n, kBlock)), dim3(kBlock), 0, st, n, x, r, d, out);
+    return hipGetLastError();
+}
+
 // ---------------------------------------------------------------------------
 // PCG vector steps (src/vamp.cpp:671-757), K right-hand sides per launch
 // ---------------------------------------------------------------------------

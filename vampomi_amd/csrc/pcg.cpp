@@ -45,6 +45,7 @@ static vampomi_status cg_loop(vampomi_ctx* c, int max_iter, Enqueue&& enqueue, c
         if (i < max_iter) STCHK(enqueue(i, &cur));
         c->stats.host_syncs++;
         STCHK(wait_flag(c, prev));  // step i-1 decided
+        STCHK(op_check_err(c));     // (its decision is void if its operator launch timed out)
         const vk::CgMirror* m = c->h_cgm + ((i - 1) & 1);
         if (__atomic_load_n(&m->seq, __ATOMIC_ACQUIRE) != prev)
             return fail(VAMPOMI_ERR_STATE, "CG step " + std::to_string(i - 1) + ": decision slot holds sequence " +

@@ -250,13 +250,10 @@ vampomi_status probit_step(vampomi_ctx* c, VampRun& R) {
     if (res && res->prior_hist) std::memcpy(res->prior_hist + (int64_t)(it - 1) * (1 + 2 * VAMPOMI_MAX_L), prior,
                                             sizeof prior);
     if (R.write && c->rank == 0) {  // :430-435
-        if (!vio::csv_write_row(R.p_params, it, R.params, 8) || !vio::csv_write_row(R.p_metrics, it, R.metrics, 12) ||
-            !vio::csv_write_row(R.p_prior, it, prior, np)) {
-            R.io_err = true;
-            R.io_msg = "cannot write CSV rows";
-        }
+        write_row(R, R.p_params, it, R.params, 8);
+        write_row(R, R.p_metrics, it, R.metrics, 12);
+        write_row(R, R.p_prior, it, prior, np);
     }
-    if (R.write) STCHK(agree_io(c, R));  // write_bins' and the rows' failures, on every rank at once
     if (R.prm.verbosity >= 1 && c->rank == 0)
         std::printf("it %d: alpha1 %.6g beta1 %.6g gam1 %.6g tau1 %.6g alpha2 %.6g beta2 %.6g L %d cg %d/%d\n", it,
                     R.alpha1, R.beta1, R.gam1, R.tau1, R.alpha2, R.beta2, R.mix.L, sx.iters, so.iters);
@@ -264,6 +261,7 @@ vampomi_status probit_step(vampomi_ctx* c, VampRun& R) {
     // stopping criteria (:444-458)
     const double NMSE = std::sqrt(R.nm[0] / R.nm[1]);
     if ((it > 1 && NMSE < R.prm.stop_criteria_thr) || it >= R.prm.max_iter) R.stopped = true;
+    STCHK(end_iteration_io(c, R));  // write_bins' and the rows' failures, on every rank at once
     R.have_next = next && !R.stopped;
     if (R.have_next) R.alpha1_next = R.sum_d / (double)Mt;
     if (res) {

@@ -6,6 +6,7 @@
 #include <vector>
 
 #include "ctx.h"
+#include "writer.h"
 
 struct Mixture {
     int L = 0;
@@ -36,6 +37,9 @@ struct VampRun {
     // rank-locally; a rank that stopped there would leave the others waiting)
     bool io_err = false;
     std::string io_msg;
+    // per-iteration vectors and CSV rows, written off the critical path
+    // (writer.h); created on the first iteration that writes or keeps history
+    std::unique_ptr<IterWriter> writer;
     Mixture mix, mix_next;
     bool have_next = false;  // x1n, alpha1_next, mix_next, z1 (nb3 slot 2), atx0 valid
     double gam1 = 0, gam2 = 0, gamw = 0;
@@ -92,9 +96,19 @@ vampomi_status em_finish(vampomi_ctx* c, const EmParams& P, Mixture& m, double g
 vampomi_status denoise_into(vampomi_ctx* c, const Mixture& m, double gam1, const double* r1, double* x1,
                             const double* x1_prev, bool damp, double rho, double* x1d, DotBatch& b, double* sum_out);
 vampomi_status upload_or_zero(vampomi_ctx* c, double* dst, const double* host, int64_t n);
+// queues this iteration's x1/sqrt(N), r1/sqrt(N) for the _it_K.bin /
+// _r1_it_K.bin files and the x1/r1 history (R.writer)
 vampomi_status write_bins(vampomi_ctx* c, VampRun& R);
-// a rank-local I/O failure (R.io_err) becomes every rank's ERR_IO. COLLECTIVE
-vampomi_status agree_io(vampomi_ctx* c, VampRun& R);
+// queues a CSV row (rank 0 writes them) behind the iteration's vectors
+void write_row(VampRun& R, const std::string& path, int it, const double* vals, int n);
+// a rank-local I/O failure (R.io_err, or a finished writer job) becomes every
+// rank's ERR_IO; wait_all: first wait for every queued write (the last
+// iteration).  COLLECTIVE
+vampomi_status agree_io(vampomi_ctx* c, VampRun& R, bool wait_all = false);
+// the end of an iteration's output (after R.stopped is decided): the history
+// row is in place, and write failures so far (all writes after the last
+// iteration) are agreed over the ranks.  COLLECTIVE when writing files
+vampomi_status end_iteration_io(vampomi_ctx* c, VampRun& R);
 // probit.cpp
 vampomi_status probit_begin(vampomi_ctx* c, VampRun& R);
 vampomi_status probit_step(vampomi_ctx* c, VampRun& R);

@@ -38,6 +38,7 @@
 #include "run.h"
 
 VampRun::~VampRun() {
+    writer.reset();  // drains: its kernels read x1 / r1, its thread writes the caller's history arrays
     for (double** p : {&r1, &x1, &x1p, &x1n, &x1d, &r2, &x2, &bern, &invQ, &v, &atxy, &ts, &tmpM, &atx0, &z1buf,
                        &nb3, &nsc, &ax2, &p1, &p2, &z1h, &x1s, &x1sn, &x2s})
         dev_free(*p);
@@ -271,7 +272,7 @@ extern "C" vampomi_status vampomi_vamp_begin(vampomi_ctx* c, const vampomi_param
             r->a_passes_exec = 0;
         }
         STCHK(probit_begin(c, R));
-        HIPCHK(hipStreamSynchronize(c->st));
+        STCHK(sync_stream(c, c->st));
         return VAMPOMI_OK;
     }
     {  // A^T y is the same every iteration (y fixed, src/vamp.cpp:303): one pass
@@ -305,42 +306,76 @@ extern "C" vampomi_status vampomi_vamp_begin(vampomi_ctx* c, const vampomi_param
         r->a_passes_ref = 0;
         r->a_passes_exec = 0;
     }
-    HIPCHK(hipStreamSynchronize(c->st));
+    STCHK(sync_stream(c, c->st));
     return VAMPOMI_OK;
 }
 
+static bool keeps_hist(const VampRun& R) { return R.res && (R.res->x1_hist || R.res->r1_hist); }
+
+static vampomi_status ensure_writer(vampomi_ctx* c, VampRun& R) {
+    if (R.writer) return VAMPOMI_OK;
+    std::unique_ptr<IterWriter> w(new IterWriter());
+    STCHK(w->open(c));
+    R.writer = std::move(w);
+    return VAMPOMI_OK;
+}
+
+// x1_hat_scaled (src/vamp.cpp:237-238) and r1_scaled (:246-248), written by
+// R.writer while the iteration goes on (writer.h)
 vampomi_status write_bins(vampomi_ctx* c, VampRun& R) {
-    const bool hist = R.res && (R.res->x1_hist || R.res->r1_hist);
+    const bool hist = keeps_hist(R);
     if (!R.write && !hist) return VAMPOMI_OK;
-    const int64_t M = c->M;
-    std::vector<double> hx((size_t)std::max<int64_t>(M, 1)), hr((size_t)std::max<int64_t>(M, 1));
-    HIPCHK(hipMemcpyAsync(hx.data(), R.x1, (size_t)M * 8, hipMemcpyDeviceToHost, c->st));
-    HIPCHK(hipMemcpyAsync(hr.data(), R.r1, (size_t)M * 8, hipMemcpyDeviceToHost, c->st));
-    STCHK(host_sync(c));
-    const double sqrtN = std::sqrt((double)c->N);
-    for (int64_t i = 0; i < M; ++i) {
-        hx[i] = hx[i] / sqrtN;  // x1_hat_scaled (src/vamp.cpp:237-238)
-        hr[i] = hr[i] / sqrtN;  // r1_scaled (:246-248)
-    }
-    if (R.res && R.res->x1_hist) std::memcpy(R.res->x1_hist + (int64_t)(R.it - 1) * M, hx.data(), (size_t)M * 8);
-    if (R.res && R.res->r1_hist) std::memcpy(R.res->r1_hist + (int64_t)(R.it - 1) * M, hr.data(), (size_t)M * 8);
+    STCHK(ensure_writer(c, R));
+    const int64_t off = (int64_t)(R.it - 1) * c->M;
+    std::string px, pr;
     if (R.write) {
         const std::string base = R.out_dir + "/" + R.out_name;
-        if (!vio::store_vec(base + "_it_" + std::to_string(R.it) + ".bin", hx.data(), c->S, M) ||
-            !vio::store_vec(base + "_r1_it_" + std::to_string(R.it) + ".bin", hr.data(), c->S, M)) {
-            R.io_err = true;  // reported by agree_io at the end of the iteration
-            R.io_msg = "cannot write iteration vectors to " + R.out_dir;
-        }
+        px = base + "_it_" + std::to_string(R.it) + ".bin";
+        pr = base + "_r1_it_" + std::to_string(R.it) + ".bin";
     }
-    return VAMPOMI_OK;
+    return R.writer->submit_vectors(c, R.x1, R.r1, px, pr, hist && R.res->x1_hist ? R.res->x1_hist + off : nullptr,
+                                    hist && R.res->r1_hist ? R.res->r1_hist + off : nullptr);
 }
 
-vampomi_status agree_io(vampomi_ctx* c, VampRun& R) {
+void write_row(VampRun& R, const std::string& path, int it, const double* vals, int n) {
+    std::vector<double> v(vals, vals + n);
+    auto job = [path, it, v](std::string* msg) {
+        if (vio::csv_write_row(path, it, v.data(), (int)v.size())) return true;
+        *msg = "cannot write CSV rows to " + path;
+        return false;
+    };
+    if (R.writer) {
+        R.writer->submit_host(job);
+    } else {
+        std::string msg;
+        if (!job(&msg)) {
+            R.io_err = true;
+            R.io_msg = msg;
+        }
+    }
+}
+
+vampomi_status agree_io(vampomi_ctx* c, VampRun& R, bool wait_all) {
+    if (R.writer && !R.io_err) {
+        std::string msg;
+        if (wait_all ? R.writer->drain(&msg) : R.writer->failed(&msg)) {
+            R.io_err = true;
+            R.io_msg = msg;
+        }
+    }
     double bad = 0.0;
     STCHK(sum_over_ranks(c, R.io_err ? 1.0 : 0.0, &bad));
     if (bad > 0)
         return fail(VAMPOMI_ERR_IO, R.io_err ? R.io_msg
                                              : "output file write failed on " + std::to_string((int)bad) + " other rank(s)");
+    return VAMPOMI_OK;
+}
+
+vampomi_status end_iteration_io(vampomi_ctx* c, VampRun& R) {
+    if (keeps_hist(R) && R.writer) R.writer->drain(nullptr);  // the history row of this iteration is in place
+    if (R.write) return agree_io(c, R, R.stopped);  // files written so far; all of them after the last iteration
+    std::string msg;
+    if (R.writer && R.writer->failed(&msg)) return fail(VAMPOMI_ERR_HIP, msg);
     return VAMPOMI_OK;
 }
 
@@ -542,12 +577,9 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
     if (res && res->params) std::memcpy(res->params + (int64_t)(it - 1) * 5, R.params, 5 * sizeof(double));
     if (res && res->metrics) std::memcpy(res->metrics + (int64_t)(it - 1) * 6, R.metrics, 6 * sizeof(double));
     if (R.write && c->rank == 0) {  // :388-393
-        if (!vio::csv_write_row(R.p_params, it, R.params, 5) || !vio::csv_write_row(R.p_metrics, it, R.metrics, 6)) {
-            R.io_err = true;
-            R.io_msg = "cannot write CSV rows";
-        }
+        write_row(R, R.p_params, it, R.params, 5);
+        write_row(R, R.p_metrics, it, R.metrics, 6);
     }
-    if (R.write) STCHK(agree_io(c, R));  // write_bins' and the rows' failures, on every rank at once
     if (R.prm.verbosity >= 1 && c->rank == 0)
         std::printf("it %d: alpha1 %.6g gam1 %.6g alpha2 %.6g gam2 %.6g gamw %.6g L %d cg %d/%d\n", it, R.alpha1,
                     R.gam1, R.alpha2, R.gam2, R.gamw, R.mix.L, sx.iters, so.iters);
@@ -555,6 +587,7 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
     // stopping criteria (:409-423)
     const double NMSE = std::sqrt(R.nm[0] / R.nm[1]);
     if ((it > 1 && NMSE < R.prm.stop_criteria_thr) || it >= R.prm.max_iter) R.stopped = true;
+    STCHK(end_iteration_io(c, R));
     R.have_next = next && !R.stopped;
     if (R.have_next) R.alpha1_next = R.sum_d / (double)Mt;
     if (res) {
@@ -571,6 +604,13 @@ extern "C" vampomi_status vampomi_vamp_end(vampomi_ctx* c) {
     if (!c || !c->run) return fail(VAMPOMI_ERR_STATE, "vampomi_vamp_begin not called");
     VampRun& R = *c->run;
     vampomi_result* res = R.res;
+    if (R.writer) {  // (a run ended before its last iteration: the writes queued so far)
+        std::string msg;
+        if (R.writer->drain(&msg)) {
+            c->run.reset();
+            return fail(VAMPOMI_ERR_IO, msg);
+        }
+    }
     if (res) {
         if (res->x1_final && c->M > 0) {
             HIPCHK(hipMemcpyAsync(res->x1_final, R.x1, (size_t)c->M * 8, hipMemcpyDeviceToHost, c->st));
