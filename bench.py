@@ -65,6 +65,8 @@ def parse_args(argv=None):
     ap.add_argument("--timing-period", type=int, default=1,
                     help="time one A/A^T launch in this many of each (kernel, K) with HIP events")
     ap.add_argument("--batch-rhs", type=int, default=4)
+    ap.add_argument("--op-variant", type=int, default=None,
+                    help="one-pass operator plan (development hook, vampomi_dev_set_variant(ctx, 3, v))")
     ap.add_argument("--write", nargs="?", const=os.environ.get("TMPDIR", "/tmp"), default=None, metavar="DIR",
                     help="also time the same window with the per-iteration output files on (the main_meth.exe "
                          "drop-in rate: _it_K.bin, _r1_it_K.bin and CSV rows into a fresh directory under DIR)")
@@ -212,7 +214,8 @@ def write_rate(args, d, R, opts, beta, barrier, el_nowrite: float) -> dict:
     """The same W + K iterations again with the reference's per-iteration
     output on (src/vamp.cpp:235-249 _it_K.bin / _r1_it_K.bin, :388-393 CSV
     rows) into a fresh directory under args.write: what a main_meth.exe user
-    gets per iteration.  Timing off, so both windows time the same work."""
+    gets per iteration, with the main window's kernel timing, so the two
+    windows differ only by the writes."""
     import dataclasses
     import shutil
     import tempfile
@@ -225,7 +228,7 @@ def write_rate(args, d, R, opts, beta, barrier, el_nowrite: float) -> dict:
         R.dist.broadcast_object_list(obj, src=0)
         out = obj[0]
     try:
-        d.set_timing(False)
+        d.set_timing(not args.no_timing, args.timing_period)  # as in the main window: the ratio is the writes'
         v = va.Vamp(d, dataclasses.replace(opts, out_dir=out, out_name="bench"), true_signal=beta)
         v.begin()
         for _ in range(args.warmup):
@@ -247,7 +250,7 @@ def write_rate(args, d, R, opts, beta, barrier, el_nowrite: float) -> dict:
             "rate_vs_no_write": round(el_nowrite / el, 4), "files": len(files), "bytes_written": int(nbytes),
             "out_dir": args.write,
             "what": "the same iterations with _it_K.bin, _r1_it_K.bin (every iteration, every rank) and the CSV rows "
-                    "written (async writer thread, writer.h); HIP-event timing off in this window"}
+                    "written (async writer thread, writer.h); HIP-event timing as in the main window"}
 
 
 def per_rank_times(R, st, el: float) -> list:
@@ -454,6 +457,8 @@ def main():
     else:
         beta = d.simulate_phen(args.seed + 1, lam=0.1, h2=0.8)
     t_setup = time.perf_counter() - t0
+    if args.op_variant is not None:
+        d.set_variant(3, args.op_variant)
 
     opts = va.VampOptions(max_iter=args.warmup + args.steps, stop_criteria_thr=0.0, batch_rhs=args.batch_rhs,
                           model=model)

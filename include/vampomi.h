@@ -298,7 +298,7 @@ vampomi_status vampomi_reset_stats(vampomi_ctx* ctx);
  * context only; the defaults are 0 (A.x), -1 (A^T.u: the per-K choice), 2
  * (association pass) and -1 (operator: whole columns per workgroup while
  * K*N fits the LDS, else teams of workgroups; 0 forces the whole-column
- * kernel, T*10 + c the team kernel with team size T and configuration c,
+ * kernel, T*10 + c (c < 10) or 1000 + T*100 + c the team kernel with team size T and configuration c,
  * vampomi_amd/csrc/atax_team.hip).  which = 4: the side stream of the
  * prefetched EM/denoiser, 0 off, 1 on (default: on with several ranks). */
 vampomi_status vampomi_dev_set_variant(vampomi_ctx* ctx, int which, int variant);
@@ -317,6 +317,14 @@ vampomi_status vampomi_dev_kernel_name(const vampomi_ctx* ctx, int which, int K,
  * no such plan exists. */
 vampomi_status vampomi_dev_op_plan(int64_t N, int64_t M, int cus, int variant, int K, int* T, int* S, int* TR,
                                    int* grid, int64_t* nslots, char* name, int cap);
+/* Device bytes the context of `rank` (of nranks, markers split by
+ * vampomi_divide_work) allocates for a VAMP run on N samples and Mt markers
+ * with `cus` compute units: the shard, marker statistics, scratch, the
+ * one-pass operator's buffers, the run state (probit != 0: the probit model's
+ * too) and, with writer != 0, the per-iteration output writer.  No device
+ * needed; RCCL's buffers and the HIP runtime are not included. */
+vampomi_status vampomi_dev_mem_plan(int64_t N, int64_t Mt, int nranks, int rank, int cus, int probit, int writer,
+                                    int64_t* bytes);
 /* One application of the one-pass CG operator (K <= 2 systems, one rank),
  * host buffers: q_k = ar_k/diag [+ beta_k*qo_k], p_k [= z_k + beta_k*p_k]
  * when z is not null (then qo and beta are required), and

@@ -226,4 +226,5 @@ def test_c5_full_shard_properties():
         _check_pfun(p[picks], st[picks], N)
         assert np.all((p >= 0) & (p <= 1)) and np.all(np.isfinite(st))
         assert np.all(st[:, 0] > 0) and np.all(st[:, 1] > 0)  # methylation values in (0, 1)
-        assert np.median(p[beta != 0]) < 1e-3 < np.median(p[beta == 0])
+        # 3,090 causal markers share h2 = 0.5: they stand out, the null ones are uniform
+        assert np.median(p[beta != 0]) < 0.02 and 0.4 < np.median(p[beta == 0]) < 0.6

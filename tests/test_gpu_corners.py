@@ -101,3 +101,31 @@ def test_update_prior_entry_point(em, lv, merge):
         p, v = d.update_prior(r1, 35.0, O.DEFAULT_PROBS, vars_s, EM_max_iter=em, learn_vars=lv, merge_vars_thr=merge)
     assert len(p) == len(po)
     assert np.allclose(p, po, rtol=1e-12, atol=0) and np.allclose(v, vo, rtol=1e-12, atol=0)
+
+
+def test_device_memory_plan_matches_the_allocations(tmp_path):
+    """vampomi_dev_mem_plan (the CPU-side budget tests/test_op_plan.py checks
+    for c3full at n = 2, 4, 8) against the device memory a C2-sized context
+    really takes during a run with the team operator and the writer on."""
+    import ctypes as C
+
+    import torch
+
+    N, Mt = 10000, 50000
+    torch.cuda.init()
+    free0, _ = torch.cuda.mem_get_info()
+    with va.Data(N, Mt) as d:
+        d.generate(3, va.GEN_GAUSS)
+        beta = d.simulate_phen(4)
+        v = va.Vamp(d, va.VampOptions(max_iter=2, stop_criteria_thr=0.0, out_dir=str(tmp_path), out_name="m"),
+                    true_signal=beta)
+        v.begin()
+        v.step()
+        free1, _ = torch.cuda.mem_get_info()
+        v.step()
+        v.end()
+        cus = torch.cuda.get_device_properties(0).multi_processor_count
+    b = C.c_int64()
+    assert va.load().vampomi_dev_mem_plan(N, Mt, 1, 0, cus, 0, 1, C.byref(b)) == 0
+    used = free0 - free1
+    assert abs(used - b.value) <= 256 * 2**20 + 0.02 * b.value, (used / 2**20, b.value / 2**20)

@@ -257,3 +257,39 @@ def test_side_stream_bitwise(monkeypatch, P, em):
             assert a[k] == b[k], k
         for k in ("x1_hist", "r1_hist", "params", "metrics"):
             np.testing.assert_array_equal(np.asarray(a[k]), np.asarray(b[k]), err_msg=k)
+
+
+@pytest.mark.parametrize("P", [1, 2])
+def test_team_operator_beside_side_stream_and_writer(monkeypatch, tmp_path, P):
+    """N = 12,000: the one-pass operator runs as teams of 4 workgroups that
+    must all be resident.  With the side stream on (EM / denoiser of the next
+    iteration) and the iteration writer's kernel + copy stream busy, every
+    team launch still completes (no hand-off timeout) and the results are
+    bitwise those of the plain one-stream run without files; the files hold
+    what the history holds."""
+    N, Mt, its = 12000, 3001, 8
+    X, y, beta = make_problem(N, Mt, seed=4)
+    out = {}
+    for busy in (0, 1):
+        def fn(r, d, busy=busy):
+            d.set_variant(4, busy)
+            kw = dict(out_dir=str(tmp_path / f"b{busy}"), out_name="t") if busy else {}
+            return _vamp(d, X, y, beta, max_iter=its, stop_criteria_thr=0.0, **kw)
+
+        if busy:
+            (tmp_path / "b1").mkdir()
+        if P == 1:
+            with va.Data(N, Mt) as d:
+                out[busy] = [fn(0, d)]
+        else:
+            out[busy] = run_ranks(monkeypatch, P, N, Mt, fn, timeout=300)
+    for a, b in zip(out[0], out[1]):
+        for k in ("iterations", "cg_iters", "ons_iters", "L"):
+            assert a[k] == b[k], k
+        for k in ("x1_hist", "r1_hist", "params"):
+            np.testing.assert_array_equal(np.asarray(a[k]), np.asarray(b[k]), err_msg=k)
+    x1 = np.concatenate([p["x1_hist"] for p in out[1]], axis=1)
+    r1 = np.concatenate([p["r1_hist"] for p in out[1]], axis=1)
+    for it in range(1, its + 1):
+        np.testing.assert_array_equal(np.fromfile(tmp_path / "b1" / f"t_it_{it}.bin", dtype="<f8"), x1[it - 1])
+        np.testing.assert_array_equal(np.fromfile(tmp_path / "b1" / f"t_r1_it_{it}.bin", dtype="<f8"), r1[it - 1])

@@ -67,3 +67,37 @@ def test_every_variant_plan_is_valid_or_refused():
                 assert p["T"] == 0
             else:
                 assert p["T"] == v // 10
+
+
+def mem_plan(N, Mt, nranks, rank=0, cus=256, probit=0, writer=0):
+    b = C.c_int64()
+    assert lib.vampomi_dev_mem_plan(N, Mt, nranks, rank, cus, probit, writer, C.byref(b)) == 0
+    return b.value
+
+
+HBM_BYTES = 288 * 10**9        # MI355X: 288 GB HBM3E per GPU
+RUNTIME_MARGIN = 4 * 2**30     # RCCL buffers, the HIP runtime, torch's context
+
+
+@pytest.mark.parametrize("n", [2, 4, 8])
+def test_c3full_fits_one_mi355x_per_rank(n):
+    """configs[2] (N = 100,000 x Mt = 500,000, 400 GB) sharded over n ranks:
+    every rank's shard plus the engine's workspace (operator hand-off buffers,
+    run state, writer) fits one GPU's 288 GB with room for RCCL and the
+    runtime; the shard is most of it."""
+    N, Mt = 100000, 500000
+    for r in range(n):
+        b = mem_plan(N, Mt, n, r, writer=1)
+        M = Mt // n + (r < Mt % n)
+        shard = M * N * 8
+        assert shard <= b < shard * 1.02 + 2**30, (n, r, b, shard)
+        assert b + RUNTIME_MARGIN < HBM_BYTES, (n, r, b / 1e9)
+    assert plan(N, M=Mt // n)["T"] == 32  # every shard on the team operator
+
+
+def test_bench_workloads_fit_one_mi355x():
+    """The 1-GPU bench workloads: c3big (300,000 markers, 240 GB) fits; c3full
+    on ONE rank (400 GB) does not, which is why it needs n >= 2."""
+    assert mem_plan(100000, 300000, 1, writer=1) + RUNTIME_MARGIN < HBM_BYTES
+    assert mem_plan(50000, 200000, 1, probit=1, writer=1) + RUNTIME_MARGIN < HBM_BYTES  # c4full
+    assert mem_plan(100000, 500000, 1) > HBM_BYTES

@@ -79,6 +79,13 @@ static constexpr TmCfg kTmCfg[] = {
     {4, 5, 2, true, 4, 2, true},     // 7
     {3, 5, 2, true, 4, 2, true},     // 8
     {2, 4, 2, true, 5, 2, true},     // 9: 3, interleaved
+    {2, 4, 2, true, 6, 2, true},     // 10: six loads per lane (T = 2 at N = 10,000)
+    {1, 4, 2, true, 6, 2, true},     // 11
+    {2, 3, 2, true, 6, 2, true},     // 12
+    {5, 5, 2, true, 3, 2, true},     // 13: deeper prefetch for short tiles (C2: T = 4, S = 3)
+    {6, 5, 2, true, 3, 2, true},     // 14
+    {8, 5, 2, true, 3, 2, true},     // 15
+    {6, 6, 3, true, 3, 2, true},     // 16
 };
 static constexpr int kTmNCfg = sizeof(kTmCfg) / sizeof(kTmCfg[0]);
 
@@ -727,6 +734,13 @@ static bool launch_tm_c(const Shard& s, const OpPlan& pl, const OpArgs& a, hipSt
         case 7: return launch_tm_s<K, 7>(pl.S, s, pl, a, st, tm, gate, occ);
         case 8: return launch_tm_s<K, 8>(pl.S, s, pl, a, st, tm, gate, occ);
         case 9: return launch_tm_s<K, 9>(pl.S, s, pl, a, st, tm, gate, occ);
+        case 10: return launch_tm_s<K, 10>(pl.S, s, pl, a, st, tm, gate, occ);
+        case 11: return launch_tm_s<K, 11>(pl.S, s, pl, a, st, tm, gate, occ);
+        case 12: return launch_tm_s<K, 12>(pl.S, s, pl, a, st, tm, gate, occ);
+        case 13: return launch_tm_s<K, 13>(pl.S, s, pl, a, st, tm, gate, occ);
+        case 14: return launch_tm_s<K, 14>(pl.S, s, pl, a, st, tm, gate, occ);
+        case 15: return launch_tm_s<K, 15>(pl.S, s, pl, a, st, tm, gate, occ);
+        case 16: return launch_tm_s<K, 16>(pl.S, s, pl, a, st, tm, gate, occ);
         default: return false;
     }
 }

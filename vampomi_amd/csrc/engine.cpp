@@ -611,6 +611,19 @@ vampomi_status atx_dev(vampomi_ctx* c, int K, const double* const* u, double* co
 // ---------------------------------------------------------------------------
 // one-pass CG operator (batch_rhs 4)
 // ---------------------------------------------------------------------------
+// doubles of the per-block reduction partials (every reduction kernel's grid)
+static size_t red_capacity(int64_t Mx) {
+    return std::max<size_t>({(size_t)vk::kRedBlocks * 3 * vk::kMaxRhs,
+                             (size_t)((Mx + 255) / 256) * (1 + 2 * (vk::kMaxL - 1)),
+                             (size_t)(Mx / 8 + 1) * vk::kMaxRhs, (size_t)4096});  // ATx partials at G >= 2
+}
+
+// 8-byte words of the team hand-off granules: M columns x K x T granule pairs,
+// then a dummy pair per workgroup and K, then one XCD word per workgroup
+static size_t op_xg_words_for(int64_t Mx, const vk::OpPlan& p) {
+    return (size_t)(Mx + p.grid) * vk::kOpMaxK * (size_t)p.T * 2 + (size_t)p.grid * (2 * vk::kOpMaxK + 1);
+}
+
 vampomi_status op_prepare(vampomi_ctx* c) {
     if (c->op_ready) return VAMPOMI_OK;
     if (c->cus <= 0) HIPCHK(hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, c->device));
@@ -639,9 +652,7 @@ vampomi_status op_prepare(vampomi_ctx* c) {
             c->op_part_slots = c->opp.nslots;
         }
         if (c->opp.T > 1) {
-            // M columns x K x T granule pairs, then a dummy pair per workgroup and K
-            const size_t words = (size_t)(M + c->opp.grid) * vk::kOpMaxK * (size_t)c->opp.T * 2 +
-                                 (size_t)c->opp.grid * (2 * vk::kOpMaxK + 1);
+            const size_t words = op_xg_words_for(M, c->opp);
             if (words > c->op_xg_words) {
                 if (c->op_xg) (void)hipFree(c->op_xg);
                 c->op_xg = nullptr;
@@ -892,9 +903,7 @@ extern "C" vampomi_status vampomi_open(const vampomi_shard_desc* d, vampomi_ctx*
     STCHK(dev_alloc(&c->y, c->ld));
     HIPCHK(hipMemsetAsync(c->y, 0, c->ld * 8, c->st));
     STCHK(dev_alloc(&c->ax_part, (size_t)c->axp.nslots * vk::kMaxRhs * c->ld));
-    c->red_cap = std::max<size_t>({(size_t)vk::kRedBlocks * 3 * vk::kMaxRhs,
-                                   (size_t)((Mx + 255) / 256) * (1 + 2 * (vk::kMaxL - 1)),
-                                   (size_t)(Mx / 8 + 1) * vk::kMaxRhs, (size_t)4096});  // ATx partials at G >= 2
+    c->red_cap = red_capacity(Mx);
     STCHK(dev_alloc(&c->red_part, c->red_cap));
     STCHK(dev_alloc(&c->red_part2, c->red_cap));
     HIPCHK(hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking));
@@ -1622,6 +1631,49 @@ extern "C" vampomi_status vampomi_dev_op_plan(int64_t N, int64_t M, int cus, int
     if (grid) *grid = p.grid;
     if (nslots) *nslots = p.nslots;
     if (name && cap > 0) std::snprintf(name, (size_t)cap, "%s", vk::op_kernel_name(K, p).c_str());
+    return VAMPOMI_OK;
+}
+
+// Device bytes one rank's context allocates for a VAMP run: the same sizes
+// vampomi_open, the data load, op_prepare (the one-pass operator's buffers,
+// batch_rhs 4), vamp_alloc / probit_begin and the iteration writer allocate,
+// summed (each hipMalloc rounded up to 2 MiB, the allocator's granularity for
+// large blocks).  RCCL's own buffers and the HIP runtime are not included.
+extern "C" vampomi_status vampomi_dev_mem_plan(int64_t N, int64_t Mt, int nranks, int rank, int cus, int probit,
+                                               int writer, int64_t* bytes) {
+    if (!bytes || N < 2 || Mt < nranks || nranks < 1 || rank < 0 || rank >= nranks || cus < 1)
+        return fail(VAMPOMI_ERR_ARG, "bad argument");
+    int64_t M = 0, S = 0, Mm = 0;
+    vampomi_divide_work(Mt, nranks, rank, &M, &S, &Mm);
+    const int64_t Mx = std::max<int64_t>(M, 1), ld = (N + 15) / 16 * 16;
+    int64_t total = 0;
+    auto add = [&](int64_t n, int64_t elem) {
+        const int64_t b = std::max<int64_t>(n, 1) * elem, g = 2 << 20;
+        total += (b + g - 1) / g * g;
+    };
+    const vk::AxPlan axp = vk::ax_plan(N, Mx);
+    add(Mx * ld, 8);                                   // X
+    add(Mx, 8), add(Mx, 8), add(ld, 8);                // mave, msig, y
+    add((int64_t)axp.nslots * vk::kMaxRhs * ld, 8);    // ax_part
+    add((int64_t)red_capacity(Mx), 8), add((int64_t)red_capacity(Mx), 8);
+    add(SL_TOTAL, 8), add(64, 4), add(64, 4);          // scal, tickets
+    add((int64_t)vk::kMaxRhs * ld, 8);                 // nbuf
+    add((int64_t)2 * vk::kMaxRhs * Mx, 8);             // mbuf
+    add((int64_t)sizeof(vk::CgState), 1);
+    vk::OpPlan op{};
+    if (vk::op_plan(N, Mx, cus, vk::kOpDefault, &op)) {
+        add((int64_t)3 * vk::kMaxRhs * ld, 8);         // op_nvec
+        add(op.nslots * vk::kMaxRhs * ld, 8);          // op_part
+        if (op.T > 1) add((int64_t)op_xg_words_for(Mx, op), 8);
+    }
+    for (int q = 0; q < 24; ++q) add(Mx, 8);           // VampRun M-vectors (14 + cgw[10])
+    add(ld, 8), add((int64_t)vk::kMaxRhs * ld, 8), add((int64_t)vk::kMaxRhs * ld, 8), add(ld, 8);
+    if (probit) {
+        for (int q = 0; q < 3; ++q) add(ld, 8);
+        for (int q = 0; q < 3; ++q) add(Mx, 8);
+    }
+    if (writer) add(2 * Mx, 8), add(2 * Mx, 8);
+    *bytes = total;
     return VAMPOMI_OK;
 }
 

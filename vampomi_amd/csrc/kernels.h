@@ -118,7 +118,7 @@ struct OpPlan {
     int TR = 0;     // rows per team member (T >= 1)
     int cfg = 0;    // team kernel configuration (prefetch, lag, polls in flight)
 };
-// variant: -1 the default choice for N; 0 the whole-column kernel; T*10 + cfg
+// variant: -1 the default choice for N; 0 the whole-column kernel; T*10 + cfg (cfg < 10) or 1000 + T*100 + cfg
 // a team plan (development hook, tools/kbench.py)
 constexpr int kOpDefault = -1;
 bool op_plan(int64_t N, int64_t M, int cus, int variant, OpPlan* out);

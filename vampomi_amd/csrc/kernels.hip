@@ -758,6 +758,7 @@ bool op_plan(int64_t N, int64_t M, int cus, int variant, OpPlan* out) {
         *out = p;
         return true;
     }
+    if (variant >= 1000) return team_plan(N, M, cus, (variant - 1000) / 100, variant % 100, out);  // 1000 + T*100 + cfg
     if (variant > 0) return team_plan(N, M, cus, variant / 10, variant % 10, out);
     for (int cfg : {7, 9}) {  // then fewer columns in flight for one more load per lane (S <= 5)
         for (int T = 2; T <= 32; T *= 2) {
