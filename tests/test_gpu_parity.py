@@ -394,3 +394,4 @@ with va.Data(800, 1500) as d:
     for it in range(5):
         a, b = outs[0][it], outs[2][it]
         assert np.linalg.norm(a - b) <= 1e-12 * max(np.linalg.norm(a), 1e-300), it
+

@@ -55,4 +55,69 @@ __device__ __forceinline__ void ticket_sum_blocks(const RedOut& ro) {
     if (lane == 0) __hip_atomic_store(ro.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// one thread: the host loop of vamp::precondCG_solver after each step's sums
+// red[3k..3k+2] = <r,z>, <r,r>, <v,mu> of system k.  The state is read into
+// registers in one burst and written back once (a chain of dependent device
+// loads and stores otherwise: this runs at the end of every CG step).
+__device__ inline void cg_decide_vals(CgState* cs, const double* red, int it, CgMirror* mirror,
+                                      unsigned long long* flag, unsigned long long seq) {
+    CgState s = *cs;
+    if (s.any) {
+        int any = 0;
+#pragma unroll
+        for (int k = 0; k < kMaxRhs; ++k) {
+            if (k >= s.K || !s.active[k]) continue;
+            s.iters[k] = it + 1;
+            const double rz_new = red[3 * k], rr = red[3 * k + 1], vmu = red[3 * k + 2];
+            if (s.onsager[k]) {  // :708-726
+                const double ons = s.gam2 * vmu;
+                const double rel = ons != 0 ? fabs((ons - s.prev_ons[k]) / ons) : 1;
+                if (rel < 1e-8) {
+                    s.active[k] = 0;
+                    continue;
+                }
+                s.prev_ons[k] = ons;
+            }
+            // :731 pow(rz, -1): the correctly rounded reciprocal; glibc's pow
+            // differs from it by one ulp on ~0.1% of inputs (tests/powm1_check.c)
+            double bt = 1.0 / s.rz[k];
+            bt *= rz_new;                 // :736
+            s.rz[k] = rz_new;
+            const double rel_err = sqrt(rr) / sqrt(s.vv[k]);  // :742-744
+            if (rel_err < s.tol) {                            // :750
+                s.active[k] = 0;
+                continue;
+            }
+            s.beta[k] = bt;
+            any = 1;
+        }
+        s.any = any;
+        *cs = s;
+    }
+    // the mirror (mapped host memory) written through and drained, then the
+    // flag: the host reads the mirror after the flag (no release fence, which
+    // would write back this XCD's whole L2 first)
+    if (mirror) {
+        CgMirror* m = mirror + (it & 1);
+        __hip_atomic_store(&m->seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&m->any, s.any, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#pragma unroll
+        for (int k = 0; k < kMaxRhs; ++k)
+            __hip_atomic_store(&m->iters[k], s.iters[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    if (flag) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+__device__ inline void cg_decide_body(CgState* cs, const double* red, int it, CgMirror* mirror, unsigned long long* flag,
+                                      unsigned long long seq) {
+    double r[3 * kMaxRhs];
+    const int K = cs->K;
+#pragma unroll
+    for (int q = 0; q < 3 * kMaxRhs; ++q) r[q] = q < 3 * K ? red[q] : 0.0;
+    cg_decide_vals(cs, r, it, mirror, flag, seq);
+}
+
 }  // namespace vk

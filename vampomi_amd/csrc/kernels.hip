@@ -1487,48 +1487,6 @@ hipError_t cg_start_from(const CgState& init, const double* sums, CgState* dst, 
     return hipGetLastError();
 }
 
-// one thread: the host loop of vamp::precondCG_solver after each step's sums
-__device__ void cg_decide_body(CgState* cs, const double* red, int it, CgMirror* mirror, unsigned long long* flag,
-                               unsigned long long seq) {
-    if (cs->any) {
-        int any = 0;
-        for (int k = 0; k < cs->K; ++k) {
-            if (!cs->active[k]) continue;
-            cs->iters[k] = it + 1;
-            const double rz_new = red[3 * k], rr = red[3 * k + 1], vmu = red[3 * k + 2];
-            if (cs->onsager[k]) {  // :708-726
-                const double ons = cs->gam2 * vmu;
-                const double rel = ons != 0 ? fabs((ons - cs->prev_ons[k]) / ons) : 1;
-                if (rel < 1e-8) {
-                    cs->active[k] = 0;
-                    continue;
-                }
-                cs->prev_ons[k] = ons;
-            }
-            // :731 pow(rz, -1): the correctly rounded reciprocal; glibc's pow
-            // differs from it by one ulp on ~0.1% of inputs (tests/powm1_check.c)
-            double bt = 1.0 / cs->rz[k];
-            bt *= rz_new;                 // :736
-            cs->rz[k] = rz_new;
-            const double rel_err = sqrt(rr) / sqrt(cs->vv[k]);  // :742-744
-            if (rel_err < cs->tol) {                            // :750
-                cs->active[k] = 0;
-                continue;
-            }
-            cs->beta[k] = bt;
-            any = 1;
-        }
-        cs->any = any;
-    }
-    if (mirror) {
-        CgMirror* m = mirror + (it & 1);
-        m->seq = seq;
-        m->any = cs->any;
-        for (int k = 0; k < kMaxRhs; ++k) m->iters[k] = cs->iters[k];
-    }
-    if (flag) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
 __global__ void cg_decide_kernel(CgState* cs, const double* __restrict__ red, int it, CgMirror* mirror,
                                  unsigned long long* flag, unsigned long long seq) {
     if (threadIdx.x == 0) cg_decide_body(cs, red, it, mirror, flag, seq);
