@@ -106,12 +106,23 @@ __device__ bool red_finish(const RedOut& ro, int nq, double* /*lds4*/) {
         }
         __syncthreads();
         if (threadIdx.x == 0)
-            for (int c = 0; c < nc; ++c) ro.out[q0 + c] = ((lds[c] + lds[8 + c]) + lds[16 + c]) + lds[24 + c];
+            for (int c = 0; c < nc; ++c) {
+                const double v = ((lds[c] + lds[8 + c]) + lds[16 + c]) + lds[24 + c];
+                if (ro.flag)  // mapped host memory: written through, drained before the flag below
+                    __hip_atomic_store(ro.out + q0 + c, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                else
+                    ro.out[q0 + c] = v;
+            }
     }
     if (threadIdx.x == 0) {
         __hip_atomic_store(ro.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        // host completion flag: the results above are visible to the host first
-        if (ro.flag) __hip_atomic_store(ro.flag, ro.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        // host completion flag, after the results above have landed (drained
+        // write-through stores: no release fence, which would first write back
+        // this XCD's whole L2, MI355X_MICROARCH.md)
+        if (ro.flag) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(ro.flag, ro.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
     return true;
 }
