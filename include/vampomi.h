@@ -320,9 +320,10 @@ vampomi_status vampomi_dev_op_plan(int64_t N, int64_t M, int cus, int variant, i
 /* Device bytes the context of `rank` (of nranks, markers split by
  * vampomi_divide_work) allocates for a VAMP run on N samples and Mt markers
  * with `cus` compute units: the shard, marker statistics, scratch, the
- * one-pass operator's buffers, the run state (probit != 0: the probit model's
- * too) and, with writer != 0, the per-iteration output writer.  No device
- * needed; RCCL's buffers and the HIP runtime are not included. */
+ * one-pass operator's buffers and the run state (probit != 0: the probit
+ * model's too); the per-iteration output writer stages in pinned host memory
+ * (`writer` is kept for the ABI and ignored).  No device needed; RCCL's
+ * buffers and the HIP runtime are not included. */
 vampomi_status vampomi_dev_mem_plan(int64_t N, int64_t Mt, int nranks, int rank, int cus, int probit, int writer,
                                     int64_t* bytes);
 /* One application of the one-pass CG operator (K <= 2 systems, one rank),

@@ -3,9 +3,16 @@
  * hot path.  TEST INFRASTRUCTURE ONLY (see vamp_oracle.h header): tests/,
  * __graft_entry__.smoke() and bench.py's cpu_baseline leg are the only users.
  *
- * PARITY UNPINNED — the reference is unbuildable here (Boost absent) and ships
- * no fixtures; this file restates it function by function with file:line
- * citations into /root/reference/src.  Deviations P1/P2: see vamp_oracle.h.
+ * Parity pins, by part:
+ *  - the OPERATORS (A.x, A^T.u, marker statistics, read_phen) are pinned to
+ *    the reference itself: its own src/data.cpp, compiled where it lies
+ *    (oracle/Makefile target ref), on the reference-written data_sim.py files
+ *    and a generated problem (tests/test_ref_pin.py, tests/golden/ref_data_pin.npz);
+ *  - the ITERATION (g1/g1d, EM, PCG, Onsager, noise precision, probit) is
+ *    parity unpinned: src/vamp.cpp / vamp_probit.cpp need Boost, absent here,
+ *    so no reference-run vector exists; this file restates them function by
+ *    function with file:line citations into /root/reference/src.
+ * Deviations P1/P2: see vamp_oracle.h.
  *
  * Determinism: every reduction is blocked with a fixed block size and summed
  * in block order, so results do not depend on the OpenMP thread count.

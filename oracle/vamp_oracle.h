@@ -5,11 +5,17 @@
  * bench.py's cpu_baseline leg may load this library, and only as the checker
  * (or the timed CPU baseline), never as the product path.
  *
- * PARITY UNPINNED: the reference (medical-genomics-group/VAMPomi @ 2025-07-11)
- * cannot be built in this image (it #includes Boost.Math / Boost.uBLAS /
- * Boost.StringAlgo, which are absent, and its published linear path indexes
- * two never-sized vectors at src/vamp.cpp:70,77,204-205), and it ships no
- * tests, fixtures or golden vectors.  This restatement follows the reference
+ * Pinning, by part:
+ *  - OPERATORS pinned to the reference: its src/data.cpp (no Boost) builds here
+ *    where it lies (oracle/Makefile target ref -> oracle/_ref/ref_data), and
+ *    this file's A.x, A^T.u, marker statistics and read_phen reproduce its
+ *    outputs (tests/test_ref_pin.py: A.x bit-exact, the rest <= 4e-15);
+ *  - ITERATION PARITY UNPINNED: the reference's src/vamp.cpp / vamp_probit.cpp
+ *    (medical-genomics-group/VAMPomi @ 2025-07-11) cannot be built in this
+ *    image (Boost.Math / Boost.uBLAS / Boost.StringAlgo are absent, and the
+ *    published linear path indexes two never-sized vectors at
+ *    src/vamp.cpp:70,77,204-205), and it ships no tests, fixtures or golden
+ *    vectors.  This restatement follows the reference
  * source line by line (citations on every function) with two documented
  * deviations that the reference itself needs to be runnable at all:
  *   P1  x1_hat and r1 are sized M (the commented-out lines src/vamp.cpp:70,77);

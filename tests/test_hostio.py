@@ -108,7 +108,8 @@ def test_cli_rendezvous_never_reads_an_earlier_jobs_file(harness, tmp_path):
 
     def env(**kw):
         e = {k: v for k, v in os.environ.items()
-             if k not in ("VAMPOMI_RUN_ID", "TORCHELASTIC_RUN_ID", "MASTER_ADDR", "MASTER_PORT")}
+             if k not in ("VAMPOMI_RUN_ID", "TORCHELASTIC_RUN_ID", "MASTER_ADDR", "MASTER_PORT", "PMIX_NAMESPACE",
+                          "OMPI_MCA_ess_base_jobid", "PMI_KVSNAME", "SLURM_JOB_ID", "SLURM_STEP_ID")}
         e.update(kw)
         return e
 
@@ -132,10 +133,24 @@ def test_cli_rendezvous_never_reads_an_earlier_jobs_file(harness, tmp_path):
     assert get(0, 2000, TORCHELASTIC_RUN_ID="t3") == "job-three"
     pub("job-four", MASTER_ADDR="127.0.0.1", MASTER_PORT="29511")
     assert get(0, 300, MASTER_ADDR="127.0.0.1", MASTER_PORT="29512") == "TIMEOUT"
+    # the MPI / PMIx job namespace and slurm's job.step too
+    pub("job-five", PMIX_NAMESPACE="ns1")
+    assert get(0, 300, PMIX_NAMESPACE="ns2") == "TIMEOUT"
+    assert get(0, 2000, PMIX_NAMESPACE="ns1") == "job-five"
+    pub("job-six", SLURM_JOB_ID="77", SLURM_STEP_ID="0")
+    assert get(0, 300, SLURM_JOB_ID="77", SLURM_STEP_ID="1") == "TIMEOUT"
     # no nonce at all: a file older than the job is ignored
     pub("old")
     assert get(time.time() + 5, 300) == "TIMEOUT"
-    assert get(time.time() - 60, 2000) == "old"
+    assert get(time.time() - 60, 2000) == "old"  # (accepted once it is still there 3 s later)
+    # ... and a stale file inside the time window that this job's rank 0
+    # replaces while a reader looks at it: the reader takes the new id
+    pub("stale")
+    rd = subprocess.Popen([harness, "rdzv-get", path, str(time.time() - 60), "8000"], stdout=subprocess.PIPE,
+                          text=True, env=env())
+    time.sleep(1.0)
+    pub("fresh")
+    assert rd.communicate(timeout=30)[0].strip() == "fresh"
     # rank 0 removes the file after communicator init
     subprocess.run([harness, "rdzv-rm", path], check=True)
     assert not os.path.exists(path)

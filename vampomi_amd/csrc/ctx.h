@@ -46,6 +46,7 @@ struct CollScope {
     vampomi_ctx* prev;
 };
 struct VampRun;
+class IterWriter;
 struct LoopbackComm;  // engine.cpp: test-only in-process communicator
 
 struct TimedLaunch {
@@ -132,6 +133,7 @@ struct vampomi_ctx {
     vampomi_stats stats{};
 
     std::unique_ptr<VampRun> run;
+    std::unique_ptr<IterWriter> writer;  // per-iteration output (writer.h), created with the context
 
     vk::Shard shard() const { return vk::Shard{X, ld, N, M, mave, msig}; }
     vampomi_ctx();   // defined in vamp.cpp, where VampRun is complete

@@ -31,6 +31,7 @@
 
 #include "ctx.h"
 #include "hostio.h"
+#include "writer.h"
 
 // ---------------------------------------------------------------------------
 // errors and device memory
@@ -867,6 +868,7 @@ void release_ctx_resources(vampomi_ctx* c) {
         if (*e) (void)hipEventDestroy(*e), *e = nullptr;
     if (c->st2) (void)hipStreamDestroy(c->st2);
     c->st2 = nullptr;
+
     if (c->st) (void)hipStreamDestroy(c->st);
     c->st = nullptr;
 }
@@ -907,6 +909,8 @@ extern "C" vampomi_status vampomi_open(const vampomi_shard_desc* d, vampomi_ctx*
     STCHK(dev_alloc(&c->red_part, c->red_cap));
     STCHK(dev_alloc(&c->red_part2, c->red_cap));
     HIPCHK(hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking));
+    c->writer.reset(new IterWriter());  // the per-iteration output (writer.h): staging and thread now
+    STCHK(c->writer->open(c.get()));
     HIPCHK(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
     STCHK(dev_alloc(&c->scal, SL_TOTAL));
@@ -1672,7 +1676,7 @@ extern "C" vampomi_status vampomi_dev_mem_plan(int64_t N, int64_t Mt, int nranks
         for (int q = 0; q < 3; ++q) add(ld, 8);
         for (int q = 0; q < 3; ++q) add(Mx, 8);
     }
-    if (writer) add(2 * Mx, 8), add(2 * Mx, 8);
+    (void)writer;  // the writer's staging is pinned host memory (writer.h), allocated with every context
     *bytes = total;
     return VAMPOMI_OK;
 }

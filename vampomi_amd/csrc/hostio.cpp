@@ -144,10 +144,16 @@ bool csv_write_row(const std::string& path, int it, const double* vals, int n) {
 static const char kRdzvMagic[] = "VAMPOMI-RDZV1";
 
 std::string rdzv_nonce() {
-    for (const char* v : {"VAMPOMI_RUN_ID", "TORCHELASTIC_RUN_ID"}) {
+    // a job id every rank of the job sees: ours, torchrun's, the MPI / PMIx
+    // namespace (mpirun), slurm's job and step
+    for (const char* v : {"VAMPOMI_RUN_ID", "TORCHELASTIC_RUN_ID", "PMIX_NAMESPACE", "OMPI_MCA_ess_base_jobid",
+                          "PMI_KVSNAME"}) {
         const char* e = std::getenv(v);
         if (e && *e) return std::string(v) + "=" + e;
     }
+    const char* sj = std::getenv("SLURM_JOB_ID");
+    const char* ss = std::getenv("SLURM_STEP_ID");
+    if (sj && *sj) return std::string("slurm=") + sj + "." + (ss ? ss : "");
     const char* a = std::getenv("MASTER_ADDR");
     const char* p = std::getenv("MASTER_PORT");
     if (a && p && *a && *p) return std::string("master=") + a + ":" + p;
@@ -183,8 +189,25 @@ static bool rdzv_try(const std::string& path, const std::string& nonce, double n
 bool rdzv_fetch(const std::string& path, const std::string& nonce, double not_before, void* id, int nbytes,
                 int timeout_ms) {
     const auto t0 = std::chrono::steady_clock::now();
+    std::vector<unsigned char> first((size_t)nbytes), again((size_t)nbytes);
     for (;;) {
-        if (rdzv_try(path, nonce, not_before, id, nbytes)) return true;
+        if (rdzv_try(path, nonce, not_before, first.data(), nbytes)) {
+            if (!nonce.empty()) {
+                std::memcpy(id, first.data(), (size_t)nbytes);
+                return true;
+            }
+            // No job id: a file left by an earlier job whose rank 0 died before
+            // removing it could pass the time window.  Rank 0 of THIS job
+            // replaces any such file as it starts; accept only an id that is
+            // still there, unchanged, 3 s later.
+            std::this_thread::sleep_for(std::chrono::seconds(3));
+            if (rdzv_try(path, nonce, not_before, again.data(), nbytes) &&
+                std::memcmp(first.data(), again.data(), (size_t)nbytes) == 0) {
+                std::memcpy(id, again.data(), (size_t)nbytes);
+                return true;
+            }
+            continue;
+        }
         if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(timeout_ms)) return false;
         std::this_thread::sleep_for(std::chrono::milliseconds(50));
     }

@@ -37,11 +37,12 @@ std::string csv_format_row(int it, const double* vals, int n);
 
 // Rendezvous file of a multi-process CLI job (replaces mpirun's bootstrap):
 // rank 0 publishes the RCCL id, the other ranks fetch it.  The file carries a
-// run nonce (VAMPOMI_RUN_ID, else torchrun's TORCHELASTIC_RUN_ID, else
-// MASTER_ADDR:MASTER_PORT); a reader accepts only a file with its own nonce,
-// and without a nonce only one written after not_before (seconds since the
-// epoch), so a file left by an earlier job into the same directory is never
-// read.  Rank 0 removes the file once the communicator is up (rdzv_remove).
+// run nonce (VAMPOMI_RUN_ID, torchrun's TORCHELASTIC_RUN_ID, the MPI / PMIx
+// job namespace, slurm's job.step, else MASTER_ADDR:MASTER_PORT); a reader
+// accepts only a file with its own nonce.  Without any of them: only a file
+// written after not_before (seconds since the epoch) whose id is still there,
+// unchanged, 3 s later (rank 0 of a new job replaces a stale file as it
+// starts).  Rank 0 removes the file once the communicator is up (rdzv_remove).
 std::string rdzv_nonce();
 bool rdzv_publish(const std::string& path, const std::string& nonce, const void* id, int nbytes);
 bool rdzv_fetch(const std::string& path, const std::string& nonce, double not_before, void* id, int nbytes,

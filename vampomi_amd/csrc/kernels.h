@@ -259,6 +259,8 @@ hipError_t mul_scalar(int64_t n, const double* x, double a, double* out, hipStre
 
 // ---- host completion flag (system-scope store into mapped host memory) -------
 hipError_t signal_host(unsigned long long* flag, unsigned long long seq, hipStream_t st);
+// the same with a relaxed store (what it announces was written by earlier kernels)
+hipError_t post_flag(unsigned long long* flag, unsigned long long seq, hipStream_t st);
 // copies a[0..na) -> ha and b[0..nb) -> hb (mapped host memory), then stores seq into flag
 hipError_t publish_host(const double* a, int na, double* ha, const double* b, int nb, double* hb,
                         unsigned long long* flag, unsigned long long seq, hipStream_t st);

@@ -2021,6 +2021,18 @@ __global__ void signal_kernel(unsigned long long* flag, unsigned long long seq) 
     __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// a sequence number into mapped host memory after everything earlier on the
+// stream (relaxed: the writes it announces were made by earlier kernels,
+// complete at their end); the iteration writer's "slot landed" word
+__global__ void post_flag_kernel(unsigned long long* flag, unsigned long long seq) {
+    __hip_atomic_store(flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+hipError_t post_flag(unsigned long long* flag, unsigned long long seq, hipStream_t st) {
+    hipLaunchKernelGGL(post_flag_kernel, dim3(1), dim3(1), 0, st, flag, seq);
+    return hipGetLastError();
+}
+
 hipError_t signal_host(unsigned long long* flag, unsigned long long seq, hipStream_t st) {
     hipLaunchKernelGGL(signal_kernel, dim3(1), dim3(1), 0, st, flag, seq);
     return hipGetLastError();

@@ -37,9 +37,9 @@ struct VampRun {
     // rank-locally; a rank that stopped there would leave the others waiting)
     bool io_err = false;
     std::string io_msg;
-    // per-iteration vectors and CSV rows, written off the critical path
-    // (writer.h); created on the first iteration that writes or keeps history
-    std::unique_ptr<IterWriter> writer;
+    // per-iteration vectors and CSV rows, written off the critical path: the
+    // context's writer (writer.h) while this run writes files or keeps history
+    IterWriter* writer = nullptr;
     Mixture mix, mix_next;
     bool have_next = false;  // x1n, alpha1_next, mix_next, z1 (nb3 slot 2), atx0 valid
     double gam1 = 0, gam2 = 0, gamw = 0;

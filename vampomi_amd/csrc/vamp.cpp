@@ -38,7 +38,7 @@
 #include "run.h"
 
 VampRun::~VampRun() {
-    writer.reset();  // drains: its kernels read x1 / r1, its thread writes the caller's history arrays
+    if (writer) writer->drain(nullptr);  // its kernels read x1 / r1, its thread writes the caller's history arrays
     for (double** p : {&r1, &x1, &x1p, &x1n, &x1d, &r2, &x2, &bern, &invQ, &v, &atxy, &ts, &tmpM, &atx0, &z1buf,
                        &nb3, &nsc, &ax2, &p1, &p2, &z1h, &x1s, &x1sn, &x2s})
         dev_free(*p);
@@ -49,6 +49,7 @@ vampomi_ctx::vampomi_ctx() = default;
 
 vampomi_ctx::~vampomi_ctx() {
     run.reset();
+    writer.reset();  // drained, its thread joined, before the staging buffers go
     release_ctx_resources(this);
 }
 
@@ -211,6 +212,9 @@ vampomi_status upload_or_zero(vampomi_ctx* c, double* dst, const double* host, i
     return VAMPOMI_OK;
 }
 
+static bool keeps_hist(const VampRun& R) { return R.res && (R.res->x1_hist || R.res->r1_hist); }
+vampomi_status ensure_writer(vampomi_ctx* c, VampRun& R);
+
 static vampomi_status vamp_alloc(vampomi_ctx* c, VampRun& R) {
     const size_t M = (size_t)std::max<int64_t>(c->M, 1), ld = (size_t)c->ld;
     for (double** p : {&R.r1, &R.x1, &R.x1p, &R.x1n, &R.x1d, &R.r2, &R.x2, &R.bern, &R.invQ, &R.v, &R.atxy, &R.ts,
@@ -258,6 +262,7 @@ extern "C" vampomi_status vampomi_vamp_begin(vampomi_ctx* c, const vampomi_param
     R.gamw = 1.0 / (1.0 - p->h2);  // src/main_meth.cpp:52
     R.gam2 = 0;
     STCHK(vamp_alloc(c, R));
+    if (R.write || keeps_hist(R)) STCHK(ensure_writer(c, R));  // its pinned buffers before iteration 1
     STCHK(upload_or_zero(c, R.ts, p->true_signal, c->M));
     // P1 (src/vamp.cpp:70-79): x1_hat = r1 = x1hat_init / sqrt(N)
     std::vector<double> h((size_t)std::max<int64_t>(c->M, 1), 0.0);
@@ -310,13 +315,12 @@ extern "C" vampomi_status vampomi_vamp_begin(vampomi_ctx* c, const vampomi_param
     return VAMPOMI_OK;
 }
 
-static bool keeps_hist(const VampRun& R) { return R.res && (R.res->x1_hist || R.res->r1_hist); }
-
-static vampomi_status ensure_writer(vampomi_ctx* c, VampRun& R) {
+vampomi_status ensure_writer(vampomi_ctx* c, VampRun& R) {
     if (R.writer) return VAMPOMI_OK;
-    std::unique_ptr<IterWriter> w(new IterWriter());
-    STCHK(w->open(c));
-    R.writer = std::move(w);
+    if (!c->writer) return fail(VAMPOMI_ERR_STATE, "context without an iteration writer");
+    c->writer->drain(nullptr);  // (an earlier run that ended with an error)
+    c->writer->clear_error();
+    R.writer = c->writer.get();
     return VAMPOMI_OK;
 }
 

@@ -1,24 +1,25 @@
 // writer.cpp — see writer.h.
 #include "writer.h"
 
+#include <chrono>
 #include <cmath>
 #include <cstring>
 
 #include "hostio.h"
 
 vampomi_status IterWriter::open(vampomi_ctx* c) {
-    device_ = c->device;
     M_ = c->M;
     S_ = c->S;
     sqrtN_ = std::sqrt((double)c->N);
+    st_ = c->st;
     const size_t n = 2 * (size_t)std::max<int64_t>(M_, 1);
-    HIPCHK(hipStreamCreateWithFlags(&cs_, hipStreamNonBlocking));
     for (int k = 0; k < kSlots; ++k) {
-        STCHK(dev_alloc(&dbuf_[k], n));
-        HIPCHK(hipHostMalloc((void**)&hbuf_[k], n * 8, hipHostMallocDefault));
-        HIPCHK(hipEventCreateWithFlags(&ev_ready_[k], hipEventDisableTiming));
-        HIPCHK(hipEventCreateWithFlags(&ev_copied_[k], hipEventDisableTiming));
+        HIPCHK(hipHostMalloc((void**)&hbuf_[k], n * 8, hipHostMallocMapped | hipHostMallocCoherent));
+        HIPCHK(hipHostGetDevicePointer((void**)&dbuf_[k], hbuf_[k], 0));
     }
+    HIPCHK(hipHostMalloc((void**)&hflag_, 64, hipHostMallocMapped | hipHostMallocCoherent));
+    std::memset(hflag_, 0, 64);
+    HIPCHK(hipHostGetDevicePointer((void**)&dflag_, hflag_, 0));
     th_ = std::thread(&IterWriter::loop, this);
     return VAMPOMI_OK;
 }
@@ -32,13 +33,9 @@ IterWriter::~IterWriter() {
         cv_.notify_all();
         th_.join();  // the loop leaves only with the queue empty
     }
-    for (int k = 0; k < kSlots; ++k) {
-        if (ev_ready_[k]) (void)hipEventDestroy(ev_ready_[k]);
-        if (ev_copied_[k]) (void)hipEventDestroy(ev_copied_[k]);
+    for (int k = 0; k < kSlots; ++k)
         if (hbuf_[k]) (void)hipHostFree(hbuf_[k]);
-        dev_free(dbuf_[k]);
-    }
-    if (cs_) (void)hipStreamDestroy(cs_);
+    if (hflag_) (void)hipHostFree(hflag_);
 }
 
 vampomi_status IterWriter::submit_vectors(vampomi_ctx* c, const double* x1, const double* r1, const std::string& px,
@@ -51,20 +48,17 @@ vampomi_status IterWriter::submit_vectors(vampomi_ctx* c, const double* x1, cons
         next_ = (next_ + 1) % kSlots;
         busy_[k] = true;
     }
-    auto undo = [&](vampomi_status s) {
+    const unsigned long long seq = ++seq_;
+    hipError_t e = vk::div2_scalar(M_, x1, r1, sqrtN_, dbuf_[k], c->st);
+    if (e == hipSuccess) e = vk::post_flag(dflag_, seq, c->st);
+    if (e != hipSuccess) {
         std::lock_guard<std::mutex> lk(mu_);
         busy_[k] = false;
-        return s;
-    };
-    const size_t bytes = 2 * (size_t)M_ * 8;
-    hipError_t e = vk::div2_scalar(M_, x1, r1, sqrtN_, dbuf_[k], c->st);
-    if (e == hipSuccess) e = hipEventRecord(ev_ready_[k], c->st);
-    if (e == hipSuccess) e = hipStreamWaitEvent(cs_, ev_ready_[k], 0);
-    if (e == hipSuccess && bytes) e = hipMemcpyAsync(hbuf_[k], dbuf_[k], bytes, hipMemcpyDeviceToHost, cs_);
-    if (e == hipSuccess) e = hipEventRecord(ev_copied_[k], cs_);
-    if (e != hipSuccess) return undo(fail(VAMPOMI_ERR_HIP, std::string("iteration writer: ") + hipGetErrorString(e)));
+        return fail(VAMPOMI_ERR_HIP, std::string("iteration writer: ") + hipGetErrorString(e));
+    }
     Job j;
     j.slot = k;
+    j.seq = seq;
     j.px = px;
     j.pr = pr;
     j.hx = hist_x;
@@ -87,6 +81,12 @@ void IterWriter::submit_host(std::function<bool(std::string*)> fn) {
         ++pending_;
     }
     cv_.notify_all();
+}
+
+void IterWriter::clear_error() {
+    std::lock_guard<std::mutex> lk(mu_);
+    err_ = false;
+    msg_.clear();
 }
 
 bool IterWriter::failed(std::string* msg) {
@@ -116,8 +116,28 @@ void IterWriter::finish(int slot, bool ok, const std::string& msg) {
     cv_.notify_all();
 }
 
+// the stream has stored seq (its staging slot has landed); false if the
+// stream failed first or nothing arrived within 10 minutes
+bool IterWriter::wait_landed(unsigned long long seq, std::string* msg) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned spin = 0;; ++spin) {
+        if (__atomic_load_n(hflag_, __ATOMIC_ACQUIRE) >= seq) return true;
+        if ((spin & 63) == 63) {
+            const hipError_t e = hipStreamQuery(st_);
+            if (e != hipSuccess && e != hipErrorNotReady) {
+                *msg = std::string("iteration writer: ") + hipGetErrorString(e);
+                return false;
+            }
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::minutes(10)) {
+                *msg = "iteration writer: the device did not deliver an iteration's output within 10 minutes";
+                return false;
+            }
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+}
+
 void IterWriter::loop() {
-    (void)hipSetDevice(device_);
     for (;;) {
         Job j;
         {
@@ -131,20 +151,14 @@ void IterWriter::loop() {
         bool ok = true;
         if (j.slot < 0) {
             ok = j.fn(&msg);
-        } else {
-            const hipError_t e = hipEventSynchronize(ev_copied_[j.slot]);
-            if (e != hipSuccess) {
+        } else if ((ok = wait_landed(j.seq, &msg))) {
+            const double* hx = hbuf_[j.slot];
+            const double* hr = hx + M_;
+            if (j.hx) std::memcpy(j.hx, hx, (size_t)M_ * 8);
+            if (j.hr) std::memcpy(j.hr, hr, (size_t)M_ * 8);
+            if (!j.px.empty() && !(vio::store_vec(j.px, hx, S_, M_) && vio::store_vec(j.pr, hr, S_, M_))) {
                 ok = false;
-                msg = std::string("iteration writer: ") + hipGetErrorString(e);
-            } else {
-                const double* hx = hbuf_[j.slot];
-                const double* hr = hx + M_;
-                if (j.hx) std::memcpy(j.hx, hx, (size_t)M_ * 8);
-                if (j.hr) std::memcpy(j.hr, hr, (size_t)M_ * 8);
-                if (!j.px.empty() && !(vio::store_vec(j.px, hx, S_, M_) && vio::store_vec(j.pr, hr, S_, M_))) {
-                    ok = false;
-                    msg = "cannot write iteration vectors " + j.px;
-                }
+                msg = "cannot write iteration vectors " + j.px;
             }
         }
         finish(j.slot, ok, msg);
