@@ -277,7 +277,8 @@ typedef struct {
     int64_t host_syncs;
     vampomi_kernel_stat loo;      /* association-test pass (vampomi_assoc_loo) */
     vampomi_kernel_stat op;       /* one-pass CG operator (A^T q and A d, batch_rhs 4) */
-    vampomi_kernel_stat op_k[4];
+    vampomi_kernel_stat op_k[4];  /* index K-1 for K = 1, 2 systems; index 3: the head-start launch
+                                     (one system + 3 plain A.x right-hand sides, pcg.cpp) */
     vampomi_kernel_stat coll;     /* RCCL all-reduces (several ranks): launches, bytes; with timing
                                      on, HIP events on the stream around each (its time on the
                                      stream, waits for the slowest rank included) */
@@ -300,7 +301,10 @@ vampomi_status vampomi_reset_stats(vampomi_ctx* ctx);
  * K*N fits the LDS, else teams of workgroups; 0 forces the whole-column
  * kernel, T*10 + c (c < 10) or 1000 + T*100 + c the team kernel with team size T and configuration c,
  * vampomi_amd/csrc/atax_team.hip).  which = 4: the side stream of the
- * prefetched EM/denoiser, 0 off, 1 on (default: on with several ranks). */
+ * prefetched EM/denoiser, 0 off, 1 on (default: on with several ranks).
+ * which = 5: the CG head start of the linear model (the Onsager solve's first
+ * step in the pass that starts the x2 solve, pcg.cpp), 0 off, 1 on (default
+ * on; VAMPOMI_HEADSTART=0 turns it off at vampomi_open). */
 vampomi_status vampomi_dev_set_variant(vampomi_ctx* ctx, int which, int variant);
 /* average device time (HIP events) of `reps` back-to-back launches, K RHS */
 vampomi_status vampomi_dev_time_pass(vampomi_ctx* ctx, int which, int K, int reps, double* avg_ms);

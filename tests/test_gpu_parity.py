@@ -88,10 +88,14 @@ def test_lmmse_pcg_denoise():
         assert abs(sd - gdx.sum()) <= 1e-12 * abs(gdx.sum())
 
 
-def _gpu_vamp(X, y, beta, Mt, **kw):
+def _gpu_vamp(X, y, beta, Mt, headstart=None, op_variant=None, **kw):
     N = X.shape[1]
     with va.Data(N, Mt) as d:
         d.load_meth(X)
+        if headstart is not None:
+            d.set_variant(5, 1 if headstart else 0)
+        if op_variant is not None:
+            d.set_variant(3, op_variant)
         d.set_phen(y, standardize=False)
         v = va.Vamp(d, va.VampOptions(**kw), true_signal=beta)
         x1 = v.infere(keep_hist=True)
@@ -207,10 +211,64 @@ def test_onepass_mode(N, Mt, its, kind):
     assert max(errs) <= 1e-11
     assert np.allclose(np.array(a["params"]), np.array(b["params"]), rtol=1e-11, atol=0)
     assert np.allclose(np.array(a["metrics"]), np.array(b["metrics"]), rtol=1e-10, atol=1e-13, equal_nan=True)
-    assert a["a_passes_exec"] == 1 + sum(1 + max(p, q) for p, q in zip(a["cg_iters"], a["ons_iters"]))  # + A^T y
+    assert a["a_passes_exec"] == 1 + _onepass_passes(a["cg_iters"], a["ons_iters"])  # + A^T y
     assert a["a_passes_ref"] == b["a_passes_ref"]
     ref = O.vamp_infere(X, y, Mt, true_signal=beta, max_iter=its, stop_criteria_thr=0.0)
     _assert_parity(a, ref)
+
+
+def _onepass_passes(cg, ons, headstart=True):
+    """Executed passes of the one-pass schedule: 1 + max(k1, k2) per
+    iteration; with the head start, from iteration 2 on, the Onsager solve's
+    first step rides in the pass that starts the x2 solve: 1 + max(k1, k2 - 1)."""
+    return sum(1 + (max(p, q - 1) if headstart and i > 0 else max(p, q)) for i, (p, q) in enumerate(zip(cg, ons)))
+
+
+@pytest.mark.parametrize("N,Mt,its,kind,opv", [(1000, 2000, 30, 0, None), (4099, 3001, 12, 1, None),
+                                                (301, 517, 12, 0, None), (10000, 2500, 10, 0, None),
+                                                (3000, 2000, 10, 1, 1000 + 2 * 100 + 7),
+                                                (3000, 2000, 10, 0, 1000 + 4 * 100 + 9),
+                                                (1000, 2000, 6, 0, 1000 + 1 * 100 + 0)])
+def test_headstart(N, Mt, its, kind, opv):
+    """The head start (pcg.cpp): the Onsager solve takes its first CG step in
+    the pass that starts the x2 solve, from A.bern formed one iteration early.
+    Every step is still the reference's: the same CG, Onsager and mixture
+    counts as without it, values within rounding (the plain products are
+    summed in another order), within the parity bar of the oracle, and
+    max(k1, k2 - 1) + 1 passes per iteration from iteration 2 on.  Team plans
+    forced by opv cover the hand-off kernel at small N."""
+    X, y, beta = _problem(N, Mt, kind=kind)
+    a = _gpu_vamp(X, y, beta, Mt, max_iter=its, stop_criteria_thr=0.0, headstart=True, op_variant=opv)
+    b = _gpu_vamp(X, y, beta, Mt, max_iter=its, stop_criteria_thr=0.0, headstart=False, op_variant=opv)
+    errs = [max(relerr(a["x1_hist"][k], b["x1_hist"][k]), relerr(a["r1_hist"][k], b["r1_hist"][k]))
+            for k in range(its)]
+    print("head start vs none, max rel err per iteration:", ["%.1e" % e for e in errs])
+    assert a["cg_iters"] == b["cg_iters"] and a["ons_iters"] == b["ons_iters"] and a["L"] == b["L"]
+    assert max(errs) <= 1e-11
+    assert np.allclose(np.array(a["params"]), np.array(b["params"]), rtol=1e-11, atol=0)
+    assert np.allclose(np.array(a["metrics"]), np.array(b["metrics"]), rtol=1e-10, atol=1e-13, equal_nan=True)
+    assert a["a_passes_exec"] == 1 + _onepass_passes(a["cg_iters"], a["ons_iters"], True)
+    assert b["a_passes_exec"] == 1 + _onepass_passes(b["cg_iters"], b["ons_iters"], False)
+    assert a["a_passes_ref"] == b["a_passes_ref"]
+    ref = O.vamp_infere(X, y, Mt, true_signal=beta, max_iter=its, stop_criteria_thr=0.0)
+    _assert_parity(a, ref)
+
+
+def test_headstart_cg_limits():
+    """CG_max_iter reached inside the head start: the Onsager solve stops after
+    max_iter steps of its own (its first in the head-start pass), exactly as
+    without the head start; max_iter 1 and 2 included."""
+    N, Mt = 800, 1500
+    X, y, beta = _problem(N, Mt)
+    for cgmax in (1, 2, 3):
+        a = _gpu_vamp(X, y, beta, Mt, max_iter=5, stop_criteria_thr=0.0, CG_max_iter=cgmax, headstart=True)
+        b = _gpu_vamp(X, y, beta, Mt, max_iter=5, stop_criteria_thr=0.0, CG_max_iter=cgmax, headstart=False)
+        assert a["cg_iters"] == b["cg_iters"] and a["ons_iters"] == b["ons_iters"], cgmax
+        assert max(a["ons_iters"]) <= cgmax and max(a["cg_iters"]) <= cgmax
+        for k in range(5):
+            assert relerr(a["x1_hist"][k], b["x1_hist"][k]) <= 1e-11, (cgmax, k)
+        ref = O.vamp_infere(X, y, Mt, true_signal=beta, max_iter=5, stop_criteria_thr=0.0, CG_max_iter=cgmax)
+        _assert_parity(a, ref)
 
 
 def test_deterministic_repeat():

@@ -189,12 +189,18 @@ __device__ __forceinline__ void tm_publish_l2(unsigned long long* p, const v4u& 
     asm volatile("s_nop 4\n\tglobal_store_dwordx4 %0, %1, off\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
 }
 
-template <int K, int S, int F, int L, int P, bool COMM, int E, bool FMA>
-__global__ __launch_bounds__(kTmThreads) void atax_team_kernel(const double* __restrict__ X, int64_t ld, int64_t N,
-                                                               int64_t M, const double* __restrict__ mave,
-                                                               const double* __restrict__ msig, OpArgs a, int T,
-                                                               int TR, int ilv, const int* __restrict__ gate) {
+// KP > 0 (the head-start launch, pcg.cpp): KP plain right-hand sides ride
+// along, z_kp = A x_kp = sum_i (X_i - mave_i) * (msig_i * x_kp[i]) (data::Ax,
+// src/data.cpp:340-373): their coefficients are known when the column is
+// loaded, so the streaming waves accumulate them in the column's own step
+// (no hand-off), into partial slots K .. K+KP-1 of the team.
+template <int K, int S, int F, int L, int P, bool COMM, int E, bool FMA, int KP>
+__device__ __forceinline__ void atax_team_body(const double* __restrict__ X, int64_t ld, int64_t N, int64_t M,
+                                               const double* __restrict__ mave, const double* __restrict__ msig,
+                                               const OpArgs& a, int T, int TR, int ilv,
+                                               const int* __restrict__ gate) {
     if (gate && !*gate) return;
+    static_assert(K + KP <= kMaxRhs, "partial slots per team");
     // timing experiments (VAMPOMI_OP_DBG): with a hand-off only in a TM_DBG
     // build (the branches cost the hand-off wave's chain 2 % at the C3 shard);
     // T = 1 keeps them: at 252-256 VGPRs its schedule without them waits more
@@ -262,13 +268,13 @@ __global__ __launch_bounds__(kTmThreads) void atax_team_kernel(const double* __r
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             if (lane == 1 + k) scp = a.p.p[k];
-            if (lane == 1 + K + k && a.fuse) scp = a.z.p[k];
+            if (lane == 1 + K + k && ((a.fuse >> k) & 1)) scp = a.z.p[k];
         }
         scp += mb;  // column m (relative) is scp[m * cs]
         double bk[K], dpacc[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            bk[k] = a.fuse ? a.beta[k] : 0.0;
+            bk[k] = ((a.fuse >> k) & 1) ? a.beta[k] : 0.0;
             dpacc[k] = 0.0;
         }
         v4u pl[RING];
@@ -357,7 +363,7 @@ __global__ __launch_bounds__(kTmThreads) void atax_team_kernel(const double* __r
                             double t = sg * readlane_d(v, 32 * k);  // sigma_inv * dpa
                             t *= a.scale;                           // ATx[mloc] *= 1/sqrt(N)
                             double p = readlane_d(scv, 1 + k);
-                            if (a.fuse) p = readlane_d(scv, 1 + K + k) + bk[k] * p;  // p = z + beta p
+                            if ((a.fuse >> k) & 1) p = readlane_d(scv, 1 + K + k) + bk[k] * p;  // p = z + beta p
                             double val = t * a.tau;  // res[i] *= tau
                             val += a.gam2 * p;       // res[i] += gam2 * v[i]
                             tsc[k] = t;
@@ -426,7 +432,7 @@ __global__ __launch_bounds__(kTmThreads) void atax_team_kernel(const double* __r
                 if (jl + h < nrows) {
                     const int64_t j = r0 + jl + h;
                     q = a.ar.p[k][j] / a.diag;
-                    if (a.fuse) q = q + a.beta[k] * a.qo.p[k][j];
+                    if ((a.fuse >> k) & 1) q = q + a.beta[k] * a.qo.p[k][j];
                 }
                 q_lds[k * QS + jl + h] = q;
             }
@@ -434,15 +440,19 @@ __global__ __launch_bounds__(kTmThreads) void atax_team_kernel(const double* __r
     }
     double bk[K];
 #pragma unroll
-    for (int k = 0; k < K; ++k) bk[k] = a.fuse ? a.beta[k] : 0.0;
-    // per-lane source of the column's scalars: lane 0 mave, 1 msig, 2.. p_k, 2+K.. z_k
+    for (int k = 0; k < K; ++k) bk[k] = ((a.fuse >> k) & 1) ? a.beta[k] : 0.0;
+    // per-lane source of the column's scalars: lane 0 mave, 1 msig, 2.. p_k,
+    // 2+K.. z_k, 2+2K.. the plain right-hand sides x_kp
     const double* pkp = mave;
     if (lane == 1) pkp = msig;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         if (lane == 2 + k) pkp = a.p.p[k];
-        if (lane == 2 + K + k && a.fuse) pkp = a.z.p[k];
+        if (lane == 2 + K + k && ((a.fuse >> k) & 1)) pkp = a.z.p[k];
     }
+#pragma unroll
+    for (int k = 0; k < KP; ++k)
+        if (lane == 2 + 2 * K + k) pkp = a.px.p[k];
     pkp += mb;  // column m (relative) is pkp[m * cs]
     bool valid[S];
 #pragma unroll
@@ -457,6 +467,14 @@ __global__ __launch_bounds__(kTmThreads) void atax_team_kernel(const double* __r
     double dpacc[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) dpacc[k] = 0.0;
+    constexpr int KPA = KP > 0 ? KP : 1;
+    double accp[KPA][S][E];  // the plain right-hand sides' rows of A x
+#pragma unroll
+    for (int k = 0; k < KPA; ++k)
+#pragma unroll
+        for (int s = 0; s < S; ++s)
+#pragma unroll
+            for (int e = 0; e < E; ++e) accp[k][s][e] = 0.0;
 
     double xr[RING][S][E];
     double pk[RING];
@@ -480,6 +498,12 @@ __global__ __launch_bounds__(kTmThreads) void atax_team_kernel(const double* __r
     // slot is centred in place (x - mave), the form finish() uses
     auto dot = [&](int slot, int par) {
         const double mu = readlane_d(pk[slot], 0);
+        double cp[KPA];  // msig_i * x_kp[i]: Ax's (x - mave) * (msig * x_i)
+        if constexpr (KP > 0) {
+            const double sgp = readlane_d(pk[slot], 1);
+#pragma unroll
+            for (int k = 0; k < KP; ++k) cp[k] = sgp * readlane_d(pk[slot], 2 + 2 * K + k);
+        }
         double v[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) v[k] = 0.0;
@@ -493,6 +517,17 @@ __global__ __launch_bounds__(kTmThreads) void atax_team_kernel(const double* __r
             for (int e = 0; e < E; ++e) {
                 dx[e] = xr[slot][s][e] - me_;
                 xr[slot][s][e] = dx[e];
+            }
+            if constexpr (KP > 0) {
+#pragma unroll
+                for (int k = 0; k < KP; ++k)
+#pragma unroll
+                    for (int e = 0; e < E; ++e) {
+                        if constexpr (FMA)
+                            accp[k][s][e] = __builtin_fma(dx[e], cp[k], accp[k][s][e]);
+                        else
+                            accp[k][s][e] += dx[e] * cp[k];
+                    }
             }
 #pragma unroll
             for (int k = 0; k < K; ++k) {
@@ -545,7 +580,7 @@ __global__ __launch_bounds__(kTmThreads) void atax_team_kernel(const double* __r
                 double t = sg * tot[k];  // sigma_inv * dpa
                 t *= a.scale;            // ATx[mloc] *= 1/sqrt(N)
                 double p = readlane_d(pk[slot], 2 + k);
-                if (a.fuse) p = readlane_d(pk[slot], 2 + K + k) + bk[k] * p;  // p = z + beta p
+                if ((a.fuse >> k) & 1) p = readlane_d(pk[slot], 2 + K + k) + bk[k] * p;  // p = z + beta p
                 double val = t * a.tau;  // res[i] *= tau
                 val += a.gam2 * p;       // res[i] += gam2 * v[i]
                 if (own) {
@@ -617,6 +652,13 @@ __global__ __launch_bounds__(kTmThreads) void atax_team_kernel(const double* __r
 #pragma unroll
             for (int e = 0; e < E; ++e)
                 if (jl + e < nrows) dst[(int64_t)k * ld + jl + e] = acc[k][s][e];
+        if constexpr (KP > 0) {
+#pragma unroll
+            for (int k = 0; k < KP; ++k)
+#pragma unroll
+                for (int e = 0; e < E; ++e)
+                    if (jl + e < nrows) dst[(int64_t)(K + k) * ld + jl + e] = accp[k][s][e];
+        }
     }
     // <d_k, p_k>: each workgroup's sums over the columns it owns, in order
     // (COMM: the hand-off wave's, put before the barrier below); the last
@@ -628,6 +670,26 @@ __global__ __launch_bounds__(kTmThreads) void atax_team_kernel(const double* __r
         for (int k = 0; k < K; ++k) red_put(a.ro, (int64_t)blockIdx.x * K + k, dpacc[k]);
     }
     if (wave == 0) ticket_sum_blocks<K>(a.ro);
+}
+
+template <int K, int S, int F, int L, int P, bool COMM, int E, bool FMA>
+__global__ __launch_bounds__(kTmThreads) void atax_team_kernel(const double* __restrict__ X, int64_t ld, int64_t N,
+                                                               int64_t M, const double* __restrict__ mave,
+                                                               const double* __restrict__ msig, OpArgs a, int T,
+                                                               int TR, int ilv, const int* __restrict__ gate) {
+    atax_team_body<K, S, F, L, P, COMM, E, FMA, 0>(X, ld, N, M, mave, msig, a, T, TR, ilv, gate);
+}
+
+// the head-start launch: one operator system (the Onsager solve's first CG
+// step) and kTmPlain plain right-hand sides (pcg.cpp)
+static constexpr int kTmPlain = kOpPlain;
+template <int S, int F, int L, int P, bool COMM, int E, bool FMA>
+__global__ __launch_bounds__(kTmThreads) void atax_team_plain_kernel(const double* __restrict__ X, int64_t ld,
+                                                                     int64_t N, int64_t M,
+                                                                     const double* __restrict__ mave,
+                                                                     const double* __restrict__ msig, OpArgs a, int T,
+                                                                     int TR, int ilv, const int* __restrict__ gate) {
+    atax_team_body<1, S, F, L, P, COMM, E, FMA, kTmPlain>(X, ld, N, M, mave, msig, a, T, TR, ilv, gate);
 }
 
 // ---------------------------------------------------------------------------
@@ -670,13 +732,20 @@ bool team_plan(int64_t N, int64_t M, int cus, int T, int cfg, OpPlan* out) {
 }
 
 // occ != null: no launch, *occ = the workgroups of this instantiation one CU
-// holds at once (hipOccupancyMaxActiveBlocksPerMultiprocessor)
-template <int K, int S, int C>
+// holds at once (hipOccupancyMaxActiveBlocksPerMultiprocessor).  PL: the
+// head-start kernel (K = 1 operator system + kTmPlain plain right-hand sides)
+template <int K, int S, int C, bool PL>
 static void launch_tm(const Shard& s, const OpPlan& pl, const OpArgs& a, hipStream_t st, const Timing& tm,
                       const int* gate, int* occ) {
     constexpr TmCfg c = kTmCfg[C];
     constexpr int CW = c.comm ? 7 : 8;
-    auto kern = atax_team_kernel<K, S, c.F, c.L, c.P, c.comm, c.E, (bool)TM_FMA>;
+    static_assert(!PL || K == 1, "the head-start kernel has one operator system");
+    void (*kern)(const double*, int64_t, int64_t, int64_t, const double*, const double*, OpArgs, int, int, int,
+                 const int*);
+    if constexpr (PL)
+        kern = atax_team_plain_kernel<S, c.F, c.L, c.P, c.comm, c.E, (bool)TM_FMA>;
+    else
+        kern = atax_team_kernel<K, S, c.F, c.L, c.P, c.comm, c.E, (bool)TM_FMA>;
     const int64_t QS = tm_qstride(K, S, c.comm, c.E, std::min<int64_t>(pl.TR, s.N));
     const size_t lds = (size_t)(K * QS + 2 * CW * K + 2 * K) * sizeof(double);
     static std::once_flag once;  // more than 64 KiB of dynamic LDS must be allowed explicitly
@@ -692,55 +761,71 @@ static void launch_tm(const Shard& s, const OpPlan& pl, const OpArgs& a, hipStre
                           s.mave, s.msig, a, pl.T, pl.TR, c.ilv ? 1 : 0, gate);
 }
 
-template <int K, int C, int S>
+// the most loads per lane per column the head-start kernel is instantiated
+// for, per configuration (0: none): its 3 plain accumulators cost 12*S
+// registers beside the ring (register counts and spills checked with
+// tools/regcheck.sh)
+static constexpr int tm_plain_maxS(int cfg) {
+    return cfg == 0 ? 8 : cfg == 7 ? 3 : cfg == 9 ? 5 : 0;
+}
+
+template <int K, int C, int S, bool PL>
 static bool launch_tm_if(const Shard& s, const OpPlan& pl, const OpArgs& a, hipStream_t st, const Timing& tm,
                          const int* gate, int* occ) {
-    if constexpr (S <= kTmCfg[C].maxS) {
-        launch_tm<K, S, C>(s, pl, a, st, tm, gate, occ);
+    if constexpr (S <= (PL ? tm_plain_maxS(C) : kTmCfg[C].maxS)) {
+        launch_tm<K, S, C, PL>(s, pl, a, st, tm, gate, occ);
         return true;
     }
     return false;
 }
 
-template <int K, int C>
+template <int K, int C, bool PL>
 static bool launch_tm_s(int S, const Shard& s, const OpPlan& pl, const OpArgs& a, hipStream_t st,
                         const Timing& tm, const int* gate, int* occ) {
     switch (S) {
-        case 1: return launch_tm_if<K, C, 1>(s, pl, a, st, tm, gate, occ);
-        case 2: return launch_tm_if<K, C, 2>(s, pl, a, st, tm, gate, occ);
-        case 3: return launch_tm_if<K, C, 3>(s, pl, a, st, tm, gate, occ);
-        case 4: return launch_tm_if<K, C, 4>(s, pl, a, st, tm, gate, occ);
-        case 5: return launch_tm_if<K, C, 5>(s, pl, a, st, tm, gate, occ);
-        case 6: return launch_tm_if<K, C, 6>(s, pl, a, st, tm, gate, occ);
-        case 7: return launch_tm_if<K, C, 7>(s, pl, a, st, tm, gate, occ);
-        case 8: return launch_tm_if<K, C, 8>(s, pl, a, st, tm, gate, occ);
-        case 9: return launch_tm_if<K, C, 9>(s, pl, a, st, tm, gate, occ);
-        case 10: return launch_tm_if<K, C, 10>(s, pl, a, st, tm, gate, occ);
+        case 1: return launch_tm_if<K, C, 1, PL>(s, pl, a, st, tm, gate, occ);
+        case 2: return launch_tm_if<K, C, 2, PL>(s, pl, a, st, tm, gate, occ);
+        case 3: return launch_tm_if<K, C, 3, PL>(s, pl, a, st, tm, gate, occ);
+        case 4: return launch_tm_if<K, C, 4, PL>(s, pl, a, st, tm, gate, occ);
+        case 5: return launch_tm_if<K, C, 5, PL>(s, pl, a, st, tm, gate, occ);
+        case 6: return launch_tm_if<K, C, 6, PL>(s, pl, a, st, tm, gate, occ);
+        case 7: return launch_tm_if<K, C, 7, PL>(s, pl, a, st, tm, gate, occ);
+        case 8: return launch_tm_if<K, C, 8, PL>(s, pl, a, st, tm, gate, occ);
+        case 9: return launch_tm_if<K, C, 9, PL>(s, pl, a, st, tm, gate, occ);
+        case 10: return launch_tm_if<K, C, 10, PL>(s, pl, a, st, tm, gate, occ);
         default: return false;
     }
 }
 
-template <int K>
+template <int K, bool PL = false>
 static bool launch_tm_c(const Shard& s, const OpPlan& pl, const OpArgs& a, hipStream_t st, const Timing& tm,
                         const int* gate, int* occ = nullptr) {
+    if constexpr (PL) {
+        switch (pl.cfg) {
+            case 0: return launch_tm_s<1, 0, true>(pl.S, s, pl, a, st, tm, gate, occ);
+            case 7: return launch_tm_s<1, 7, true>(pl.S, s, pl, a, st, tm, gate, occ);
+            case 9: return launch_tm_s<1, 9, true>(pl.S, s, pl, a, st, tm, gate, occ);
+            default: return false;
+        }
+    }
     switch (pl.cfg) {
-        case 0: return launch_tm_s<K, 0>(pl.S, s, pl, a, st, tm, gate, occ);
-        case 1: return launch_tm_s<K, 1>(pl.S, s, pl, a, st, tm, gate, occ);
-        case 2: return launch_tm_s<K, 2>(pl.S, s, pl, a, st, tm, gate, occ);
-        case 3: return launch_tm_s<K, 3>(pl.S, s, pl, a, st, tm, gate, occ);
-        case 4: return launch_tm_s<K, 4>(pl.S, s, pl, a, st, tm, gate, occ);
-        case 5: return launch_tm_s<K, 5>(pl.S, s, pl, a, st, tm, gate, occ);
-        case 6: return launch_tm_s<K, 6>(pl.S, s, pl, a, st, tm, gate, occ);
-        case 7: return launch_tm_s<K, 7>(pl.S, s, pl, a, st, tm, gate, occ);
-        case 8: return launch_tm_s<K, 8>(pl.S, s, pl, a, st, tm, gate, occ);
-        case 9: return launch_tm_s<K, 9>(pl.S, s, pl, a, st, tm, gate, occ);
-        case 10: return launch_tm_s<K, 10>(pl.S, s, pl, a, st, tm, gate, occ);
-        case 11: return launch_tm_s<K, 11>(pl.S, s, pl, a, st, tm, gate, occ);
-        case 12: return launch_tm_s<K, 12>(pl.S, s, pl, a, st, tm, gate, occ);
-        case 13: return launch_tm_s<K, 13>(pl.S, s, pl, a, st, tm, gate, occ);
-        case 14: return launch_tm_s<K, 14>(pl.S, s, pl, a, st, tm, gate, occ);
-        case 15: return launch_tm_s<K, 15>(pl.S, s, pl, a, st, tm, gate, occ);
-        case 16: return launch_tm_s<K, 16>(pl.S, s, pl, a, st, tm, gate, occ);
+        case 0: return launch_tm_s<K, 0, false>(pl.S, s, pl, a, st, tm, gate, occ);
+        case 1: return launch_tm_s<K, 1, false>(pl.S, s, pl, a, st, tm, gate, occ);
+        case 2: return launch_tm_s<K, 2, false>(pl.S, s, pl, a, st, tm, gate, occ);
+        case 3: return launch_tm_s<K, 3, false>(pl.S, s, pl, a, st, tm, gate, occ);
+        case 4: return launch_tm_s<K, 4, false>(pl.S, s, pl, a, st, tm, gate, occ);
+        case 5: return launch_tm_s<K, 5, false>(pl.S, s, pl, a, st, tm, gate, occ);
+        case 6: return launch_tm_s<K, 6, false>(pl.S, s, pl, a, st, tm, gate, occ);
+        case 7: return launch_tm_s<K, 7, false>(pl.S, s, pl, a, st, tm, gate, occ);
+        case 8: return launch_tm_s<K, 8, false>(pl.S, s, pl, a, st, tm, gate, occ);
+        case 9: return launch_tm_s<K, 9, false>(pl.S, s, pl, a, st, tm, gate, occ);
+        case 10: return launch_tm_s<K, 10, false>(pl.S, s, pl, a, st, tm, gate, occ);
+        case 11: return launch_tm_s<K, 11, false>(pl.S, s, pl, a, st, tm, gate, occ);
+        case 12: return launch_tm_s<K, 12, false>(pl.S, s, pl, a, st, tm, gate, occ);
+        case 13: return launch_tm_s<K, 13, false>(pl.S, s, pl, a, st, tm, gate, occ);
+        case 14: return launch_tm_s<K, 14, false>(pl.S, s, pl, a, st, tm, gate, occ);
+        case 15: return launch_tm_s<K, 15, false>(pl.S, s, pl, a, st, tm, gate, occ);
+        case 16: return launch_tm_s<K, 16, false>(pl.S, s, pl, a, st, tm, gate, occ);
         default: return false;
     }
 }
@@ -760,6 +845,35 @@ hipError_t atax_team(const Shard& s, const OpPlan& pl, int K, const OpArgs& a, h
     return hipGetLastError();
 }
 
+hipError_t atax_team_plain(const Shard& s, const OpPlan& pl, const OpArgs& a, hipStream_t st, const Timing& tm,
+                           const int* gate) {
+    if (pl.T < 1 || pl.grid < pl.T || pl.grid % pl.T) return hipErrorInvalidValue;
+    if (pl.T > 1 && (!a.xg || !a.err || a.tag == 0)) return hipErrorInvalidValue;
+    for (int k = 0; k < kTmPlain; ++k)
+        if (!a.px.p[k]) return hipErrorInvalidValue;
+    if (s.M <= 0) return hipSuccess;
+    if (!launch_tm_c<1, true>(s, pl, a, st, tm, gate)) return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
+bool team_plain_plan(int64_t N, int64_t M, int cus, const OpPlan& main, OpPlan* out) {
+    // the main plan's team size when the head-start kernel fits its rows, else
+    // larger teams (fewer rows per member); configurations with short rings
+    const int cfgs1[] = {0};
+    const int cfgsT[] = {7, 9};
+    for (int T = std::max(main.T, 1); T <= kTmMaxT; T *= 2) {
+        const int* cf = T == 1 ? cfgs1 : cfgsT;
+        const int ncf = T == 1 ? 1 : 2;
+        for (int i = 0; i < ncf; ++i) {
+            OpPlan p{};
+            if (!team_plan(N, M, cus, T, cf[i], &p) || p.S > tm_plain_maxS(cf[i])) continue;
+            *out = p;
+            return true;
+        }
+    }
+    return false;
+}
+
 int team_occupancy(const OpPlan& pl, int K) {
     int occ = 0;
     const Shard s{nullptr, 0, (int64_t)pl.TR * pl.T, 1, nullptr, nullptr};  // the LDS size needs TR and N only
@@ -768,6 +882,7 @@ int team_occupancy(const OpPlan& pl, int K) {
     switch (K) {
         case 1: ok = launch_tm_c<1>(s, pl, a, nullptr, Timing{}, nullptr, &occ); break;
         case 2: ok = launch_tm_c<2>(s, pl, a, nullptr, Timing{}, nullptr, &occ); break;
+        case 1 + kTmPlain: ok = launch_tm_c<1, true>(s, pl, a, nullptr, Timing{}, nullptr, &occ); break;
         default: break;
     }
     return ok ? occ : 0;
@@ -776,8 +891,12 @@ int team_occupancy(const OpPlan& pl, int K) {
 std::string team_kernel_name(int K, const OpPlan& pl) {
     const TmCfg& c = kTmCfg[pl.cfg];
     char b[128];
-    std::snprintf(b, sizeof b, "atax_team_kernel<%d, %d, %d, %d, %d, %s, %d>", K, pl.S, c.F, c.L, c.P,
-                  c.comm ? "true" : "false", c.E);
+    if (K == 1 + kTmPlain)  // the head-start kernel
+        std::snprintf(b, sizeof b, "atax_team_plain_kernel<%d, %d, %d, %d, %s, %d>", pl.S, c.F, c.L, c.P,
+                      c.comm ? "true" : "false", c.E);
+    else
+        std::snprintf(b, sizeof b, "atax_team_kernel<%d, %d, %d, %d, %d, %s, %d>", K, pl.S, c.F, c.L, c.P,
+                      c.comm ? "true" : "false", c.E);
     return b;
 }
 

@@ -118,10 +118,15 @@ struct vampomi_ctx {
     int cus = 0;                // compute units of the device (the operator's grid)
     double* op_part = nullptr;  // opp.nslots x kMaxRhs x ld partial A d
     int64_t op_part_slots = 0;
-    double* op_nvec = nullptr;  // 3 x kMaxRhs x ld: A r, q = A p, A d (+ <d,p> tail)
+    double* op_nvec = nullptr;  // 3 x kMaxRhs x ld + 16: A r, q = A p, A d (+ <d,p> tail)
     unsigned long long* op_xg = nullptr;  // team hand-off granules (M x kOpMaxK x T x 2), zeroed once
     size_t op_xg_words = 0;
     unsigned op_tag = 0;        // the last team launch's tag
+    // the head-start launch (pcg.cpp): its plan and whether it runs (default
+    // on; VAMPOMI_HEADSTART=0 or vampomi_dev_set_variant(c, 5, 0) turns it off)
+    vk::OpPlan opp_hs{};
+    bool hs_ok = false;
+    bool hs_on = true;
     double* nbuf = nullptr;     // kMaxRhs * ld scratch N-vectors (API calls)
     double* mbuf = nullptr;     // (2*kMaxRhs) * M scratch M-vectors (API calls)
 
@@ -259,13 +264,33 @@ struct CgSystem {
 // ar0 (may be null; onepass only): ar0[k] (device, ld, may be null) already
 // holds A r0 of system k (its start is zero, so r0 = v), and the first A.x
 // pass covers only the systems without it (no pass if none).
+//
+// hs (may be null; onepass, K = 2, extra_x): the HEAD START.  System 0 must
+// start from zero (r0 = v, e.g. the Onsager solve, whose v is a probe known an
+// iteration early).  hs->abern (device ld) holds A v of system 0: then system
+// 0's first CG step runs in the pass that would only compute A r0 of system 1
+// and A extra_x (one operator launch with plain right-hand sides,
+// op_dev_plain), and the two systems step together from there, system 0 one
+// step ahead, so the solve takes 1 + max(k1 - 1, k2) passes instead of
+// 1 + max(k1, k2).  Every step is the reference's (src/vamp.cpp:697-757).
+// hs->xnext (may be null, device M): one more right-hand side of that pass,
+// hs->axnext = A xnext (the next solve's abern).  Without hs->abern the first
+// A.x pass carries xnext instead.
+struct HeadStart {
+    const double* abern = nullptr;
+    const double* xnext = nullptr;
+    double* axnext = nullptr;
+    bool used = false;  // out: the head start ran
+};
 vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double tau, double gam2, int max_iter,
                        double tol, double* nscratch, int64_t* ref_passes, DotBatch* init,
                        const double* extra_x = nullptr, double* ex_out = nullptr, bool onepass = false,
-                       const double* const* ar0 = nullptr);
+                       const double* const* ar0 = nullptr, HeadStart* hs = nullptr);
 // plans the one-pass operator (c->opp, c->op_ok) and allocates its buffers
 // (idempotent until the variant changes)
 vampomi_status op_prepare(vampomi_ctx* c);
+// whether pcg_run's head start can run on this context (plans the operator)
+vampomi_status headstart_available(vampomi_ctx* c, bool* yes);
 // the device word a team launch sets when a hand-off timed out, and its host view
 unsigned* op_err_dev(vampomi_ctx* c);
 vampomi_status op_check_err(vampomi_ctx* c);
@@ -274,3 +299,11 @@ vampomi_status op_check_err(vampomi_ctx* c);
 // scal[SL_DP+k]) from one pass over X.  COLLECTIVE.  reduce = false (one
 // rank only): the per-slot A d partials stay in op_part for cg_update to sum
 vampomi_status op_dev(vampomi_ctx* c, int K, const vk::OpArgs& a, const int* gate, bool reduce = true);
+// the head-start launch (c->opp_hs): op_dev's work for ONE system (a, K = 1),
+// and out[kp] = A px[kp] (device ld, /sqrt(N), summed over ranks) for the
+// kOpPlain plain right-hand sides, from the same pass over X.  One rank: the
+// system's A d partials stay in op_part (opp_hs.nslots slots) for cg_update;
+// several: its A d is op_nvec's A d block row 0, <d,p> at A d + (1 + kOpPlain)*ld.
+// COLLECTIVE
+vampomi_status op_dev_plain(vampomi_ctx* c, const vk::OpArgs& a, const double* const* px, double* const* out,
+                            const int* gate);

@@ -642,18 +642,25 @@ vampomi_status op_prepare(vampomi_ctx* c) {
                                                  std::to_string(c->cus) + " CUs");
         }
     }
+    // the head-start plan: optional (no plan, or a grid the device cannot
+    // hold, only means the solves start without it)
+    c->hs_ok = c->op_ok && vk::team_plain_plan(c->N, M, c->cus, c->opp, &c->opp_hs);
+    if (c->hs_ok && (int64_t)vk::team_occupancy(c->opp_hs, 1 + vk::kOpPlain) * c->cus < c->opp_hs.grid)
+        c->hs_ok = false;
     if (!c->op_nvec) {
-        STCHK(dev_alloc(&c->op_nvec, (size_t)3 * vk::kMaxRhs * c->ld));
-        HIPCHK(hipMemsetAsync(c->op_nvec, 0, (size_t)3 * vk::kMaxRhs * c->ld * 8, c->st));
+        STCHK(dev_alloc(&c->op_nvec, (size_t)3 * vk::kMaxRhs * c->ld + 16));
+        HIPCHK(hipMemsetAsync(c->op_nvec, 0, ((size_t)3 * vk::kMaxRhs * c->ld + 16) * 8, c->st));
     }
     if (c->op_ok) {
-        if (c->opp.nslots > c->op_part_slots) {
+        const int64_t slots = std::max<int64_t>(c->opp.nslots, c->hs_ok ? c->opp_hs.nslots : 0);
+        if (slots > c->op_part_slots) {
             dev_free(c->op_part);
-            STCHK(dev_alloc(&c->op_part, (size_t)c->opp.nslots * vk::kMaxRhs * c->ld));
-            c->op_part_slots = c->opp.nslots;
+            STCHK(dev_alloc(&c->op_part, (size_t)slots * vk::kMaxRhs * c->ld));
+            c->op_part_slots = slots;
         }
-        if (c->opp.T > 1) {
-            const size_t words = op_xg_words_for(M, c->opp);
+        if (c->opp.T > 1 || (c->hs_ok && c->opp_hs.T > 1)) {
+            size_t words = c->opp.T > 1 ? op_xg_words_for(M, c->opp) : 0;
+            if (c->hs_ok && c->opp_hs.T > 1) words = std::max(words, op_xg_words_for(M, c->opp_hs));
             if (words > c->op_xg_words) {
                 if (c->op_xg) (void)hipFree(c->op_xg);
                 c->op_xg = nullptr;
@@ -665,6 +672,14 @@ vampomi_status op_prepare(vampomi_ctx* c) {
         }
     }
     c->op_ready = true;
+    return VAMPOMI_OK;
+}
+
+vampomi_status headstart_available(vampomi_ctx* c, bool* yes) {
+    *yes = false;
+    if (!c->have_X || !c->hs_on) return VAMPOMI_OK;
+    STCHK(op_prepare(c));
+    *yes = c->op_ok && c->hs_ok;
     return VAMPOMI_OK;
 }
 
@@ -710,14 +725,15 @@ static void team_gate_leave(vampomi_ctx* c) {  // after the context's stream has
     c->team_reg = false;
 }
 
+// T: the launch's team size (its plan's)
 template <class Launch>
-static vampomi_status team_launch(vampomi_ctx* c, Launch&& launch) {
+static vampomi_status team_launch(vampomi_ctx* c, int T, Launch&& launch) {
     if (c->side_open && c->st2) {  // never beside the context's own side-stream work (not reached: batches join first)
         HIPCHK(hipEventRecord(c->ev_join, c->st2));
         HIPCHK(hipStreamWaitEvent(c->st, c->ev_join, 0));
         c->side_open = false;
     }
-    if (c->opp.T <= 1 || !c->team_reg) {
+    if (T <= 1 || !c->team_reg) {
         HIPCHK(launch());
         return VAMPOMI_OK;
     }
@@ -778,7 +794,8 @@ vampomi_status op_dev(vampomi_ctx* c, int K, const vk::OpArgs& a, const int* gat
     x.ro = vk::RedOut{c->red_part, c->use_comm ? ad + (int64_t)K * c->ld : c->scal + SL_DP, c->ticket, nullptr, 0,
                       gate};
     TimedLaunch t = launch_stat(c, 3, K, pass_bytes(c, K), 2.0 * pass_flops(c, K));
-    STCHK(team_launch(c, [&] { return vk::atax(c->shard(), c->opp, K, x, c->st, vk::Timing{t.a, t.b}, gate); }));
+    STCHK(team_launch(c, c->opp.T,
+                      [&] { return vk::atax(c->shard(), c->opp, K, x, c->st, vk::Timing{t.a, t.b}, gate); }));
     c->stats.a_passes_exec++;
     vk::Ptrs os{};
     for (int k = 0; k < K; ++k) os.p[k] = ad + (int64_t)k * c->ld;
@@ -788,6 +805,48 @@ vampomi_status op_dev(vampomi_ctx* c, int K, const vk::OpArgs& a, const int* gat
         HIPCHK(vk::op_reduce(c->opp, K, c->N, c->ld, c->op_part, os, 0.0, c->st, gate));
         STCHK(allreduce_dev(c, ad, (size_t)K * c->ld + K));  // src/data.cpp:367
         HIPCHK(vk::vec_div(K, c->N, c->ld, os, c->sqrtN, c->st));
+    }
+    return VAMPOMI_OK;
+}
+
+vampomi_status op_dev_plain(vampomi_ctx* c, const vk::OpArgs& a, const double* const* px, double* const* out,
+                            const int* gate) {
+    if (!c->have_X) return fail(VAMPOMI_ERR_STATE, "A before the methylation data was loaded");
+    STCHK(op_prepare(c));
+    if (!c->hs_ok) return fail(VAMPOMI_ERR_ARG, "head-start launch: no plan for N = " + std::to_string(c->N));
+    constexpr int KT = 1 + vk::kOpPlain;  // partial slots: the system's A d, then the plain products
+    double* ad = c->op_nvec + (int64_t)2 * vk::kMaxRhs * c->ld;
+    vk::OpArgs x = a;
+    x.part = c->op_part;
+    x.scale = 1.0 / c->sqrtN;
+    for (int k = 0; k < vk::kOpPlain; ++k) x.px.p[k] = px[k];
+    if (c->opp_hs.T > 1) {
+        x.xg = c->op_xg;
+        if (++c->op_tag == 0) ++c->op_tag;
+        x.tag = c->op_tag;
+        x.err = op_err_dev(c);
+    }
+    x.dbg = 0;
+    x.ro = vk::RedOut{c->red_part, c->use_comm ? ad + (int64_t)KT * c->ld : c->scal + SL_DP, c->ticket, nullptr, 0,
+                      gate};
+    TimedLaunch t = launch_stat(c, 3, KT, pass_bytes(c, KT), pass_flops(c, 1) + pass_flops(c, KT));
+    STCHK(team_launch(c, c->opp_hs.T, [&] {
+        return vk::atax_team_plain(c->shard(), c->opp_hs, x, c->st, vk::Timing{t.a, t.b}, gate);
+    }));
+    c->stats.a_passes_exec++;
+    if (!c->use_comm) {
+        vk::Ptrs os{};
+        for (int k = 0; k < vk::kOpPlain; ++k) os.p[k] = out[k];
+        HIPCHK(vk::op_reduce(c->opp_hs, vk::kOpPlain, c->N, c->ld, c->op_part, os, c->sqrtN, c->st, gate, 1));
+    } else {
+        vk::Ptrs os{};
+        for (int k = 0; k < KT; ++k) os.p[k] = ad + (int64_t)k * c->ld;
+        HIPCHK(vk::op_reduce(c->opp_hs, KT, c->N, c->ld, c->op_part, os, 0.0, c->st, gate));
+        STCHK(allreduce_dev(c, ad, (size_t)KT * c->ld + 1));  // src/data.cpp:367
+        HIPCHK(vk::vec_div(KT, c->N, c->ld, os, c->sqrtN, c->st));
+        for (int k = 0; k < vk::kOpPlain; ++k)
+            HIPCHK(hipMemcpyAsync(out[k], ad + (int64_t)(1 + k) * c->ld, (size_t)c->N * 8, hipMemcpyDeviceToDevice,
+                                  c->st));
     }
     return VAMPOMI_OK;
 }
@@ -943,6 +1002,7 @@ extern "C" vampomi_status vampomi_open(const vampomi_shard_desc* d, vampomi_ctx*
     // cross-queue events cost more than the 5-17 us kernels they overlap)
     c->side_on = c->use_comm;
     if (const char* sv = std::getenv("VAMPOMI_SIDE_STREAM")) c->side_on = std::atoi(sv) != 0;
+    if (const char* hv = std::getenv("VAMPOMI_HEADSTART")) c->hs_on = std::atoi(hv) != 0;
     const char* mode = std::getenv("VAMPOMI_COMM");
     if (c->use_comm && mode && std::strcmp(mode, "loopback") == 0) {
         if (!d->comm_id) return fail(VAMPOMI_ERR_ARG, "the loopback communicator needs a communicator id");
@@ -1504,6 +1564,9 @@ extern "C" vampomi_status vampomi_dev_set_variant(vampomi_ctx* c, int which, int
     } else if (which == 4) {  // side stream for the prefetched denoiser/EM: 0 off, 1 on
         if (variant != 0 && variant != 1) return fail(VAMPOMI_ERR_ARG, "side stream: 0 or 1");
         c->side_on = variant == 1;
+    } else if (which == 5) {  // the CG head start (pcg.cpp): 0 off, 1 on
+        if (variant != 0 && variant != 1) return fail(VAMPOMI_ERR_ARG, "head start: 0 or 1");
+        c->hs_on = variant == 1;
     } else {
         if (!vk::loo_variant_ok(variant)) return fail(VAMPOMI_ERR_ARG, "no such association-pass variant");
         c->loo_variant = variant;
@@ -1556,7 +1619,7 @@ extern "C" vampomi_status vampomi_dev_time_pass(vampomi_ctx* c, int which, int K
             }
             x.dbg = std::getenv("VAMPOMI_OP_DBG") ? std::atoi(std::getenv("VAMPOMI_OP_DBG")) : 0;
             if (c->opp.T > 1) x.err = op_err_dev(c);
-            STCHK(team_launch(c, [&] { return vk::atax(c->shard(), c->opp, K, x, c->st); }));
+            STCHK(team_launch(c, c->opp.T, [&] { return vk::atax(c->shard(), c->opp, K, x, c->st); }));
         }
         else  // association pass: ymod = nbuf slot 0, x1 = mbuf slot 0, sums in mbuf slots 3..7
             HIPCHK(vk::loo_sums(c->shard(), c->nbuf, c->mbuf, c->sqrtN, c->mbuf + 3 * Mx, c->st, c->loo_variant));
@@ -1608,7 +1671,7 @@ extern "C" vampomi_status vampomi_dev_op_apply(vampomi_ctx* c, int K, const doub
         if (Mx < K) return fail(VAMPOMI_ERR_ARG, "vampomi_dev_op_apply: fused form needs M >= K");
         STCHK(stage_in(c, beta, K, VAMPOMI_MEM_HOST, dbeta));
         a.beta = dbeta;
-        a.fuse = 1;
+        a.fuse = (1 << K) - 1;
     }
     a.diag = diag;
     a.tau = tau;
@@ -1664,14 +1727,18 @@ extern "C" vampomi_status vampomi_dev_mem_plan(int64_t N, int64_t Mt, int nranks
     add((int64_t)vk::kMaxRhs * ld, 8);                 // nbuf
     add((int64_t)2 * vk::kMaxRhs * Mx, 8);             // mbuf
     add((int64_t)sizeof(vk::CgState), 1);
-    vk::OpPlan op{};
+    vk::OpPlan op{}, hs{};
     if (vk::op_plan(N, Mx, cus, vk::kOpDefault, &op)) {
-        add((int64_t)3 * vk::kMaxRhs * ld, 8);         // op_nvec
-        add(op.nslots * vk::kMaxRhs * ld, 8);          // op_part
-        if (op.T > 1) add((int64_t)op_xg_words_for(Mx, op), 8);
+        const bool h = vk::team_plain_plan(N, Mx, cus, op, &hs);
+        add((int64_t)3 * vk::kMaxRhs * ld + 16, 8);    // op_nvec
+        add(std::max<int64_t>(op.nslots, h ? hs.nslots : 0) * vk::kMaxRhs * ld, 8);  // op_part
+        size_t w = op.T > 1 ? op_xg_words_for(Mx, op) : 0;
+        if (h && hs.T > 1) w = std::max(w, op_xg_words_for(Mx, hs));
+        if (w) add((int64_t)w, 8);
     }
-    for (int q = 0; q < 24; ++q) add(Mx, 8);           // VampRun M-vectors (14 + cgw[10])
+    for (int q = 0; q < 25; ++q) add(Mx, 8);           // VampRun M-vectors (15 + cgw[10])
     add(ld, 8), add((int64_t)vk::kMaxRhs * ld, 8), add((int64_t)vk::kMaxRhs * ld, 8), add(ld, 8);
+    add(ld, 8);                                        // abern (the head start)
     if (probit) {
         for (int q = 0; q < 3; ++q) add(ld, 8);
         for (int q = 0; q < 3; ++q) add(Mx, 8);
@@ -1687,6 +1754,11 @@ static std::string op_name(const vampomi_ctx* c, int K) {
     int cus = c->cus;
     if (cus <= 0 && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess) cus = 256;
     if (!vk::op_plan(c->N, std::max<int64_t>(c->M, 1), cus, c->op_variant, &p)) return "(no one-pass plan)";
+    if (K == 1 + vk::kOpPlain) {  // the head-start launch
+        vk::OpPlan h{};
+        if (!vk::team_plain_plan(c->N, std::max<int64_t>(c->M, 1), cus, p, &h)) return "(no head-start plan)";
+        return vk::team_kernel_name(K, h);
+    }
     return vk::op_kernel_name(K, p);
 }
 

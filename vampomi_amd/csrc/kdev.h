@@ -60,14 +60,18 @@ __device__ __forceinline__ void ticket_sum_blocks(const RedOut& ro) {
 // registers in one burst and written back once (a chain of dependent device
 // loads and stores otherwise: this runs at the end of every CG step).
 __device__ inline void cg_decide_vals(CgState* cs, const double* red, int it, CgMirror* mirror,
-                                      unsigned long long* flag, unsigned long long seq) {
+                                      unsigned long long* flag, unsigned long long seq, int mask) {
     CgState s = *cs;
     if (s.any) {
         int any = 0;
 #pragma unroll
         for (int k = 0; k < kMaxRhs; ++k) {
             if (k >= s.K || !s.active[k]) continue;
-            s.iters[k] = it + 1;
+            if (!((mask >> k) & 1)) {  // not this step's: unchanged, still running
+                any = 1;
+                continue;
+            }
+            s.iters[k] = it + 1 + s.off[k];
             const double rz_new = red[3 * k], rr = red[3 * k + 1], vmu = red[3 * k + 2];
             if (s.onsager[k]) {  // :708-726
                 const double ons = s.gam2 * vmu;
@@ -89,6 +93,10 @@ __device__ inline void cg_decide_vals(CgState* cs, const double* red, int it, Cg
                 continue;
             }
             s.beta[k] = bt;
+            if (s.iters[k] >= s.maxit) {  // the solver's loop bound (:697)
+                s.active[k] = 0;
+                continue;
+            }
             any = 1;
         }
         s.any = any;
@@ -98,7 +106,7 @@ __device__ inline void cg_decide_vals(CgState* cs, const double* red, int it, Cg
     // flag: the host reads the mirror after the flag (no release fence, which
     // would write back this XCD's whole L2 first)
     if (mirror) {
-        CgMirror* m = mirror + (it & 1);
+        CgMirror* m = mirror + (it & 1);  // (it >= 0 whenever a mirror is given)
         __hip_atomic_store(&m->seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(&m->any, s.any, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 #pragma unroll
@@ -112,12 +120,12 @@ __device__ inline void cg_decide_vals(CgState* cs, const double* red, int it, Cg
 }
 
 __device__ inline void cg_decide_body(CgState* cs, const double* red, int it, CgMirror* mirror, unsigned long long* flag,
-                                      unsigned long long seq) {
+                                      unsigned long long seq, int mask) {
     double r[3 * kMaxRhs];
     const int K = cs->K;
 #pragma unroll
     for (int q = 0; q < 3 * kMaxRhs; ++q) r[q] = q < 3 * K ? red[q] : 0.0;
-    cg_decide_vals(cs, r, it, mirror, flag, seq);
+    cg_decide_vals(cs, r, it, mirror, flag, seq, mask);
 }
 
 }  // namespace vk

@@ -110,6 +110,9 @@ hipError_t atx(const Shard& s, int K, CPtrs u, Ptrs out, double scale, int mode,
 //    the rows of each column and hand the column dots over inside the launch
 //    (T = 1: no hand-off), for N up to 32 x 8 x 896 rows.
 constexpr int kOpMaxK = 2;
+// the head-start launch (pcg.cpp): one operator system plus kOpPlain plain
+// right-hand sides A x_kp from the same read of X (stats: K = 1 + kOpPlain)
+constexpr int kOpPlain = 3;
 struct OpPlan {
     int grid;       // workgroups (at most one per CU)
     int S;          // 16-byte loads per lane per column
@@ -128,9 +131,11 @@ struct OpArgs {
     CPtrs ar, qo;       // q_k = ar_k/diag [+ beta_k*qo_k when fuse] (N-space, replicated)
     CPtrs p, z;         // p_k [= z_k + beta_k*p_k when fuse] (M-space)
     const double* beta; // device (CgState.beta)
-    int fuse;
+    int fuse;           // bit k: system k's direction update p = z + beta p is fused into this launch
     double diag, scale, tau, gam2;
     Ptrs d, sraw;       // d_k (M); sraw_k = t_k (may be null)
+    CPtrs px;           // head-start launch only: the kOpPlain plain right-hand sides (M), A x_kp into
+                        // partial slots 1 .. kOpPlain
     double* part;       // nslots x kMaxRhs x ld partial A d (before the sum over slots)
     RedOut ro;          // <d_k, p_k> summed over the shard (K values)
     // team kernel with T > 1: hand-off granules ((M + grid) x kOpMaxK x T x 2
@@ -155,9 +160,16 @@ hipError_t atax(const Shard& s, const OpPlan& pl, int K, const OpArgs& a, hipStr
                 const int* gate = nullptr);
 hipError_t atax_team(const Shard& s, const OpPlan& pl, int K, const OpArgs& a, hipStream_t st, const Timing& tm,
                      const int* gate);
-// out_k[j] = sum_b part[b][k][j] (slots in order); if div > 0 then /= div
+// the head-start launch: the team kernel with K = 1 and the kOpPlain plain
+// right-hand sides a.px (plan from team_plain_plan)
+hipError_t atax_team_plain(const Shard& s, const OpPlan& pl, const OpArgs& a, hipStream_t st, const Timing& tm,
+                           const int* gate);
+// a team plan for the head-start kernel (the main plan's team size if its rows
+// fit, else larger teams); false: none (the solve starts without a head start)
+bool team_plain_plan(int64_t N, int64_t M, int cus, const OpPlan& main, OpPlan* out);
+// out_k[j] = sum_b part[b][k0 + k][j] (slots in order); if div > 0 then /= div
 hipError_t op_reduce(const OpPlan& pl, int K, int64_t N, int64_t ld, const double* part, Ptrs out, double div,
-                     hipStream_t st, const int* gate = nullptr);
+                     hipStream_t st, const int* gate = nullptr, int k0 = 0);
 
 // ---- marker statistics (data::compute_markers_statistics) ----------------
 hipError_t marker_stats(const double* X, int64_t ld, int64_t N, int64_t M, double nonas,
@@ -311,11 +323,13 @@ hipError_t cg_init(int K, int64_t M, const CgVecs& c, double diag, const RedOut&
 // when the host reads step i-1's decision, step i is already queued and may
 // have decided too (a gated step decides in microseconds); one shared slot let
 // ranks read different steps' decisions and issue different collectives.
+// off[k]: steps system k took before step 0 (the head start, pcg.cpp), so its
+// count after step `it` is it + 1 + off[k]; a system stops after maxit steps.
 struct CgState {
     double rz[kMaxRhs], vv[kMaxRhs], prev_ons[kMaxRhs], beta[kMaxRhs];
     double gam2, tol;
-    int active[kMaxRhs], iters[kMaxRhs], onsager[kMaxRhs];
-    int K, any;
+    int active[kMaxRhs], iters[kMaxRhs], onsager[kMaxRhs], off[kMaxRhs];
+    int K, any, maxit;
 };
 struct CgMirror {
     unsigned long long seq;  // the step's flag value: the slot holds that step's decision
@@ -333,17 +347,22 @@ hipError_t cg_start_from(const CgState& init, const double* sums, CgState* dst, 
 // rank: the sums are final): the last block also takes cg_decide's decisions.
 struct CgDecide {
     int on = 0, it = 0;
+    int mask = 0xf;  // the systems this step is for (the others keep their state; see cg_update)
     CgMirror* mirror = nullptr;
     unsigned long long* flag = nullptr;
     unsigned long long seq = 0;
 };
 // pp_dev (may be null): dp_dev holds |A p_k|^2 and pp_dev |p_k|^2, and
-// <d,p> = tau*|A p|^2 + gam2*|p|^2 (c.tau, c.gam2)
+// <d,p> = tau*|A p|^2 + gam2*|p|^2 (c.tau, c.gam2).  fuse: bit k set when
+// system k's direction update is fused into this step; dc.mask: the systems
+// this step updates (the others are left as they are: the head start's step
+// of one system, pcg.cpp)
 hipError_t cg_update(int K, int64_t M, const CgVecs& c, double diag, CgState* cs, const double* dp_dev,
                      const double* pp_dev, int fuse, const RedOut& ro, const CgDecide& dc, hipStream_t st);
 // step `it`'s decisions from red (the 3K sums of cg_update, summed over ranks),
-// src/vamp.cpp:700-750; then mirror and flag (stored even when gated off)
+// src/vamp.cpp:700-750, for the systems in mask; then mirror and flag (each
+// stored when non-null, even when gated off)
 hipError_t cg_decide(CgState* cs, const double* red, int it, CgMirror* mirror, unsigned long long* flag,
-                     unsigned long long seq, hipStream_t st);
+                     unsigned long long seq, hipStream_t st, int mask = 0xf);
 
 }  // namespace vk

@@ -831,7 +831,7 @@ __global__ __launch_bounds__(kOpThreads) void atax_kernel(const double* __restri
                 const int jj = OP_J(s) + h;
                 if (jj < N) {
                     double q = a.ar.p[k][jj] / a.diag;              // A z = A r / diag
-                    if (a.fuse) q = q + a.beta[k] * a.qo.p[k][jj];  // A p = A z + beta A p
+                    if ((a.fuse >> k) & 1) q = q + a.beta[k] * a.qo.p[k][jj];  // A p = A z + beta A p
                     q_lds[k * NL + jj] = q;
                 }
             }
@@ -840,7 +840,7 @@ __global__ __launch_bounds__(kOpThreads) void atax_kernel(const double* __restri
     __syncthreads();  // the zero pair and q[N] (thread 0) are read by other threads
     double bk[K];
 #pragma unroll
-    for (int k = 0; k < K; ++k) bk[k] = a.fuse ? a.beta[k] : 0.0;
+    for (int k = 0; k < K; ++k) bk[k] = ((a.fuse >> k) & 1) ? a.beta[k] : 0.0;
     double dpacc[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) dpacc[k] = 0.0;
@@ -895,7 +895,7 @@ __global__ __launch_bounds__(kOpThreads) void atax_kernel(const double* __restri
             double t = sg * dot;  // sigma_inv * dpa
             t *= a.scale;         // ATx[mloc] *= 1/sqrt(N)
             double pk = a.p.p[k][m];
-            if (a.fuse) pk = a.z.p[k][m] + bk[k] * pk;  // p = z + beta p
+            if ((a.fuse >> k) & 1) pk = a.z.p[k][m] + bk[k] * pk;  // p = z + beta p
             double val = t * a.tau;  // res[i] *= tau
             val += a.gam2 * pk;      // res[i] += gam2 * v[i]
             if (threadIdx.x == 0) {
@@ -1072,11 +1072,12 @@ __global__ __launch_bounds__(256) void op_reduce_kernel(int64_t N, int64_t ld, i
 }
 
 hipError_t op_reduce(const OpPlan& pl, int K, int64_t N, int64_t ld, const double* part, Ptrs out, double div,
-                     hipStream_t st, const int* gate) {
+                     hipStream_t st, const int* gate, int k0) {
     const int64_t n = (int64_t)K * N;
     if (n <= 0) return hipSuccess;
+    if (k0 < 0 || k0 + K > kMaxRhs) return hipErrorInvalidValue;
     hipLaunchKernelGGL(op_reduce_kernel, dim3((unsigned)(K * cdiv(N, 128))), dim3(256), 0, st, N, ld, (int)pl.nslots,
-                       part, out, div, gate);
+                       part + (int64_t)k0 * ld, out, div, gate);
     return hipGetLastError();
 }
 
@@ -1499,8 +1500,8 @@ hipError_t cg_start_from(const CgState& init, const double* sums, CgState* dst, 
 }
 
 __global__ void cg_decide_kernel(CgState* cs, const double* __restrict__ red, int it, CgMirror* mirror,
-                                 unsigned long long* flag, unsigned long long seq) {
-    if (threadIdx.x == 0) cg_decide_body(cs, red, it, mirror, flag, seq);
+                                 unsigned long long* flag, unsigned long long seq, int mask) {
+    if (threadIdx.x == 0) cg_decide_body(cs, red, it, mirror, flag, seq, mask);
 }
 
 __global__ __launch_bounds__(kBlock) void cg_update_kernel(int K, int64_t M, CgVecs c, double diag,
@@ -1516,7 +1517,7 @@ __global__ __launch_bounds__(kBlock) void cg_update_kernel(int K, int64_t M, CgV
     bool on[kMaxRhs];
 #pragma unroll
     for (int k = 0; k < kMaxRhs; ++k) {
-        on[k] = k < K && cs->active[k];
+        on[k] = k < K && cs->active[k] && ((dc.mask >> k) & 1);
         const double dp = pp_dev ? c.tau * dp_dev[k] + c.gam2 * pp_dev[k] : dp_dev[k];  // <d,p>
         alpha[k] = on[k] ? cs->rz[k] / dp : 0.0;  // :702
     }
@@ -1524,8 +1525,12 @@ __global__ __launch_bounds__(kBlock) void cg_update_kernel(int K, int64_t M, CgV
 #pragma unroll
     for (int q = 0; q < 3 * kMaxRhs; ++q) acc[q] = 0.0;
     double beta[kMaxRhs];
+    bool fk[kMaxRhs];  // system k's direction update p = z + beta p rides in this step
 #pragma unroll
-    for (int k = 0; k < kMaxRhs; ++k) beta[k] = fuse && on[k] ? cs->beta[k] : 0.0;
+    for (int k = 0; k < kMaxRhs; ++k) {
+        fk[k] = on[k] && ((fuse >> k) & 1);
+        beta[k] = fk[k] ? cs->beta[k] : 0.0;
+    }
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; mpart && i < M; i += (int64_t)mblocks * kBlock) {
         // every load of the element first (the vectors may alias as far as the
         // compiler knows: loads after a store would wait for it)
@@ -1535,7 +1540,7 @@ __global__ __launch_bounds__(kBlock) void cg_update_kernel(int K, int64_t M, CgV
         for (int k = 0; k < kMaxRhs; ++k) {
             if (on[k]) {
                 pv[k] = c.p[k][i];
-                zv[k] = fuse ? c.z[k][i] : 0.0;
+                zv[k] = fk[k] ? c.z[k][i] : 0.0;
                 muv[k] = c.mu[k][i];
                 rv[k] = c.r[k][i];
                 dv[k] = c.d[k][i];
@@ -1548,7 +1553,7 @@ __global__ __launch_bounds__(kBlock) void cg_update_kernel(int K, int64_t M, CgV
         for (int k = 0; k < kMaxRhs; ++k) {
             if (on[k]) {
                 double pi = pv[k];
-                if (fuse) {  // p = z + beta p (:738-739)
+                if (fk[k]) {  // p = z + beta p (:738-739)
                     pi = zv[k] + beta[k] * pi;
                     c.p[k][i] = pi;
                 }
@@ -1581,12 +1586,13 @@ __global__ __launch_bounds__(kBlock) void cg_update_kernel(int K, int64_t M, CgV
                                           (w + 1) * ns / 4)
                                : v2d{0.0, 0.0};
             __syncthreads();
-            bool onk = false;  // on[k], alpha[k], beta[k] without indexing registers at run time
+            bool onk = false, fuk = false;  // on[k], fk[k], alpha[k], beta[k] without indexing registers at run time
             double alk = 0.0, bek = 0.0;
 #pragma unroll
             for (int kk = 0; kk < kOpMaxK; ++kk)
                 if (kk == k) {
                     onk = on[kk];
+                    fuk = fk[kk];
                     alk = alpha[kk];
                     bek = beta[kk];
                 }
@@ -1597,7 +1603,7 @@ __global__ __launch_bounds__(kBlock) void cg_update_kernel(int K, int64_t M, CgV
                     const int64_t j = i + e;
                     if (j >= c.nA) break;
                     double q = c.AR[k][j] / diag;
-                    if (fuse) q = q + bek * c.Q[k][j];
+                    if (fuk) q = q + bek * c.Q[k][j];
                     c.Q[k][j] = q;
                     if (c.AW[k]) c.AW[k][j] = c.AW[k][j] + alk * q;
                     c.AR[k][j] = c.AR[k][j] - ad[e] * alk;
@@ -1612,7 +1618,7 @@ __global__ __launch_bounds__(kBlock) void cg_update_kernel(int K, int64_t M, CgV
             for (int k = 0; k < kMaxRhs; ++k)
                 if (on[k]) {
                     ar[k] = c.AR[k][i];
-                    qo[k] = fuse ? c.Q[k][i] : 0.0;
+                    qo[k] = fk[k] ? c.Q[k][i] : 0.0;
                     ad[k] = c.AD[k][i];
                     aw[k] = c.AW[k] ? c.AW[k][i] : 0.0;
                 }
@@ -1620,7 +1626,7 @@ __global__ __launch_bounds__(kBlock) void cg_update_kernel(int K, int64_t M, CgV
             for (int k = 0; k < kMaxRhs; ++k)
                 if (on[k]) {
                     double q = ar[k] / diag;  // A z = A r / diag
-                    if (fuse) q = q + beta[k] * qo[k];  // A p = A z + beta A p
+                    if (fk[k]) q = q + beta[k] * qo[k];  // A p = A z + beta A p
                     c.Q[k][i] = q;
                     if (c.AW[k]) c.AW[k][i] = aw[k] + alpha[k] * q;
                     c.AR[k][i] = ar[k] - ad[k] * alpha[k];
@@ -1642,7 +1648,7 @@ __global__ __launch_bounds__(kBlock) void cg_update_kernel(int K, int64_t M, CgV
     block_put_sums<3 * kMaxRhs>(acc, 3 * K, ro, (int64_t)blockIdx.x * 3 * K);
     // one rank: the last block decides the step itself (its sums are final)
     if (red_finish(ro, 3 * K, lds) && dc.on && threadIdx.x == 0)
-        cg_decide_body(cs, ro.out, dc.it, dc.mirror, dc.flag, dc.seq);
+        cg_decide_body(cs, ro.out, dc.it, dc.mirror, dc.flag, dc.seq, dc.mask);
 }
 
 hipError_t cg_update(int K, int64_t M, const CgVecs& c, double diag, CgState* cs, const double* dp_dev,
@@ -1662,8 +1668,8 @@ hipError_t cg_update(int K, int64_t M, const CgVecs& c, double diag, CgState* cs
 }
 
 hipError_t cg_decide(CgState* cs, const double* red, int it, CgMirror* mirror, unsigned long long* flag,
-                     unsigned long long seq, hipStream_t st) {
-    hipLaunchKernelGGL(cg_decide_kernel, dim3(1), dim3(64), 0, st, cs, red, it, mirror, flag, seq);
+                     unsigned long long seq, hipStream_t st, int mask) {
+    hipLaunchKernelGGL(cg_decide_kernel, dim3(1), dim3(64), 0, st, cs, red, it, mirror, flag, seq, mask);
     return hipGetLastError();
 }
 

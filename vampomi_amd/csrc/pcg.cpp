@@ -62,16 +62,30 @@ static vampomi_status cg_loop(vampomi_ctx* c, int max_iter, Enqueue&& enqueue, c
 
 vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double tau, double gam2, int max_iter,
                        double tol, double* nscratch, int64_t* ref_passes, DotBatch* init, const double* extra_x,
-                       double* ex_out, bool onepass, const double* const* ar0) {
+                       double* ex_out, bool onepass, const double* const* ar0, HeadStart* hs) {
     const int64_t M = c->M, N = c->N;
     const double diag = tau * (double)(N - 1) / (double)N + gam2;  // :676-677
     const int K = (int)sys.size();
     if (K < 1 || K > vk::kMaxRhs) return fail(VAMPOMI_ERR_ARG, "pcg: 1..4 systems");
     if (extra_x && (!ex_out || K + 1 >= vk::kMaxRhs)) return fail(VAMPOMI_ERR_ARG, "pcg: extra A.x needs K <= 2");
-    auto extra_alone = [&]() -> vampomi_status {  // no CG step carries it
-        if (!extra_x) return VAMPOMI_OK;
-        STCHK(ax_dev(c, 1, &extra_x, nscratch));
-        HIPCHK(hipMemcpyAsync(ex_out, nscratch, (size_t)N * 8, hipMemcpyDeviceToDevice, c->st));
+    if (hs) {
+        hs->used = false;
+        if (!onepass || K != 2 || !extra_x || ar0 || sys[0]->mu0_nonzero || (hs->xnext && !hs->axnext))
+            return fail(VAMPOMI_ERR_ARG, "pcg: the head start needs the one-pass form, two systems, extra_x, "
+                                         "system 0 from zero and no ar0");
+    }
+    const double* xnext = hs ? hs->xnext : nullptr;
+    auto extra_alone = [&]() -> vampomi_status {  // no CG step carries them
+        const double* px[2];
+        double* out[2];
+        int n = 0;
+        if (extra_x) px[n] = extra_x, out[n++] = ex_out;
+        if (xnext) px[n] = xnext, out[n++] = hs->axnext;
+        if (n == 0) return VAMPOMI_OK;
+        STCHK(ax_dev(c, n, px, nscratch));
+        for (int j = 0; j < n; ++j)
+            HIPCHK(hipMemcpyAsync(out[j], nscratch + (int64_t)j * c->ld, (size_t)N * 8, hipMemcpyDeviceToDevice,
+                                  c->st));
         return VAMPOMI_OK;
     };
     // initial residual r = v - lmmse_mult(mu0)  (:681-684)
@@ -104,10 +118,16 @@ vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double
         cv.atx0[k] = s->mu0_nonzero ? s->atx0 : nullptr;
         cv.d[k] = (s->mu0_nonzero && !s->atx0) ? s->d : nullptr;
     }
+    if (onepass && K <= vk::kOpMaxK && c->have_X) STCHK(op_prepare(c));
+    // the head start (ctx.h, HeadStart): system 0's first step rides in the pass
+    // that starts the solve; it is then one step ahead (CgState.off)
+    const bool head = hs && hs->abern && c->hs_on && c->hs_ok && c->op_ok && max_iter > 0;
     vk::CgState s0{};
     s0.K = K;
     s0.gam2 = gam2;
     s0.tol = tol;
+    s0.maxit = max_iter;
+    s0.off[0] = head ? 1 : 0;
     s0.any = max_iter > 0 ? 1 : 0;
     for (int k = 0; k < K; ++k) {
         s0.active[k] = 1;
@@ -135,7 +155,6 @@ vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double
     }
     const int* gate = field<int>(c->cgs, offsetof(vk::CgState, any));
     const double* beta = field<double>(c->cgs, offsetof(vk::CgState, beta));
-    if (onepass && K <= vk::kOpMaxK && c->have_X) STCHK(op_prepare(c));
     if (onepass && K <= vk::kOpMaxK && c->have_X && c->op_ok) {
         // ---- one pass over X per CG step (vk::atax) ----
         // A r0 for every system (and A extra_x) by one A.x pass; then each step
@@ -146,13 +165,23 @@ vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double
         const double* AD = c->op_nvec + (int64_t)2 * vk::kMaxRhs * c->ld;
         bool given = false;
         for (int k = 0; k < K; ++k) given = given || (ar0 && ar0[k]);
-        if (!given) {
+        if (head) {
+            // A r0 of system 0 is hs->abern (r0 = v); its first step's launch
+            // (below, once the step's vectors are set up) also forms A r0 of
+            // system 1, A extra_x and A xnext
+            HIPCHK(hipMemcpyAsync(AR, hs->abern, (size_t)N * 8, hipMemcpyDeviceToDevice, c->st));
+        } else if (!given) {
             const double* px[vk::kMaxRhs];
             for (int k = 0; k < K; ++k) px[k] = sys[k]->r;
-            if (extra_x) px[K] = extra_x;
-            STCHK(ax_dev(c, extra_x ? K + 1 : K, px, AR));
+            int n = K;
+            if (extra_x) px[n++] = extra_x;
+            if (xnext) px[n++] = xnext;
+            STCHK(ax_dev(c, n, px, AR));
             if (extra_x)
                 HIPCHK(hipMemcpyAsync(ex_out, AR + (int64_t)K * c->ld, (size_t)N * 8, hipMemcpyDeviceToDevice, c->st));
+            if (xnext)
+                HIPCHK(hipMemcpyAsync(hs->axnext, AR + (int64_t)(n - 1) * c->ld, (size_t)N * 8,
+                                      hipMemcpyDeviceToDevice, c->st));
         } else {  // A r0 given for some systems (zero starts, r0 = v): one pass for the others, if any
             const double* px[vk::kMaxRhs];
             int slot[vk::kMaxRhs], n = 0;
@@ -208,8 +237,44 @@ vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double
         if (rec)
             for (int k = 0; k < K; ++k)
                 if (!sys[k]->S) return fail(VAMPOMI_ERR_ARG, "pcg: W needs an S scratch vector for every system");
+        const int all = (1 << K) - 1;
+        if (head) {
+            // system 0's step 1 (it = -1: its count becomes 1 + off - 1 + ... = 1)
+            // together with A r0 of system 1, A extra_x and A xnext: one pass
+            vk::OpArgs a{};
+            a.ar.p[0] = cu.AR[0];
+            a.qo.p[0] = cu.Q[0];
+            a.p.p[0] = sys[0]->p;
+            a.z.p[0] = sys[0]->z;
+            a.d.p[0] = sys[0]->d;
+            a.sraw.p[0] = rec ? sys[0]->S : nullptr;
+            a.beta = beta;
+            a.fuse = 0;
+            a.diag = diag;
+            a.tau = tau;
+            a.gam2 = gam2;
+            const double* px[vk::kOpPlain] = {sys[1]->r, extra_x, xnext ? xnext : extra_x};
+            double* out[vk::kOpPlain] = {cu.AR[1], ex_out, xnext ? hs->axnext : nscratch};
+            STCHK(op_dev_plain(c, a, px, out, gate));
+            vk::CgVecs ch = cu;
+            if (!c->use_comm) ch.adslots = (int)c->opp_hs.nslots;
+            const double* dp = c->use_comm ? AD + (int64_t)(1 + vk::kOpPlain) * c->ld : c->scal + SL_DP;
+            const vk::RedOut ro{c->red_part, c->scal + SL_CG, c->ticket, nullptr, 0, gate};
+            vk::CgDecide dc{};  // no mirror, no flag: the host does not wait for this step
+            dc.on = !c->use_comm;
+            dc.it = -1;
+            dc.mask = 1;
+            HIPCHK(vk::cg_update(1, M, ch, diag, c->cgs, dp, nullptr, 0, ro, dc, c->st));
+            if (c->use_comm) {
+                STCHK(allreduce_dev(c, c->scal + SL_CG, 3));
+                HIPCHK(vk::cg_decide(c->cgs, c->scal + SL_CG, -1, nullptr, nullptr, 0, c->st, 1));
+            }
+            hs->used = true;
+        }
         auto enqueue = [&](int i, unsigned long long* seq) -> vampomi_status {
-            const bool fuse = i > 0;
+            // the direction updates fused into step i: every system's from step
+            // 1 on; at step 0 those of the systems already under way (head start)
+            const int fuse = i > 0 ? all : head ? 1 : 0;
             vk::OpArgs a{};
             for (int k = 0; k < K; ++k) {
                 a.ar.p[k] = cu.AR[k];
@@ -220,7 +285,7 @@ vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double
                 a.sraw.p[k] = rec ? sys[k]->S : nullptr;
             }
             a.beta = beta;
-            a.fuse = fuse ? 1 : 0;
+            a.fuse = fuse;
             a.diag = diag;
             a.tau = tau;
             a.gam2 = gam2;
@@ -236,7 +301,7 @@ vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double
                 dc.flag = c->d_flag;
                 dc.seq = *seq;
             }
-            HIPCHK(vk::cg_update(K, M, cu, diag, c->cgs, dp, nullptr, fuse ? 1 : 0, ro, dc, c->st));
+            HIPCHK(vk::cg_update(K, M, cu, diag, c->cgs, dp, nullptr, fuse, ro, dc, c->st));
             if (c->use_comm) {
                 STCHK(allreduce_dev(c, c->scal + SL_CG, (size_t)(3 * K)));
                 HIPCHK(vk::cg_decide(c->cgs, c->scal + SL_CG, i, c->d_cgm, c->d_flag, *seq, c->st));
@@ -251,6 +316,10 @@ vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double
             if (ref_passes) *ref_passes += 2 * (int64_t)sys[k]->iters;
         }
         return VAMPOMI_OK;
+    }
+    if (xnext) {  // (no one-pass plan: the head start's next product by its own pass)
+        STCHK(ax_dev(c, 1, &xnext, nscratch));
+        HIPCHK(hipMemcpyAsync(hs->axnext, nscratch, (size_t)N * 8, hipMemcpyDeviceToDevice, c->st));
     }
     const double* pp[vk::kMaxRhs];
     const double* zz[vk::kMaxRhs];
@@ -342,7 +411,8 @@ vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double
             dc.flag = c->d_flag;
             dc.seq = *seq;
         }
-        HIPCHK(vk::cg_update(K, M, cu, diag, c->cgs, c->scal + SL_DP, pp_dev, fuse ? 1 : 0, ro, dc, c->st));
+        HIPCHK(vk::cg_update(K, M, cu, diag, c->cgs, c->scal + SL_DP, pp_dev, fuse ? (1 << K) - 1 : 0, ro, dc,
+                             c->st));
         if (c->use_comm) {  // the sums are final after the all-reduce
             STCHK(allreduce_dev(c, c->scal + SL_CG, (size_t)(3 * K)));
             HIPCHK(vk::cg_decide(c->cgs, c->scal + SL_CG, i, c->d_cgm, c->d_flag, *seq, c->st));

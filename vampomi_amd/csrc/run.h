@@ -29,6 +29,7 @@ struct VampRun {
     int z1n_slot = 2;    // nb3 slot of the prefetched z1
     int bern_it = 0;     // probit: the iteration whose probe bern holds (drawn one iteration early)
     int abern_it = 0;    // probit: the iteration whose A.bern is in nb3 slot 3
+    int hs_it = 0;       // linear: the iteration whose A.bern is in abern (the CG head start)
     std::string out_dir, out_name, p_params, p_metrics, p_prior;
     int it = 0;
     bool stopped = false;
@@ -56,6 +57,8 @@ struct VampRun {
     // device N-vectors (ld each)
     double *z1buf = nullptr, *nb3 = nullptr /* A.x2, A.invQ, A.x1_next */, *nsc = nullptr;
     double* ax2 = nullptr;  // arec: A x2, carried from iteration to iteration
+    double* abern = nullptr;      // the head start: A.bern of iteration hs_it (ld)
+    double* bern_next = nullptr;  // ... and the next iteration's probe (M)
     const double* z1 = nullptr;
     int64_t passes_ref = 0;
     // probit (src/vamp_probit.cpp) state

@@ -40,7 +40,7 @@
 VampRun::~VampRun() {
     if (writer) writer->drain(nullptr);  // its kernels read x1 / r1, its thread writes the caller's history arrays
     for (double** p : {&r1, &x1, &x1p, &x1n, &x1d, &r2, &x2, &bern, &invQ, &v, &atxy, &ts, &tmpM, &atx0, &z1buf,
-                       &nb3, &nsc, &ax2, &p1, &p2, &z1h, &x1s, &x1sn, &x2s})
+                       &nb3, &nsc, &ax2, &p1, &p2, &z1h, &x1s, &x1sn, &x2s, &abern, &bern_next})
         dev_free(*p);
     for (auto& p : cgw) dev_free(p);
 }
@@ -218,14 +218,16 @@ vampomi_status ensure_writer(vampomi_ctx* c, VampRun& R);
 static vampomi_status vamp_alloc(vampomi_ctx* c, VampRun& R) {
     const size_t M = (size_t)std::max<int64_t>(c->M, 1), ld = (size_t)c->ld;
     for (double** p : {&R.r1, &R.x1, &R.x1p, &R.x1n, &R.x1d, &R.r2, &R.x2, &R.bern, &R.invQ, &R.v, &R.atxy, &R.ts,
-                       &R.tmpM, &R.atx0})
+                       &R.tmpM, &R.atx0, &R.bern_next})
         STCHK(dev_alloc(p, M));
     for (auto& p : R.cgw) STCHK(dev_alloc(&p, M));
     STCHK(dev_alloc(&R.z1buf, ld));
     STCHK(dev_alloc(&R.nb3, vk::kMaxRhs * ld));  // probit: slot 3 carries the next A.bern_vec
     STCHK(dev_alloc(&R.nsc, vk::kMaxRhs * ld));
     STCHK(dev_alloc(&R.ax2, ld));
+    STCHK(dev_alloc(&R.abern, ld));
     HIPCHK(hipMemsetAsync(R.ax2, 0, ld * 8, c->st));
+    HIPCHK(hipMemsetAsync(R.abern, 0, ld * 8, c->st));
     HIPCHK(hipMemsetAsync(R.z1buf, 0, ld * 8, c->st));
     HIPCHK(hipMemsetAsync(R.nb3, 0, vk::kMaxRhs * ld * 8, c->st));
     HIPCHK(hipMemsetAsync(R.nsc, 0, vk::kMaxRhs * ld * 8, c->st));
@@ -481,9 +483,29 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
         if (it == 1) HIPCHK(hipMemsetAsync(R.ax2, 0, (size_t)ld * 8, c->st));
         sx.AW = R.ax2;
     }
-    if (R.fuse) {
+    // the head start (pcg.cpp, ctx.h HeadStart): the Onsager solve (system 0)
+    // takes its first CG step in the pass that starts the x2 solve, from
+    // A.bern computed one iteration early (bern depends on (seed, it, marker)
+    // only, P2); that pass also forms A.bern of the next iteration
+    bool hs_av = false;
+    if (R.fuse && arec && R.onepass) STCHK(headstart_available(c, &hs_av));
+    HeadStart hs;
+    if (hs_av) {
+        hs.abern = R.hs_it == it ? R.abern : nullptr;
+        if (it < R.prm.max_iter) {
+            HIPCHK(vk::bernoulli(R.prm.seed, it + 1, c->S, M, std::sqrt((double)Mt), R.bern_next, c->st));
+            hs.xnext = R.bern_next;
+            hs.axnext = R.abern;  // (its A.bern was copied out first, in stream order)
+        }
+    }
+    if (R.fuse && hs_av) {
+        STCHK(pcg_run(c, {&so, &sx}, R.gamw, R.gam2, R.prm.CG_max_iter, R.prm.CG_err_tol, R.nsc, &R.passes_ref,
+                      nullptr, R.x1, R.z1buf, true, nullptr, &hs));
+        R.hs_it = hs.xnext ? it + 1 : 0;
+    } else if (R.fuse) {
         STCHK(pcg_run(c, {&sx, &so}, R.gamw, R.gam2, R.prm.CG_max_iter, R.prm.CG_err_tol, R.nsc, &R.passes_ref,
                       arec ? nullptr : &e1, arec ? R.x1 : nullptr, arec ? R.z1buf : nullptr, R.onepass));
+        R.hs_it = 0;
     } else {
         STCHK(pcg_run(c, {&sx}, R.gamw, R.gam2, R.prm.CG_max_iter, R.prm.CG_err_tol, R.nsc, &R.passes_ref, &e1));
         STCHK(pcg_run(c, {&so}, R.gamw, R.gam2, R.prm.CG_max_iter, R.prm.CG_err_tol, R.nsc, &R.passes_ref, nullptr));
