@@ -321,6 +321,11 @@ vampomi_status vampomi_dev_kernel_name(const vampomi_ctx* ctx, int which, int K,
  * no such plan exists. */
 vampomi_status vampomi_dev_op_plan(int64_t N, int64_t M, int cus, int variant, int K, int* T, int* S, int* TR,
                                    int* grid, int64_t* nslots, char* name, int cap);
+/* Experiment builds only (atax_team.hip compiled with TM_TS=1, and
+ * VAMPOMI_OP_TS=1 set before the context's first operator use): the last
+ * operator launch's per-workgroup {start, end, XCC id, HW_ID} (s_memrealtime
+ * ticks, 100 MHz), *n = min(cap, 4 x grid) words. VAMPOMI_ERR_STATE otherwise. */
+vampomi_status vampomi_dev_op_timestamps(vampomi_ctx* ctx, unsigned long long* out, int cap, int* n);
 /* Device bytes the context of `rank` (of nranks, markers split by
  * vampomi_divide_work) allocates for a VAMP run on N samples and Mt markers
  * with `cus` compute units: the shard, marker statistics, scratch, the

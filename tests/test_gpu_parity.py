@@ -254,6 +254,22 @@ def test_headstart(N, Mt, its, kind, opv):
     _assert_parity(a, ref)
 
 
+@pytest.mark.parametrize("N,Mt,its,opv", [(10000, 2500, 10, 1417), (3000, 2000, 10, 1218), (50001, 700, 6, 2617)])
+def test_dynamic_chunks_vamp(N, Mt, its, opv):
+    """A VAMP run on a dynamic-chunk operator plan (the teams claim columns at
+    run time, atax_team.hip): the same CG, Onsager and mixture counts as the
+    static plan of the same team size, values within rounding, and within the
+    parity bar of the oracle."""
+    X, y, beta = _problem(N, Mt)
+    a = _gpu_vamp(X, y, beta, Mt, max_iter=its, stop_criteria_thr=0.0, op_variant=opv)
+    b = _gpu_vamp(X, y, beta, Mt, max_iter=its, stop_criteria_thr=0.0, op_variant=opv - 10)
+    assert a["cg_iters"] == b["cg_iters"] and a["ons_iters"] == b["ons_iters"] and a["L"] == b["L"]
+    for k in range(its):
+        assert relerr(a["x1_hist"][k], b["x1_hist"][k]) <= 1e-11, f"x1 it {k + 1}"
+    ref = O.vamp_infere(X, y, Mt, true_signal=beta, max_iter=its, stop_criteria_thr=0.0)
+    _assert_parity(a, ref)
+
+
 def test_headstart_cg_limits():
     """CG_max_iter reached inside the head start: the Onsager solve stops after
     max_iter steps of its own (its first in the head-start pass), exactly as

@@ -142,6 +142,7 @@ SIGNATURES = {
                                       C.c_int]),
     "vampomi_dev_op_apply": (C.c_int, [_P, C.c_int, _P, _P, _P, _P, _P, C.c_double, C.c_double, C.c_double, _P, _P,
                                        _P]),
+    "vampomi_dev_op_timestamps": (C.c_int, [_P, _P, C.c_int, C.POINTER(C.c_int)]),
     "vampomi_all_ok": (C.c_int, [_P, C.c_int, C.POINTER(C.c_int)]),
     "vampomi_comm_abort": (C.c_int, [_P]),
 }

@@ -647,6 +647,10 @@ vampomi_status op_prepare(vampomi_ctx* c) {
     c->hs_ok = c->op_ok && vk::team_plain_plan(c->N, M, c->cus, c->opp, &c->opp_hs);
     if (c->hs_ok && (int64_t)vk::team_occupancy(c->opp_hs, 1 + vk::kOpPlain) * c->cus < c->opp_hs.grid)
         c->hs_ok = false;
+    if (!c->op_ts && std::getenv("VAMPOMI_OP_TS") && std::atoi(std::getenv("VAMPOMI_OP_TS"))) {
+        HIPCHK(hipMalloc((void**)&c->op_ts, (size_t)4 * 8 * std::max(c->cus, 1) * 2));
+        HIPCHK(hipMemsetAsync(c->op_ts, 0, (size_t)4 * 8 * std::max(c->cus, 1) * 2, c->st));
+    }
     if (!c->op_nvec) {
         STCHK(dev_alloc(&c->op_nvec, (size_t)3 * vk::kMaxRhs * c->ld + 16));
         HIPCHK(hipMemsetAsync(c->op_nvec, 0, ((size_t)3 * vk::kMaxRhs * c->ld + 16) * 8, c->st));
@@ -669,6 +673,16 @@ vampomi_status op_prepare(vampomi_ctx* c) {
                 HIPCHK(hipMemsetAsync(c->op_xg, 0, words * 8, c->st));  // tags start below every launch's
                 c->op_xg_words = words;
             }
+        }
+        // dynamic chunks: claim counter, finish ticket and chunk rings (zero, re-armed by each launch)
+        const int64_t dw = std::max(vk::team_dyn_words(c->opp), c->hs_ok ? vk::team_dyn_words(c->opp_hs) : 0);
+        if (dw > c->op_dyn_words) {
+            if (c->op_dyn) (void)hipFree(c->op_dyn);
+            c->op_dyn = nullptr;
+            c->op_dyn_words = 0;
+            HIPCHK(hipMalloc((void**)&c->op_dyn, (size_t)dw * 8));
+            HIPCHK(hipMemsetAsync(c->op_dyn, 0, (size_t)dw * 8, c->st));
+            c->op_dyn_words = dw;
         }
     }
     c->op_ready = true;
@@ -763,7 +777,10 @@ static vampomi_status team_launch(vampomi_ctx* c, int T, Launch&& launch) {
 // reads and clears the word: each check reports the launches since the last
 // one, so one timed-out launch does not fail every later solve of the context
 vampomi_status op_check_err(vampomi_ctx* c) {
-    if (c->h_flag && __atomic_exchange_n(reinterpret_cast<unsigned*>(c->h_flag + 4), 0u, __ATOMIC_ACQ_REL))
+    const unsigned e = c->h_flag ? __atomic_exchange_n(reinterpret_cast<unsigned*>(c->h_flag + 4), 0u, __ATOMIC_ACQ_REL) : 0u;
+    if (e > 1)  // TM_SAFE diagnostic builds: address-check codes above the flag bit
+        return fail(VAMPOMI_ERR_HIP, "one-pass operator: address checks failed (codes " + std::to_string(e >> 1) + ")");
+    if (e)
         return fail(VAMPOMI_ERR_HIP, "one-pass operator: a team hand-off timed out (a workgroup of the team never "
                                      "ran: fewer compute units than planned?)");
     return VAMPOMI_OK;
@@ -784,12 +801,14 @@ vampomi_status op_dev(vampomi_ctx* c, int K, const vk::OpArgs& a, const int* gat
     x.scale = 1.0 / c->sqrtN;
     if (c->opp.T > 1) {
         x.xg = c->op_xg;
+        x.dyn = c->op_dyn;
         if (++c->op_tag == 0) ++c->op_tag;
         x.tag = c->op_tag;
         x.err = op_err_dev(c);
     }
     static const int dbg = std::getenv("VAMPOMI_OP_DBG") ? std::atoi(std::getenv("VAMPOMI_OP_DBG")) : 0;
     x.dbg = dbg;
+    x.ts = c->op_ts;
     // <d,p>: one rank into scal[SL_DP+k]; several: behind the A d block, all-reduced with it
     x.ro = vk::RedOut{c->red_part, c->use_comm ? ad + (int64_t)K * c->ld : c->scal + SL_DP, c->ticket, nullptr, 0,
                       gate};
@@ -822,6 +841,7 @@ vampomi_status op_dev_plain(vampomi_ctx* c, const vk::OpArgs& a, const double* c
     for (int k = 0; k < vk::kOpPlain; ++k) x.px.p[k] = px[k];
     if (c->opp_hs.T > 1) {
         x.xg = c->op_xg;
+        x.dyn = c->op_dyn;
         if (++c->op_tag == 0) ++c->op_tag;
         x.tag = c->op_tag;
         x.err = op_err_dev(c);
@@ -906,6 +926,11 @@ void release_ctx_resources(vampomi_ctx* c) {
         dev_free(*p);
     if (c->op_xg) (void)hipFree(c->op_xg);
     c->op_xg = nullptr;
+    if (c->op_ts) (void)hipFree(c->op_ts);
+    c->op_ts = nullptr;
+    if (c->op_dyn) (void)hipFree(c->op_dyn);
+    c->op_dyn = nullptr;
+    c->op_dyn_words = 0;
     c->op_xg_words = 0;
     c->op_part_slots = 0;
     c->op_ready = false;
@@ -1613,12 +1638,14 @@ extern "C" vampomi_status vampomi_dev_time_pass(vampomi_ctx* c, int which, int K
             x.ro = vk::RedOut{c->red_part, c->scal + SL_DP, c->ticket, nullptr, 0, nullptr};
             if (c->opp.T > 1) {
                 x.xg = c->op_xg;
+                x.dyn = c->op_dyn;
                 if (++c->op_tag == 0) ++c->op_tag;
                 x.tag = c->op_tag;
                 x.err = op_err_dev(c);
             }
             x.dbg = std::getenv("VAMPOMI_OP_DBG") ? std::atoi(std::getenv("VAMPOMI_OP_DBG")) : 0;
             if (c->opp.T > 1) x.err = op_err_dev(c);
+            x.ts = c->op_ts;
             STCHK(team_launch(c, c->opp.T, [&] { return vk::atax(c->shard(), c->opp, K, x, c->st); }));
         }
         else  // association pass: ymod = nbuf slot 0, x1 = mbuf slot 0, sums in mbuf slots 3..7
@@ -1687,6 +1714,17 @@ extern "C" vampomi_status vampomi_dev_op_apply(vampomi_ctx* c, int K, const doub
     return op_check_err(c);
 }
 
+// experiment builds (TM_TS=1, VAMPOMI_OP_TS=1): the last operator launch's
+// per-workgroup {start, end, XCC id, HW id}, 4 x grid words
+extern "C" vampomi_status vampomi_dev_op_timestamps(vampomi_ctx* c, unsigned long long* out, int cap, int* n) {
+    if (!c || !out || !n) return fail(VAMPOMI_ERR_ARG, "null argument");
+    if (!c->op_ts) return fail(VAMPOMI_ERR_STATE, "no timestamps (VAMPOMI_OP_TS=1 at the first operator use)");
+    STCHK(sync_stream(c, c->st));
+    *n = std::min(cap, 4 * c->opp.grid);
+    HIPCHK(hipMemcpy(out, c->op_ts, (size_t)*n * 8, hipMemcpyDeviceToHost));
+    return VAMPOMI_OK;
+}
+
 extern "C" vampomi_status vampomi_dev_op_plan(int64_t N, int64_t M, int cus, int variant, int K, int* T, int* S,
                                               int* TR, int* grid, int64_t* nslots, char* name, int cap) {
     vk::OpPlan p{};
@@ -1735,6 +1773,8 @@ extern "C" vampomi_status vampomi_dev_mem_plan(int64_t N, int64_t Mt, int nranks
         size_t w = op.T > 1 ? op_xg_words_for(Mx, op) : 0;
         if (h && hs.T > 1) w = std::max(w, op_xg_words_for(Mx, hs));
         if (w) add((int64_t)w, 8);
+        const int64_t dw = std::max(vk::team_dyn_words(op), h ? vk::team_dyn_words(hs) : 0);
+        if (dw) add(dw, 8);
     }
     for (int q = 0; q < 25; ++q) add(Mx, 8);           // VampRun M-vectors (15 + cgw[10])
     add(ld, 8), add((int64_t)vk::kMaxRhs * ld, 8), add((int64_t)vk::kMaxRhs * ld, 8), add(ld, 8);

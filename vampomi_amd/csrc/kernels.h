@@ -146,6 +146,10 @@ struct OpArgs {
     unsigned long long* xg;
     unsigned tag;
     unsigned* err;
+    unsigned long long* ts;  // experiment builds (TM_TS=1) only: per workgroup {start, end, XCC id, HW id}
+    // team kernels with dynamic chunks: the claim counter, finish ticket and
+    // chunk rings (team_dyn_words of the plan; zeroed once, re-armed by each launch)
+    unsigned long long* dyn;
     int dbg;  // timing experiments only (VAMPOMI_OP_DBG; results are wrong when set, except bit 5):
               // bit 0 no poll waits, 1 no publishes, 2 no butterfly, 3 no A d accumulation,
               // 5 write-through hand-off even when the team shares an XCD
@@ -156,6 +160,8 @@ std::string team_kernel_name(int K, const OpPlan& pl);
 // CU holds at once (0: it cannot run); a plan needs grid <= this x CUs, since
 // a team launch needs all its workgroups resident together
 int team_occupancy(const OpPlan& pl, int K);
+// words of OpArgs.dyn a launch of plan pl needs (0: a static plan)
+int64_t team_dyn_words(const OpPlan& pl);
 hipError_t atax(const Shard& s, const OpPlan& pl, int K, const OpArgs& a, hipStream_t st, const Timing& tm = Timing{},
                 const int* gate = nullptr);
 hipError_t atax_team(const Shard& s, const OpPlan& pl, int K, const OpArgs& a, hipStream_t st, const Timing& tm,
