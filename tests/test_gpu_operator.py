@@ -27,7 +27,8 @@ from oracle import pyoracle as O  # noqa: E402  (checker: the generator and mark
 SHAPES = [(1000, 3000, 0), (10000, 4000, 0), (50001, 1500, 1), (100000, 600, 1),
           (50001, 7, 0)]  # fewer markers than teams: empty teams
 CANDIDATES = [0] + [T * 10 + c for T in (1, 2, 4, 8, 16, 32) for c in range(10)] + \
-    [1000 + T * 100 + c for T in (2, 4, 8, 16, 32) for c in (17, 18)]  # dynamic chunks
+    [1000 + T * 100 + c for T in (2, 4, 8, 16, 32) for c in (17, 18)] + \
+    [1000 + T * 100 + c for T in (2, 4, 8, 16, 32) for c in (10, 11, 12, 13, 14, 15, 16, 19, 20)]
 
 
 def _ref(X, mave, msig, ar, qo, p, z, beta, diag, tau, gam2):

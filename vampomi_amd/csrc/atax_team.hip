@@ -95,6 +95,8 @@ static constexpr TmCfg kTmCfg[] = {
     {6, 6, 3, true, 3, 2, true},     // 16
     {4, 5, 2, true, 4, 2, true, true},  // 17: 7 with dynamic chunks
     {2, 4, 2, true, 5, 2, true, true},  // 18: 9 with dynamic chunks
+    {4, 8, 3, true, 3, 2, true},     // 19: a longer lag for short tiles (C2: T = 4, S = 3): members may
+    {4, 11, 3, true, 3, 2, true},    // 20: drift further apart before a team waits for its slowest
 };
 static constexpr int kTmNCfg = sizeof(kTmCfg) / sizeof(kTmCfg[0]);
 
@@ -1106,6 +1108,8 @@ static bool launch_tm_c(const Shard& s, const OpPlan& pl, const OpArgs& a, hipSt
         case 16: return launch_tm_s<K, 16, false>(pl.S, s, pl, a, st, tm, gate, occ);
         case 17: return launch_tm_s<K, 17, false>(pl.S, s, pl, a, st, tm, gate, occ);
         case 18: return launch_tm_s<K, 18, false>(pl.S, s, pl, a, st, tm, gate, occ);
+        case 19: return launch_tm_s<K, 19, false>(pl.S, s, pl, a, st, tm, gate, occ);
+        case 20: return launch_tm_s<K, 20, false>(pl.S, s, pl, a, st, tm, gate, occ);
         default: return false;
     }
 }
