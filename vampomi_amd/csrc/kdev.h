@@ -56,12 +56,12 @@ __device__ __forceinline__ void ticket_sum_blocks(const RedOut& ro) {
 }
 
 // one thread: the host loop of vamp::precondCG_solver after each step's sums
-// red[3k..3k+2] = <r,z>, <r,r>, <v,mu> of system k.  The state is read into
-// registers in one burst and written back once (a chain of dependent device
-// loads and stores otherwise: this runs at the end of every CG step).
-__device__ inline void cg_decide_vals(CgState* cs, const double* red, int it, CgMirror* mirror,
+// red[3k..3k+2] = <r,z>, <r,r>, <v,mu> of system k.  s: the state as *cs holds
+// it (read by the caller in one burst); it is written back once (a chain of
+// dependent device loads and stores otherwise: this runs at the end of every
+// CG step).
+__device__ inline void cg_decide_from(CgState s, CgState* cs, const double* red, int it, CgMirror* mirror,
                                       unsigned long long* flag, unsigned long long seq, int mask) {
-    CgState s = *cs;
     if (s.any) {
         int any = 0;
 #pragma unroll
@@ -121,11 +121,11 @@ __device__ inline void cg_decide_vals(CgState* cs, const double* red, int it, Cg
 
 __device__ inline void cg_decide_body(CgState* cs, const double* red, int it, CgMirror* mirror, unsigned long long* flag,
                                       unsigned long long seq, int mask) {
+    const CgState s = *cs;
     double r[3 * kMaxRhs];
-    const int K = cs->K;
 #pragma unroll
-    for (int q = 0; q < 3 * kMaxRhs; ++q) r[q] = q < 3 * K ? red[q] : 0.0;
-    cg_decide_vals(cs, r, it, mirror, flag, seq, mask);
+    for (int q = 0; q < 3 * kMaxRhs; ++q) r[q] = q < 3 * s.K ? red[q] : 0.0;
+    cg_decide_from(s, cs, r, it, mirror, flag, seq, mask);
 }
 
 }  // namespace vk

@@ -70,7 +70,9 @@ __device__ __forceinline__ void block_put_sums(double (&v)[NQ], int nq, const Re
 // operations of block_sum, so the sums are bitwise those of one block_sum per
 // result, with one barrier round per 8 results instead of one per result.
 // Returns true in the last block (after out[] is written; thread 0 wrote it).
-__device__ bool red_finish(const RedOut& ro, int nq, double* /*lds4*/) {
+// keep (LDS, may be null): thread 0 also leaves the results there (a caller
+// that goes on with them in thread 0 then reads no global memory).
+__device__ bool red_finish(const RedOut& ro, int nq, double* /*lds4*/, double* keep = nullptr) {
     __shared__ int is_last;
     __shared__ double lds[4 * 8];
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
@@ -112,6 +114,7 @@ __device__ bool red_finish(const RedOut& ro, int nq, double* /*lds4*/) {
                     __hip_atomic_store(ro.out + q0 + c, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 else
                     ro.out[q0 + c] = v;
+                if (keep) keep[q0 + c] = v;
             }
     }
     if (threadIdx.x == 0) {
@@ -1039,6 +1042,13 @@ hipError_t atax(const Shard& s, const OpPlan& pl, int K, const OpArgs& a, hipStr
 __device__ __forceinline__ v2d slot_sum(const double* src, int64_t ss, int t0, int t1) {
     v2d acc = {0.0, 0.0};
     int t = t0;
+    for (; t + 16 <= t1; t += 16) {  // (C2: 16 slots per wave, one round trip)
+        v2d x[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) x[u] = *reinterpret_cast<const v2d*>(src + (t + u) * ss);
+#pragma unroll
+        for (int u = 0; u < 16; ++u) acc += x[u];
+    }
     for (; t + 8 <= t1; t += 8) {
         v2d x[8];
 #pragma unroll
@@ -1504,12 +1514,25 @@ __global__ void cg_decide_kernel(CgState* cs, const double* __restrict__ red, in
     if (threadIdx.x == 0) cg_decide_body(cs, red, it, mirror, flag, seq, mask);
 }
 
+// Latency, not bytes, sets this kernel's time at C2 (~25 MB in ~16 us): a
+// chain of dependent memory round trips.  So every scalar comes in one burst
+// (the whole CgState: the deciding block needs no further state load), both
+// M-elements of a thread and a tile's N-vectors are loaded before the
+// dependent work, and the decision takes its sums from LDS.
 __global__ __launch_bounds__(kBlock) void cg_update_kernel(int K, int64_t M, CgVecs c, double diag,
                                                            CgState* cs, const double* __restrict__ dp_dev,
                                                            const double* __restrict__ pp_dev, int fuse, RedOut ro,
                                                            CgDecide dc, int mblocks) {
-    if (!cs->any) return;
+    const CgState st = *cs;
+    double dpv[kMaxRhs], ppv[kMaxRhs];
+#pragma unroll
+    for (int k = 0; k < kMaxRhs; ++k) {
+        dpv[k] = dp_dev[k];
+        ppv[k] = pp_dev ? pp_dev[k] : 0.0;
+    }
+    if (!st.any) return;
     __shared__ double lds[4];
+    __shared__ double fin[3 * kMaxRhs];  // the step's final sums, for the deciding thread
     // blocks [0, mblocks) stream the M-vectors; with c.adpart the blocks past
     // them sum the operator's A d partials and update the N-vectors
     const bool mpart = (int)blockIdx.x < mblocks;
@@ -1517,9 +1540,9 @@ __global__ __launch_bounds__(kBlock) void cg_update_kernel(int K, int64_t M, CgV
     bool on[kMaxRhs];
 #pragma unroll
     for (int k = 0; k < kMaxRhs; ++k) {
-        on[k] = k < K && cs->active[k] && ((dc.mask >> k) & 1);
-        const double dp = pp_dev ? c.tau * dp_dev[k] + c.gam2 * pp_dev[k] : dp_dev[k];  // <d,p>
-        alpha[k] = on[k] ? cs->rz[k] / dp : 0.0;  // :702
+        on[k] = k < K && st.active[k] && ((dc.mask >> k) & 1);
+        const double dp = pp_dev ? c.tau * dpv[k] + c.gam2 * ppv[k] : dpv[k];  // <d,p>
+        alpha[k] = on[k] ? st.rz[k] / dp : 0.0;  // :702
     }
     double acc[3 * kMaxRhs];
 #pragma unroll
@@ -1529,44 +1552,58 @@ __global__ __launch_bounds__(kBlock) void cg_update_kernel(int K, int64_t M, CgV
 #pragma unroll
     for (int k = 0; k < kMaxRhs; ++k) {
         fk[k] = on[k] && ((fuse >> k) & 1);
-        beta[k] = fk[k] ? cs->beta[k] : 0.0;
+        beta[k] = fk[k] ? st.beta[k] : 0.0;
     }
-    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; mpart && i < M; i += (int64_t)mblocks * kBlock) {
-        // every load of the element first (the vectors may alias as far as the
-        // compiler knows: loads after a store would wait for it)
-        double pv[kMaxRhs], zv[kMaxRhs], muv[kMaxRhs], rv[kMaxRhs], dv[kMaxRhs], vv[kMaxRhs], wv[kMaxRhs],
-            sv[kMaxRhs];
+    // two elements per round (i, i + stride), both loaded before either is
+    // stored (the vectors may alias as far as the compiler knows: loads after
+    // a store would wait for it); the sums still run over i, i + stride, ...
+    // in order, as one element per round would
+    const int64_t mstride = (int64_t)mblocks * kBlock;
+    for (int64_t i0 = (int64_t)blockIdx.x * kBlock + threadIdx.x; mpart && i0 < M; i0 += 2 * mstride) {
+        double pv[2][kMaxRhs], zv[2][kMaxRhs], muv[2][kMaxRhs], rv[2][kMaxRhs], dv[2][kMaxRhs], vv[2][kMaxRhs],
+            wv[2][kMaxRhs], sv[2][kMaxRhs];
+        const bool two = i0 + mstride < M;
 #pragma unroll
-        for (int k = 0; k < kMaxRhs; ++k) {
-            if (on[k]) {
-                pv[k] = c.p[k][i];
-                zv[k] = fk[k] ? c.z[k][i] : 0.0;
-                muv[k] = c.mu[k][i];
-                rv[k] = c.r[k][i];
-                dv[k] = c.d[k][i];
-                vv[k] = c.v[k][i];
-                wv[k] = c.W[k] ? c.W[k][i] : 0.0;
-                sv[k] = c.W[k] ? c.S[k][i] : 0.0;
+        for (int h = 0; h < 2; ++h) {
+            const int64_t i = i0 + h * mstride;
+            if (h == 1 && !two) break;
+#pragma unroll
+            for (int k = 0; k < kMaxRhs; ++k) {
+                if (on[k]) {
+                    pv[h][k] = c.p[k][i];
+                    zv[h][k] = fk[k] ? c.z[k][i] : 0.0;
+                    muv[h][k] = c.mu[k][i];
+                    rv[h][k] = c.r[k][i];
+                    dv[h][k] = c.d[k][i];
+                    vv[h][k] = c.v[k][i];
+                    wv[h][k] = c.W[k] ? c.W[k][i] : 0.0;
+                    sv[h][k] = c.W[k] ? c.S[k][i] : 0.0;
+                }
             }
         }
 #pragma unroll
-        for (int k = 0; k < kMaxRhs; ++k) {
-            if (on[k]) {
-                double pi = pv[k];
-                if (fk[k]) {  // p = z + beta p (:738-739)
-                    pi = zv[k] + beta[k] * pi;
-                    c.p[k][i] = pi;
+        for (int h = 0; h < 2; ++h) {
+            const int64_t i = i0 + h * mstride;
+            if (h == 1 && !two) break;
+#pragma unroll
+            for (int k = 0; k < kMaxRhs; ++k) {
+                if (on[k]) {
+                    double pi = pv[h][k];
+                    if (fk[k]) {  // p = z + beta p (:738-739)
+                        pi = zv[h][k] + beta[k] * pi;
+                        c.p[k][i] = pi;
+                    }
+                    const double mu = muv[h][k] + alpha[k] * pi;  // mu += alpha * p
+                    const double r = rv[h][k] - dv[h][k] * alpha[k];  // r -= d * alpha
+                    const double z = r / diag;
+                    c.mu[k][i] = mu;
+                    c.r[k][i] = r;
+                    c.z[k][i] = z;
+                    if (c.W[k]) c.W[k][i] = wv[h][k] + alpha[k] * sv[h][k];  // A^T A mu, as mu += alpha p
+                    acc[3 * k] += r * z;
+                    acc[3 * k + 1] += r * r;
+                    acc[3 * k + 2] += vv[h][k] * mu;
                 }
-                const double mu = muv[k] + alpha[k] * pi;  // mu += alpha * p
-                const double r = rv[k] - dv[k] * alpha[k];  // r -= d * alpha
-                const double z = r / diag;
-                c.mu[k][i] = mu;
-                c.r[k][i] = r;
-                c.z[k][i] = z;
-                if (c.W[k]) c.W[k][i] = wv[k] + alpha[k] * sv[k];  // A^T A mu, as mu += alpha p
-                acc[3 * k] += r * z;
-                acc[3 * k + 1] += r * r;
-                acc[3 * k + 2] += vv[k] * mu;
             }
         }
     }
@@ -1582,10 +1619,6 @@ __global__ __launch_bounds__(kBlock) void cg_update_kernel(int K, int64_t M, CgV
             const int k = (int)(tile / tpk);
             const int64_t i = (tile - k * tpk) * 128 + 2 * lane;  // < adld (a multiple of 16)
             const bool ok = i < c.nA;
-            wsum[w][lane] = ok ? slot_sum(c.adpart + (int64_t)k * c.adld + i, (int64_t)kMaxRhs * c.adld, w * ns / 4,
-                                          (w + 1) * ns / 4)
-                               : v2d{0.0, 0.0};
-            __syncthreads();
             bool onk = false, fuk = false;  // on[k], fk[k], alpha[k], beta[k] without indexing registers at run time
             double alk = 0.0, bek = 0.0;
 #pragma unroll
@@ -1596,17 +1629,30 @@ __global__ __launch_bounds__(kBlock) void cg_update_kernel(int K, int64_t M, CgV
                     alk = alpha[kk];
                     bek = beta[kk];
                 }
-            if (w == 0 && ok && onk) {
+            // wave 0's N-vectors of the tile, loaded before the slot sums (pairs
+            // of samples: i + 1 < adld, the pads lie inside the vectors)
+            const bool upd = w == 0 && ok && onk;
+            v2d arv{0.0, 0.0}, qov{0.0, 0.0}, awv{0.0, 0.0};
+            if (upd) {
+                arv = *reinterpret_cast<const v2d*>(c.AR[k] + i);
+                if (fuk) qov = *reinterpret_cast<const v2d*>(c.Q[k] + i);
+                if (c.AW[k]) awv = *reinterpret_cast<const v2d*>(c.AW[k] + i);
+            }
+            wsum[w][lane] = ok ? slot_sum(c.adpart + (int64_t)k * c.adld + i, (int64_t)kMaxRhs * c.adld, w * ns / 4,
+                                          (w + 1) * ns / 4)
+                               : v2d{0.0, 0.0};
+            __syncthreads();
+            if (upd) {
                 const v2d ad = (((wsum[0][lane] + wsum[1][lane]) + wsum[2][lane]) + wsum[3][lane]) / c.addiv;
 #pragma unroll
                 for (int e = 0; e < 2; ++e) {
                     const int64_t j = i + e;
                     if (j >= c.nA) break;
-                    double q = c.AR[k][j] / diag;
-                    if (fuk) q = q + bek * c.Q[k][j];
+                    double q = arv[e] / diag;
+                    if (fuk) q = q + bek * qov[e];
                     c.Q[k][j] = q;
-                    if (c.AW[k]) c.AW[k][j] = c.AW[k][j] + alk * q;
-                    c.AR[k][j] = c.AR[k][j] - ad[e] * alk;
+                    if (c.AW[k]) c.AW[k][j] = awv[e] + alk * q;
+                    c.AR[k][j] = arv[e] - ad[e] * alk;
                 }
             }
             __syncthreads();
@@ -1646,9 +1692,14 @@ __global__ __launch_bounds__(kBlock) void cg_update_kernel(int K, int64_t M, CgV
             if (on[k] && c.AW[k]) c.AW[k][i] = aw[k] + alpha[k] * as[k];
     }
     block_put_sums<3 * kMaxRhs>(acc, 3 * K, ro, (int64_t)blockIdx.x * 3 * K);
-    // one rank: the last block decides the step itself (its sums are final)
-    if (red_finish(ro, 3 * K, lds) && dc.on && threadIdx.x == 0)
-        cg_decide_body(cs, ro.out, dc.it, dc.mirror, dc.flag, dc.seq, dc.mask);
+    // one rank: the last block decides the step itself (its sums are final),
+    // from the state read at the start (only this decision writes it)
+    if (red_finish(ro, 3 * K, lds, fin) && dc.on && threadIdx.x == 0) {
+        double r[3 * kMaxRhs];
+#pragma unroll
+        for (int q = 0; q < 3 * kMaxRhs; ++q) r[q] = q < 3 * K ? fin[q] : 0.0;
+        cg_decide_from(st, cs, r, dc.it, dc.mirror, dc.flag, dc.seq, dc.mask);
+    }
 }
 
 hipError_t cg_update(int K, int64_t M, const CgVecs& c, double diag, CgState* cs, const double* dp_dev,
