@@ -2,7 +2,7 @@
 # A library change that must not move a bit (e.g. the cg_update latency
 # rework): old build (build_old/lib) vs the tree's build on one box.
 #   1. the same VAMP runs (linear C2 window shape, probit) with each build, compared bitwise;
-#   2. the GPU parity / PCG / probit tests on the new build;
+#   2. the whole -m gpu suite on the new build;
 #   3. the C2 bench alternating old / new, three times.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
@@ -18,8 +18,7 @@ for m in linear bin_class; do
   done
   python tools/lib_bitwise.py cmp gpurun_out/${tag}_${m}_old.npz gpurun_out/${tag}_${m}_new.npz
 done
-timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_probit.py tests/test_gpu_corners.py tests/test_gpu_sharded.py \
-    -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/${tag}_tests.log 2>&1 || { echo "tests failed"; tail -30 gpurun_out/${tag}_tests.log; exit 1; }
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/${tag}_tests.log 2>&1 || { echo "tests failed"; tail -30 gpurun_out/${tag}_tests.log; exit 1; }
 tail -1 gpurun_out/${tag}_tests.log
 run() {  # name lib
   local name=$1 lib=$2

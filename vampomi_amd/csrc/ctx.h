@@ -208,6 +208,15 @@ class DotBatch {
    public:
     explicit DotBatch(vampomi_ctx* c) : c_(c) {}
     vampomi_status add(std::initializer_list<vk::DotTerm> terms, int64_t n, bool sync, double* out);
+    // several groups of terms over the same length n in ONE kernel (<= 8 terms
+    // in all): each group's results reach its out at flush(), exactly as its
+    // own add() would give them (per-term sums do not depend on the other terms)
+    struct Group {
+        std::vector<vk::DotTerm> terms;
+        bool sync;
+        double* out;
+    };
+    vampomi_status add_many(int64_t n, const std::vector<Group>& groups);
     // reserves nq result slots for a fused reduction kernel: *ro says where the
     // kernel writes; the values reach out[0..nq) at flush()
     vampomi_status sink(int nq, bool sync, double* out, vk::RedOut* ro);

@@ -478,6 +478,51 @@ vampomi_status DotBatch::add(std::initializer_list<vk::DotTerm> terms, int64_t n
     return VAMPOMI_OK;
 }
 
+vampomi_status DotBatch::add_many(int64_t n, const std::vector<Group>& groups) {
+    // terms in the order [local groups..., synced groups...]: each kind's
+    // results land in one contiguous slot range (out, then out2 from split)
+    vk::DotArgs a{};
+    int nloc = 0, nsyn = 0;
+    for (const Group& g : groups) (g.sync ? nsyn : nloc) += (int)g.terms.size();
+    a.nt = nloc + nsyn;
+    if (a.nt < 1 || a.nt > vk::kMaxTerms) return fail(VAMPOMI_ERR_ARG, "DotBatch: 1..8 terms");
+    if (nloc + nlocal_ > SL_NLOCAL || nsyn + nsync_ > SL_NSYNC) return fail(VAMPOMI_ERR_STATE, "DotBatch overflow");
+    double* base = c_->use_comm ? c_->scal : c_->d_hscal;
+    int ql = 0, qs = nloc;
+    for (bool want_sync : {false, true}) {
+        for (const Group& g : groups) {
+            if (g.sync != want_sync) continue;
+            int& q = g.sync ? qs : ql;
+            sinks_.push_back(Sink{g.sync ? SL_SYNC + nsync_ + (q - nloc) : SL_LOCAL + nlocal_ + q,
+                                  (int)g.terms.size(), g.out});
+            for (const auto& t : g.terms) {
+                a.t[q] = t;
+                if (t.op == vk::SUM) a.t[q].b = t.a;  // the kernel loads both operands of every term
+                ++q;
+            }
+        }
+    }
+    vk::RedOut ro{};
+    ro.part = on_side_ ? c_->red_part2 : c_->red_part;
+    ro.ticket = on_side_ ? c_->ticket2 : c_->ticket;
+    ro.out = base + SL_LOCAL + nlocal_;
+    ro.out2 = base + SL_SYNC + nsync_;
+    ro.split = nloc;
+    if (!c_->use_comm && c_->h_flag) {  // one flag for the launch (see sink)
+        if (on_side_) {
+            ro.flag = c_->d_flag + 1;
+            ro.seq = side_seq_ = ++c_->side_seq;
+        } else {
+            ro.flag = c_->d_flag;
+            ro.seq = last_seq_ = ++c_->sync_seq;
+        }
+    }
+    nlocal_ += nloc;
+    nsync_ += nsyn;
+    HIPCHK(vk::dots(a, n, ro, stream()));
+    return VAMPOMI_OK;
+}
+
 hipStream_t DotBatch::stream() const { return on_side_ ? c_->st2 : c_->st; }
 
 vampomi_status DotBatch::fork() {

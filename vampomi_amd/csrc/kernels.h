@@ -20,7 +20,9 @@ struct Timing { hipEvent_t start = nullptr, stop = nullptr; };
 // per-block partials in part, the final sums in out[0..nq) (device memory or
 // mapped host memory), ticket a zeroed device counter the kernel re-arms;
 // flag (may be null): the last block stores seq there (system scope, after out);
-// gate (may be null): the launch does nothing while *gate == 0
+// gate (may be null): the launch does nothing while *gate == 0;
+// out2 (may be null): results q >= split go to out2[q - split] instead (one
+// launch serving two slot ranges, DotBatch::add_many)
 struct RedOut {
     double* part;
     double* out;
@@ -28,6 +30,8 @@ struct RedOut {
     unsigned long long* flag = nullptr;
     unsigned long long seq = 0;
     const int* gate = nullptr;
+    double* out2 = nullptr;
+    int split = 0;
 };
 struct Ptrs { double* p[kMaxRhs]; };
 

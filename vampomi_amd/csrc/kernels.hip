@@ -110,10 +110,12 @@ __device__ bool red_finish(const RedOut& ro, int nq, double* /*lds4*/, double* k
         if (threadIdx.x == 0)
             for (int c = 0; c < nc; ++c) {
                 const double v = ((lds[c] + lds[8 + c]) + lds[16 + c]) + lds[24 + c];
+                const int q = q0 + c;
+                double* dst = ro.out2 && q >= ro.split ? ro.out2 + (q - ro.split) : ro.out + q;
                 if (ro.flag)  // mapped host memory: written through, drained before the flag below
-                    __hip_atomic_store(ro.out + q0 + c, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    __hip_atomic_store(dst, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 else
-                    ro.out[q0 + c] = v;
+                    *dst = v;
                 if (keep) keep[q0 + c] = v;
             }
     }

@@ -177,12 +177,17 @@ vampomi_status denoise_into(vampomi_ctx* c, const Mixture& m, double gam1, const
     return VAMPOMI_OK;
 }
 
-// err_measures (src/vamp.cpp:760-852): the reductions (queued) ...
+// err_measures (src/vamp.cpp:760-852): the reductions (queued) ...  xm / xn:
+// another group of reductions over M / over N that shares the launch (one
+// kernel per vector length instead of one per group)
 static vampomi_status err_queue(vampomi_ctx* c, VampRun& R, const double* xhat, const double* Axest, DotBatch& b,
-                                double* m3, double* n2, double* s3) {
-    STCHK(b.add({T(xhat, R.ts), T(xhat, xhat), T(R.ts, R.ts)}, c->M, true, m3));
-    STCHK(b.add({T(c->y, Axest, vk::DIFF2), T(c->y, c->y)}, c->N, false, n2));  // l2_norm2(., 0)
-    return b.add({T(Axest, c->y), T(Axest, Axest), T(c->y, c->y)}, c->N, true, s3);
+                                double* m3, double* n2, double* s3, std::vector<DotBatch::Group> gm = {},
+                                std::vector<DotBatch::Group> gn = {}) {
+    gm.push_back({{T(xhat, R.ts), T(xhat, xhat), T(R.ts, R.ts)}, true, m3});
+    gn.push_back({{T(c->y, Axest, vk::DIFF2), T(c->y, c->y)}, false, n2});  // l2_norm2(., 0)
+    gn.push_back({{T(Axest, c->y), T(Axest, Axest), T(c->y, c->y)}, true, s3});
+    STCHK(b.add_many(c->M, gm));
+    return b.add_many(c->N, gn);
 }
 
 // ... and the scalar formulas once they are back
@@ -514,8 +519,11 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
     if (res && res->ons_iters) res->ons_iters[it - 1] = so.iters;
     {
         DotBatch b(c);
-        STCHK(b.add({T(R.bern, R.invQ)}, M, true, &R.a2));
-        if (arec) STCHK(err_queue(c, R, R.x1, R.z1, b, R.e1m, R.e1n, R.e1s));  // :272
+        const DotBatch::Group ga2{{T(R.bern, R.invQ)}, true, &R.a2};  // :498
+        if (arec)
+            STCHK(err_queue(c, R, R.x1, R.z1, b, R.e1m, R.e1n, R.e1s, {ga2}));  // :272
+        else
+            STCHK(b.add_many(M, {ga2}));
         STCHK(b.flush());
         R.alpha2 = R.gam2 * R.a2;  // :498
     }
@@ -548,11 +556,14 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
 
     // ---- updateNoisePrec (:504-529) + the next z1 in the same pass ----
     const double* ax2 = R.nb3;  // A.x2_hat
+    // updateNoisePrec's two sums ride in err_measures' launches (one per length)
+    DotBatch::Group gtn{{}, false, &R.tn}, gtc{{T(R.bern, R.tmpM)}, true, &R.tc};  // l2_norm2(temp, 0); <u, A^T A invQ>
+    bool shared = false;
     if (arec) {  // no pass: A x2 came with the CG, the next z1 comes with the next CG
         ax2 = R.ax2;
         R.passes_ref += 3;  // :508, :518, :519
-        STCHK(fin.add({T(R.ax2, c->y, vk::DIFF2)}, N, false, &R.tn));  // l2_norm2(temp, 0)
-        STCHK(fin.add({T(R.bern, R.tmpM)}, M, true, &R.tc));           // <u, A^T A invQ>
+        gtn.terms = {T(R.ax2, c->y, vk::DIFF2)};
+        shared = true;
     } else if (rec) {  // A.x2 and the next z1 in one pass; the A^T products came with the CG
         const double* xs[2] = {R.x2, R.x1n};
         STCHK(ax_dev(c, next ? 2 : 1, xs, R.nb3));
@@ -573,7 +584,13 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
         R.passes_ref += 1;
         STCHK(fin.add({T(R.bern, R.tmpM)}, M, true, &R.tc));
     }
-    STCHK(err_queue(c, R, R.x2, ax2, fin, R.e2m, R.e2n, R.e2s));  // :365 (A.x2_hat of :826)
+    // (shared: the NMSE sums (:409-413) too; they read x1 and x1_prev, which
+    // the prefetched denoising below does not write)
+    const DotBatch::Group gnm{{T(R.x1p, R.x1, vk::DIFF2), T(R.x1p, R.x1p)}, true, R.nm};
+    if (shared)
+        STCHK(err_queue(c, R, R.x2, ax2, fin, R.e2m, R.e2n, R.e2s, {gtc, gnm}, {gtn}));  // :365 (A.x2_hat of :826)
+    else
+        STCHK(err_queue(c, R, R.x2, ax2, fin, R.e2m, R.e2n, R.e2s));
     R.passes_ref += 1;
     // Second stream (batch_rhs >= 3, north_star): iteration it+1's EM sums run
     // on the side stream beside these reductions and share their all-reduce
@@ -590,7 +607,7 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
         STCHK(denoise_into(c, R.mix_next, R.gam1, R.r1, R.x1n, R.x1, true, R.prm.rho, R.x1d, fin, &R.sum_d));
         STCHK(fin.side(false));
     }
-    STCHK(fin.add({T(R.x1p, R.x1, vk::DIFF2), T(R.x1p, R.x1p)}, M, true, R.nm));  // NMSE (:409-413)
+    if (!shared) STCHK(fin.add_many(M, {gnm}));  // NMSE (:409-413)
     STCHK(fin.flush());
     const double trace_corr = R.tc * (double)Mt;  // :521
     if (R.prm.verbosity >= 1 && c->rank == 0)
