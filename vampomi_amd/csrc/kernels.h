@@ -245,6 +245,28 @@ hipError_t axpby(int64_t n, double a, const double* x, double b, const double* y
 // bern[i] = (2*bit(seed,it,S+i) - 1) / sqrtMt
 hipError_t bernoulli(uint64_t seed, int it, int64_t S, int64_t M, double sqrtMt, double* out,
                      hipStream_t st);
+// The linear iteration's elementwise work before its CG solves, one launch
+// (the same arithmetic as the separate kernels above, element for element):
+//   r2 = (eta1*x1 - gam1*r1) / gam2      (src/vamp.cpp:259-261)
+//   v = gamw*atxy + gam2*r2              (:303-306)
+//   bern = the probe of iteration it     (:295-296, P2); bern_next: of it + 1 (may be null)
+//   zero[z][i] = 0 for the non-null zero[z] (the CG solves' zero starts)
+struct Prelude {
+    double eta1, gam1, gam2, gamw;
+    const double* x1;
+    const double* r1;
+    const double* atxy;
+    double* r2;
+    double* v;
+    uint64_t seed;
+    int it;
+    int64_t S;
+    double sqrtMt;
+    double* bern;
+    double* bern_next;
+    double* zero[2];
+};
+hipError_t prelude(int64_t M, const Prelude& p, hipStream_t st);
 // out = x / d
 hipError_t div_scalar(int64_t n, const double* x, double d, double* out, hipStream_t st);
 // out[0, n) = x / d and out[n, 2n) = r / d in one launch (the iteration writer)

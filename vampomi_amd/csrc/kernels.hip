@@ -1412,6 +1412,24 @@ hipError_t bernoulli(uint64_t seed, int it, int64_t S, int64_t M, double sqrtMt,
     return hipGetLastError();
 }
 
+__global__ void prelude_kernel(int64_t M, Prelude p) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= M) return;
+    const double r2 = (p.eta1 * p.x1[i] - p.gam1 * p.r1[i]) / p.gam2;  // lincomb_div's expression
+    p.r2[i] = r2;
+    p.v[i] = p.gamw * p.atxy[i] + p.gam2 * r2;                         // axpby's
+    p.bern[i] = (double)(2 * bern_bit(p.seed, p.it, p.S + i) - 1) / p.sqrtMt;
+    if (p.bern_next) p.bern_next[i] = (double)(2 * bern_bit(p.seed, p.it + 1, p.S + i) - 1) / p.sqrtMt;
+    if (p.zero[0]) p.zero[0][i] = 0.0;
+    if (p.zero[1]) p.zero[1][i] = 0.0;
+}
+
+hipError_t prelude(int64_t M, const Prelude& p, hipStream_t st) {
+    if (M <= 0) return hipSuccess;
+    hipLaunchKernelGGL(prelude_kernel, dim3((unsigned)cdiv(M, kBlock)), dim3(kBlock), 0, st, M, p);
+    return hipGetLastError();
+}
+
 __global__ void set_scalar_kernel(double* p, double v) {
     if (threadIdx.x == 0) *p = v;
 }

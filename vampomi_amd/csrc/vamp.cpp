@@ -438,15 +438,14 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
     R.eta1 = R.gam1 / R.alpha1;  // :230
     STCHK(write_bins(c, R));     // :235-249
     R.gam2 = smin(smax(R.eta1 - R.gam1, 1e-11), 1e11);  // :255-256
-    HIPCHK(vk::lincomb_div(M, R.eta1, R.x1, R.gam1, R.r1, R.gam2, R.r2, c->st));  // r2 (:259-261)
     DotBatch e1(c);
     if (!R.arec) STCHK(err_queue(c, R, R.x1, R.z1, e1, R.e1m, R.e1n, R.e1s));  // :272, flushed with the CG start
     R.params[0] = R.alpha1;
     R.params[1] = R.gam1;
 
     // ---------------- LMMSE (:289-350) ----------------
-    HIPCHK(vk::bernoulli(R.prm.seed, it, c->S, M, std::sqrt((double)Mt), R.bern, c->st));  // :295-296 (P2)
-    HIPCHK(vk::axpby(M, R.gamw, R.atxy, R.gam2, R.r2, R.v, c->st));  // v = gamw ATx(y) + gam2 r2 (:303-306)
+    // (r2 (:259-261), the probe bern (:295-296, P2) and v = gamw ATx(y) + gam2 r2
+    // (:303-306) are formed by the prelude launch below, with the zero starts)
     R.passes_ref += 1;
     CgSystem sx{}, so{};
     sx.v = R.v;
@@ -465,7 +464,6 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
     so.p = R.cgw[6];
     so.d = R.cgw[7];
     if (it == 1) HIPCHK(hipMemsetAsync(R.x2, 0, (size_t)std::max<int64_t>(M, 1) * 8, c->st));
-    HIPCHK(hipMemsetAsync(R.invQ, 0, (size_t)std::max<int64_t>(M, 1) * 8, c->st));
     // batch_rhs 2: updateNoisePrec's A^T(A x2) (the next warm start, :681) and
     // A^T(A invQ) (the trace, :519) are carried through the CG steps as
     // W += alpha * A^T(A p) beside mu += alpha * p, instead of one more pass
@@ -473,7 +471,6 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
     const bool rec = R.recur && R.fuse && (it == 1 || sx.atx0);
     if (rec) {
         if (it == 1) HIPCHK(hipMemsetAsync(R.atx0, 0, (size_t)std::max<int64_t>(M, 1) * 8, c->st));
-        HIPCHK(hipMemsetAsync(R.tmpM, 0, (size_t)std::max<int64_t>(M, 1) * 8, c->st));
         sx.W = R.atx0;  // holds A^T A mu0 on entry (the warm start's product), in place
         sx.S = R.cgw[8];
         so.W = R.tmpM;  // invQ starts from zeros
@@ -498,11 +495,31 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
     if (hs_av) {
         hs.abern = R.hs_it == it ? R.abern : nullptr;
         if (it < R.prm.max_iter) {
-            HIPCHK(vk::bernoulli(R.prm.seed, it + 1, c->S, M, std::sqrt((double)Mt), R.bern_next, c->st));
-            hs.xnext = R.bern_next;
+            hs.xnext = R.bern_next;  // the probe of it + 1, formed by the prelude below
             hs.axnext = R.abern;  // (its A.bern was copied out first, in stream order)
         }
     }
+    // the iteration's elementwise work before the CG solves, in one launch
+    // (it replaces five: r2, bern, v, and the zeroed invQ (:496) and its W)
+    vk::Prelude pr{};
+    pr.eta1 = R.eta1;
+    pr.gam1 = R.gam1;
+    pr.gam2 = R.gam2;
+    pr.gamw = R.gamw;
+    pr.x1 = R.x1;
+    pr.r1 = R.r1;
+    pr.atxy = R.atxy;
+    pr.r2 = R.r2;
+    pr.v = R.v;
+    pr.seed = R.prm.seed;
+    pr.it = it;
+    pr.S = c->S;
+    pr.sqrtMt = std::sqrt((double)Mt);
+    pr.bern = R.bern;
+    pr.bern_next = hs.xnext ? R.bern_next : nullptr;
+    pr.zero[0] = R.invQ;
+    pr.zero[1] = rec ? R.tmpM : nullptr;
+    HIPCHK(vk::prelude(M, pr, c->st));
     if (R.fuse && hs_av) {
         STCHK(pcg_run(c, {&so, &sx}, R.gamw, R.gam2, R.prm.CG_max_iter, R.prm.CG_err_tol, R.nsc, &R.passes_ref,
                       nullptr, R.x1, R.z1buf, true, nullptr, &hs));
