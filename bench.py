@@ -546,7 +546,7 @@ def main():
         # committed c3big line (same N and design, 300,000 markers resident on
         # one MI355X, another run and build): its time per executed pass per
         # marker, times this run's markers and executed passes per iteration
-        src = "profiles/r02j_bench_c3big.json"
+        src = "profiles/r03e_bench_c3big.json"
         try:
             ref = json.load(open(os.path.join(ROOT, src)))
             per_pass_marker = ref["ms_per_step"] / (ref["passes_exec_per_step"] * ref["config"]["Mt"])
