@@ -29,3 +29,11 @@ for rep in 1 2 3; do
   run old$rep "$OLD"
   run new$rep "$NEW"
 done
+# the operator alone (tools/kbench.py op, default plan), old / new / old / new
+for rep in 1 2; do
+  for b in old new; do
+    lib=$OLD; [ $b = new ] && lib=$NEW
+    VAMPOMI_LIB=$lib OP_PLANS=-1 timeout -k 10 120 python -u tools/kbench.py 10000 50000 20 op > gpurun_out/${tag}_kb_$b$rep.txt 2>&1 || { echo "kbench $b failed"; exit 1; }
+    echo "kbench $b$rep $(grep '^op ' gpurun_out/${tag}_kb_$b$rep.txt | cut -c1-160)"
+  done
+done
