@@ -1046,7 +1046,7 @@ static void launch_tm(const Shard& s, const OpPlan& pl, const OpArgs& a, hipStre
 // registers beside the ring (register counts and spills checked with
 // tools/regcheck.sh)
 static constexpr int tm_plain_maxS(int cfg) {
-    return cfg == 0 ? 8 : cfg == 7 ? 3 : cfg == 9 ? 5 : 0;
+    return cfg == 0 ? 8 : cfg == 7 ? 3 : cfg == 8 ? 4 : cfg == 9 ? 5 : 0;
 }
 
 template <int K, int C, int S, bool PL>
@@ -1084,6 +1084,7 @@ static bool launch_tm_c(const Shard& s, const OpPlan& pl, const OpArgs& a, hipSt
         switch (pl.cfg) {
             case 0: return launch_tm_s<1, 0, true>(pl.S, s, pl, a, st, tm, gate, occ);
             case 7: return launch_tm_s<1, 7, true>(pl.S, s, pl, a, st, tm, gate, occ);
+            case 8: return launch_tm_s<1, 8, true>(pl.S, s, pl, a, st, tm, gate, occ);
             case 9: return launch_tm_s<1, 9, true>(pl.S, s, pl, a, st, tm, gate, occ);
             default: return false;
         }
@@ -1145,10 +1146,10 @@ bool team_plain_plan(int64_t N, int64_t M, int cus, const OpPlan& main, OpPlan* 
     // the main plan's team size when the head-start kernel fits its rows, else
     // larger teams (fewer rows per member); configurations with short rings
     const int cfgs1[] = {0};
-    const int cfgsT[] = {7, 9};
+    const int cfgsT[] = {7, 8, 9};
     for (int T = std::max(main.T, 1); T <= kTmMaxT; T *= 2) {
         const int* cf = T == 1 ? cfgs1 : cfgsT;
-        const int ncf = T == 1 ? 1 : 2;
+        const int ncf = T == 1 ? 1 : 3;
         for (int i = 0; i < ncf; ++i) {
             OpPlan p{};
             if (!team_plan(N, M, cus, T, cf[i], &p) || p.S > tm_plain_maxS(cf[i])) continue;
