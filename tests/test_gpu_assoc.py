@@ -133,7 +133,37 @@ def test_every_loo_variant_is_bitwise_identical():
             if ref is None:
                 ref = (p, st)
             assert np.array_equal(st, ref[1]) and np.array_equal(p, ref[0]), v
-        _lib.check(lib.vampomi_dev_set_variant(d.ctx, 2, 2))
+        _lib.check(lib.vampomi_dev_set_variant(d.ctx, 2, 16))  # the default
+
+
+@pytest.mark.parametrize("N,Mt,kind", [(4099, 301, 1), (20000, 64, 0), (5, 7, 0), (257, 5, 1)])
+def test_workgroup_loo_variants(N, Mt, kind):
+    """Variants 8-19 (loo_wg_kernel: the waves of a workgroup share its G
+    markers and split the rows) against the oracle with the LOO bars, odd N
+    (the zero pad row) and fewer markers than a workgroup takes included;
+    variants with the same number of waves W are bitwise identical."""
+    from vampomi_amd import _lib
+
+    X, y, beta = make_problem(N, Mt, kind=kind)
+    est = _estimate(beta, N)
+    po, sto = O.assoc_loo(X, y, est)
+    spread = _order_spread(X, y, est, po)
+    lib = va.load()
+    by_w = {}
+    with va.Data(N, Mt) as d:
+        d.load_meth(X)
+        d.set_phen(y, standardize=False)
+        for v, w in ((8, 8), (9, 8), (10, 8), (11, 8), (12, 4), (13, 4), (14, 4), (15, 4), (16, 8), (17, 2), (18, 2),
+                     (19, 2)):
+            _lib.check(lib.vampomi_dev_set_variant(d.ctx, 2, v))
+            assert d.kernel_name(2, 1, v).startswith("loo_wg_kernel"), d.kernel_name(2, 1, v)
+            p, st = d.assoc_loo(est)
+            _check_pfun(p, st, N)
+            _check_loo(p, st, po, sto, spread)
+            if w in by_w:
+                assert np.array_equal(st, by_w[w]), v
+            by_w[w] = st
+        _lib.check(lib.vampomi_dev_set_variant(d.ctx, 2, 16))  # the default
 
 
 def test_se_parity():

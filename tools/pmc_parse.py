@@ -27,7 +27,7 @@ for counter in ("FETCH_SIZE", "WRITE_SIZE"):
                 continue
             acc[r["Kernel_Name"]].append(float(r["Counter_Value"]))
     for k, v in acc.items():
-        if "ax_partial" in k or "atx_kernel" in k or "atax_kernel" in k or "atax_team_kernel" in k or "loo_kernel" in k:
+        if "ax_partial" in k or "atx_kernel" in k or "atax_kernel" in k or "atax_team_kernel" in k or "loo_kernel" in k or "loo_wg_kernel" in k:
             d = out.setdefault(k, {})
             real = [x for x in v if x >= 0.01 * max(v)] or v
             d[counter + "_KB_avg"] = sum(real) / len(real)

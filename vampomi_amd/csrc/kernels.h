@@ -66,7 +66,7 @@ inline int64_t ax_slots(const AxPlan& p, int64_t t) { return ((t + 1) * p.sa - 1
 // Kernel variants (tuning tables in kernels.hip) are per-context launch
 // settings: the defaults are the measured winners, other values are
 // development hooks (tools/kbench.py, vampomi_dev_set_variant).
-constexpr int kAxDefault = 0, kAtxDefault = -1 /* per-K choice */, kLooDefault = 2;
+constexpr int kAxDefault = 0, kAtxDefault = -1 /* per-K choice */, kLooDefault = 16;
 AxPlan ax_plan(int64_t N, int64_t M, int variant = kAxDefault);
 int ax_variant_count();
 bool ax_variant_ok(int v);

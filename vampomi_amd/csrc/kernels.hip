@@ -1944,20 +1944,106 @@ __global__ __launch_bounds__(kBlock) void loo_kernel(const double* __restrict__ 
         }
 }
 
-struct LooVariant { int G, UJ; bool FD; };
+// The same sums with W waves of a workgroup sharing its G markers: wave w,
+// lane l takes rows 2l + 128 (w + W t), so one load round of the workgroup
+// reads W KiB contiguous of each column (the wave-per-marker form above reads
+// 1 KiB per wave from columns all over the shard); the W wave sums meet in
+// LDS and are added in wave order.
+template <int G, int UJ, int W>
+__global__ __launch_bounds__(64 * W) void loo_wg_kernel(const double* __restrict__ X, int64_t ld, int64_t N, int64_t M,
+                                                        const double* __restrict__ ymod, const double* __restrict__ x1,
+                                                        double sqrtN, double* __restrict__ stats) {
+    __shared__ double part[W][5 * G];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t m0 = (int64_t)blockIdx.x * G;
+    const double rinv = 1.0 / sqrtN;
+    double acc[G][5];
+    double xj[G];
+    const double* col[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        const int64_t m = (m0 + g < M) ? m0 + g : M - 1;  // clamp: in-bounds, discarded
+        xj[g] = x1[m];
+        col[g] = X + m * ld;
+#pragma unroll
+        for (int q = 0; q < 5; ++q) acc[g][q] = 0.0;
+    }
+    auto add = [&](int g, double m, double y) {  // loo_kernel's, fma-corrected division
+        const double q0 = m * rinv;
+        const double q = __builtin_fma(__builtin_fma(-q0, sqrtN, m), rinv, q0);
+        const double ym = y + q * xj[g];
+        acc[g][0] += m;
+        acc[g][1] += m * m;
+        acc[g][2] += m * ym;
+        acc[g][3] += ym;
+        acc[g][4] += ym * ym;
+    };
+    constexpr int64_t RS = 128 * W;  // rows per load round of the workgroup
+    int64_t j = 2 * lane + 128 * wave;
+    for (; j + RS * (UJ - 1) < N; j += RS * UJ) {
+        v2d yy[UJ], xx[UJ][G];
+#pragma unroll
+        for (int t = 0; t < UJ; ++t)
+#pragma unroll
+            for (int g = 0; g < G; ++g) xx[t][g] = ld_stream(col[g] + j + RS * t);
+#pragma unroll
+        for (int t = 0; t < UJ; ++t) yy[t] = ld2(ymod + j + RS * t);
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int t = 0; t < UJ; ++t) {
+                add(g, xx[t][g].x, yy[t].x);
+                add(g, xx[t][g].y, yy[t].y);
+            }
+    }
+    for (; j < N; j += RS) {  // (N even or the pad row: ld-padded columns, zero pads)
+        v2d xx[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) xx[g] = ld_stream(col[g] + j);
+        const v2d yy = ld2(ymod + j);
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            add(g, xx[g].x, yy.x);
+            add(g, xx[g].y, yy.y);
+        }
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int q = 0; q < 5; ++q) {
+            const double s = wave_sum(acc[g][q]);
+            if (lane == 0) part[wave][5 * g + q] = s;
+        }
+    __syncthreads();
+    if ((int)threadIdx.x < 5 * G && m0 + threadIdx.x / 5 < M) {
+        double s = 0.0;
+#pragma unroll
+        for (int w = 0; w < W; ++w) s += part[w][threadIdx.x];
+        stats[5 * m0 + threadIdx.x] = s;
+    }
+}
+
+struct LooVariant { int G, UJ; bool FD; int W = 0; };  // W > 0: loo_wg_kernel
 static constexpr LooVariant kLooVariants[] = {
     {4, 2, true}, {4, 2, false}, {2, 2, true}, {8, 1, true}, {4, 1, true}, {4, 4, true}, {2, 4, true}, {8, 2, true},
+    {1, 2, true, 8}, {2, 2, true, 8}, {1, 4, true, 8}, {2, 4, true, 8}, {2, 2, true, 4}, {4, 2, true, 4},
+    {4, 1, true, 4}, {8, 1, true, 4}, {4, 2, true, 8}, {4, 2, true, 2}, {8, 2, true, 2}, {4, 4, true, 2},
 };
 static constexpr int kNumLooVariants = sizeof(kLooVariants) / sizeof(kLooVariants[0]);
-// default: G=2, UJ=2, fma-corrected division: 6.80 TB/s at the c5 shard (N=100,000 x 62,500) on
-// MI355X vs 5.63 TB/s with the IEEE division sequence (tools/kbench.py, profiles/r01_kbench_loo.json)
+// default (round 3): 16, loo_wg_kernel<4, 2, 8>: 7.00 TB/s at the c5 shard (N=100,000 x 62,500) on
+// MI355X against 6.81 TB/s for the round-1 default 2 (loo_kernel<2, 2, true>, fma-corrected division,
+// itself 6.80 against 5.63 TB/s with the IEEE division sequence); tools/kbench.py,
+// profiles/r03l_kbench_loo.txt, profiles/r01_kbench_loo.json
 int loo_variant_count() { return kNumLooVariants; }
 bool loo_variant_ok(int v) { return v >= 0 && v < kNumLooVariants; }
 
 std::string loo_kernel_name(int variant) {
     const LooVariant& v = kLooVariants[loo_variant_ok(variant) ? variant : kLooDefault];
     char b[64];
-    std::snprintf(b, sizeof b, "loo_kernel<%d, %d, %s>", v.G, v.UJ, v.FD ? "true" : "false");
+    if (v.W > 0)
+        std::snprintf(b, sizeof b, "loo_wg_kernel<%d, %d, %d>", v.G, v.UJ, v.W);
+    else
+        std::snprintf(b, sizeof b, "loo_kernel<%d, %d, %s>", v.G, v.UJ, v.FD ? "true" : "false");
     return b;
 }
 
@@ -1971,10 +2057,29 @@ static void launch_loo(const Shard& s, const double* ymod, const double* x1, dou
                           tm.stop, 0, s.X, s.ld, s.N, s.M, ymod, x1, sqrtN, stats);
 }
 
+template <int G, int UJ, int W>
+static void launch_loo_wg(const Shard& s, const double* ymod, const double* x1, double sqrtN, double* stats,
+                          hipStream_t st, const Timing& tm) {
+    hipExtLaunchKernelGGL((loo_wg_kernel<G, UJ, W>), dim3((unsigned)cdiv(s.M, G)), dim3(64 * W), 0, st, tm.start,
+                          tm.stop, 0, s.X, s.ld, s.N, s.M, ymod, x1, sqrtN, stats);
+}
+
 hipError_t loo_sums(const Shard& s, const double* ymod, const double* x1, double sqrtN, double* stats,
                     hipStream_t st, int variant, const Timing& tm) {
     if (s.M <= 0) return hipSuccess;
     switch (variant) {
+        case 8: launch_loo_wg<1, 2, 8>(s, ymod, x1, sqrtN, stats, st, tm); break;
+        case 9: launch_loo_wg<2, 2, 8>(s, ymod, x1, sqrtN, stats, st, tm); break;
+        case 10: launch_loo_wg<1, 4, 8>(s, ymod, x1, sqrtN, stats, st, tm); break;
+        case 11: launch_loo_wg<2, 4, 8>(s, ymod, x1, sqrtN, stats, st, tm); break;
+        case 12: launch_loo_wg<2, 2, 4>(s, ymod, x1, sqrtN, stats, st, tm); break;
+        case 13: launch_loo_wg<4, 2, 4>(s, ymod, x1, sqrtN, stats, st, tm); break;
+        case 14: launch_loo_wg<4, 1, 4>(s, ymod, x1, sqrtN, stats, st, tm); break;
+        case 15: launch_loo_wg<8, 1, 4>(s, ymod, x1, sqrtN, stats, st, tm); break;
+        case 16: launch_loo_wg<4, 2, 8>(s, ymod, x1, sqrtN, stats, st, tm); break;
+        case 17: launch_loo_wg<4, 2, 2>(s, ymod, x1, sqrtN, stats, st, tm); break;
+        case 18: launch_loo_wg<8, 2, 2>(s, ymod, x1, sqrtN, stats, st, tm); break;
+        case 19: launch_loo_wg<4, 4, 2>(s, ymod, x1, sqrtN, stats, st, tm); break;
         case 0: launch_loo<4, 2, true>(s, ymod, x1, sqrtN, stats, st, tm); break;
         case 1: launch_loo<4, 2, false>(s, ymod, x1, sqrtN, stats, st, tm); break;
         case 2: launch_loo<2, 2, true>(s, ymod, x1, sqrtN, stats, st, tm); break;
