@@ -9,7 +9,7 @@ cd "${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 mkdir -p gpurun_out
 N=${1:-10000}
 MT=${2:-50000}
-for dbg in 0 64 256 1 3 4 8 12 0; do
+for dbg in ${DBGS:-0 64 256 1 3 4 8 12 0}; do
   VAMPOMI_LIB=$PWD/build_dbg/lib/libvampomi.so VAMPOMI_OP_DBG=$dbg OP_PLANS=-1 timeout -k 10 120 \
     python -u tools/kbench.py $N $MT 20 op > gpurun_out/r03a_dbg$dbg.txt 2>&1 || { echo "dbg $dbg failed"; tail -5 gpurun_out/r03a_dbg$dbg.txt; exit 1; }
   echo "dbg $dbg: $(grep '^op ' gpurun_out/r03a_dbg$dbg.txt | cut -c1-200) $(grep 'slow polls' gpurun_out/r03a_dbg$dbg.txt | tail -1)"

@@ -589,7 +589,7 @@ __device__ __forceinline__ void atax_team_body(const double* __restrict__ X, int
                         if (own) {
 #pragma unroll
                             for (int k = 0; k < K; ++k) {
-                                if (lane == 0) {
+                                if (lane == 0 && !(dbg & 1024)) {  // (timing experiment 1024: no d stores)
                                     if (a.sraw.p[0]) a.sraw.p[k][mg] = tsc[k];
                                     *tm_chk(a.d.p[k] + mg, a.d.p[k], a.d.p[k] + M, 128, a.err) = dval[k];
                                 }
