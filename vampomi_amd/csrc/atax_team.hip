@@ -55,6 +55,9 @@ typedef unsigned int v2u __attribute__((ext_vector_type(2)));
 #ifndef TM_TS
 #define TM_TS 0  // 1: record each workgroup's start/end time (s_memrealtime, 100 MHz) into OpArgs.ts
 #endif
+#ifndef TM_TEAMS_BY_XCD
+#define TM_TEAMS_BY_XCD 1
+#endif
 #ifndef TM_DBG
 #define TM_DBG 0  // 1: honour OpArgs.dbg (timing experiments); 0: its branches compile out
 #endif
@@ -300,8 +303,17 @@ __device__ __forceinline__ void atax_team_body(const double* __restrict__ X, int
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int g = blockIdx.x >> 3;
     const int member = g % T;
-    const int team = (blockIdx.x & 7) + 8 * (g / T);  // members share blockIdx % 8: one XCD (speed only)
-    const int nteams = gridDim.x / T;
+    const int nteams = gridDim.x / T;  // a multiple of 8 (team_plan)
+    // members share blockIdx % 8: one XCD (speed only).  Teams t of one XCD are
+    // numbered consecutively (t = local + nteams/8 * xcd), so under interleaved
+    // columns the markers of one 64-byte line of d (8 neighbours) belong to teams
+    // of one XCD and their 8-byte owner stores merge in that XCD's L2
+    // (TM_TEAMS_BY_XCD 0: xcd + 8 * local, the round-2 numbering)
+#if TM_TEAMS_BY_XCD
+    const int team = g / T + (nteams >> 3) * (int)(blockIdx.x & 7);
+#else
+    const int team = (blockIdx.x & 7) + 8 * (g / T);
+#endif
     // the team's columns: mb + cs*m, m < n (a contiguous range, or every nteams-th);
     // DYN: column of step m is colof(m) (mb = 0, cs = 1), n known at run time
     const int64_t cs = (ilv || DYN) ? (DYN ? 1 : nteams) : 1;
