@@ -70,8 +70,11 @@ static hipEvent_t ev_get(vampomi_ctx* c) {
         c->ev_pool.pop_back();
         return e;
     }
+    // timestamps only: no system-scope fence (neutral at C2,
+    // profiles/r03t_event_fence_ab.txt; timed launches cost 1-2.6 % of a C2
+    // iteration either way, hence the sampled timing, bench.py --timing-period)
     hipEvent_t e;
-    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess) return nullptr;
     return e;
 }
 
@@ -93,8 +96,8 @@ static vampomi_kernel_stat* stat_k_of(vampomi_ctx* c, int cls, int K) {
 }
 
 // Every launch is counted exactly (launches, algorithmic bytes and flops);
-// with timing on, one in tperiod launches of each (class, K) also gets HIP
-// events in its dispatch packet.  The per-class time is the sampled average
+// with timing on, one in tperiod launches of each (class, K) (hashed
+// positions) also gets HIP events in its dispatch packet.  The per-class time is the sampled average
 // times the exact launch count (vampomi_get_stats), so skipped or dropped
 // samples never inflate it.
 TimedLaunch launch_stat(vampomi_ctx* c, int cls, int K, double bytes, double flops) {
@@ -105,7 +108,15 @@ TimedLaunch launch_stat(vampomi_ctx* c, int cls, int K, double bytes, double flo
         x->flops_total += flops;
     }
     TimedLaunch t{};
-    if (!c->timing || c->tcount[cls][K - 1]++ % c->tperiod != 0) return t;
+    // which launches carry events: a hash of the launch's index in its class,
+    // so the sampled launches fall at every position of a CG solve alike (a
+    // fixed stride of 4 met the same steps of every 8-launch iteration)
+    if (!c->timing) return t;
+    uint64_t h = (uint64_t)c->tcount[cls][K - 1]++ * 0x9E3779B97F4A7C15ULL + (uint64_t)(cls * 8 + K);
+    h ^= h >> 31;
+    h *= 0xBF58476D1CE4E5B9ULL;
+    h ^= h >> 29;
+    if (c->tperiod > 1 && h % (uint64_t)c->tperiod != 0) return t;
     t.a = ev_get(c);
     t.b = ev_get(c);
     t.cls = cls;
