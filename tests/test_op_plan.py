@@ -25,7 +25,9 @@ def plan(N, M=62500, cus=256, variant=-1, K=2):
 
 def test_default_plans_of_the_baseline_shapes():
     c2, c3, c4 = plan(10000), plan(100000), plan(50000)
-    assert c2["T"] == 4 and c2["S"] == 3 and c2["name"] == "atax_team_kernel<2, 3, 4, 5, 2, true, 2>"
+    # C2: a team of 2 with six loads per lane (configuration 12, round 3)
+    assert c2["T"] == 2 and c2["S"] == 6 and c2["name"] == "atax_team_kernel<2, 6, 2, 3, 2, true, 2>"
+    assert plan(9217)["T"] == 2 and plan(10752)["T"] == 2 and plan(10753)["T"] == 4
     assert plan(9216)["T"] == 1 and plan(9216)["name"] == "atax_team_kernel<2, 9, 1, 0, 0, false, 2>"
     assert c3["T"] == 32 and c3["S"] == 4 and c3["TR"] == 3200 and c3["nslots"] == 8
     assert c3["name"] == "atax_team_kernel<2, 4, 4, 5, 2, true, 2>"

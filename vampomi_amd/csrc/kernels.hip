@@ -764,6 +764,18 @@ bool op_plan(int64_t N, int64_t M, int cus, int variant, OpPlan* out) {
             return true;
         }
     }
+    if (variant == kOpDefault) {
+        // just past one workgroup's rows (9,216 < N <= 10,752, C2 among them): a
+        // team of 2 with six loads per lane (configuration 12: F = 2, L = 3,
+        // 253 VGPRs) beats the team of 4 (C2: 589.7-590.2 against 594.5-595.8 us
+        // per launch in VAMP, 192.0-192.3 against 191.0-191.3 it/s, three rounds
+        // on one box, profiles/r03pl_c2_plans.txt)
+        OpPlan p{};
+        if (team_plan(N, M, cus, 2, 12, &p)) {
+            *out = p;
+            return true;
+        }
+    }
     if (variant == 0) {
         if (!whole_column_ok(N)) return false;
         OpPlan p{};
