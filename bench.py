@@ -10,7 +10,13 @@ resident in HBM.  --stop-criteria-thr is 0, so exactly W+K iterations run; W
 are untimed.
 
 Workloads (synthetic, generated on the device):
-  auto (default)  n = 1: c2; n > 1: c3full (the metric's own problem).
+  auto (default)  c2 at every n: n = 1 is BASELINE configs[1]; n > 1 is its
+          weak-scaling form c2-weak (50,000 markers per GPU), so the driver's
+          1 -> 8 curve compares one workload family.  At n > 1 the same line
+          also carries `headline_c3full`, configs[2] itself (N=100,000 x
+          Mt=500,000, the metric's own problem) run in the same job, and the
+          1-GPU bases both are read against, measured in the same job on
+          rank 0's GPU before the n-rank phases (`one_gpu`).
   c2      N=10,000 x Mt=50,000 i.i.d. Gaussian design (BASELINE configs[1]);
           with n > 1: weak scaling over markers (the reference's own
           sharding): N = 10,000, Mt = 50,000*n, 4 GB per GPU ("c2-weak").
@@ -31,6 +37,15 @@ itself (127.0.0.1 rendezvous) before touching the GPU and exits with their
 status; rank 0 prints the line.  The data path uses libvampomi's RCCL
 communicator; torch.distributed (gloo) only broadcasts its id, runs the
 barriers and takes the max-over-ranks time.
+
+Failure is bounded and reported: every rank runs a watchdog (--deadline-s,
+default 420 s from the start) and records its stage (init / basis / generate
+/ warmup / timed / cpu / ...) in a per-job directory under $TMPDIR; on expiry
+rank 0 prints ONE JSON line with "error" and every rank's last stage and all
+ranks exit non-zero (torchrun then stops the rest).  RCCL creation is
+non-blocking and bounded (VAMPOMI_COMM_INIT_TIMEOUT_S, 90 s here) and a
+collective that never completes fails after VAMPOMI_COLL_TIMEOUT_S (120 s
+here), so a stuck transport ends in the same JSON line, not in silence.
 """
 from __future__ import annotations
 
@@ -40,6 +55,7 @@ import os
 import socket
 import subprocess
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -76,6 +92,13 @@ def parse_args(argv=None):
                          "drop-in rate: _it_K.bin, _r1_it_K.bin and CSV rows into a fresh directory under DIR)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher / rendezvous / max-over-ranks path only: no GPU work (CPU tests)")
+    ap.add_argument("--dry-run-hang-rank", type=int, default=-1,
+                    help="(tests) with --dry-run: this rank stops answering after the rendezvous")
+    ap.add_argument("--deadline-s", type=float, default=420.0,
+                    help="the whole run's time limit: past it every rank stops and rank 0 prints a JSON line with "
+                         "\"error\" and each rank's last stage (keep it under the caller's own limit)")
+    ap.add_argument("--no-headline", action="store_true",
+                    help="n > 1 with --config auto: skip the configs[2] (c3full) phase and its 1-GPU basis")
     return ap.parse_args(argv)
 
 
@@ -88,19 +111,40 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def spawn_ranks(n: int, argv) -> int:
+def spawn_ranks(n: int, argv, deadline_s: float) -> int:
     """Start n rank processes of this script (RANK / LOCAL_RANK / WORLD_SIZE /
     MASTER_* set; one GPU each).  Runs before this process imports torch or
     touches the GPU.  Rank 0 prints the JSON line on the shared stdout.  If a
-    rank fails, the others are stopped; returns the first failing rank's code."""
+    rank fails, the others are stopped; returns the first failing rank's code.
+    The ranks' own watchdogs end the job at the deadline; if they cannot (a
+    rank stuck where Python never runs again) this parent kills every rank
+    a little later and prints the failure line itself, with the stages the
+    ranks reported."""
     port = _free_port()
+    run_id = f"bench-{os.getpid()}-{port}"
+    t0 = time.time()
     procs = []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), VAMPOMI_RUN_ID=f"bench-{os.getpid()}-{port}")
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env))
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), VAMPOMI_RUN_ID=run_id,
+                   VAMPOMI_BENCH_T0=repr(t0))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else None, text=True))
+    # relay rank 0's stdout, noting whether its JSON line came
+    seen = {"line": False}
+
+    def relay(f):
+        for ln in f:
+            if ln.startswith("{"):
+                seen["line"] = True
+            sys.stdout.write(ln)
+            sys.stdout.flush()
+
+    th = threading.Thread(target=relay, args=(procs[0].stdout,), daemon=True)
+    th.start()
     rc = 0
     live = list(procs)
+    hard = t0 + deadline_s + 30.0  # the ranks' watchdogs fire at t0 + deadline_s
     while live:
         for p in list(live):
             code = p.poll()
@@ -111,8 +155,116 @@ def spawn_ranks(n: int, argv) -> int:
                 rc = code
                 for q in live:  # a rank failed: do not leave the others waiting in a collective
                     q.kill()
+        if live and time.time() > hard:
+            for q in live:
+                q.kill()
+            for q in live:
+                q.wait()
+            live = []
+            rc = rc or 124
         time.sleep(0.05)
+    th.join(5.0)
+    if rc != 0 and not seen["line"]:
+        print(json.dumps(failure_line(n, argv, f"rank processes ended with status {rc} before rank 0 reported",
+                                      read_stages(stage_dir(run_id), n, t0))), flush=True)
     return rc
+
+
+# ---------------------------------------------------------------------------
+# stages and the watchdog (bounded, diagnosable failure)
+# ---------------------------------------------------------------------------
+def run_key() -> str:
+    if os.environ.get("VAMPOMI_RUN_ID"):
+        return os.environ["VAMPOMI_RUN_ID"]
+    return "tr-{}-{}-{}".format(os.environ.get("MASTER_PORT", "0"), os.environ.get("TORCHELASTIC_RUN_ID", "none"),
+                                os.environ.get("WORLD_SIZE", "1"))
+
+
+def stage_dir(key: str) -> str:
+    return os.path.join(os.environ.get("TMPDIR", "/tmp"), f"vampomi_stages_{key}")
+
+
+def read_stages(d: str, n: int, t0: float) -> dict:
+    """Each rank's last reported stage (and seconds since the job start)."""
+    out = {}
+    for r in range(n):
+        try:
+            rec = json.load(open(os.path.join(d, f"rank{r}.json")))
+            out[str(r)] = rec if rec.get("wall", 0) >= t0 - 5 else {"stage": "no report from this run"}
+        except Exception:
+            out[str(r)] = {"stage": "no report (not started?)"}
+    return out
+
+
+def failure_line(n: int, argv, why: str, stages: dict) -> dict:
+    try:
+        a = parse_args(argv)
+        steps, warmup = a.steps, a.warmup
+    except SystemExit:
+        steps = warmup = None
+    return {"metric": "VAMP iterations/s (+ achieved HBM GB/s of the A/A^T kernels)", "value": None,
+            "unit": "iterations/s", "n_gpus": n, "steps": steps, "warmup": warmup, "higher_is_better": True,
+            "error": why, "rank_stages": stages}
+
+
+class Watchdog:
+    """Stage reports of this rank (a file per rank under stage_dir) and the
+    deadline: at t0 + deadline_s, rank 0 prints the failure line (unless the
+    result line is out already) and every rank exits (os._exit: no Python
+    teardown that could block on the device)."""
+
+    def __init__(self, args, rank: int, world: int):
+        self.rank, self.world = rank, world
+        self.t0 = float(os.environ.get("VAMPOMI_BENCH_T0", time.time()))
+        self.deadline = self.t0 + args.deadline_s
+        self.dir = stage_dir(run_key())
+        self.argv = sys.argv[1:]
+        self.lock = threading.Lock()
+        self.printed = False
+        self.finished = False  # this rank's part of the run is complete (teardown only)
+        self.partial = None  # rank 0: the finished part of the line, printed if a later phase hangs
+        os.makedirs(self.dir, exist_ok=True)
+        self.stage("start")
+        threading.Thread(target=self._run, daemon=True).start()
+
+    def stage(self, what: str):
+        self.cur = what
+        tmp = os.path.join(self.dir, f".rank{self.rank}.{os.getpid()}")
+        try:
+            with open(tmp, "w") as f:
+                json.dump({"stage": what, "t_s": round(time.time() - self.t0, 1), "wall": time.time(),
+                           "pid": os.getpid()}, f)
+            os.replace(tmp, os.path.join(self.dir, f"rank{self.rank}.json"))
+        except OSError:
+            pass
+
+    def emit(self, line: dict) -> bool:
+        """Print the one JSON line (rank 0), once."""
+        with self.lock:
+            if self.printed:
+                return False
+            self.printed = True
+            print(json.dumps(line), flush=True)
+            return True
+
+    def _run(self):
+        while time.time() < self.deadline:
+            time.sleep(min(1.0, max(0.05, self.deadline - time.time())))
+        why = f"deadline of {self.deadline - self.t0:.0f} s passed (rank {self.rank} at stage '{self.cur}')"
+        sys.stderr.write(f"bench.py rank {self.rank}: {why}\n")
+        sys.stderr.flush()
+        done = self.printed or (self.finished and self.rank != 0)
+        if self.rank == 0 and not done:
+            stages = read_stages(self.dir, self.world, self.t0)
+            if self.partial is not None:
+                line = dict(self.partial)
+                line["error_after_result"] = why
+                line["rank_stages"] = stages
+            else:
+                line = failure_line(self.world, self.argv, why, stages)
+            self.emit(line)
+            done = self.partial is not None
+        os._exit(0 if done else 124)
 
 
 # ---------------------------------------------------------------------------
@@ -153,7 +305,7 @@ def roofline(ks, kname: str, workload: str, period: int) -> dict:
                       "over the timed region (positions hashed from the launch index); launch counts exact"}
 
 
-def cpu_baseline(d, w: dict, beta, seed: int, warmup: int, steps: int, gpu_ref_passes: float,
+def cpu_baseline(y, w: dict, beta, seed: int, warmup: int, steps: int, gpu_ref_passes: float,
                  budget_s: float) -> dict:
     """The CPU oracle (C restatement, OpenMP) on the same workload.  Where
     W + k iterations fit the budget, it times the GPU's own window, iterations
@@ -167,7 +319,6 @@ def cpu_baseline(d, w: dict, beta, seed: int, warmup: int, steps: int, gpu_ref_p
     t0 = time.perf_counter()
     X = O.generate_markers(seed, w["kind"], N, 0, Mt)  # bit-identical to the device shard
     tgen = time.perf_counter() - t0
-    y = d.get_phen()
     probe = O.vamp_infere(X, y, Mt, true_signal=beta, max_iter=2, stop_criteria_thr=0.0, keep_hist=False, model=model)
     t_it = probe["it_end_s"][-1] / 2
     k = max(0, min(steps, int((budget_s - warmup * t_it) / max(t_it, 1e-3))))
@@ -189,29 +340,76 @@ def cpu_baseline(d, w: dict, beta, seed: int, warmup: int, steps: int, gpu_ref_p
                        f"{gpu_ref_passes:.2f} passes per iteration (W + k iterations exceed the {budget_s:.0f} s budget)")
 
 
-def cpu_reference_ops(w: dict, seed: int, threads: int, k_cg: float):
-    """The reference's OWN Ax / ATx (src/data.cpp:294-373, compiled from its
-    sources into oracle/_ref/ref_data in the build container) timed on a
-    generated matrix of the workload's shape, on the same host threads; the
-    projected reference iteration rate uses its own call counts per
-    iteration (it > 1): 5 + k Ax and 3 + k ATx with k = k1 + k2 CG steps
-    (src/vamp.cpp:232,303,508,518-519,653-654,681,826), k from
-    the GPU window.  The denoiser/EM (< 1 % of its CPU time) is left out."""
+INT_MAX = 2**31 - 1
+
+
+def ref_ops_time(w: dict, seed: int, threads: int) -> dict:
+    """The reference's OWN data::Ax / data::ATx (src/data.cpp:294-373,
+    compiled from its sources into oracle/_ref/ref_data in the build
+    container) timed on a generated N x Ms matrix on `threads` host threads:
+    ms per call at the workload's full marker count.  The reference indexes
+    the matrix with a 32-bit int (`i*N`, src/data.cpp:297,351),
+    which overflows once M*N > 2^31 - 1 (it crashed with SIGSEGV at the C3
+    shard), so a larger shard is timed on its first floor((2^31-1)/N)
+    markers and projected linearly per marker (both kernels loop over markers
+    with per-marker work of N)."""
     exe = os.path.join(ROOT, "oracle", "_ref", "ref_data")
     if not os.path.exists(exe):
         return {"skipped": "oracle/_ref/ref_data not built (needs /root/reference in the build container)"}
+    N, Mt = w["N"], w["Mt"]
+    Ms = Mt if N * Mt <= INT_MAX else INT_MAX // N
     env = dict(os.environ, OMP_NUM_THREADS=str(threads))
-    out = subprocess.run([exe, "time", str(w["N"]), str(w["Mt"]), "2", str(seed)], env=env, capture_output=True,
-                         text=True, timeout=300)
+    out = subprocess.run([exe, "time", str(N), str(Ms), "2", str(seed)], env=env, capture_output=True, text=True,
+                         timeout=300)
     if out.returncode != 0:
         return {"error": f"ref_data exit {out.returncode}: {out.stderr[-300:]}"}
     r = json.loads(out.stdout.strip().splitlines()[-1])
+    scale = Mt / Ms
+    res = {"threads": r["threads"], "ax_ms": r["ax_ms"] * scale, "atx_ms": r["atx_ms"] * scale, "Ms": Ms}
+    if Ms < Mt:
+        res["projected_from"] = (f"{N} x {Ms} (the largest shard whose M*N fits the reference's 32-bit int index, "
+                                 f"src/data.cpp:297,351; it overflows at the full {N} x {Mt} shard), "
+                                 f"x {scale:.3f} per marker: Ax {r['ax_ms']:.1f} ms, ATx {r['atx_ms']:.1f} ms measured")
+    return res
+
+
+def cpu_reference_ops(w: dict, seed: int, threads: int, k_cg: float):
+    """The reference's own Ax / ATx (ref_ops_time) and its projected iteration
+    rate from its own call counts per iteration (it > 1): 5 + k Ax and 3 + k
+    ATx with k = k1 + k2 CG steps (src/vamp.cpp:232,303,508,518-519,653-654,
+    681,826), k from the GPU window.  The denoiser/EM (< 1 % of
+    its CPU time) is left out."""
+    r = ref_ops_time(w, seed, threads)
+    if "ax_ms" not in r:
+        return r
     t_it = ((5 + k_cg) * r["ax_ms"] + (3 + k_cg) * r["atx_ms"]) * 1e-3
-    return {"value": 1.0 / t_it, "unit": "VAMP iterations/s", "kind": "reference", "projected": True,
-            "cores": r["threads"], "ax_ms": r["ax_ms"], "atx_ms": r["atx_ms"],
-            "sample": f"Ax and ATx (mean of 2 calls each) of the reference's src/data.cpp (oracle/_ref) on a generated "
-                      f"{w['N']} x {w['Mt']} matrix, {r['threads']} OpenMP threads; iteration = (5 + k) Ax + (3 + k) "
-                      f"ATx, k = {k_cg:.2f} (the GPU window's mean CG + Onsager steps)"}
+    out = {"value": 1.0 / t_it, "unit": "VAMP iterations/s", "kind": "reference", "projected": True,
+           "cores": r["threads"], "ax_ms": round(r["ax_ms"], 3), "atx_ms": round(r["atx_ms"], 3),
+           "sample": f"Ax and ATx (mean of 2 calls each) of the reference's src/data.cpp (oracle/_ref) on a generated "
+                     f"{w['N']} x {r['Ms']} matrix, {r['threads']} OpenMP threads; iteration = (5 + k) Ax + (3 + k) "
+                     f"ATx, k = {k_cg:.2f} (the GPU window's mean CG + Onsager steps)"}
+    if "projected_from" in r:
+        out["projected_from"] = r["projected_from"]
+    return out
+
+
+def cpu_reference_ops_assoc(w: dict, seed: int, threads: int):
+    """c5: of one LOO test (src/main_meth.cpp:245-264) only the reference's
+    z1 = A x1_hat (data::Ax) builds here; data::pvals_loo (src/data.cpp:385-417)
+    calls linear_reg1d_pvals from the Boost-dependent src/utilities.cpp.  So
+    this times the reference's Ax and reports the rate a test could at most
+    reach if its per-marker pass were free: an UPPER bound on the reference."""
+    r = ref_ops_time(w, seed, threads)
+    if "ax_ms" not in r:
+        return r
+    out = {"value": w["Mt"] / (r["ax_ms"] * 1e-3), "unit": "markers/s", "kind": "reference", "projected": True,
+           "upper_bound": True, "cores": r["threads"], "ax_ms": round(r["ax_ms"], 3),
+           "sample": f"the reference's data::Ax (src/data.cpp:340-373, oracle/_ref) on a generated {w['N']} x "
+                     f"{r['Ms']} matrix, {r['threads']} OpenMP threads: the test's A x1_hat only (pvals_loo needs "
+                     "Boost, absent), so markers / Ax time bounds the reference's rate from above"}
+    if "projected_from" in r:
+        out["projected_from"] = r["projected_from"]
+    return out
 
 
 def write_rate(args, d, R, opts, beta, barrier, el_nowrite: float) -> dict:
@@ -301,15 +499,17 @@ def cpu_baseline_assoc(d, w: dict, est, seed: int) -> dict:
 class Ranks:
     """torch.distributed (gloo) for the id broadcast, barriers and max-over-ranks time."""
 
-    def __init__(self):
+    def __init__(self, timeout_s: float = 1800.0):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        import datetime
+
         import torch.distributed as dist
 
         self.dist = dist
         if self.world > 1:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=max(30.0, timeout_s)))
 
     def max(self, v: float) -> float:
         if self.world == 1:
@@ -333,28 +533,357 @@ class Ranks:
         if self.world > 1:
             self.dist.barrier()
 
+    def bcast(self, obj):
+        if self.world == 1:
+            return obj
+        box = [obj]
+        self.dist.broadcast_object_list(box, src=0)
+        return box[0]
+
     def close(self):
         if self.world > 1:
             self.dist.destroy_process_group()
 
 
-def dry_run(args, R: Ranks):
+class Solo:
+    """Ranks of a one-rank measurement inside a multi-rank job (rank 0's 1-GPU
+    bases): no collectives."""
+    world, rank = 1, 0
+    dist = None
+
+    def __init__(self, local: int):
+        self.local = local
+
+    def max(self, v):
+        return v
+
+    def sum(self, v):
+        return v
+
+    def barrier(self):
+        pass
+
+    def bcast(self, obj):
+        return obj
+
+
+def dry_run(args, R: Ranks, wd: Watchdog):
     """The launcher, rendezvous, barrier and max-over-ranks path without a GPU."""
+    wd.stage("dry-run barrier")
     R.barrier()
+    if R.rank == args.dry_run_hang_rank:
+        wd.stage("dry-run hang (test)")
+        while True:  # a rank that stops answering: the watchdogs must end the job
+            time.sleep(3600)
+    wd.stage("dry-run timed")
     t0 = time.perf_counter()
     for _ in range(args.steps):
         time.sleep(0.001)
     R.barrier()
     el = R.max(time.perf_counter() - t0)
     seen = int(R.sum(1.0))
+    wd.finished = True
     if R.rank == 0:
-        print(json.dumps({"metric": "dry run", "value": 0.0, "unit": "none", "n_gpus": R.world, "steps": args.steps,
-                          "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3),
-                          "ranks_seen": seen, "dry_run": True}), flush=True)
+        wd.emit({"metric": "dry run", "value": 0.0, "unit": "none", "n_gpus": R.world, "steps": args.steps,
+                 "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3), "ranks_seen": seen,
+                 "dry_run": True})
     R.close()
 
 
-def bench_assoc(args, d, w, R: Ranks, t_start):
+def open_data(R, w: dict, device: int):
+    """A context for workload w over R's ranks (an RCCL communicator if
+    R.world > 1; its id made on rank 0 and broadcast over gloo)."""
+    import vampomi_amd as va
+
+    comm_id = R.bcast(va.comm_unique_id() if R.rank == 0 else None) if R.world > 1 else None
+    return va.Data(w["N"], w["Mt"], rank=R.rank, nranks=R.world, comm_id=comm_id, device=device)
+
+
+def vamp_window(args, R, w: dict, wd: Watchdog, steps: int, warmup: int, tag: str, keep=False) -> dict:
+    """Generate workload w on the device, run `warmup` untimed and `steps`
+    timed VAMP iterations over R's ranks; returns the measurements (and,
+    with keep, the open context and run for the caller's further legs)."""
+    import torch
+
+    import vampomi_amd as va
+
+    wd.stage(f"{tag}: open {w['workload']} (N={w['N']}, Mt={w['Mt']}, {R.world} rank(s))")
+    d = open_data(R, w, R.local)
+    try:
+        wd.stage(f"{tag}: generate")
+        t0 = time.perf_counter()
+        d.generate(args.seed, w["kind"])
+        model = w.get("model", "linear")
+        if model == "bin_class":
+            beta = d.simulate_phen_binary(args.seed + 1, lam=0.1, h2=0.8)
+        else:
+            beta = d.simulate_phen(args.seed + 1, lam=0.1, h2=0.8)
+        t_setup = time.perf_counter() - t0
+        if args.op_variant is not None:
+            d.set_variant(3, args.op_variant)
+        opts = va.VampOptions(max_iter=warmup + steps, stop_criteria_thr=0.0, batch_rhs=args.batch_rhs, model=model)
+        v = va.Vamp(d, opts, true_signal=beta)
+        wd.stage(f"{tag}: warmup ({warmup} iterations)")
+        v.begin()
+        for _ in range(warmup):
+            v.step()
+        ref0, _ = v.a_passes
+        d.reset_stats()
+        d.set_timing(not args.no_timing, args.timing_period)
+
+        def barrier():
+            d.sync()
+            torch.cuda.synchronize() if torch.cuda.is_available() else None
+            R.barrier()
+
+        wd.stage(f"{tag}: timed ({steps} iterations)")
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            v.step()
+        barrier()
+        el = R.max(time.perf_counter() - t0)
+        st = d.stats()
+        ref1, _ = v.a_passes
+        res = {"el": el, "st": st, "summ": v.summary(), "ref_passes": (ref1 - ref0) / steps, "setup": t_setup,
+               "M": d.M, "nranks": d.nranks, "steps": steps, "warmup": warmup, "model": model, "beta": beta,
+               "opts": opts, "barrier": barrier}
+        res["rank_times"] = per_rank_times(R, st, el) if R.world > 1 else per_rank_times(Solo(R.local), st, el)
+        v.end()
+        if keep:
+            res["d"] = d
+            d = None
+        return res
+    finally:
+        if d is not None:
+            wd.stage(f"{tag}: close")
+            d.close()
+
+
+def dominant_roofline(args, res: dict, w: dict, kernel_name) -> dict:
+    """roofline of the (kernel class, K) with the most device time."""
+    st = res["st"]
+    cands = []
+    for which, arr in ((0, st.ax_k), (1, st.atx_k), (3, st.op_k)):
+        for k in range(4):
+            if arr[k].timed:
+                cands.append((arr[k].ms_total, which, k + 1, arr[k]))
+    if not cands:
+        return None
+    _, which, K, ks = max(cands, key=lambda c: c[0])
+    # A^T.u in the CG carries the lmmse_mult epilogue (mode 1); the one-pass
+    # operator's instantiation depends on N (passed as mode)
+    return roofline(ks, kernel_name(which, K, w["N"] if which == 3 else 1), w["workload"], args.timing_period)
+
+
+def summary_of(res: dict, w: dict, strong: bool, n: int) -> dict:
+    """A compact record of one vamp_window (1-GPU bases, the headline phase)."""
+    st, el, steps = res["st"], res["el"], res["steps"]
+    all_ms = st.ax.ms_total + st.atx.ms_total + st.op.ms_total
+    all_bytes = st.ax.bytes_total + st.atx.bytes_total + st.op.bytes_total
+    it_s = steps / el
+    return {"workload": w["workload"], "N": w["N"], "Mt": w["Mt"], "M_per_gpu": res["M"], "n_gpus": n,
+            "iterations_timed": f"{res['warmup'] + 1}-{res['warmup'] + steps}",
+            "iterations_per_s": round(it_s, 4), "value": round(it_s if (strong or n == 1) else n * it_s, 4),
+            "ms_per_step": round(el / steps * 1e3, 3), "passes_exec_per_step": round(st.a_passes_exec / steps, 2),
+            "hbm_gbs_all_A_kernels": round(all_bytes / (all_ms * 1e-3) / 1e9, 1) if all_ms > 0 else None,
+            "a_kernel_frac_of_step": round(all_ms * 1e-3 / el, 4) if el > 0 else None,
+            "cg_iters": res["summ"]["cg_iters"][res["warmup"]:], "ons_iters": res["summ"]["ons_iters"][res["warmup"]:],
+            "setup_s": round(res["setup"], 2)}
+
+
+def per_pass_marker_ms(rec: dict) -> float:
+    """ms per executed pass over X per marker (a 1-GPU basis at another Mt)."""
+    return rec["ms_per_step"] / (rec["passes_exec_per_step"] * rec["M_per_gpu"])
+
+
+def one_gpu_bases(args, R: Ranks, wd: Watchdog, w: dict, headline: bool) -> dict:
+    """Rank 0 alone, on its own GPU, before any n-rank context exists (the
+    other ranks wait at a gloo barrier): the 1-GPU runs the n-rank line is read
+    against, measured in this job on this node.
+      same_problem: the n-rank workload's WHOLE problem on one GPU, when it
+        fits (c2-weak: 4n GB): the same iterations, so speedup = this run's
+        iterations/s over it, exactly;
+      c3big: N = 100,000 x 300,000 (240 GB, the most of configs[2] one
+        MI355X holds), for the headline configs[2] phase (400 GB, which no
+        single GPU holds): its ms per executed pass per marker, times the
+        headline's markers and passes, is the 1-GPU equivalent."""
+    out = {}
+    if R.rank == 0:
+        solo = Solo(R.local)
+        if w["N"] * w["Mt"] * 8 <= 200e9:
+            wd.stage("basis: same problem on 1 GPU")
+            try:
+                r = vamp_window(args, solo, dict(w, workload=w["workload"] + "@1gpu"), wd, args.steps, args.warmup,
+                                "basis same-problem")
+                out["same_problem"] = summary_of(r, w, True, 1)
+            except Exception as e:
+                out["same_problem"] = {"error": repr(e)}
+        if headline:
+            from vampomi_amd.workloads import workload
+
+            wb = workload("c3big", 1)
+            try:
+                r = vamp_window(args, solo, wb, wd, 4, 1, "basis c3big")
+                rec = summary_of(r, wb, False, 1)
+                rec["ms_per_pass_per_marker"] = per_pass_marker_ms(rec)
+                out["c3big"] = rec
+            except Exception as e:
+                out["c3big"] = {"error": repr(e)}
+    wd.stage("basis: barrier")
+    R.barrier()
+    return out
+
+
+def run_linear(args, R: Ranks, wd: Watchdog, w: dict, t_start: float) -> dict:
+    """The linear / probit VAMP line of workload w on R's ranks."""
+    import vampomi_amd as va
+
+    n = R.world
+    strong = w.get("scaling") == "strong"
+    auto_multi = args.config == "auto" and n > 1
+    headline = auto_multi and not args.no_headline
+    bases = one_gpu_bases(args, R, wd, w, headline or (strong and w["workload"] == "c3full")) if n > 1 else {}
+
+    res = vamp_window(args, R, w, wd, args.steps, args.warmup, "main", keep=True)
+    d, st, el, model = res["d"], res["st"], res["el"], res["model"]
+    try:
+        roof = dominant_roofline(args, res, w, d.kernel_name)
+        y = d.get_phen() if (R.rank == 0 and n == 1 and not args.no_cpu_baseline) else None
+        with_writes = (write_rate(args, d, R, res["opts"], res["beta"], res["barrier"], el) if args.write else None)
+    finally:
+        wd.stage("main: close")
+        d.close()
+    it_s = args.steps / el
+    all_ms = st.ax.ms_total + st.atx.ms_total + st.op.ms_total
+    all_bytes = st.ax.bytes_total + st.atx.bytes_total + st.op.bytes_total
+    line = {
+        "metric": "VAMP iterations/s (+ achieved HBM GB/s of the A/A^T kernels)",
+        "value": round(it_s if strong else n * it_s, 4),
+        "unit": "iterations/s" if (strong or n == 1) else "shard-iterations/s",
+        "n_gpus": n, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(el / args.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "strong" if strong else "weak", "vs_baseline": None,
+        "dtype": "f64", "data": "synthetic (index-keyed dyadic generator, generated in HBM)",
+        "config": {"workload": w["workload"], "model": model, "N": w["N"], "Mt": w["Mt"], "M_per_gpu": res["M"],
+                   "design": "gaussian" if w["kind"] == va.GEN_GAUSS else "methylation-like",
+                   "iterations_timed": f"{args.warmup + 1}-{args.warmup + args.steps}",
+                   "parallelism": f"markers sharded over {n} GPU(s)" + (", RCCL all-reduce" if n > 1 else ""),
+                   "comm": {"backend": "rccl" if n > 1 else "none", "nranks": res["nranks"]}},
+        "roofline": roof,
+        "hbm_gbs_all_A_kernels": round(all_bytes / (all_ms * 1e-3) / 1e9, 1) if all_ms > 0 else None,
+        "passes_exec_per_step": round(st.a_passes_exec / args.steps, 2),  # stats reset at the timed region
+        "passes_ref_per_step": round(res["ref_passes"], 2),
+        # device time of the A-kernels over the wall time: each (kernel, K)'s
+        # average over its sampled launches (hashed positions, unbiased over the
+        # solve's steps) times its exact launch count; --timing-period 1 times
+        # every launch (a measured sum, at 1-2.6 % of the iteration rate)
+        "a_kernel_frac_of_step": round(all_ms * 1e-3 / el, 4) if el > 0 else None,
+        "a_kernel_timing": {"timed_launches": int(st.ax.timed + st.atx.timed + st.op.timed),
+                            "launches": int(st.ax.launches + st.atx.launches + st.op.launches),
+                            "period": args.timing_period},
+        "per_rank": res["rank_times"],
+        "cg_iters": res["summ"]["cg_iters"][args.warmup:], "ons_iters": res["summ"]["ons_iters"][args.warmup:],
+        "setup_s": round(res["setup"], 2),
+        "cpu_baseline": None,
+    }
+    line["config"]["output_files"] = ("not written in the timed window (BASELINE.md: the metric excludes output-file "
+                                      "writes); see with_writes" if args.write else
+                                      "not written in the timed window (BASELINE.md: the metric excludes output-file "
+                                      "writes; bench.py --write times them)")
+    if with_writes:
+        ws = with_writes.pop("elapsed_s")
+        with_writes["value"] = round(args.steps / ws if strong else n * args.steps / ws, 4)
+        line["with_writes"] = with_writes
+    if n > 1:
+        line["scaling_basis"] = (
+            "read against the n = 1 line of the same workload family: `python bench.py --gpus 1` (c2, configs[1]: "
+            "N = 10,000 x 50,000, the same per-GPU shard as c2-weak)" if w["workload"] == "c2-weak" else
+            "one_gpu.c3big (measured in this job; configs[2] does not fit one GPU)" if strong else
+            f"the n = 1 line of --config {args.config}")
+        one = {}
+        if "same_problem" in bases:
+            sp = bases["same_problem"]
+            one["same_problem"] = sp
+            if "iterations_per_s" in sp:
+                one["same_problem"]["speedup_of_this_run"] = round(it_s / sp["iterations_per_s"], 4)
+                one["same_problem"]["note"] = (f"the whole {w['N']} x {w['Mt']} problem of this line on rank 0's GPU "
+                                               "alone, same iterations: strong scaling of this exact problem")
+        if "c3big" in bases:
+            one["c3big"] = bases["c3big"]
+        if one:
+            line["one_gpu"] = one
+        if strong and "c3big" in bases and "ms_per_pass_per_marker" in bases["c3big"]:
+            line["one_gpu_equivalent"] = equivalent(bases["c3big"], w["Mt"], line["passes_exec_per_step"], it_s, n)
+    wd.partial = line  # a hang in a later phase still reports this
+    if headline:
+        line["headline_c3full"] = run_headline(args, R, wd, bases.get("c3big"))
+        wd.partial = line
+    if model == "bin_class":
+        line["parity_note"] = ("probit: x1_hat/r1 parity bar is max(1e-10, k x the oracle's own rank-count spread), "
+                               "integers exact (DESIGN.md §3)")
+    if R.rank == 0 and n == 1 and not args.no_cpu_baseline:
+        wd.stage("cpu baseline")
+        if w["workload"] == "c3big":
+            # the oracle's leg would generate the whole 240 GB matrix on the host
+            line["cpu_baseline"] = {"skipped": "240 GB matrix; see the --config c3 line (same N, 62,500-marker shard)"}
+        else:
+            try:
+                line["cpu_baseline"] = cpu_baseline(y, w, res["beta"], args.seed, args.warmup, args.steps,
+                                                    res["ref_passes"], args.cpu_budget)
+            except Exception as e:  # reported, never fatal for the GPU number
+                line["cpu_baseline"] = {"error": repr(e)}
+        if model == "linear":
+            try:
+                k_cg = (sum(line["cg_iters"]) + sum(line["ons_iters"])) / max(len(line["cg_iters"]), 1)
+                threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+                line["cpu_reference_ops"] = cpu_reference_ops(w, args.seed, threads, k_cg)
+            except Exception as e:
+                line["cpu_reference_ops"] = {"error": repr(e)}
+    line["wall_s_since_start"] = round(time.perf_counter() - t_start, 1)
+    return line
+
+
+def equivalent(c3big: dict, Mt: int, passes: float, it_s: float, n: int) -> dict:
+    """The 1-GPU iterations/s of an Mt-marker problem at N = 100,000 from the
+    measured c3big basis: its ms per executed pass per marker x Mt x this
+    run's executed passes per iteration (no single MI355X holds the problem)."""
+    one = 1e3 / (c3big["ms_per_pass_per_marker"] * Mt * passes)
+    return {"value": round(one, 4), "unit": "iterations/s", "measured_in_this_job": True,
+            "source": f"one_gpu.c3big (N = 100,000 x 300,000 on rank 0's GPU alone, {c3big['ms_per_step']} ms per "
+                      f"iteration at {c3big['passes_exec_per_step']} passes) x Mt = {Mt} x this run's {passes} passes "
+                      "per iteration; the problem itself does not fit one GPU",
+            "strong_scaling_efficiency": round(it_s / (n * one), 4)}
+
+
+def run_headline(args, R: Ranks, wd: Watchdog, c3big) -> dict:
+    """configs[2] itself (N = 100,000 x Mt = 500,000, 400 GB) sharded over
+    this job's ranks, after the main phase: north_star's headline problem at
+    n = 2 / 4 / 8 (it does not fit one GPU).  Fewer timed iterations (at most
+    10) keep the job short; errors are recorded, not fatal for the line."""
+    from vampomi_amd.workloads import workload
+
+    w = workload("c3full", R.world)
+    steps = min(args.steps, 10)
+    try:
+        res = vamp_window(args, R, w, wd, steps, args.warmup, "headline", keep=True)
+        d = res["d"]
+        try:
+            roof = dominant_roofline(args, res, w, d.kernel_name)
+        finally:
+            d.close()
+        rec = summary_of(res, w, True, R.world)
+        rec["roofline"] = roof
+        rec["per_rank"] = res["rank_times"]
+        if c3big and "ms_per_pass_per_marker" in c3big:
+            rec["one_gpu_equivalent"] = equivalent(c3big, w["Mt"], rec["passes_exec_per_step"],
+                                                   rec["iterations_per_s"], R.world)
+        return rec
+    except Exception as e:
+        return {"error": repr(e), "workload": "c3full"}
+
+
+def bench_assoc(args, R: Ranks, wd: Watchdog, w: dict, t_start):
     """--config c5: the LOO association test (src/main_meth.cpp:245-264) on
     device-resident inputs; a step is one whole test."""
     import ctypes as C
@@ -365,6 +894,9 @@ def bench_assoc(args, d, w, R: Ranks, t_start):
     import vampomi_amd as va
 
     N, Mt = w["N"], w["Mt"]
+    wd.stage("c5: open + generate")
+    d = open_data(R, w, R.local)
+    d.generate(args.seed, w["kind"])
     beta = d.simulate_phen(args.seed + 1, lam=0.1, h2=0.5)
     t_setup = time.perf_counter() - t_start
     est = beta * 0.9 / np.sqrt(N)  # an estimate file's values (x1_hat / sqrt(N))
@@ -377,6 +909,7 @@ def bench_assoc(args, d, w, R: Ranks, t_start):
         va._lib.check(lib.vampomi_assoc_loo(d.ctx, C.c_void_p(e_t.data_ptr()), C.c_void_p(p_t.data_ptr()), None,
                                             va.MEM_DEVICE))
 
+    wd.stage("c5: warmup")
     for _ in range(args.warmup):
         step()
     d.reset_stats()
@@ -387,6 +920,7 @@ def bench_assoc(args, d, w, R: Ranks, t_start):
         torch.cuda.synchronize()
         R.barrier()
 
+    wd.stage("c5: timed")
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -413,180 +947,76 @@ def bench_assoc(args, d, w, R: Ranks, t_start):
         "cpu_baseline": None,
     }
     if R.rank == 0 and R.world == 1 and not args.no_cpu_baseline:
+        wd.stage("cpu baseline")
         try:
             line["cpu_baseline"] = cpu_baseline_assoc(d, w, est, args.seed)
         except Exception as e:
             line["cpu_baseline"] = {"error": repr(e)}
+        try:
+            threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+            line["cpu_reference_ops"] = cpu_reference_ops_assoc(w, args.seed, threads)
+        except Exception as e:
+            line["cpu_reference_ops"] = {"error": repr(e)}
     d.close()
-    if R.rank == 0:
-        print(json.dumps(line), flush=True)
-    R.close()
+    return line
 
 
 def main():
     args = parse_args()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         # start the ranks before this process touches the GPU (or imports torch)
-        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
-
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:], args.deadline_s))
+    rank, world = int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1"))
+    wd = Watchdog(args, rank, world)
+    # bounded RCCL (engine.cpp): creation and every collective fail with a
+    # status instead of waiting for a peer that never comes
+    os.environ.setdefault("VAMPOMI_COMM_INIT_TIMEOUT_S", "90")
+    os.environ.setdefault("VAMPOMI_COLL_TIMEOUT_S", "120")
+    t_start = time.perf_counter()
+    wd.stage("import torch")
     import torch  # noqa: F401  (before libvampomi: one HIP runtime per process)
 
-    R = Ranks()
-    if args.dry_run:
-        return dry_run(args, R)
-    if args.gpus != R.world:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={R.world}: launch one process per GPU")
+    wd.stage("gloo rendezvous")
+    R = Ranks(timeout_s=args.deadline_s)
+    try:
+        if args.dry_run:
+            return dry_run(args, R, wd)
+        if args.gpus != R.world:
+            raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={R.world}: launch one process per GPU")
+        from vampomi_amd.workloads import workload
 
-    import vampomi_amd as va
-    from vampomi_amd.workloads import workload
+        if torch.cuda.is_available():
+            # one GPU per local rank; more ranks than visible GPUs share them
+            # modulo (RCCL then refuses the job at creation: "Duplicate GPU",
+            # reported in the line like any other failure)
+            R.local = R.local % max(1, torch.cuda.device_count())
+            torch.cuda.set_device(R.local)  # torch's own context on this rank's GPU, not on GPU 0
+        w = workload(args.config, R.world)
+        if w.get("model") == "loo":
+            line = bench_assoc(args, R, wd, w, t_start)
+        else:
+            line = run_linear(args, R, wd, w, t_start)
+        wd.finished = True
+        if R.rank == 0:
+            wd.emit(line)
+        wd.stage("done")
+    except SystemExit:
+        raise
+    except BaseException as e:  # one diagnosable line instead of a bare traceback
+        import traceback
 
-    if torch.cuda.is_available():
-        torch.cuda.set_device(R.local)  # torch's own context on this rank's GPU, not on GPU 0
-    n = R.world
-    w = workload(args.config, n)
-    N, Mt = w["N"], w["Mt"]
-    comm_id = None
-    if n > 1:
-        obj = [va.comm_unique_id() if R.rank == 0 else None]
-        R.dist.broadcast_object_list(obj, src=0)
-        comm_id = obj[0]
-    d = va.Data(N, Mt, rank=R.rank, nranks=n, comm_id=comm_id, device=R.local)
-    t0 = time.perf_counter()
-    d.generate(args.seed, w["kind"])
-    model = w.get("model", "linear")
-    if model == "loo":
-        return bench_assoc(args, d, w, R, t0)
-    if model == "bin_class":
-        beta = d.simulate_phen_binary(args.seed + 1, lam=0.1, h2=0.8)
-    else:
-        beta = d.simulate_phen(args.seed + 1, lam=0.1, h2=0.8)
-    t_setup = time.perf_counter() - t0
-    if args.op_variant is not None:
-        d.set_variant(3, args.op_variant)
-
-    opts = va.VampOptions(max_iter=args.warmup + args.steps, stop_criteria_thr=0.0, batch_rhs=args.batch_rhs,
-                          model=model)
-    v = va.Vamp(d, opts, true_signal=beta)
-    v.begin()
-    for _ in range(args.warmup):
-        v.step()
-    ref0, _ = v.a_passes
-    d.reset_stats()
-    d.set_timing(not args.no_timing, args.timing_period)
-
-    def barrier():
-        d.sync()
-        torch.cuda.synchronize() if torch.cuda.is_available() else None
-        R.barrier()
-
-    barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        v.step()
-    barrier()
-    el = R.max(time.perf_counter() - t0)
-    st = d.stats()
-    rank_times = per_rank_times(R, st, el)
-    ref1, _ = v.a_passes
-    summ = v.summary()
-    v.end()
-    with_writes = write_rate(args, d, R, opts, beta, barrier, el) if args.write else None
-
-    it_s = args.steps / el
-    strong = w.get("scaling") == "strong"
-    # dominant kernel: the (class, batch width) with the most device time
-    cands = []
-    for which, arr in ((0, st.ax_k), (1, st.atx_k), (3, st.op_k)):
-        for k in range(4):
-            if arr[k].timed:
-                cands.append((arr[k].ms_total, which, k + 1, arr[k]))
-    roof = None
-    if cands:
-        _, which, K, ks = max(cands, key=lambda c: c[0])
-        # A^T.u in the CG carries the lmmse_mult epilogue (mode 1); the one-pass
-        # operator's instantiation depends on N (passed as mode)
-        roof = roofline(ks, d.kernel_name(which, K, N if which == 3 else 1), w["workload"], args.timing_period)
-    all_ms = st.ax.ms_total + st.atx.ms_total + st.op.ms_total
-    all_bytes = st.ax.bytes_total + st.atx.bytes_total + st.op.bytes_total
-    ref_passes = (ref1 - ref0) / args.steps
-    line = {
-        "metric": "VAMP iterations/s (+ achieved HBM GB/s of the A/A^T kernels)",
-        "value": round(it_s if strong else n * it_s, 4),
-        "unit": "iterations/s" if (strong or n == 1) else "shard-iterations/s",
-        "n_gpus": n, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": round(el / args.steps * 1e3, 3),
-        "higher_is_better": True, "scaling": "strong" if strong else "weak", "vs_baseline": None,
-        "dtype": "f64", "data": "synthetic (index-keyed dyadic generator, generated in HBM)",
-        "config": {"workload": w["workload"], "model": model, "N": N, "Mt": Mt, "M_per_gpu": d.M,
-                   "design": "gaussian" if w["kind"] == va.GEN_GAUSS else "methylation-like",
-                   "iterations_timed": f"{args.warmup + 1}-{args.warmup + args.steps}",
-                   "parallelism": f"markers sharded over {n} GPU(s)" + (", RCCL all-reduce" if n > 1 else ""),
-                   "comm": {"backend": "rccl" if n > 1 else "none", "nranks": d.nranks}},
-        "roofline": roof,
-        "hbm_gbs_all_A_kernels": round(all_bytes / (all_ms * 1e-3) / 1e9, 1) if all_ms > 0 else None,
-        "passes_exec_per_step": round(st.a_passes_exec / args.steps, 2),  # stats reset at the timed region
-        "passes_ref_per_step": round(ref_passes, 2),
-        # device time of the A-kernels over the wall time: each (kernel, K)'s
-        # average over its sampled launches (hashed positions, unbiased over the
-        # solve's steps) times its exact launch count; --timing-period 1 times
-        # every launch (a measured sum, at 1-2.6 % of the iteration rate)
-        "a_kernel_frac_of_step": round(all_ms * 1e-3 / el, 4) if el > 0 else None,
-        "a_kernel_timing": {"timed_launches": int(st.ax.timed + st.atx.timed + st.op.timed),
-                            "launches": int(st.ax.launches + st.atx.launches + st.op.launches),
-                            "period": args.timing_period},
-        "per_rank": rank_times,
-        "cg_iters": summ["cg_iters"][args.warmup:], "ons_iters": summ["ons_iters"][args.warmup:],
-        "setup_s": round(t_setup, 2),
-        "cpu_baseline": None,
-    }
-    line["config"]["output_files"] = ("not written in the timed window (BASELINE.md: the metric excludes output-file "
-                                      "writes); see with_writes" if args.write else
-                                      "not written in the timed window (BASELINE.md: the metric excludes output-file "
-                                      "writes; bench.py --write times them)")
-    if with_writes:
-        ws = with_writes.pop("elapsed_s")
-        with_writes["value"] = round(args.steps / ws if strong else n * args.steps / ws, 4)
-        line["with_writes"] = with_writes
-    if strong and n > 1:
-        # the problem does not fit one GPU.  ESTIMATE of its 1-GPU rate from the
-        # committed c3big line (same N and design, 300,000 markers resident on
-        # one MI355X, another run and build): its time per executed pass per
-        # marker, times this run's markers and executed passes per iteration
-        src = "profiles/r03e_bench_c3big.json"
-        try:
-            ref = json.load(open(os.path.join(ROOT, src)))
-            per_pass_marker = ref["ms_per_step"] / (ref["passes_exec_per_step"] * ref["config"]["Mt"])
-            one = 1e3 / (per_pass_marker * Mt * (st.a_passes_exec / args.steps))
-            line["one_gpu_equivalent"] = {
-                "estimate": True, "value": round(one, 4), "unit": "iterations/s",
-                "source": f"{src} (N=100,000 x 300,000 on 1 GPU, {ref['ms_per_step']} ms per iteration at "
-                          f"{ref['passes_exec_per_step']} passes): ms per pass per marker x Mt x this run's "
-                          "passes per iteration; not a measurement of this problem on one GPU (it does not fit)",
-                "strong_scaling_efficiency_estimate": round(it_s / (n * one), 4)}
-        except Exception as e:
-            line["one_gpu_equivalent"] = {"error": repr(e)}
-    if model == "bin_class":
-        line["parity_note"] = ("probit: x1_hat/r1 parity bar is max(1e-10, 10x the oracle's own rank-count spread), "
-                               "integers exact (DESIGN.md §3)")
-    if R.rank == 0 and n == 1 and not args.no_cpu_baseline and w["workload"] == "c3big":
-        # the oracle's leg would generate the whole 240 GB matrix on the host
-        line["cpu_baseline"] = {"skipped": "240 GB matrix; see the --config c3 line (same N, 62,500-marker shard)"}
-    elif R.rank == 0 and n == 1 and not args.no_cpu_baseline:
-        try:
-            line["cpu_baseline"] = cpu_baseline(d, w, beta, args.seed, args.warmup, args.steps, ref_passes,
-                                                args.cpu_budget)
-        except Exception as e:  # reported, never fatal for the GPU number
-            line["cpu_baseline"] = {"error": repr(e)}
-        if model == "linear":
-            try:
-                k_cg = (sum(line["cg_iters"]) + sum(line["ons_iters"])) / max(len(line["cg_iters"]), 1)
-                threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-                line["cpu_reference_ops"] = cpu_reference_ops(w, args.seed, threads, k_cg)
-            except Exception as e:
-                line["cpu_reference_ops"] = {"error": repr(e)}
-    d.close()
-    if R.rank == 0:
-        print(json.dumps(line), flush=True)
+        traceback.print_exc()
+        wd.stage(f"failed: {e!r}"[:300])
+        if R.rank == 0:
+            time.sleep(1.0)  # let the other ranks record where they are
+            line = wd.partial
+            if line is not None:
+                line = dict(line, error_after_result=repr(e))
+            else:
+                line = failure_line(R.world, sys.argv[1:], f"rank 0: {e!r}", read_stages(wd.dir, R.world, wd.t0))
+            wd.emit(line)
+        sys.stdout.flush()
+        os._exit(0 if (R.rank == 0 and wd.partial is not None) else 1)
     R.close()
 
 

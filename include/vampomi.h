@@ -296,15 +296,20 @@ vampomi_status vampomi_reset_stats(vampomi_ctx* ctx);
  * which: 0 = A.x partial-sum kernel, 1 = A^T.u kernel, 2 = association-test pass
  * (K = 1), 3 = one-pass CG operator (K = 1, 2).  Variants index the
  * tuning tables in vampomi_amd/csrc/kernels.hip and are settings of this
- * context only; the defaults are 0 (A.x), -1 (A^T.u: the per-K choice), 2
- * (association pass) and -1 (operator: whole columns per workgroup while
+ * context only; the defaults are 0 (A.x), -1 (A^T.u: the per-K choice), 16
+ * (association pass: loo_wg_kernel<4,2,8>; variants 8-19 are the kernels whose
+ * workgroups share their markers, and they add the sums in another order than
+ * the wave-per-marker variants 0-7, so results differ at rounding level) and
+ * -1 (operator: whole columns per workgroup while
  * K*N fits the LDS, else teams of workgroups; 0 forces the whole-column
  * kernel, T*10 + c (c < 10) or 1000 + T*100 + c the team kernel with team size T and configuration c,
  * vampomi_amd/csrc/atax_team.hip).  which = 4: the side stream of the
  * prefetched EM/denoiser, 0 off, 1 on (default: on with several ranks).
  * which = 5: the CG head start of the linear model (the Onsager solve's first
  * step in the pass that starts the x2 solve, pcg.cpp), 0 off, 1 on (default
- * on; VAMPOMI_HEADSTART=0 turns it off at vampomi_open). */
+ * on; VAMPOMI_HEADSTART=0 turns it off at vampomi_open).  Several ranks run the
+ * head start only if every rank has it on (agreed at the next collective
+ * call: it changes the job's collective sequence). */
 vampomi_status vampomi_dev_set_variant(vampomi_ctx* ctx, int which, int variant);
 /* average device time (HIP events) of `reps` back-to-back launches, K RHS */
 vampomi_status vampomi_dev_time_pass(vampomi_ctx* ctx, int which, int K, int reps, double* avg_ms);

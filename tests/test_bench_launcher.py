@@ -40,7 +40,9 @@ def test_workload_selection():
     from vampomi_amd.workloads import workload
 
     assert workload("auto", 1)["workload"] == "c2"
-    w = workload("auto", 8)
+    w = workload("auto", 8)  # the n = 1 line's family: c2's shard per GPU (bench.py adds the c3full phase)
+    assert (w["workload"], w["N"], w["Mt"], w.get("scaling")) == ("c2-weak", 10000, 400000, None)
+    w = workload("c3full", 8)
     assert (w["workload"], w["N"], w["Mt"], w.get("scaling")) == ("c3full", 100000, 500000, "strong")
     assert workload("c3full", 2)["Mt"] == 500000
     with pytest.raises(ValueError):
@@ -61,3 +63,131 @@ def test_cpu_reference_ops_leg():
     assert r["kind"] == "reference" and r["cores"] == 2 and r["ax_ms"] > 0 and r["atx_ms"] > 0
     want = 1.0 / ((15 * r["ax_ms"] + 13 * r["atx_ms"]) * 1e-3)
     assert abs(r["value"] - want) <= 1e-9 * want
+
+
+def _lines(p):
+    return [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_hung_rank_ends_in_one_failure_line():
+    """A rank that stops answering (here: after the rendezvous, so rank 0
+    waits in a barrier for it) ends the job at --deadline-s: rank 0's watchdog
+    prints ONE JSON line with "error" and every rank's last stage, and the
+    launcher exits non-zero, instead of the job hanging until the caller's
+    own limit with nothing printed."""
+    import time
+
+    t0 = time.monotonic()
+    p = _run("--gpus", "2", "--steps", "2", "--dry-run", "--dry-run-hang-rank", "1", "--deadline-s", "25")
+    took = time.monotonic() - t0
+    assert p.returncode != 0
+    recs = _lines(p)
+    assert len(recs) == 1, p.stdout
+    rec = recs[0]
+    assert rec["value"] is None and "deadline" in rec["error"] and rec["n_gpus"] == 2
+    assert "hang" in rec["rank_stages"]["1"]["stage"] and rec["rank_stages"]["0"]["stage"] == "dry-run timed"
+    assert took < 25 + 30, took
+
+
+def test_hung_rank_under_torchrun():
+    """The same under the driver's launcher (torchrun, WORLD_SIZE set): rank
+    0's watchdog prints the line and exits; torchrun stops the hung rank."""
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+                        "--gpus", "2", "--steps", "2", "--dry-run", "--dry-run-hang-rank", "1", "--deadline-s", "25"],
+                       capture_output=True, text=True, env=env, timeout=240)
+    assert p.returncode != 0
+    recs = _lines(p)
+    assert len(recs) == 1, p.stdout + p.stderr[-3000:]
+    assert "deadline" in recs[0]["error"] and "hang" in recs[0]["rank_stages"]["1"]["stage"]
+
+
+class _Ranks:
+    def __init__(self, world, rank=0):
+        self.world, self.rank, self.local = world, rank, rank
+
+    def max(self, v):
+        return v
+
+    def sum(self, v):
+        return v * self.world
+
+    def barrier(self):
+        pass
+
+    def bcast(self, obj):
+        return obj
+
+
+class _Wd:
+    partial = None
+    dir = "/nonexistent"
+    t0 = 0.0
+
+    def stage(self, what):
+        self.cur = what
+
+
+def _fake_window(calls):
+    from types import SimpleNamespace as NS
+
+    def fake(args, R, w, wd, steps, warmup, tag, keep=False):
+        calls.append((tag, w["workload"], R.world, steps, warmup))
+        per_pass_ms = 0.6 * w["N"] * w["Mt"] / 5e8 / R.world  # C2: 0.6 ms a pass
+        z = NS(ms_total=0.0, ms_timed=0.0, timed=0, launches=0, bytes_total=0.0)
+        op = NS(ms_total=8.3 * steps * per_pass_ms, ms_timed=10 * per_pass_ms, timed=10, launches=8.3 * steps,
+                bytes_total=8.3 * steps * 8.0 * w["N"] * w["Mt"] / R.world)
+        st = NS(ax=z, atx=z, op=op, coll=z, ax_k=[z] * 4, atx_k=[z] * 4, op_k=[op, z, z, z],
+                a_passes_exec=8.3 * steps)
+        el = steps * (8.3 * per_pass_ms + 0.3) * 1e-3
+        res = {"el": el, "st": st, "summ": {"cg_iters": [7] * (steps + warmup), "ons_iters": [8] * (steps + warmup)},
+               "ref_passes": 37.7, "setup": 0.1, "M": w["Mt"] // R.world, "nranks": R.world, "steps": steps,
+               "warmup": warmup, "model": "linear", "beta": None, "opts": None, "barrier": None,
+               "rank_times": [{"rank": r} for r in range(R.world)]}
+        if keep:
+            res["d"] = NS(kernel_name=lambda which, K, mode: "atax_team_kernel<2, 6, 2, 3, 2, true, 2>",
+                          close=lambda: None, get_phen=lambda: None)
+        return res
+
+    return fake
+
+
+def test_multi_rank_line_assembly(monkeypatch):
+    """The n > 1 line's assembly (no GPU: the VAMP windows are stubbed): the
+    value is c2-weak's, rank 0 measured the 1-GPU bases first, the configs[2]
+    headline phase follows the main one, and the line is one JSON object with
+    the bases it is read against."""
+    sys.path.insert(0, ROOT)
+    import bench
+    from vampomi_amd.workloads import workload
+
+    calls = []
+    monkeypatch.setattr(bench, "vamp_window", _fake_window(calls))
+    args = bench.parse_args(["--gpus", "4", "--steps", "20", "--warmup", "5"])
+    line = bench.run_linear(args, _Ranks(4), _Wd(), workload("auto", 4), 0.0)
+    json.dumps(line)
+    assert [c[0] for c in calls] == ["basis same-problem", "basis c3big", "main", "headline"]
+    assert calls[0][1:4] == ("c2-weak@1gpu", 1, 20) and calls[1][1:3] == ("c3big", 1)
+    assert calls[2][1:3] == ("c2-weak", 4) and calls[3][1:4] == ("c3full", 4, 10)
+    assert line["config"]["workload"] == "c2-weak" and line["scaling"] == "weak" and line["n_gpus"] == 4
+    assert line["value"] == round(4 * 20 / ((8.3 * 0.6 + 0.3) * 20e-3), 4)
+    sp = line["one_gpu"]["same_problem"]
+    assert sp["n_gpus"] == 1 and sp["Mt"] == 200000 and 3.0 < sp["speedup_of_this_run"] < 4.0
+    h = line["headline_c3full"]
+    assert h["workload"] == "c3full" and h["Mt"] == 500000 and h["n_gpus"] == 4
+    eq = h["one_gpu_equivalent"]
+    assert eq["measured_in_this_job"] and 0.5 < eq["strong_scaling_efficiency"] < 1.2
+    assert "n = 1 line" in line["scaling_basis"]
+
+    # explicit c3full: the strong line itself carries the measured equivalent
+    calls.clear()
+    args = bench.parse_args(["--gpus", "2", "--steps", "20", "--warmup", "5", "--config", "c3full"])
+    line = bench.run_linear(args, _Ranks(2), _Wd(), workload("c3full", 2), 0.0)
+    assert [c[0] for c in calls] == ["basis c3big", "main"]
+    assert line["scaling"] == "strong" and line["one_gpu_equivalent"]["measured_in_this_job"]

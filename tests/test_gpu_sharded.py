@@ -293,3 +293,30 @@ def test_team_operator_beside_side_stream_and_writer(monkeypatch, tmp_path, P):
     for it in range(1, its + 1):
         np.testing.assert_array_equal(np.fromfile(tmp_path / "b1" / f"t_it_{it}.bin", dtype="<f8"), x1[it - 1])
         np.testing.assert_array_equal(np.fromfile(tmp_path / "b1" / f"t_r1_it_{it}.bin", dtype="<f8"), r1[it - 1])
+
+
+def test_headstart_agreed_over_ranks(monkeypatch):
+    """The head start changes the collective sequence (its launch's all-reduce
+    replaces ax_dev's), and each rank reads its own switch (VAMPOMI_HEADSTART,
+    set_variant(5)).  With the switch off on ONE rank the job must neither hang
+    nor mismatch: op_prepare agrees the choice over the ranks, so both ranks
+    run without it and equal the one-rank run with it off (bitwise: the same
+    schedule, the same rank-ordered sums)."""
+    N, Mt, its = 1001, 2003, 8
+    X, y, beta = make_problem(N, Mt)
+    kw = dict(max_iter=its, stop_criteria_thr=0.0)
+    with va.Data(N, Mt) as d:
+        d.set_variant(5, 0)
+        off = _vamp(d, X, y, beta, **kw)
+
+    def fn(r, d):
+        if r == 1:
+            d.set_variant(5, 0)
+        return _vamp(d, X, y, beta, **kw)
+
+    parts = run_ranks(monkeypatch, 2, N, Mt, fn)
+    for p in parts:
+        assert p["cg_iters"] == off["cg_iters"] and p["ons_iters"] == off["ons_iters"]
+        assert np.allclose(p["params"], off["params"], rtol=1e-11)
+    for k in range(its):
+        assert relerr(_cat(parts, "x1_hist")[k], off["x1_hist"][k]) < 1e-12, k

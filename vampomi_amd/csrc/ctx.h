@@ -298,10 +298,13 @@ vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double
                        double tol, double* nscratch, int64_t* ref_passes, DotBatch* init,
                        const double* extra_x = nullptr, double* ex_out = nullptr, bool onepass = false,
                        const double* const* ar0 = nullptr, HeadStart* hs = nullptr);
-// plans the one-pass operator (c->opp, c->op_ok) and allocates its buffers
-// (idempotent until the variant changes)
-vampomi_status op_prepare(vampomi_ctx* c);
-// whether pcg_run's head start can run on this context (plans the operator)
+// plans the one-pass operator (c->opp, c->op_ok, c->hs_ok) and allocates its
+// buffers (idempotent until the plan or the head-start switch changes).
+// COLLECTIVE when collective (several ranks): the ranks agree on op_ok and
+// hs_ok (both change the collective sequence); false only for one-rank hooks
+vampomi_status op_prepare(vampomi_ctx* c, bool collective = true);
+// whether pcg_run's head start can run on this context (plans the operator;
+// the same answer on every rank).  COLLECTIVE
 vampomi_status headstart_available(vampomi_ctx* c, bool* yes);
 // the device word a team launch sets when a hand-off timed out, and its host view
 unsigned* op_err_dev(vampomi_ctx* c);

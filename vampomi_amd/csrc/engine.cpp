@@ -216,6 +216,48 @@ static vampomi_status job_failed(vampomi_ctx* c, const char* why) {
     return fail(c->use_comm ? VAMPOMI_ERR_RCCL : VAMPOMI_ERR_HIP, msg);
 }
 
+// The communicator is NON-BLOCKING (ncclConfig_t.blocking = 0, vampomi_open):
+// any RCCL call may return ncclInProgress, and the next call on the
+// communicator must wait until ncclCommGetAsyncError leaves that state.  Every
+// call goes through here: it returns at once on ncclSuccess (the steady
+// state), otherwise polls the communicator until it settles, at most
+// limit_s seconds, and aborts it after that (a peer that never joins the
+// bootstrap, a transport that never connects) instead of blocking forever.
+static vampomi_status nccl_settle(vampomi_ctx* c, ncclResult_t r, const char* what, double limit_s) {
+    if (r == ncclSuccess) return VAMPOMI_OK;
+    if (r != ncclInProgress || !c->comm)
+        return fail(VAMPOMI_ERR_RCCL, std::string(what) + ": " + ncclGetErrorString(r));
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint64_t spin = 1;; ++spin) {
+        ncclResult_t s = ncclSuccess;
+        const ncclResult_t q = ncclCommGetAsyncError(c->comm, &s);
+        if (q != ncclSuccess) return fail(VAMPOMI_ERR_RCCL, std::string(what) + ": " + ncclGetErrorString(q));
+        if (s == ncclSuccess) return VAMPOMI_OK;
+        if (s != ncclInProgress) {
+            const std::string msg = std::string(what) + ": " + ncclGetErrorString(s) + " (rank " + std::to_string(c->rank) + ")";
+            comm_abort(c, msg);
+            return fail(VAMPOMI_ERR_RCCL, msg);
+        }
+        if ((spin & 1023) == 0 &&
+            std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit_s) {
+            const std::string msg = std::string(what) + ": not finished within " + std::to_string((int)limit_s) +
+                                    " s (a peer rank never joined?) (rank " + std::to_string(c->rank) + ")";
+            comm_abort(c, msg);
+            return fail(VAMPOMI_ERR_RCCL, msg);
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(spin < 4096 ? 1 : 200));
+    }
+}
+
+// seconds the communicator's creation may take (VAMPOMI_COMM_INIT_TIMEOUT_S,
+// default 120): the bootstrap waits for every rank, so a rank that died or
+// never started shows up here
+static double comm_init_timeout_s() {
+    const char* e = std::getenv("VAMPOMI_COMM_INIT_TIMEOUT_S");
+    const double v = e ? std::atof(e) : 0.0;
+    return v > 0 ? v : 120.0;
+}
+
 vampomi_status wait_flag(vampomi_ctx* c, unsigned long long seq, int word) {
     const auto t0 = std::chrono::steady_clock::now();
     hipStream_t st = word == 1 ? c->st2 : c->st;  // word 1: the side stream's sequence
@@ -379,7 +421,8 @@ static vampomi_status rccl_check(vampomi_ctx* c, size_t n, const char* site, int
     const double v[3] = {(double)c->coll_seq, (double)n, (double)line};
     double h[6] = {v[0], v[1], v[2], -v[0], -v[1], -v[2]};
     HIPCHK(hipMemcpyAsync(d, h, sizeof h, hipMemcpyHostToDevice, c->st));
-    NCCLCHK(ncclAllReduce(d, d, 6, ncclDouble, ncclMax, c->comm, c->st));
+    STCHK(nccl_settle(c, ncclAllReduce(d, d, 6, ncclDouble, ncclMax, c->comm, c->st), "ncclAllReduce (check)",
+                      coll_timeout_s()));
     HIPCHK(hipMemcpyAsync(h, d, sizeof h, hipMemcpyDeviceToHost, c->st));
     STCHK(sync_stream(c, c->st));
     for (int q = 0; q < 3; ++q)
@@ -397,7 +440,8 @@ vampomi_status allreduce_dev(vampomi_ctx* c, double* buf, size_t n, const char* 
     if (check) STCHK(rccl_check(c, n, site, line));
     const TimedLaunch t = launch_stat(c, 4, 1, 8.0 * (double)n, 0.0);
     if (t.a) HIPCHK(hipEventRecord(t.a, c->st));
-    NCCLCHK(ncclAllReduce(buf, buf, n, ncclDouble, ncclSum, c->comm, c->st));
+    STCHK(nccl_settle(c, ncclAllReduce(buf, buf, n, ncclDouble, ncclSum, c->comm, c->st), "ncclAllReduce",
+                      coll_timeout_s()));
     if (t.b) HIPCHK(hipEventRecord(t.b, c->st));
     return VAMPOMI_OK;
 }
@@ -681,21 +725,24 @@ static size_t op_xg_words_for(int64_t Mx, const vk::OpPlan& p) {
     return (size_t)(Mx + p.grid) * vk::kOpMaxK * (size_t)p.T * 2 + (size_t)p.grid * (2 * vk::kOpMaxK + 1);
 }
 
-vampomi_status op_prepare(vampomi_ctx* c) {
+vampomi_status op_prepare(vampomi_ctx* c, bool collective) {
     if (c->op_ready) return VAMPOMI_OK;
     if (c->cus <= 0) HIPCHK(hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, c->device));
     const int64_t M = std::max<int64_t>(c->M, 1);
     c->op_ok = vk::op_plan(c->N, M, c->cus, c->op_variant, &c->opp);
     if (c->op_ok && c->opp.T >= 1) {
         // a team launch waits for members that must all be resident at once:
-        // the device must hold the whole grid (one workgroup per CU) for every K
-        for (int K = 1; K <= vk::kOpMaxK; ++K) {
+        // the device must hold the whole grid (one workgroup per CU) for every
+        // K; a device that cannot (or an occupancy query that failed) runs the
+        // CG on the two-pass schedule instead
+        for (int K = 1; K <= vk::kOpMaxK && c->op_ok; ++K) {
             const int occ = vk::team_occupancy(c->opp, K);
-            if ((int64_t)occ * c->cus < c->opp.grid)
-                return fail(VAMPOMI_ERR_HIP, "one-pass operator: " + vk::team_kernel_name(K, c->opp) + " fits " +
-                                                 std::to_string(occ) + " workgroup(s) per CU; the plan needs " +
-                                                 std::to_string(c->opp.grid) + " resident on " +
-                                                 std::to_string(c->cus) + " CUs");
+            if ((int64_t)occ * c->cus < c->opp.grid) {
+                std::fprintf(stderr, "libvampomi: one-pass operator off: %s fits %d workgroup(s) per CU; the plan "
+                                     "needs %lld resident on %d CUs (two passes per CG step)\n",
+                             vk::team_kernel_name(K, c->opp).c_str(), occ, (long long)c->opp.grid, c->cus);
+                c->op_ok = false;
+            }
         }
     }
     // the head-start plan: optional (no plan, or a grid the device cannot
@@ -703,6 +750,21 @@ vampomi_status op_prepare(vampomi_ctx* c) {
     c->hs_ok = c->op_ok && vk::team_plain_plan(c->N, M, c->cus, c->opp, &c->opp_hs);
     if (c->hs_ok && (int64_t)vk::team_occupancy(c->opp_hs, 1 + vk::kOpPlain) * c->cus < c->opp_hs.grid)
         c->hs_ok = false;
+    // Both choices change the job's collective sequence (one-pass vs two-pass
+    // CG steps; the head-start launch's all-reduce vs ax_dev's), and each rank
+    // made them from its own shard size, CU count and VAMPOMI_HEADSTART /
+    // set_variant(5).  A job runs a choice only if every rank made it: one
+    // all-reduce of the three refusals, each in its own base-2^10 digit.
+    if (collective && c->use_comm) {
+        const double mine = (c->op_ok ? 0.0 : 1.0) + (c->hs_ok ? 0.0 : 1024.0) + (c->hs_on ? 0.0 : 1048576.0);
+        double all = 0.0;
+        STCHK(sum_over_ranks(c, mine, &all));
+        const int64_t a = (int64_t)all;
+        if (a % 1024 != 0) c->op_ok = false;
+        if ((a / 1024) % 1024 != 0 || a / 1048576 != 0 || !c->op_ok) c->hs_ok = false;
+    } else if (!c->hs_on) {
+        c->hs_ok = false;
+    }
     if (!c->op_ts && std::getenv("VAMPOMI_OP_TS") && std::atoi(std::getenv("VAMPOMI_OP_TS"))) {
         HIPCHK(hipMalloc((void**)&c->op_ts, (size_t)4 * 8 * std::max(c->cus, 1) * 2));
         HIPCHK(hipMemsetAsync(c->op_ts, 0, (size_t)4 * 8 * std::max(c->cus, 1) * 2, c->st));
@@ -747,8 +809,8 @@ vampomi_status op_prepare(vampomi_ctx* c) {
 
 vampomi_status headstart_available(vampomi_ctx* c, bool* yes) {
     *yes = false;
-    if (!c->have_X || !c->hs_on) return VAMPOMI_OK;
-    STCHK(op_prepare(c));
+    if (!c->have_X) return VAMPOMI_OK;
+    STCHK(op_prepare(c));  // hs_ok: agreed over the ranks, VAMPOMI_HEADSTART / set_variant(5) included
     *yes = c->op_ok && c->hs_ok;
     return VAMPOMI_OK;
 }
@@ -1002,7 +1064,14 @@ void release_ctx_resources(vampomi_ctx* c) {
     c->h_cgm = nullptr;
     if (c->cgs) (void)hipFree(c->cgs);
     c->cgs = nullptr;
-    if (c->comm) (void)ncclCommDestroy(c->comm);
+    if (c->comm) {
+        // a non-blocking communicator: finalize (flushes its pending work,
+        // may return ncclInProgress), then destroy; abort if it never settles
+        if (nccl_settle(c, ncclCommFinalize(c->comm), "ncclCommFinalize", 30.0) == VAMPOMI_OK && c->comm)
+            (void)ncclCommDestroy(c->comm);
+        else if (c->comm)
+            (void)ncclCommAbort(c->comm);
+    }
     c->comm = nullptr;
     for (hipEvent_t* e : {&c->ev_fork, &c->ev_join})
         if (*e) (void)hipEventDestroy(*e), *e = nullptr;
@@ -1094,7 +1163,13 @@ extern "C" vampomi_status vampomi_open(const vampomi_shard_desc* d, vampomi_ctx*
             std::memcpy(&id, d->comm_id, sizeof id);
         else
             NCCLCHK(ncclGetUniqueId(&id));
-        NCCLCHK(ncclCommInitRank(&c->comm, c->nranks, id, c->rank));
+        // non-blocking creation, bounded: the bootstrap waits for every rank,
+        // so a rank that never arrives fails this one after
+        // VAMPOMI_COMM_INIT_TIMEOUT_S instead of hanging the job
+        ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+        cfg.blocking = 0;
+        STCHK(nccl_settle(c.get(), ncclCommInitRankConfig(&c->comm, c->nranks, id, c->rank, &cfg),
+                          "ncclCommInitRankConfig", comm_init_timeout_s()));
     }
     STCHK(sync_stream(c.get(), c->st));
     *out = c.release();
@@ -1648,6 +1723,7 @@ extern "C" vampomi_status vampomi_dev_set_variant(vampomi_ctx* c, int which, int
     } else if (which == 5) {  // the CG head start (pcg.cpp): 0 off, 1 on
         if (variant != 0 && variant != 1) return fail(VAMPOMI_ERR_ARG, "head start: 0 or 1");
         c->hs_on = variant == 1;
+        c->op_ready = false;  // re-planned (and re-agreed over the ranks) at the next collective use
     } else {
         if (!vk::loo_variant_ok(variant)) return fail(VAMPOMI_ERR_ARG, "no such association-pass variant");
         c->loo_variant = variant;
@@ -1661,7 +1737,7 @@ extern "C" vampomi_status vampomi_dev_time_pass(vampomi_ctx* c, int which, int K
     if (!c->have_X) return fail(VAMPOMI_ERR_STATE, "no methylation data loaded");
     HIPCHK(hipSetDevice(c->device));
     if (which == 3) {
-        STCHK(op_prepare(c));
+        STCHK(op_prepare(c, false));  // a one-rank timing hook: no agreement
         if (!c->op_ok) return fail(VAMPOMI_ERR_ARG, "no one-pass operator plan for this N");
     }
     const int64_t Mx = std::max<int64_t>(c->M, 1);
@@ -1730,7 +1806,7 @@ extern "C" vampomi_status vampomi_dev_op_apply(vampomi_ctx* c, int K, const doub
         return fail(VAMPOMI_ERR_ARG, "bad argument");
     if (c->use_comm) return fail(VAMPOMI_ERR_ARG, "vampomi_dev_op_apply: one rank only");
     HIPCHK(hipSetDevice(c->device));
-    STCHK(op_prepare(c));
+    STCHK(op_prepare(c, false));
     if (!c->op_ok) return fail(VAMPOMI_ERR_ARG, "no one-pass operator plan for this N");
     const int64_t Mx = std::max<int64_t>(c->M, 1);
     double* AR = c->op_nvec;

@@ -191,6 +191,9 @@ bool rdzv_fetch(const std::string& path, const std::string& nonce, double not_be
     const auto t0 = std::chrono::steady_clock::now();
     std::vector<unsigned char> first((size_t)nbytes), again((size_t)nbytes);
     for (;;) {
+        // checked on every path round the loop: a file rewritten or flapping
+        // within the recheck below must not keep this rank here past the limit
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(timeout_ms)) return false;
         if (rdzv_try(path, nonce, not_before, first.data(), nbytes)) {
             if (!nonce.empty()) {
                 std::memcpy(id, first.data(), (size_t)nbytes);
@@ -208,7 +211,6 @@ bool rdzv_fetch(const std::string& path, const std::string& nonce, double not_be
             }
             continue;
         }
-        if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(timeout_ms)) return false;
         std::this_thread::sleep_for(std::chrono::milliseconds(50));
     }
 }

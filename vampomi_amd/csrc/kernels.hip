@@ -2216,10 +2216,14 @@ __global__ void signal_kernel(unsigned long long* flag, unsigned long long seq) 
 }
 
 // a sequence number into mapped host memory after everything earlier on the
-// stream (relaxed: the writes it announces were made by earlier kernels,
-// complete at their end); the iteration writer's "slot landed" word
+// stream; the iteration writer's "slot landed" word.  The staging data it
+// announces was written by an earlier kernel with plain stores, so the store
+// is a system-scope RELEASE: it writes back the L2 (the whole device's, not
+// only this kernel's writes) before the word can be seen by the host, which
+// does not rely on the packet fence scope or on the staging memory's mapping
+// type.  One thread, once per iteration: the writeback costs nothing
 __global__ void post_flag_kernel(unsigned long long* flag, unsigned long long seq) {
-    __hip_atomic_store(flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 hipError_t post_flag(unsigned long long* flag, unsigned long long seq, hipStream_t st) {

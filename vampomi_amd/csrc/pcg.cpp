@@ -121,7 +121,7 @@ vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double
     if (onepass && K <= vk::kOpMaxK && c->have_X) STCHK(op_prepare(c));
     // the head start (ctx.h, HeadStart): system 0's first step rides in the pass
     // that starts the solve; it is then one step ahead (CgState.off)
-    const bool head = hs && hs->abern && c->hs_on && c->hs_ok && c->op_ok && max_iter > 0;
+    const bool head = hs && hs->abern && c->hs_ok && c->op_ok && max_iter > 0;  // hs_ok: agreed, hs_on included
     vk::CgState s0{};
     s0.K = K;
     s0.gam2 = gam2;
