@@ -57,6 +57,7 @@ import subprocess
 import sys
 import threading
 import time
+import traceback
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -718,6 +719,7 @@ def one_gpu_bases(args, R: Ranks, wd: Watchdog, w: dict, headline: bool) -> dict
                                 "basis same-problem")
                 out["same_problem"] = summary_of(r, w, True, 1)
             except Exception as e:
+                traceback.print_exc()
                 out["same_problem"] = {"error": repr(e)}
         if headline:
             from vampomi_amd.workloads import workload
@@ -729,6 +731,7 @@ def one_gpu_bases(args, R: Ranks, wd: Watchdog, w: dict, headline: bool) -> dict
                 rec["ms_per_pass_per_marker"] = per_pass_marker_ms(rec)
                 out["c3big"] = rec
             except Exception as e:
+                traceback.print_exc()
                 out["c3big"] = {"error": repr(e)}
     wd.stage("basis: barrier")
     R.barrier()
@@ -1003,8 +1006,6 @@ def main():
     except SystemExit:
         raise
     except BaseException as e:  # one diagnosable line instead of a bare traceback
-        import traceback
-
         traceback.print_exc()
         wd.stage(f"failed: {e!r}"[:300])
         if R.rank == 0:
@@ -1015,6 +1016,8 @@ def main():
             else:
                 line = failure_line(R.world, sys.argv[1:], f"rank 0: {e!r}", read_stages(wd.dir, R.world, wd.t0))
             wd.emit(line)
+        else:
+            time.sleep(5.0)  # rank 0 prints the line (with every rank's stage) before this rank's exit ends the job
         sys.stdout.flush()
         os._exit(0 if (R.rank == 0 and wd.partial is not None) else 1)
     R.close()

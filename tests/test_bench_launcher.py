@@ -110,7 +110,10 @@ def test_hung_rank_under_torchrun():
 
 class _Ranks:
     def __init__(self, world, rank=0):
+        from types import SimpleNamespace as NS
+
         self.world, self.rank, self.local = world, rank, rank
+        self.dist = NS(all_gather_object=lambda out, mine: out.__setitem__(slice(None), [mine] * len(out)))
 
     def max(self, v):
         return v
@@ -191,3 +194,86 @@ def test_multi_rank_line_assembly(monkeypatch):
     line = bench.run_linear(args, _Ranks(2), _Wd(), workload("c3full", 2), 0.0)
     assert [c[0] for c in calls] == ["basis c3big", "main"]
     assert line["scaling"] == "strong" and line["one_gpu_equivalent"]["measured_in_this_job"]
+
+
+def test_vamp_window_and_bases_with_a_stub_library(monkeypatch):
+    """bench.py's real vamp_window / one_gpu_bases code over a stub of the
+    library's Python mirror (no GPU): every leg of the n > 1 flow runs without
+    a Python error, so the driver's first multi-GPU run cannot die on one."""
+    from types import SimpleNamespace as NS
+
+    sys.path.insert(0, ROOT)
+    import bench
+    import vampomi_amd as va
+    from vampomi_amd.workloads import workload
+
+    z = NS(ms_total=0.0, ms_timed=0.0, timed=0, launches=0, bytes_total=0.0)
+
+    class Data:
+        def __init__(self, N, Mt, rank=0, nranks=1, comm_id=None, device=-1):
+            assert nranks == 1 or comm_id is not None
+            self.N, self.Mt, self.M, self.nranks = N, Mt, Mt // nranks, nranks
+
+        def generate(self, seed, kind):
+            pass
+
+        def simulate_phen(self, seed, lam, h2):
+            return [0.0] * self.M
+
+        simulate_phen_binary = simulate_phen
+
+        def set_variant(self, w, v):
+            pass
+
+        def reset_stats(self):
+            pass
+
+        def set_timing(self, on, period=1):
+            pass
+
+        def sync(self):
+            pass
+
+        def stats(self):
+            op = NS(ms_total=5.0, ms_timed=0.6, timed=1, launches=8, bytes_total=8 * 8.0 * self.N * self.M)
+            return NS(ax=z, atx=z, op=op, coll=z, ax_k=[z] * 4, atx_k=[z] * 4, op_k=[op, z, z, z], a_passes_exec=8)
+
+        def kernel_name(self, which, K, mode):
+            return "k"
+
+        def get_phen(self):
+            return None
+
+        def close(self):
+            pass
+
+    class Vamp:
+        def __init__(self, d, opts, true_signal=None):
+            self.n = 0
+
+        def begin(self):
+            pass
+
+        def step(self):
+            self.n += 1
+
+        @property
+        def a_passes(self):
+            return 37.7 * self.n, 8.3 * self.n
+
+        def summary(self):
+            return {"cg_iters": [7] * self.n, "ons_iters": [8] * self.n}
+
+        def end(self):
+            pass
+
+    monkeypatch.setattr(va, "Data", Data)
+    monkeypatch.setattr(va, "Vamp", Vamp)
+    monkeypatch.setattr(va, "comm_unique_id", lambda: b"x" * va.UNIQUE_ID_BYTES)
+    args = bench.parse_args(["--gpus", "2", "--steps", "3", "--warmup", "1"])
+    out = bench.one_gpu_bases(args, _Ranks(2), _Wd(), workload("auto", 2), True)
+    assert set(out) == {"same_problem", "c3big"}, out
+    assert "error" not in out["same_problem"] and "error" not in out["c3big"], out
+    line = bench.run_linear(args, _Ranks(2), _Wd(), workload("auto", 2), 0.0)
+    json.dumps(line)
+    assert "error" not in line["headline_c3full"], line["headline_c3full"]
