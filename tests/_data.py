@@ -91,3 +91,28 @@ def oracle_with_spread(X, y, beta, Mt, ranks=(2, 3, 4), **kw):
                 e = np.where(np.isnan(a) & np.isnan(b), 0.0, np.abs(a - b) / np.maximum(np.abs(b), 1e-300))
             sp[key] = np.maximum(sp.get(key, np.zeros_like(e)), e)
     return ref, sp
+
+
+# The probit parity bar's multiple of the oracle's own rank-count spread
+# (DESIGN.md §3): the GPU must stay within PROBIT_K x the amount by which the
+# reference's own result moves when its all-reduce order changes.  Set to
+# about twice the largest gap / spread ratio measured over every probit GPU
+# test (record_probit_ratio; VAMPOMI_PROBIT_RATIOS=<file> appends them).
+PROBIT_K = 6.0
+
+
+def record_probit_ratio(test: str, key: str, gap, spread, floor: float = 1e-10):
+    """gap / spread per iteration where the bar is the spread's (k * spread >
+    floor), appended as one JSON line to $VAMPOMI_PROBIT_RATIOS; returns the
+    largest ratio (0 where the floor sets the bar everywhere)."""
+    import json
+    import os
+
+    gap, spread = np.atleast_1d(np.asarray(gap, dtype=float)), np.atleast_1d(np.asarray(spread, dtype=float))
+    m = (spread > 0) & (PROBIT_K * spread > floor)
+    r = float(np.max(gap[m] / spread[m])) if np.any(m) else 0.0
+    f = os.environ.get("VAMPOMI_PROBIT_RATIOS")
+    if f:
+        with open(f, "a") as fh:
+            fh.write(json.dumps({"test": test, "key": key, "max_ratio": r, "n": int(np.sum(m))}) + "\n")
+    return r

@@ -226,8 +226,8 @@ def _onepass_passes(cg, ons, headstart=True):
 
 @pytest.mark.parametrize("N,Mt,its,kind,opv", [(1000, 2000, 30, 0, None), (4099, 3001, 12, 1, None),
                                                 (301, 517, 12, 0, None), (10000, 2500, 10, 0, None),
-                                                (3000, 2000, 10, 1, 1000 + 2 * 100 + 7),
-                                                (3000, 2000, 10, 0, 1000 + 4 * 100 + 9),
+                                                (3000, 2000, 10, 1, 1000 + 2 * 100 + 2),
+                                                (3000, 2000, 10, 0, 1000 + 4 * 100 + 4),
                                                 (1000, 2000, 6, 0, 1000 + 1 * 100 + 0)])
 def test_headstart(N, Mt, its, kind, opv):
     """The head start (pcg.cpp): the Onsager solve takes its first CG step in
@@ -250,22 +250,6 @@ def test_headstart(N, Mt, its, kind, opv):
     assert a["a_passes_exec"] == 1 + _onepass_passes(a["cg_iters"], a["ons_iters"], True)
     assert b["a_passes_exec"] == 1 + _onepass_passes(b["cg_iters"], b["ons_iters"], False)
     assert a["a_passes_ref"] == b["a_passes_ref"]
-    ref = O.vamp_infere(X, y, Mt, true_signal=beta, max_iter=its, stop_criteria_thr=0.0)
-    _assert_parity(a, ref)
-
-
-@pytest.mark.parametrize("N,Mt,its,opv", [(10000, 2500, 10, 1417), (3000, 2000, 10, 1218), (50001, 700, 6, 2617)])
-def test_dynamic_chunks_vamp(N, Mt, its, opv):
-    """A VAMP run on a dynamic-chunk operator plan (the teams claim columns at
-    run time, atax_team.hip): the same CG, Onsager and mixture counts as the
-    static plan of the same team size, values within rounding, and within the
-    parity bar of the oracle."""
-    X, y, beta = _problem(N, Mt)
-    a = _gpu_vamp(X, y, beta, Mt, max_iter=its, stop_criteria_thr=0.0, op_variant=opv)
-    b = _gpu_vamp(X, y, beta, Mt, max_iter=its, stop_criteria_thr=0.0, op_variant=opv - 10)
-    assert a["cg_iters"] == b["cg_iters"] and a["ons_iters"] == b["ons_iters"] and a["L"] == b["L"]
-    for k in range(its):
-        assert relerr(a["x1_hist"][k], b["x1_hist"][k]) <= 1e-11, f"x1 it {k + 1}"
     ref = O.vamp_infere(X, y, Mt, true_signal=beta, max_iter=its, stop_criteria_thr=0.0)
     _assert_parity(a, ref)
 

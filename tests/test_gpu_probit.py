@@ -6,8 +6,10 @@ iteration 1 tau1 = gam1 = 1e-6, the x2 solve is almost gam2*I, alpha2 =
 1 - O(1e-8), and 1 - alpha2 (:338, :345, :354) amplifies any difference in
 summation order by ~1e8.  The reference's own result moves by up to ~3e-7
 (relative) when it runs on 2, 3 or 4 MPI ranks instead of 1.  The bar is
-therefore, per iteration, max(1e-10, 10 x that rank-count spread of the
-oracle) for x1_hat / r1 and the scalar parameters, plus: iteration, CG,
+therefore, per iteration, max(1e-10, PROBIT_K x that rank-count spread of the
+oracle) for x1_hat / r1 and the scalar parameters (PROBIT_K, tests/_data.py:
+about twice the largest gap / spread ratio measured over these tests, which
+record it), plus: iteration, CG,
 Onsager and mixture-size counts identical, confusion counts identical, and
 the headerless CSV files laid out byte for byte like the oracle's."""
 import os
@@ -17,7 +19,7 @@ import numpy as np
 import pytest
 
 from conftest import relerr
-from _data import make_problem, oracle_with_spread
+from _data import PROBIT_K, make_problem, oracle_with_spread, record_probit_ratio
 
 pytestmark = pytest.mark.gpu
 
@@ -46,19 +48,28 @@ def _gpu_probit(X, y, beta, Mt, **kw):
     return s
 
 
-def _assert_probit_parity(s, ref, spread, k=10.0):
+def _assert_probit_parity(s, ref, spread, k=PROBIT_K, test=None):
+    test = test or os.environ.get("PYTEST_CURRENT_TEST", "?").split(" ")[0]
     assert s["iterations"] == ref["iterations"]
     assert s["cg_iters"] == ref["cg_iters"].tolist()
     assert s["ons_iters"] == ref["ons_iters"].tolist()
     assert s["L"] == ref["L"].tolist()
-    for i in range(s["iterations"]):
-        for key in ("x1", "r1"):
-            e = relerr(s[f"{key}_hist"][i], ref[f"{key}_hist"][i])
-            assert e <= max(1e-10, k * spread[key][i]), f"{key} it {i + 1}: {e:.2e} vs spread {spread[key][i]:.2e}"
-    last = s["iterations"] - 1
-    assert relerr(s["x1_final"], ref["x1_final"]) <= max(1e-10, k * spread["x1"][last])
+    its = s["iterations"]
+    gaps = {key: np.array([relerr(s[f"{key}_hist"][i], ref[f"{key}_hist"][i]) for i in range(its)])
+            for key in ("x1", "r1")}
     p, pr = np.array(s["params"]), ref["params"]
-    assert np.all(np.abs(p - pr) <= np.maximum(1e-9, k * spread["params"]) * np.abs(pr)), "params"
+    pgap = np.abs(p - pr) / np.maximum(np.abs(pr), 1e-300)
+    # the measured gap / spread ratios, recorded before any assertion
+    for key in ("x1", "r1"):
+        record_probit_ratio(test, key, gaps[key], spread[key][:its])
+    record_probit_ratio(test, "params", pgap, spread["params"], floor=1e-9)
+    for i in range(its):
+        for key in ("x1", "r1"):
+            e = gaps[key][i]
+            assert e <= max(1e-10, k * spread[key][i]), f"{key} it {i + 1}: {e:.2e} vs spread {spread[key][i]:.2e}"
+    last = its - 1
+    assert relerr(s["x1_final"], ref["x1_final"]) <= max(1e-10, k * spread["x1"][last])
+    assert np.all(pgap <= np.maximum(1e-9, k * spread["params"])), "params"
     m, mr = np.array(s["metrics"]), ref["metrics"]
     for o in (0, 6):
         assert np.array_equal(m[:, o:o + 4], mr[:, o:o + 4]), "confusion counts"
@@ -69,11 +80,15 @@ def _assert_probit_parity(s, ref, spread, k=10.0):
     pg, po = np.array(s["prior"]), ref["prior"]
     assert np.array_equal(pg[:, 0], po[:, 0])
     # the mixture (EM ratios of sums over markers) has its own sensitivity to
-    # the summation order: the bar is 10x the larger of the params' and the
+    # the summation order: the bar is k x the larger of the params' and the
     # prior rows' own rank-count spreads (at N = 12,000 the prior's is ~2e-9
     # where the params' is ~1e-10)
     own = np.max(spread["prior"], axis=1, keepdims=True) if "prior" in spread else 0.0
-    tol = np.maximum(1e-9, k * np.maximum(np.max(spread["params"], axis=1, keepdims=True), own))
+    sp = np.maximum(np.max(spread["params"], axis=1, keepdims=True), own)
+    with np.errstate(invalid="ignore", divide="ignore"):
+        prgap = np.abs(pg - po) / np.maximum(np.abs(po), 1e-300)
+    record_probit_ratio(test, "prior", np.max(prgap, axis=1), sp[:, 0], floor=1e-9)
+    tol = np.maximum(1e-9, k * sp)
     assert np.all(np.abs(pg - po) <= tol * np.abs(po) + 1e-300), "prior rows"
 
 
@@ -169,8 +184,8 @@ def test_cli_bin_class_files(tmp_path):
     for it in range(1, its + 1):
         a = np.fromfile(out_g / ("ex_it_%d.bin" % it), dtype="<f8")
         b = np.fromfile(out_o / ("ex_it_%d.bin" % it), dtype="<f8")
-        assert relerr(a, b) <= max(1e-10, 10 * spread["x1"][it - 1])
-    assert relerr(x_lib, ref["x1_final"]) <= max(1e-10, 10 * spread["x1"][its - 1])
+        assert relerr(a, b) <= max(1e-10, PROBIT_K * spread["x1"][it - 1])
+    assert relerr(x_lib, ref["x1_final"]) <= max(1e-10, PROBIT_K * spread["x1"][its - 1])
 
 
 def test_c4_shape_properties():
@@ -210,7 +225,7 @@ def test_c4_samples_production_schedule_vs_oracle():
     """configs[3]'s sample count, N = 50,000, on the production schedule
     (batch_rhs 4: the team operator with T = 16 and the merged first launch of
     every iteration) against the oracle at a reduced Mt, with the probit bar
-    (max(1e-10, 10 x the oracle's own rank-count spread)) and every integer
+    (max(1e-10, PROBIT_K x the oracle's own rank-count spread)) and every integer
     exact.  src/vamp_probit.cpp:19-467."""
     N, Mt, its = 50000, 1800, 8
     assert _team_plan(N) == 16
@@ -236,7 +251,7 @@ def test_c4_full_shard_production_vs_sequential(monkeypatch):
     production schedule against batch_rhs 1 (bitwise the reference's
     sequential order, test_probit_batched_bitwise_equal_to_sequential): counts
     exact, x1_hat / r1 / params within the probit bar, measured here on the
-    device itself as 10 x the change of the sequential run when the same
+    device itself as PROBIT_K x the change of the sequential run when the same
     problem runs on 2 or 3 ranks (loopback), i.e. the reference's own
     sensitivity to the all-reduce order."""
     from test_gpu_sharded import run_ranks
@@ -266,12 +281,18 @@ def test_c4_full_shard_production_vs_sequential(monkeypatch):
         spread["params"] = np.maximum(spread["params"], np.abs(a - b) / np.maximum(np.abs(b), 1e-300))
     for key in ("iterations", "cg_iters", "ons_iters", "L"):
         assert prod[key] == seq[key], key
+    gaps = {key: np.array([relerr(prod[f"{key}_hist"][k], seq[f"{key}_hist"][k]) for k in range(its)])
+            for key in ("x1", "r1")}
+    p, ps = np.array(prod["params"]), np.array(seq["params"])
+    pgap = np.abs(p - ps) / np.maximum(np.abs(ps), 1e-300)
+    for key in ("x1", "r1"):
+        record_probit_ratio("test_c4_full_shard_production_vs_sequential", key, gaps[key], spread[key])
+    record_probit_ratio("test_c4_full_shard_production_vs_sequential", "params", pgap, spread["params"], floor=1e-9)
     for k in range(its):
         for key in ("x1", "r1"):
-            e = relerr(prod[f"{key}_hist"][k], seq[f"{key}_hist"][k])
-            assert e <= max(1e-10, 10 * spread[key][k]), f"{key} it {k + 1}: {e:.2e} vs spread {spread[key][k]:.2e}"
-    p, ps = np.array(prod["params"]), np.array(seq["params"])
-    assert np.all(np.abs(p - ps) <= np.maximum(1e-9, 10 * spread["params"]) * np.abs(ps))
+            e = gaps[key][k]
+            assert e <= max(1e-10, PROBIT_K * spread[key][k]), f"{key} it {k + 1}: {e:.2e} vs spread {spread[key][k]:.2e}"
+    assert np.all(pgap <= np.maximum(1e-9, PROBIT_K * spread["params"]))
     m, ms = np.array(prod["metrics"]), np.array(seq["metrics"])
     for o in (0, 6):
         assert np.all(m[:, o:o + 4].sum(axis=1) == c["N"])

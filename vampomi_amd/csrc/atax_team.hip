@@ -67,66 +67,33 @@ static constexpr unsigned kTmMaxSpins = 1u << 21;  // ~2 s of polling, then the 
 
 // configurations: F columns prefetched, L steps of lag, P polls in flight,
 // hand-off (T > 1), the most loads per lane per column that fit 256 VGPRs at
-// K = 2 without spilling (gfx950, ROCm 7.2 compiler), and E doubles per lane
-// per load (2: 16-byte loads, rows in steps of 128 per wave; 1: 8-byte
-// loads, steps of 64, for tiles that 16-byte steps would pad by up to 14 %)
+// K = 2 without spilling (gfx950, ROCm 7.2 compiler), E doubles per lane per
+// load (2: 16-byte loads, rows in steps of 128 per wave), and whether team t
+// takes columns t, t + nteams, ... (interleaved) or a contiguous range.  Only
+// the configurations op_plan / team_plain_plan select are kept, plus 6 (the
+// interleaving ablation).  (Round 3 numbered them differently: 7 -> 2, 8 -> 3,
+// 9 -> 4, 12 -> 5; the dynamic-chunk configurations 17/18 and the other
+// swept entries were removed in round 4, profiles/r03_op_experiments.txt.)
 struct TmCfg {
     int F, L, P;
     bool comm;
     int maxS;
     int E;
     bool ilv;  // team t takes columns t, t + nteams, ... (else a contiguous range)
-    bool dyn = false;  // teams claim chunks of columns at run time (see "Dynamic chunks" below)
 };
 static constexpr TmCfg kTmCfg[] = {
     {1, 0, 0, false, 10, 2, false},  // 0: T = 1, one column prefetched
     {2, 0, 0, false, 8, 2, false},   // 1: T = 1, two
-    {3, 5, 2, true, 4, 2, false},    // 2
-    {2, 4, 2, true, 5, 2, false},    // 3
-    {3, 6, 3, true, 4, 2, false},    // 4
-    {3, 6, 2, true, 4, 2, false},    // 5
-    {4, 5, 2, true, 4, 2, false},    // 6
-    {4, 5, 2, true, 4, 2, true},     // 7
-    {3, 5, 2, true, 4, 2, true},     // 8
-    {2, 4, 2, true, 5, 2, true},     // 9: 3, interleaved
-    {2, 4, 2, true, 6, 2, true},     // 10: six loads per lane (T = 2 at N = 10,000)
-    {1, 4, 2, true, 6, 2, true},     // 11
-    {2, 3, 2, true, 6, 2, true},     // 12
-    {5, 5, 2, true, 3, 2, true},     // 13: deeper prefetch for short tiles (C2: T = 4, S = 3)
-    {6, 5, 2, true, 3, 2, true},     // 14
-    {8, 5, 2, true, 3, 2, true},     // 15
-    {6, 6, 3, true, 3, 2, true},     // 16
-    {4, 5, 2, true, 4, 2, true, true},  // 17: 7 with dynamic chunks
-    {2, 4, 2, true, 5, 2, true, true},  // 18: 9 with dynamic chunks
-    {4, 8, 3, true, 3, 2, true},     // 19: a longer lag for short tiles (C2: T = 4, S = 3): members may
-    {4, 11, 3, true, 3, 2, true},    // 20: drift further apart before a team waits for its slowest
+    {4, 5, 2, true, 4, 2, true},     // 2: teams, four loads per lane (large N)
+    {3, 5, 2, true, 4, 2, true},     // 3: the head-start kernel's short ring
+    {2, 4, 2, true, 5, 2, true},     // 4: one more load per lane, fewer columns in flight
+    {2, 3, 2, true, 6, 2, true},     // 5: six loads per lane (T = 2 at N = 10,000: C2)
+    {4, 5, 2, true, 4, 2, false},    // 6: 2 with contiguous column ranges (interleaving ablation)
 };
 static constexpr int kTmNCfg = sizeof(kTmCfg) / sizeof(kTmCfg[0]);
 
 __host__ __device__ constexpr int tm_rows_per_step(bool comm, int E) { return 64 * E * (comm ? 7 : 8); }
 
-// Dynamic chunks (configurations with dyn): a team's steps come in chunks of
-// kTmChunk consecutive columns.  Its first tm_ns() chunks are static (chunk
-// k: id k*nteams + team); after that, member 0's hand-off wave claims the
-// next chunk id from a launch-wide counter (one agent-scope atomic add per
-// chunk, tm_ca() steps before the chunk starts) and publishes it in the
-// team's ring of chunk slots; every member's hand-off wave polls the slot
-// (a lane of its per-step scalar load) and hands the id to its streaming
-// waves through LDS.  A team stops at the first chunk id past the shard.
-// So the teams that stream faster take more chunks: the launch ends when the
-// columns run out, not when the slowest of 8-64 teams has done 1/nteams of
-// them (C2: team end times spread over 35-50 us of a 600 us launch, at
-// random, tools/op_skew.py).  Which team sums which column then varies from
-// launch to launch: A d and <d,p> are summed in another order each time
-// (rounding-level differences; the static configurations are bitwise
-// reproducible).
-static constexpr int kTmChunk = 8;
-static constexpr int kTmRingSlots = 16;  // chunk slots per team (16 bytes each)
-__host__ __device__ constexpr int tm_ca(int F, int P) { return F + 2 * P + 6; }  // claim-ahead steps
-__host__ __device__ constexpr int tm_ns(int F, int P) { return (tm_ca(F, P) - F + kTmChunk - 1) / kTmChunk; }
-// words of OpArgs.dyn: the claim counter [0], the finish ticket [16], the
-// teams' chunk rings from word 32, then 2 dummy words per workgroup
-__host__ __device__ constexpr int64_t tm_dyn_words(int grid) { return 32 + (int64_t)grid * kTmRingSlots * 2 + 2 * grid; }
 // q in LDS: every lane row of the S steps (zeros past the tile, so those
 // rows need no mask) when that fits beside the partials, else the tile only
 // (rows past it masked)
@@ -218,38 +185,6 @@ template <int N>
 __device__ __forceinline__ void tm_wait2(v4u& r, v2u& q) {
     asm volatile("s_waitcnt vmcnt(%2)" : "+v"(r), "+v"(q) : "n"(N) : "memory");
 }
-// DYN: the scalar load bypasses L1 (one lane polls a chunk slot written by
-// another CU), the claim (agent-scope atomic add, returns the old value) or a
-// same-count dummy load, and the wait that covers all three
-__device__ __forceinline__ void tm_load8_sc1(v2u& dst, const void* p) {
-    asm volatile("global_load_dwordx2 %0, %1, off sc1" : "=v"(dst) : "v"(p) : "memory");
-}
-// ONE asm statement for both forms, lane 0 only (exec switched inside): two
-// statements writing one variable made the compiler merge their results with
-// a register copy taken before the loads returned, and a load landing later
-// overwrote a register meanwhile given to another value
-__device__ __forceinline__ void tm_claim_or_load(unsigned& dst, unsigned claim, unsigned* ctr, const unsigned* dmy) {
-    unsigned long long sv;
-    asm volatile(
-        "s_mov_b64 %[sv], exec\n\t"
-        "s_mov_b64 exec, 1\n\t"
-        "v_cmp_ne_u32 vcc, 0, %[c]\n\t"
-        "s_and_b64 vcc, vcc, exec\n\t"
-        "s_cbranch_vccz 1f\n\t"
-        "global_atomic_add %[d], %[a], %[one], off sc0\n\t"
-        "s_branch 2f\n"
-        "1:\n\t"
-        "global_load_dword %[d], %[b], off\n"
-        "2:\n\t"
-        "s_mov_b64 exec, %[sv]"
-        : [d] "=&v"(dst), [sv] "=&s"(sv)
-        : [c] "v"(claim), [a] "v"(ctr), [b] "v"(dmy), [one] "v"(1u)
-        : "memory", "vcc", "scc");
-}
-template <int N>
-__device__ __forceinline__ void tm_wait3(v4u& r, v2u& q, unsigned& c) {
-    asm volatile("s_waitcnt vmcnt(%3)" : "+v"(r), "+v"(q), "+v"(c) : "n"(N) : "memory");
-}
 __device__ __forceinline__ void tm_publish(unsigned long long* p, const v4u& v) {
     asm volatile("s_nop 4\n\tglobal_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
 }
@@ -276,14 +211,13 @@ __device__ __forceinline__ Tp* tm_chk(Tp* p, const void* lo, const void* hi, uns
     return p;
 }
 
-template <int K, int S, int F, int L, int P, bool COMM, int E, bool FMA, int KP, bool DYN>
+template <int K, int S, int F, int L, int P, bool COMM, int E, bool FMA, int KP>
 __device__ __forceinline__ void atax_team_body(const double* __restrict__ X, int64_t ld, int64_t N, int64_t M,
                                                const double* __restrict__ mave, const double* __restrict__ msig,
                                                const OpArgs& a, int T, int TR, int ilv,
                                                const int* __restrict__ gate) {
     if (gate && !*gate) return;
     static_assert(K + KP <= kMaxRhs, "partial slots per team");
-    static_assert(!DYN || COMM, "dynamic chunks need the hand-off wave");
 #if TM_TS
     const unsigned long long ts0 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -314,30 +248,10 @@ __device__ __forceinline__ void atax_team_body(const double* __restrict__ X, int
 #else
     const int team = (blockIdx.x & 7) + 8 * (g / T);
 #endif
-    // the team's columns: mb + cs*m, m < n (a contiguous range, or every nteams-th);
-    // DYN: column of step m is colof(m) (mb = 0, cs = 1), n known at run time
-    const int64_t cs = (ilv || DYN) ? (DYN ? 1 : nteams) : 1;
-    const int64_t mb = DYN ? 0 : ilv ? team : (int64_t)team * M / nteams;
-    constexpr int CH = kTmChunk, NS = tm_ns(F, P), CA = tm_ca(F, P);
-    // DYN chunks: chunk j holds columns [j*CH, (j+1)*CH) (the last one may be
-    // partial).  (Interleaving a chunk's columns over the shard instead, as the
-    // static teams interleave theirs, was slower: C2 775 against 732 us.)
-    const int nfull = DYN ? (int)(M / CH) : 0;
-    const int nchunks = DYN ? (int)((M + CH - 1) / CH) : 0;
-    // DYN: n (the team's step count) from chunk k with id j: k*CH if j is past
-    // the shard, k*CH + (M - j*CH) if j is the partial chunk, else still unknown
-    auto ends = [&](int k, int j, int nn) -> int {
-        if (j >= nchunks) return k * CH;
-        if (j == nfull) return k * CH + (int)(M - (int64_t)j * CH);
-        return nn;
-    };
-    int n;
-    if constexpr (DYN) {
-        n = 0x7fffffff;  // the static chunks decide it, or a claimed one will
-        for (int k = NS - 1; k >= 0; --k) n = ends(k, k * nteams + team, n);
-    } else {
-        n = (int)(ilv ? (M - team + nteams - 1) / nteams : (int64_t)(team + 1) * M / nteams - mb);
-    }
+    // the team's columns: mb + cs*m, m < n (a contiguous range, or every nteams-th)
+    const int64_t cs = ilv ? nteams : 1;
+    const int64_t mb = ilv ? team : (int64_t)team * M / nteams;
+    const int n = (int)(ilv ? (M - team + nteams - 1) / nteams : (int64_t)(team + 1) * M / nteams - mb);
     const int64_t nmax = (M + nteams - 1) / nteams;  // granule rows per team
     const int64_t gwords = (M + gridDim.x) * kOpMaxK * T * 2;  // the granule block (OpArgs.xg)
     const int64_t r0 = (int64_t)member * TR;
@@ -347,20 +261,6 @@ __device__ __forceinline__ void atax_team_body(const double* __restrict__ X, int
     double* q_lds = lds;                                  // K x QS
     double* s_part = lds + K * QS;                        // [2][CW][K] wave partials of a column's dot
     double* s_tot = s_part + 2 * CW * K;                  // [2][K] team totals (hand-off)
-    // DYN: chunk kk's {id, n after it} for the streaming waves, ring of 4 pairs
-    int* s_ci = reinterpret_cast<int*>(s_tot + 2 * K);
-    // DYN: the shard column of step m of chunk k with id j (TM_SAFE builds: a
-    // column outside the shard is reported in a.err and read as column 0)
-    auto colj = [&](int m, int k, int j) -> int64_t {
-        const int64_t c = (int64_t)j * CH + (m - k * CH);
-#if TM_SAFE
-        if (m < 0 || j < 0 || c >= M) {
-            __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            return 0;
-        }
-#endif
-        return c;
-    };
     const int jb = 64 * E * wave + E * lane;              // row of this lane in step s: RS*s + jb
     // the tile of a column (E = 2: + the zero pad row for odd N)
     const int nbytes = (E == 2 ? (nrows + 1) & ~1 : nrows) * 8;
@@ -382,29 +282,9 @@ __device__ __forceinline__ void atax_team_body(const double* __restrict__ X, int
         // stays sufficient).  Every poll register passes through such a wait
         // before it is read or reused (the compiler sees the wait as its writer).
         const int nq = K * T;
-        // granules of step m at xg + gidx(m) * nq2: the team's m-th column (DYN: by shard column)
-        unsigned long long* xg = DYN ? a.xg : a.xg + (int64_t)team * nmax * nq * 2;
+        // granules of step m at xg + m * nq2: the team's m-th column
+        unsigned long long* xg = a.xg + (int64_t)team * nmax * nq * 2;
         unsigned long long* dummy = a.xg + gwords + (int64_t)blockIdx.x * 2 * K;
-        // DYN: the claim counter, this team's chunk ring, this workgroup's dummy slot
-        unsigned* dctr = reinterpret_cast<unsigned*>(a.dyn);
-        unsigned long long* ring = a.dyn + 32 + (int64_t)team * kTmRingSlots * 2;
-        unsigned long long* ddmy = a.dyn + 32 + (int64_t)gridDim.x * kTmRingSlots * 2 + (int64_t)blockIdx.x * 2;
-        constexpr int DL = 1 + 2 * K;  // the scalar load's lane that polls a chunk slot
-        // the ids of chunks kl, kl-1, kl-2, kl-3 (kl: the latest one known); the
-        // static ones by formula.  The hand-off wave's step streams (cf, the
-        // polled column, the published one) stay within the last 3 chunks
-        int kl = NS - 1, h0 = 0, h1 = 0, h2 = 0, h3 = 0;
-        auto colof = [&](int m) -> int64_t {
-            const int k = m / CH, d = kl - k;
-            const int j = k < NS ? k * nteams + team : d == 0 ? h0 : d == 1 ? h1 : d == 2 ? h2 : h3;
-            return colj(m, k, j);
-        };
-        int n_next = n;  // a consumed chunk's n applies from the next step (as in the streaming waves)
-        const bool leader = DYN && member == 0;
-        bool claim_end = false;
-        int pend_k = -1;         // the chunk whose claim is in flight (returns P steps after issue)
-        unsigned pub_x = 0;      // a returned claim to publish this step: {id | k << 16}
-        unsigned long long* pub_dst = ddmy;
         // lane 32k + j reads member j's granule of system k (j < T), so one
         // fixed 32-lane butterfly sums every team size (the zeros of lanes
         // j >= T leave the sums' bits unchanged); other lanes re-read granule 0
@@ -429,7 +309,6 @@ __device__ __forceinline__ void atax_team_body(const double* __restrict__ X, int
         }
         v4u pl[RING];
         v2u ps[RING];
-        unsigned ar[RING];  // DYN: claim results (lane 0)
         bool dead = false;
         unsigned nslow = 0, nspin = 0;
         if (n > 0) {
@@ -467,87 +346,14 @@ __device__ __forceinline__ void atax_team_body(const double* __restrict__ X, int
 #pragma unroll
                 for (int i = 0; i < RING; ++i) {
                     const int m = base + i;  // columns relative to mb (32-bit: scalar compares)
-                    if constexpr (DYN) n = n_next;
                     // the column polled now (finished P steps later), the column finished now
                     const int ci = m - L + P, cf = m - L;
                     const int cic = ci < 0 ? 0 : ci < n ? ci : n - 1;
-                    if constexpr (DYN) {
-                        // the scalars, a chunk slot polled in lane DL (chunk kp, consumed P steps
-                        // later, F + 1 steps before it starts), and the claim or its stand-in
-                        const int64_t col = colof(cic);
-                        const int kp = (m + P + F + 2) / CH;
-                        const bool poll = (m + P + F + 2) % CH == 0 && kp >= NS;
-                        const void* ad = lane == DL ? (const void*)(poll ? ring + 2 * (kp & (kTmRingSlots - 1)) : ddmy)
-                                                    : (const void*)(scp + col);
-                        const unsigned long long* dyn_hi = a.dyn + tm_dyn_words(gridDim.x);
-                        tm_load8_sc1(ps[(i + RING - L + P) % RING],
-                                     lane == DL ? tm_chk(ad, a.dyn, dyn_hi, 1, a.err)
-                                                : tm_chk(ad, scp - mb, scp - mb + M, 2, a.err));
-                        tm_poll(pl[(i + RING - L + P) % RING], tm_chk(xg + (col * nq2 + ql2), a.xg, a.xg + gwords, 4, a.err));
-                        const int kc = (m + CA) / CH;
-                        const bool claim = leader && !claim_end && (m + CA) % CH == 0 && kc >= NS && kc * CH < n;
-                        tm_claim_or_load(ar[i], claim ? 1u : 0u, tm_chk(dctr, a.dyn, dyn_hi, 8, a.err),
-                                         tm_chk(reinterpret_cast<const unsigned*>(ddmy), a.dyn, dyn_hi, 16, a.err));
-                        if (claim) pend_k = kc;
-                    } else {
-                        tm_load8(ps[(i + RING - L + P) % RING], scp + cic * csi);  // offsets < 2^31: 32-bit math
-                        tm_poll(pl[(i + RING - L + P) % RING], xg + (cic * nq2 + ql2));
-                    }
+                    tm_load8(ps[(i + RING - L + P) % RING], scp + cic * csi);  // offsets < 2^31: 32-bit math
+                    tm_poll(pl[(i + RING - L + P) % RING], xg + (cic * nq2 + ql2));
                     v4u& g = pl[(i + RING - L) % RING];
                     v2u& sc = ps[(i + RING - L) % RING];
-                    if constexpr (DYN) {
-                        // step m - P's scalars, poll and claim; 4P younger operations in flight
-                        tm_wait3<4 * P>(g, sc, ar[(i + RING - P) % RING]);
-                        if (pend_k >= 0 && (m - P + CA) % CH == 0 && (m - P + CA) / CH == pend_k) {
-                            // the claim returned: publish it (after the barrier, lane K of the publish)
-                            int j = NS * nteams + (int)__builtin_amdgcn_readlane((int)ar[(i + RING - P) % RING], 0);
-                            if (j >= nchunks) {
-                                j = 0xffff;
-                                claim_end = true;
-                            }
-                            pub_x = (unsigned)j | ((unsigned)pend_k << 16);
-                            pub_dst = ring + 2 * (pend_k & (kTmRingSlots - 1));
-                            pend_k = -1;
-                        }
-                        // the chunk whose first load the streaming waves issue two steps from now
-                        const int kk = (m + F + 2) / CH;
-                        if ((m + F + 2) % CH == 0 && kk >= NS && kk * CH < n) {
-                            unsigned x = (unsigned)__builtin_amdgcn_readlane((int)sc.x, DL);
-                            unsigned y = (unsigned)__builtin_amdgcn_readlane((int)sc.y, DL);
-                            if (!(y == tag && (x >> 16) == ((unsigned)kk & 0xffff)) && !dead) {
-#pragma unroll 1
-                                for (unsigned spins = 0;; ++spins) {  // slow path: the claim is not visible yet
-                                    if (spins >= kTmMaxSpins) {
-                                        dead = true;
-                                        if (lane == 0) __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                                        break;
-                                    }
-                                    __builtin_amdgcn_s_sleep(2);
-                                    v2u t;
-                                    tm_load8_sc1(t, tm_chk(ring + 2 * (kk & (kTmRingSlots - 1)), a.dyn,
-                                                           a.dyn + tm_dyn_words(gridDim.x), 32, a.err));
-                                    asm volatile("s_waitcnt vmcnt(0)" : "+v"(t) : : "memory");
-                                    x = (unsigned)__builtin_amdgcn_readfirstlane((int)t.x);
-                                    y = (unsigned)__builtin_amdgcn_readfirstlane((int)t.y);
-                                    if (y == tag && (x >> 16) == ((unsigned)kk & 0xffff)) break;
-                                }
-                            }
-                            int j = (int)(x & 0xffff);
-                            if (dead || j == 0xffff) j = nchunks;  // past the shard
-                            n_next = ends(kk, j, n);
-                            h3 = h2;
-                            h2 = h1;
-                            h1 = h0;
-                            h0 = j;
-                            kl = kk;
-                            if (lane == 0) {  // read by the streaming waves after this step's barrier
-                                s_ci[2 * (kk & 3)] = j;
-                                s_ci[2 * (kk & 3) + 1] = n_next;
-                            }
-                        }
-                    } else if (!(dbg & 1)) {
-                        tm_wait2<3 * P>(g, sc);  // step m - P's poll; 3P younger operations in flight
-                    }
+                    if (!(dbg & 1)) tm_wait2<3 * P>(g, sc);  // step m - P's poll; 3P younger operations in flight
                     if (cf >= 0 && cf < n) {
                         // every granule of column cf carries this launch's tag {lo, tag} {hi, tag}
                         if (!(__all(g.y == tag && g.w == tag) || dead || (dbg & 1))) {
@@ -563,8 +369,7 @@ __device__ __forceinline__ void atax_team_body(const double* __restrict__ X, int
                                     break;
                                 }
                                 __builtin_amdgcn_s_sleep(2);
-                                tm_poll(g, tm_chk(xg + ((DYN ? colof(cf) : (int64_t)cf) * nq2 + ql2), a.xg, a.xg + gwords, 64,
-                                                  a.err));
+                                tm_poll(g, tm_chk(xg + ((int64_t)cf * nq2 + ql2), a.xg, a.xg + gwords, 64, a.err));
                                 tm_wait<0>(g);
                                 if (__all(g.y == tag && g.w == tag)) break;
                             }
@@ -579,7 +384,7 @@ __device__ __forceinline__ void atax_team_body(const double* __restrict__ X, int
                         const double scv = __builtin_bit_cast(double, ((unsigned long long)sc.y << 32) | sc.x);
                         const double sg = readlane_d(scv, 0);
                         const bool own = (cf & (T - 1)) == member;  // T: a power of two
-                        const int64_t mg = DYN ? colof(cf) : mb + cf * csi;  // the shard's column index
+                        const int64_t mg = mb + cf * csi;  // the shard's column index
                         // both systems' chains first (independent: interleaved), then the
                         // LDS hand-over, then the owner's stores and <d,p>
                         double tsc[K], dval[K], pdir[K];
@@ -610,35 +415,24 @@ __device__ __forceinline__ void atax_team_body(const double* __restrict__ X, int
                         }
                     }
                     __syncthreads();
-                    if (lane < K + (DYN ? 1 : 0) && !(dbg & 2)) {  // this member's dot of column m: the streaming waves' partials in order
+                    if (lane < K && !(dbg & 2)) {  // this member's dot of column m: the streaming waves' partials in order
                         const bool real = m >= 0 && m < n;
                         double v = 0.0;
-                        if (real && lane < K) v = tree_sum<CW>(s_part + (m & 1) * CW * K + lane, K);  // fixed pairwise order
+                        if (real) v = tree_sum<CW>(s_part + (m & 1) * CW * K + lane, K);  // fixed pairwise order
                         const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
-                        v4u gr = {(unsigned)u, tag, (unsigned)(u >> 32), tag};
+                        const v4u gr = {(unsigned)u, tag, (unsigned)(u >> 32), tag};
                         unsigned long long* dst =
-                            real ? xg + ((DYN ? colof(m) : (int64_t)m) * nq2 + (lane * T + member) * 2) : dummy + 2 * lane;
-                        if (DYN && lane == K) {  // (DYN) lane K: a returned claim, {id | k << 16, tag}
-                            gr = v4u{pub_x, tag, 0u, 0u};
-                            dst = pub_dst;
-                        }
-                        dst = (DYN && lane == K) ? tm_chk(dst, a.dyn, a.dyn + tm_dyn_words(gridDim.x), 256, a.err)
-                                                 : tm_chk(dst, a.xg, a.xg + gwords + (int64_t)gridDim.x * 2 * kOpMaxK, 512, a.err);
+                            tm_chk(real ? xg + ((int64_t)m * nq2 + (lane * T + member) * 2) : dummy + 2 * lane, a.xg,
+                                   a.xg + gwords + (int64_t)gridDim.x * 2 * kOpMaxK, 512, a.err);
                         if (l2)
                             tm_publish_l2(dst, gr);
                         else
                             tm_publish(dst, gr);
                     }
-                    if constexpr (DYN) pub_dst = ddmy;
                 }
             }
 #pragma unroll
-            for (int s = 0; s < RING; ++s) {  // nothing of ours lands after the loop
-                if constexpr (DYN)
-                    tm_wait3<0>(pl[s], ps[s], ar[s]);
-                else
-                    tm_wait2<0>(pl[s], ps[s]);
-            }
+            for (int s = 0; s < RING; ++s) tm_wait2<0>(pl[s], ps[s]);  // nothing of ours lands after the loop
             if ((dbg & 64) && lane == 0) {  // timing experiments: slow-path counts into the flag block
                 __hip_atomic_fetch_add(a.err + 1, nslow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 __hip_atomic_fetch_add(a.err + 2, nspin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -716,13 +510,9 @@ __device__ __forceinline__ void atax_team_body(const double* __restrict__ X, int
 
     double xr[RING][S][E];
     double pk[RING];
-    // DYN: the id of the chunk of the step loaded now, and of the next chunk
-    // (read with the team's n from LDS one step before that chunk's first load)
-    int cid = team, cid_next = team;
     const char* xtile = reinterpret_cast<const char*>(X + mb * ld + r0);
     auto load = [&](int slot, int m) {
-        // DYN: a step past n loads (unused) the team's first column
-        const int64_t c = DYN ? (m < n ? colj(m, m / CH, cid) : (int64_t)team * CH) : m * cs;  // offset from mb
+        const int64_t c = m * cs;  // offset from mb
         pk[slot] = *tm_chk(pkp + c, pkp - mb, pkp - mb + M, 1024, a.err);  // older than the column's X loads: it lands first
         const __amdgpu_buffer_rsrc_t rs =
             __builtin_amdgcn_make_buffer_rsrc((void*)(xtile + c * ld * 8), (short)0, nbytes, 0x00020000);
@@ -861,20 +651,8 @@ __device__ __forceinline__ void atax_team_body(const double* __restrict__ X, int
 #pragma unroll
             for (int i = 0; i < RING; ++i) {
                 const int m = base + i;  // columns relative to mb (32-bit: scalar compares)
-                if constexpr (DYN) {
-                    // one step before chunk kk's first load: its id and the team's n after
-                    // it, written by the hand-off wave before the last barrier (which
-                    // applies that n from this step too: the waves agree on every round)
-                    const int kk = (m + F + 1) / CH;
-                    if ((m + F + 1) % CH == 0 && kk >= NS && kk * CH < n) {
-                        cid_next = s_ci[2 * (kk & 3)];
-                        n = s_ci[2 * (kk & 3) + 1];
-                    }
-                    const int kc = (m + F) / CH;
-                    if ((m + F) % CH == 0) cid = kc < NS ? kc * nteams + team : cid_next;
-                }
                 // every step issues one column (clamped to [0, n): fixed vmcnt counts)
-                load((i + F) % RING, DYN ? m + F : m + F < n ? m + F : n - 1);  // (DYN: load() handles steps past n)
+                load((i + F) % RING, m + F < n ? m + F : n - 1);
                 if (m >= 0 && m < n) dot(i, m & 1);
                 __syncthreads();
                 const int cf = m - L;
@@ -926,18 +704,6 @@ __device__ __forceinline__ void atax_team_body(const double* __restrict__ X, int
         for (int k = 0; k < K; ++k) red_put(a.ro, (int64_t)blockIdx.x * K + k, dpacc[k]);
     }
     if (wave == 0) ticket_sum_blocks<K>(a.ro);
-    if constexpr (DYN) {
-        // the last workgroup to get here re-arms the claim counter for the next
-        // launch (every claim of every workgroup returned before its barrier above)
-        if (threadIdx.x == 0) {
-            unsigned* w = reinterpret_cast<unsigned*>(a.dyn);
-            const unsigned old = __hip_atomic_fetch_add(w + 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (old == gridDim.x - 1) {
-                __hip_atomic_store(w, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(w + 32, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-    }
 #if TM_TS
     if (a.ts && threadIdx.x == 0) {
         unsigned xcc, hw;
@@ -957,16 +723,7 @@ __global__ __launch_bounds__(kTmThreads) void atax_team_kernel(const double* __r
                                                                int64_t M, const double* __restrict__ mave,
                                                                const double* __restrict__ msig, OpArgs a, int T,
                                                                int TR, int ilv, const int* __restrict__ gate) {
-    atax_team_body<K, S, F, L, P, COMM, E, FMA, 0, false>(X, ld, N, M, mave, msig, a, T, TR, ilv, gate);
-}
-
-// the same with dynamic chunks (configurations with dyn; a hand-off always)
-template <int K, int S, int F, int L, int P, int E, bool FMA>
-__global__ __launch_bounds__(kTmThreads) void atax_team_dyn_kernel(const double* __restrict__ X, int64_t ld, int64_t N,
-                                                                   int64_t M, const double* __restrict__ mave,
-                                                                   const double* __restrict__ msig, OpArgs a, int T,
-                                                                   int TR, int ilv, const int* __restrict__ gate) {
-    atax_team_body<K, S, F, L, P, true, E, FMA, 0, true>(X, ld, N, M, mave, msig, a, T, TR, ilv, gate);
+    atax_team_body<K, S, F, L, P, COMM, E, FMA, 0>(X, ld, N, M, mave, msig, a, T, TR, ilv, gate);
 }
 
 // the head-start launch: one operator system (the Onsager solve's first CG
@@ -978,7 +735,7 @@ __global__ __launch_bounds__(kTmThreads) void atax_team_plain_kernel(const doubl
                                                                      const double* __restrict__ mave,
                                                                      const double* __restrict__ msig, OpArgs a, int T,
                                                                      int TR, int ilv, const int* __restrict__ gate) {
-    atax_team_body<1, S, F, L, P, COMM, E, FMA, kTmPlain, false>(X, ld, N, M, mave, msig, a, T, TR, ilv, gate);
+    atax_team_body<1, S, F, L, P, COMM, E, FMA, kTmPlain>(X, ld, N, M, mave, msig, a, T, TR, ilv, gate);
 }
 
 // ---------------------------------------------------------------------------
@@ -994,7 +751,6 @@ bool team_plan(int64_t N, int64_t M, int cus, int T, int cfg, OpPlan* out) {
     if (cfg < 0 || cfg >= kTmNCfg || N < 1) return false;
     const TmCfg& c = kTmCfg[cfg];
     if ((T == 1) == c.comm) return false;
-    if (c.dyn && (M + kTmChunk - 1) / kTmChunk >= 0xffff) return false;  // chunk ids are 16 bits
     if (T < 1 || T > kTmMaxT || (T & (T - 1))) return false;
     const int grid = (cus / (8 * T)) * 8 * T;
     if (grid < T) return false;
@@ -1034,12 +790,10 @@ static void launch_tm(const Shard& s, const OpPlan& pl, const OpArgs& a, hipStre
                  const int*);
     if constexpr (PL)
         kern = atax_team_plain_kernel<S, c.F, c.L, c.P, c.comm, c.E, (bool)TM_FMA>;
-    else if constexpr (c.dyn)
-        kern = atax_team_dyn_kernel<K, S, c.F, c.L, c.P, c.E, (bool)TM_FMA>;
     else
         kern = atax_team_kernel<K, S, c.F, c.L, c.P, c.comm, c.E, (bool)TM_FMA>;
     const int64_t QS = tm_qstride(K, S, c.comm, c.E, std::min<int64_t>(pl.TR, s.N));
-    const size_t lds = (size_t)(K * QS + 2 * CW * K + 2 * K + 4) * sizeof(double);  // + DYN's chunk ring and n
+    const size_t lds = (size_t)(K * QS + 2 * CW * K + 2 * K) * sizeof(double);
     static std::once_flag once;  // more than 64 KiB of dynamic LDS must be allowed explicitly
     std::call_once(once, [&] {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1056,9 +810,9 @@ static void launch_tm(const Shard& s, const OpPlan& pl, const OpArgs& a, hipStre
 // the most loads per lane per column the head-start kernel is instantiated
 // for, per configuration (0: none): its 3 plain accumulators cost 12*S
 // registers beside the ring (register counts and spills checked with
-// tools/regcheck.sh)
+// tools/regcheck.py)
 static constexpr int tm_plain_maxS(int cfg) {
-    return cfg == 0 ? 8 : cfg == 7 ? 3 : cfg == 8 ? 4 : cfg == 9 ? 5 : 0;
+    return cfg == 0 ? 8 : cfg == 2 ? 3 : cfg == 3 ? 4 : cfg == 4 ? 5 : 0;
 }
 
 template <int K, int C, int S, bool PL>
@@ -1095,9 +849,9 @@ static bool launch_tm_c(const Shard& s, const OpPlan& pl, const OpArgs& a, hipSt
     if constexpr (PL) {
         switch (pl.cfg) {
             case 0: return launch_tm_s<1, 0, true>(pl.S, s, pl, a, st, tm, gate, occ);
-            case 7: return launch_tm_s<1, 7, true>(pl.S, s, pl, a, st, tm, gate, occ);
-            case 8: return launch_tm_s<1, 8, true>(pl.S, s, pl, a, st, tm, gate, occ);
-            case 9: return launch_tm_s<1, 9, true>(pl.S, s, pl, a, st, tm, gate, occ);
+            case 2: return launch_tm_s<1, 2, true>(pl.S, s, pl, a, st, tm, gate, occ);
+            case 3: return launch_tm_s<1, 3, true>(pl.S, s, pl, a, st, tm, gate, occ);
+            case 4: return launch_tm_s<1, 4, true>(pl.S, s, pl, a, st, tm, gate, occ);
             default: return false;
         }
     }
@@ -1109,20 +863,6 @@ static bool launch_tm_c(const Shard& s, const OpPlan& pl, const OpArgs& a, hipSt
         case 4: return launch_tm_s<K, 4, false>(pl.S, s, pl, a, st, tm, gate, occ);
         case 5: return launch_tm_s<K, 5, false>(pl.S, s, pl, a, st, tm, gate, occ);
         case 6: return launch_tm_s<K, 6, false>(pl.S, s, pl, a, st, tm, gate, occ);
-        case 7: return launch_tm_s<K, 7, false>(pl.S, s, pl, a, st, tm, gate, occ);
-        case 8: return launch_tm_s<K, 8, false>(pl.S, s, pl, a, st, tm, gate, occ);
-        case 9: return launch_tm_s<K, 9, false>(pl.S, s, pl, a, st, tm, gate, occ);
-        case 10: return launch_tm_s<K, 10, false>(pl.S, s, pl, a, st, tm, gate, occ);
-        case 11: return launch_tm_s<K, 11, false>(pl.S, s, pl, a, st, tm, gate, occ);
-        case 12: return launch_tm_s<K, 12, false>(pl.S, s, pl, a, st, tm, gate, occ);
-        case 13: return launch_tm_s<K, 13, false>(pl.S, s, pl, a, st, tm, gate, occ);
-        case 14: return launch_tm_s<K, 14, false>(pl.S, s, pl, a, st, tm, gate, occ);
-        case 15: return launch_tm_s<K, 15, false>(pl.S, s, pl, a, st, tm, gate, occ);
-        case 16: return launch_tm_s<K, 16, false>(pl.S, s, pl, a, st, tm, gate, occ);
-        case 17: return launch_tm_s<K, 17, false>(pl.S, s, pl, a, st, tm, gate, occ);
-        case 18: return launch_tm_s<K, 18, false>(pl.S, s, pl, a, st, tm, gate, occ);
-        case 19: return launch_tm_s<K, 19, false>(pl.S, s, pl, a, st, tm, gate, occ);
-        case 20: return launch_tm_s<K, 20, false>(pl.S, s, pl, a, st, tm, gate, occ);
         default: return false;
     }
 }
@@ -1131,7 +871,6 @@ hipError_t atax_team(const Shard& s, const OpPlan& pl, int K, const OpArgs& a, h
                      const int* gate) {
     if (pl.T < 1 || pl.grid < pl.T || pl.grid % pl.T) return hipErrorInvalidValue;
     if (pl.T > 1 && (!a.xg || !a.err || a.tag == 0)) return hipErrorInvalidValue;
-    if (kTmCfg[pl.cfg].dyn && !a.dyn) return hipErrorInvalidValue;
     if (s.M <= 0) return hipSuccess;
     bool ok = false;
     switch (K) {
@@ -1158,7 +897,7 @@ bool team_plain_plan(int64_t N, int64_t M, int cus, const OpPlan& main, OpPlan* 
     // the main plan's team size when the head-start kernel fits its rows, else
     // larger teams (fewer rows per member); configurations with short rings
     const int cfgs1[] = {0};
-    const int cfgsT[] = {7, 8, 9};
+    const int cfgsT[] = {2, 3, 4};
     for (int T = std::max(main.T, 1); T <= kTmMaxT; T *= 2) {
         const int* cf = T == 1 ? cfgs1 : cfgsT;
         const int ncf = T == 1 ? 1 : 3;
@@ -1171,8 +910,6 @@ bool team_plain_plan(int64_t N, int64_t M, int cus, const OpPlan& main, OpPlan* 
     }
     return false;
 }
-
-int64_t team_dyn_words(const OpPlan& pl) { return kTmCfg[pl.cfg].dyn ? tm_dyn_words(pl.grid) : 0; }
 
 int team_occupancy(const OpPlan& pl, int K) {
     int occ = 0;
@@ -1194,8 +931,6 @@ std::string team_kernel_name(int K, const OpPlan& pl) {
     if (K == 1 + kTmPlain)  // the head-start kernel
         std::snprintf(b, sizeof b, "atax_team_plain_kernel<%d, %d, %d, %d, %s, %d>", pl.S, c.F, c.L, c.P,
                       c.comm ? "true" : "false", c.E);
-    else if (c.dyn)
-        std::snprintf(b, sizeof b, "atax_team_dyn_kernel<%d, %d, %d, %d, %d, %d>", K, pl.S, c.F, c.L, c.P, c.E);
     else
         std::snprintf(b, sizeof b, "atax_team_kernel<%d, %d, %d, %d, %d, %s, %d>", K, pl.S, c.F, c.L, c.P,
                       c.comm ? "true" : "false", c.E);

@@ -127,8 +127,6 @@ struct vampomi_ctx {
     vk::OpPlan opp_hs{};
     bool hs_ok = false;
     bool hs_on = true;
-    unsigned long long* op_dyn = nullptr;  // dynamic-chunk plans: vk::team_dyn_words of them
-    int64_t op_dyn_words = 0;
     unsigned long long* op_ts = nullptr;  // VAMPOMI_OP_TS=1 (TM_TS builds): the last launch's workgroup times
     double* nbuf = nullptr;     // kMaxRhs * ld scratch N-vectors (API calls)
     double* mbuf = nullptr;     // (2*kMaxRhs) * M scratch M-vectors (API calls)

@@ -258,18 +258,33 @@ static double comm_init_timeout_s() {
     return v > 0 ? v : 120.0;
 }
 
+// hipStreamQuery is NOT free for the stream: it can put a marker packet behind
+// the work queued so far, i.e. between the last queued kernel and the next one
+// the host queues after this wait (a CG step's cg_update and the next operator
+// launch: 6-7 us of idle GPU at every C2 step, profiles/r04c_gaps.txt).  So the
+// spin asks the runtime only after kQueryAfterS of waiting (far longer than
+// any step), and every kQueryEveryS after that: a fault or a stream that
+// finished without the flag is still seen, within a second.
+static constexpr double kQueryAfterS = 0.5, kQueryEveryS = 0.25;
+
 vampomi_status wait_flag(vampomi_ctx* c, unsigned long long seq, int word) {
     const auto t0 = std::chrono::steady_clock::now();
+    double next_query = kQueryAfterS;
     hipStream_t st = word == 1 ? c->st2 : c->st;  // word 1: the side stream's sequence
     for (uint64_t spin = 1;; ++spin) {
         if (__atomic_load_n(c->h_flag + word, __ATOMIC_ACQUIRE) >= seq) return VAMPOMI_OK;
         if ((spin & 4095) == 0) {
-            const hipError_t e = hipStreamQuery(st);
-            if (e != hipSuccess && e != hipErrorNotReady)
-                return fail(VAMPOMI_ERR_HIP, std::string("stream failed: ") + hipGetErrorString(e));
-            if (e == hipSuccess) {  // finished, flag not seen yet: complete through the runtime
-                HIPCHK(hipStreamSynchronize(st));
-                return VAMPOMI_OK;
+            const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+            if (el >= next_query) {
+                next_query = el + kQueryEveryS;
+                const hipError_t e = hipStreamQuery(st);
+                if (e != hipSuccess && e != hipErrorNotReady)
+                    return fail(VAMPOMI_ERR_HIP, std::string("stream failed: ") + hipGetErrorString(e));
+                if (e == hipSuccess) {  // finished, flag not seen yet: complete through the runtime
+                    if (__atomic_load_n(c->h_flag + word, __ATOMIC_ACQUIRE) >= seq) return VAMPOMI_OK;
+                    HIPCHK(hipStreamSynchronize(st));
+                    return VAMPOMI_OK;
+                }
             }
             if (const char* why = job_broken(c, t0)) return job_failed(c, why);
         }
@@ -792,16 +807,6 @@ vampomi_status op_prepare(vampomi_ctx* c, bool collective) {
                 c->op_xg_words = words;
             }
         }
-        // dynamic chunks: claim counter, finish ticket and chunk rings (zero, re-armed by each launch)
-        const int64_t dw = std::max(vk::team_dyn_words(c->opp), c->hs_ok ? vk::team_dyn_words(c->opp_hs) : 0);
-        if (dw > c->op_dyn_words) {
-            if (c->op_dyn) (void)hipFree(c->op_dyn);
-            c->op_dyn = nullptr;
-            c->op_dyn_words = 0;
-            HIPCHK(hipMalloc((void**)&c->op_dyn, (size_t)dw * 8));
-            HIPCHK(hipMemsetAsync(c->op_dyn, 0, (size_t)dw * 8, c->st));
-            c->op_dyn_words = dw;
-        }
     }
     c->op_ready = true;
     return VAMPOMI_OK;
@@ -919,7 +924,6 @@ vampomi_status op_dev(vampomi_ctx* c, int K, const vk::OpArgs& a, const int* gat
     x.scale = 1.0 / c->sqrtN;
     if (c->opp.T > 1) {
         x.xg = c->op_xg;
-        x.dyn = c->op_dyn;
         if (++c->op_tag == 0) ++c->op_tag;
         x.tag = c->op_tag;
         x.err = op_err_dev(c);
@@ -959,7 +963,6 @@ vampomi_status op_dev_plain(vampomi_ctx* c, const vk::OpArgs& a, const double* c
     for (int k = 0; k < vk::kOpPlain; ++k) x.px.p[k] = px[k];
     if (c->opp_hs.T > 1) {
         x.xg = c->op_xg;
-        x.dyn = c->op_dyn;
         if (++c->op_tag == 0) ++c->op_tag;
         x.tag = c->op_tag;
         x.err = op_err_dev(c);
@@ -1046,9 +1049,6 @@ void release_ctx_resources(vampomi_ctx* c) {
     c->op_xg = nullptr;
     if (c->op_ts) (void)hipFree(c->op_ts);
     c->op_ts = nullptr;
-    if (c->op_dyn) (void)hipFree(c->op_dyn);
-    c->op_dyn = nullptr;
-    c->op_dyn_words = 0;
     c->op_xg_words = 0;
     c->op_part_slots = 0;
     c->op_ready = false;
@@ -1770,7 +1770,6 @@ extern "C" vampomi_status vampomi_dev_time_pass(vampomi_ctx* c, int which, int K
             x.ro = vk::RedOut{c->red_part, c->scal + SL_DP, c->ticket, nullptr, 0, nullptr};
             if (c->opp.T > 1) {
                 x.xg = c->op_xg;
-                x.dyn = c->op_dyn;
                 if (++c->op_tag == 0) ++c->op_tag;
                 x.tag = c->op_tag;
                 x.err = op_err_dev(c);
@@ -1905,8 +1904,6 @@ extern "C" vampomi_status vampomi_dev_mem_plan(int64_t N, int64_t Mt, int nranks
         size_t w = op.T > 1 ? op_xg_words_for(Mx, op) : 0;
         if (h && hs.T > 1) w = std::max(w, op_xg_words_for(Mx, hs));
         if (w) add((int64_t)w, 8);
-        const int64_t dw = std::max(vk::team_dyn_words(op), h ? vk::team_dyn_words(hs) : 0);
-        if (dw) add(dw, 8);
     }
     for (int q = 0; q < 25; ++q) add(Mx, 8);           // VampRun M-vectors (15 + cgw[10])
     add(ld, 8), add((int64_t)vk::kMaxRhs * ld, 8), add((int64_t)vk::kMaxRhs * ld, 8), add(ld, 8);

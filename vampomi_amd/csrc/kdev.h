@@ -60,8 +60,10 @@ __device__ __forceinline__ void ticket_sum_blocks(const RedOut& ro) {
 // it (read by the caller in one burst); it is written back once (a chain of
 // dependent device loads and stores otherwise: this runs at the end of every
 // CG step).
+// pack: *flag receives the decision as one word (cg_pack), no mirror.
 __device__ inline void cg_decide_from(CgState s, CgState* cs, const double* red, int it, CgMirror* mirror,
-                                      unsigned long long* flag, unsigned long long seq, int mask) {
+                                      unsigned long long* flag, unsigned long long seq, int mask, int pack = 0) {
+    const bool ran = s.any != 0;  // a step queued after the solve stopped decides (and publishes) nothing
     if (s.any) {
         int any = 0;
 #pragma unroll
@@ -102,6 +104,12 @@ __device__ inline void cg_decide_from(CgState s, CgState* cs, const double* red,
         s.any = any;
         *cs = s;
     }
+    if (pack) {  // one word, one system-scope store: nothing to order
+        if (flag && ran)
+            __hip_atomic_store(flag, cg_pack(seq, s.any, s.iters[0], s.iters[1]), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+        return;
+    }
     // the mirror (mapped host memory) written through and drained, then the
     // flag: the host reads the mirror after the flag (no release fence, which
     // would write back this XCD's whole L2 first)
@@ -120,12 +128,12 @@ __device__ inline void cg_decide_from(CgState s, CgState* cs, const double* red,
 }
 
 __device__ inline void cg_decide_body(CgState* cs, const double* red, int it, CgMirror* mirror, unsigned long long* flag,
-                                      unsigned long long seq, int mask) {
+                                      unsigned long long seq, int mask, int pack = 0) {
     const CgState s = *cs;
     double r[3 * kMaxRhs];
 #pragma unroll
     for (int q = 0; q < 3 * kMaxRhs; ++q) r[q] = q < 3 * s.K ? red[q] : 0.0;
-    cg_decide_from(s, cs, r, it, mirror, flag, seq, mask);
+    cg_decide_from(s, cs, r, it, mirror, flag, seq, mask, pack);
 }
 
 }  // namespace vk

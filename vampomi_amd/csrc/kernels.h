@@ -151,9 +151,6 @@ struct OpArgs {
     unsigned tag;
     unsigned* err;
     unsigned long long* ts;  // experiment builds (TM_TS=1) only: per workgroup {start, end, XCC id, HW id}
-    // team kernels with dynamic chunks: the claim counter, finish ticket and
-    // chunk rings (team_dyn_words of the plan; zeroed once, re-armed by each launch)
-    unsigned long long* dyn;
     int dbg;  // timing experiments only (VAMPOMI_OP_DBG; results are wrong when set, except bit 5):
               // bit 0 no poll waits, 1 no publishes, 2 no butterfly, 3 no A d accumulation,
               // 5 write-through hand-off even when the team shares an XCD
@@ -164,8 +161,6 @@ std::string team_kernel_name(int K, const OpPlan& pl);
 // CU holds at once (0: it cannot run); a plan needs grid <= this x CUs, since
 // a team launch needs all its workgroups resident together
 int team_occupancy(const OpPlan& pl, int K);
-// words of OpArgs.dyn a launch of plan pl needs (0: a static plan)
-int64_t team_dyn_words(const OpPlan& pl);
 hipError_t atax(const Shard& s, const OpPlan& pl, int K, const OpArgs& a, hipStream_t st, const Timing& tm = Timing{},
                 const int* gate = nullptr);
 hipError_t atax_team(const Shard& s, const OpPlan& pl, int K, const OpArgs& a, hipStream_t st, const Timing& tm,
@@ -363,6 +358,16 @@ struct CgState {
     int active[kMaxRhs], iters[kMaxRhs], onsager[kMaxRhs], off[kMaxRhs];
     int K, any, maxit;
 };
+// A step's decision in ONE 64-bit word (the one-pass CG: K <= 2 systems,
+// iteration counts below 2^15): the step's sequence number in the high half
+// (so the word grows with it), any in bit 30, iters[1] in bits 15-29 and
+// iters[0] in bits 0-14.  One system-scope store publishes it whole: no
+// mirror, no ordering wait.
+constexpr int kCgPackMaxIter = (1 << 15) - 2;
+__host__ __device__ inline unsigned long long cg_pack(unsigned long long seq, int any, int it0, int it1) {
+    return (seq << 32) | ((unsigned long long)(any ? 1 : 0) << 30) | ((unsigned long long)(it1 & 0x7fff) << 15) |
+           (unsigned long long)(it0 & 0x7fff);
+}
 struct CgMirror {
     unsigned long long seq;  // the step's flag value: the slot holds that step's decision
     int any;
@@ -379,6 +384,9 @@ hipError_t cg_start_from(const CgState& init, const double* sums, CgState* dst, 
 // rank: the sums are final): the last block also takes cg_decide's decisions.
 struct CgDecide {
     int on = 0, it = 0;
+    // pack: *flag receives the decision as ONE word (cg_pack) instead of the
+    // mirror slot + sequence number
+    int pack = 0;
     int mask = 0xf;  // the systems this step is for (the others keep their state; see cg_update)
     CgMirror* mirror = nullptr;
     unsigned long long* flag = nullptr;
@@ -395,6 +403,6 @@ hipError_t cg_update(int K, int64_t M, const CgVecs& c, double diag, CgState* cs
 // src/vamp.cpp:700-750, for the systems in mask; then mirror and flag (each
 // stored when non-null, even when gated off)
 hipError_t cg_decide(CgState* cs, const double* red, int it, CgMirror* mirror, unsigned long long* flag,
-                     unsigned long long seq, hipStream_t st, int mask = 0xf);
+                     unsigned long long seq, hipStream_t st, int mask = 0xf, int pack = 0);
 
 }  // namespace vk

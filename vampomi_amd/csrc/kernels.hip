@@ -766,12 +766,12 @@ bool op_plan(int64_t N, int64_t M, int cus, int variant, OpPlan* out) {
     }
     if (variant == kOpDefault) {
         // just past one workgroup's rows (9,216 < N <= 10,752, C2 among them): a
-        // team of 2 with six loads per lane (configuration 12: F = 2, L = 3,
+        // team of 2 with six loads per lane (configuration 5, round 3's 12: F = 2, L = 3,
         // 253 VGPRs) beats the team of 4 (C2: 589.7-590.2 against 594.5-595.8 us
         // per launch in VAMP, 192.0-192.3 against 191.0-191.3 it/s, three rounds
         // on one box, profiles/r03pl_c2_plans.txt)
         OpPlan p{};
-        if (team_plan(N, M, cus, 2, 12, &p)) {
+        if (team_plan(N, M, cus, 2, 5, &p)) {
             *out = p;
             return true;
         }
@@ -788,7 +788,7 @@ bool op_plan(int64_t N, int64_t M, int cus, int variant, OpPlan* out) {
     }
     if (variant >= 1000) return team_plan(N, M, cus, (variant - 1000) / 100, variant % 100, out);  // 1000 + T*100 + cfg
     if (variant > 0) return team_plan(N, M, cus, variant / 10, variant % 10, out);
-    for (int cfg : {7, 9}) {  // then fewer columns in flight for one more load per lane (S <= 5)
+    for (int cfg : {2, 4}) {  // then fewer columns in flight for one more load per lane (S <= 5)
         for (int T = 2; T <= 32; T *= 2) {
             OpPlan p{};
             if (!team_plan(N, M, cus, T, cfg, &p)) continue;
@@ -1050,13 +1050,22 @@ hipError_t atax(const Shard& s, const OpPlan& pl, int K, const OpArgs& a, hipStr
 
 // The per-slot A d partials summed over the slots: a workgroup takes 128
 // samples of one system (two per lane, 16-byte loads); wave w sums the slots
-// [w*ns/4, (w+1)*ns/4) in order with eight loads in flight, wave 0 adds the
-// four wave sums in order.  cg_update's one-rank form (cg_update_kernel,
+// [w*ns/4, (w+1)*ns/4) in order with up to 32 loads in flight, wave 0 adds
+// the four wave sums in order.  cg_update's one-rank form (cg_update_kernel,
 // c.adpart) sums in exactly this order, so the two paths agree bit for bit.
+// (Every load of a round is issued before the first add: the adds stay in
+// slot order, so the round size changes the latency, not the bits.)
 __device__ __forceinline__ v2d slot_sum(const double* src, int64_t ss, int t0, int t1) {
     v2d acc = {0.0, 0.0};
     int t = t0;
-    for (; t + 16 <= t1; t += 16) {  // (C2: 16 slots per wave, one round trip)
+    for (; t + 32 <= t1; t += 32) {  // (C2, team of 2: 128 slots, 32 per wave, one round trip)
+        v2d x[32];
+#pragma unroll
+        for (int u = 0; u < 32; ++u) x[u] = *reinterpret_cast<const v2d*>(src + (t + u) * ss);
+#pragma unroll
+        for (int u = 0; u < 32; ++u) acc += x[u];
+    }
+    for (; t + 16 <= t1; t += 16) {
         v2d x[16];
 #pragma unroll
         for (int u = 0; u < 16; ++u) x[u] = *reinterpret_cast<const v2d*>(src + (t + u) * ss);
@@ -1542,23 +1551,28 @@ hipError_t cg_start_from(const CgState& init, const double* sums, CgState* dst, 
 }
 
 __global__ void cg_decide_kernel(CgState* cs, const double* __restrict__ red, int it, CgMirror* mirror,
-                                 unsigned long long* flag, unsigned long long seq, int mask) {
-    if (threadIdx.x == 0) cg_decide_body(cs, red, it, mirror, flag, seq, mask);
+                                 unsigned long long* flag, unsigned long long seq, int mask, int pack) {
+    if (threadIdx.x == 0) cg_decide_body(cs, red, it, mirror, flag, seq, mask, pack);
 }
 
 // Latency, not bytes, sets this kernel's time at C2 (~25 MB in ~16 us): a
 // chain of dependent memory round trips.  So every scalar comes in one burst
 // (the whole CgState: the deciding block needs no further state load), both
 // M-elements of a thread and a tile's N-vectors are loaded before the
-// dependent work, and the decision takes its sums from LDS.
-__global__ __launch_bounds__(kBlock) void cg_update_kernel(int K, int64_t M, CgVecs c, double diag,
+// dependent work, and the decision takes its sums from LDS.  One
+// instantiation per system count K: the unrolled per-system loops then carry
+// K systems, not kMaxRhs (at K = 2: a quarter of the live registers, no
+// spills, and only the K systems' vector pointers loaded from the arguments);
+// every per-element operation and every sum is the same, in the same order.
+template <int K>
+__global__ __launch_bounds__(kBlock) void cg_update_kernel(int64_t M, CgVecs c, double diag,
                                                            CgState* cs, const double* __restrict__ dp_dev,
                                                            const double* __restrict__ pp_dev, int fuse, RedOut ro,
                                                            CgDecide dc, int mblocks) {
     const CgState st = *cs;
-    double dpv[kMaxRhs], ppv[kMaxRhs];
+    double dpv[K], ppv[K];
 #pragma unroll
-    for (int k = 0; k < kMaxRhs; ++k) {
+    for (int k = 0; k < K; ++k) {
         dpv[k] = dp_dev[k];
         ppv[k] = pp_dev ? pp_dev[k] : 0.0;
     }
@@ -1568,21 +1582,21 @@ __global__ __launch_bounds__(kBlock) void cg_update_kernel(int K, int64_t M, CgV
     // blocks [0, mblocks) stream the M-vectors; with c.adpart the blocks past
     // them sum the operator's A d partials and update the N-vectors
     const bool mpart = (int)blockIdx.x < mblocks;
-    double alpha[kMaxRhs];
-    bool on[kMaxRhs];
+    double alpha[K];
+    bool on[K];
 #pragma unroll
-    for (int k = 0; k < kMaxRhs; ++k) {
-        on[k] = k < K && st.active[k] && ((dc.mask >> k) & 1);
+    for (int k = 0; k < K; ++k) {
+        on[k] = st.active[k] && ((dc.mask >> k) & 1);
         const double dp = pp_dev ? c.tau * dpv[k] + c.gam2 * ppv[k] : dpv[k];  // <d,p>
         alpha[k] = on[k] ? st.rz[k] / dp : 0.0;  // :702
     }
-    double acc[3 * kMaxRhs];
+    double acc[3 * K];
 #pragma unroll
-    for (int q = 0; q < 3 * kMaxRhs; ++q) acc[q] = 0.0;
-    double beta[kMaxRhs];
-    bool fk[kMaxRhs];  // system k's direction update p = z + beta p rides in this step
+    for (int q = 0; q < 3 * K; ++q) acc[q] = 0.0;
+    double beta[K];
+    bool fk[K];  // system k's direction update p = z + beta p rides in this step
 #pragma unroll
-    for (int k = 0; k < kMaxRhs; ++k) {
+    for (int k = 0; k < K; ++k) {
         fk[k] = on[k] && ((fuse >> k) & 1);
         beta[k] = fk[k] ? st.beta[k] : 0.0;
     }
@@ -1592,15 +1606,14 @@ __global__ __launch_bounds__(kBlock) void cg_update_kernel(int K, int64_t M, CgV
     // in order, as one element per round would
     const int64_t mstride = (int64_t)mblocks * kBlock;
     for (int64_t i0 = (int64_t)blockIdx.x * kBlock + threadIdx.x; mpart && i0 < M; i0 += 2 * mstride) {
-        double pv[2][kMaxRhs], zv[2][kMaxRhs], muv[2][kMaxRhs], rv[2][kMaxRhs], dv[2][kMaxRhs], vv[2][kMaxRhs],
-            wv[2][kMaxRhs], sv[2][kMaxRhs];
+        double pv[2][K], zv[2][K], muv[2][K], rv[2][K], dv[2][K], vv[2][K], wv[2][K], sv[2][K];
         const bool two = i0 + mstride < M;
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const int64_t i = i0 + h * mstride;
             if (h == 1 && !two) break;
 #pragma unroll
-            for (int k = 0; k < kMaxRhs; ++k) {
+            for (int k = 0; k < K; ++k) {
                 if (on[k]) {
                     pv[h][k] = c.p[k][i];
                     zv[h][k] = fk[k] ? c.z[k][i] : 0.0;
@@ -1618,7 +1631,7 @@ __global__ __launch_bounds__(kBlock) void cg_update_kernel(int K, int64_t M, CgV
             const int64_t i = i0 + h * mstride;
             if (h == 1 && !two) break;
 #pragma unroll
-            for (int k = 0; k < kMaxRhs; ++k) {
+            for (int k = 0; k < K; ++k) {
                 if (on[k]) {
                     double pi = pv[h][k];
                     if (fk[k]) {  // p = z + beta p (:738-739)
@@ -1654,7 +1667,7 @@ __global__ __launch_bounds__(kBlock) void cg_update_kernel(int K, int64_t M, CgV
             bool onk = false, fuk = false;  // on[k], fk[k], alpha[k], beta[k] without indexing registers at run time
             double alk = 0.0, bek = 0.0;
 #pragma unroll
-            for (int kk = 0; kk < kOpMaxK; ++kk)
+            for (int kk = 0; kk < (K < kOpMaxK ? K : kOpMaxK); ++kk)
                 if (kk == k) {
                     onk = on[kk];
                     fuk = fk[kk];
@@ -1691,9 +1704,9 @@ __global__ __launch_bounds__(kBlock) void cg_update_kernel(int K, int64_t M, CgV
         }
     } else if (c.Q[0]) {  // one-pass operator: q (the step's A p) from A r, then A r -= A d * alpha
         for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < c.nA; i += (int64_t)gridDim.x * kBlock) {
-            double ar[kMaxRhs], qo[kMaxRhs], ad[kMaxRhs], aw[kMaxRhs];
+            double ar[K], qo[K], ad[K], aw[K];
 #pragma unroll
-            for (int k = 0; k < kMaxRhs; ++k)
+            for (int k = 0; k < K; ++k)
                 if (on[k]) {
                     ar[k] = c.AR[k][i];
                     qo[k] = fk[k] ? c.Q[k][i] : 0.0;
@@ -1701,7 +1714,7 @@ __global__ __launch_bounds__(kBlock) void cg_update_kernel(int K, int64_t M, CgV
                     aw[k] = c.AW[k] ? c.AW[k][i] : 0.0;
                 }
 #pragma unroll
-            for (int k = 0; k < kMaxRhs; ++k)
+            for (int k = 0; k < K; ++k)
                 if (on[k]) {
                     double q = ar[k] / diag;  // A z = A r / diag
                     if (fk[k]) q = q + beta[k] * qo[k];  // A p = A z + beta A p
@@ -1712,25 +1725,25 @@ __global__ __launch_bounds__(kBlock) void cg_update_kernel(int K, int64_t M, CgV
         }
     } else
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < c.nA; i += (int64_t)gridDim.x * kBlock) {
-        double aw[kMaxRhs], as[kMaxRhs];
+        double aw[K], as[K];
 #pragma unroll
-        for (int k = 0; k < kMaxRhs; ++k)
+        for (int k = 0; k < K; ++k)
             if (on[k] && c.AW[k]) {
                 aw[k] = c.AW[k][i];
                 as[k] = c.AS[k][i];
             }
 #pragma unroll
-        for (int k = 0; k < kMaxRhs; ++k)
+        for (int k = 0; k < K; ++k)
             if (on[k] && c.AW[k]) c.AW[k][i] = aw[k] + alpha[k] * as[k];
     }
-    block_put_sums<3 * kMaxRhs>(acc, 3 * K, ro, (int64_t)blockIdx.x * 3 * K);
+    block_put_sums<3 * K>(acc, 3 * K, ro, (int64_t)blockIdx.x * 3 * K);
     // one rank: the last block decides the step itself (its sums are final),
     // from the state read at the start (only this decision writes it)
     if (red_finish(ro, 3 * K, lds, fin) && dc.on && threadIdx.x == 0) {
         double r[3 * kMaxRhs];
 #pragma unroll
         for (int q = 0; q < 3 * kMaxRhs; ++q) r[q] = q < 3 * K ? fin[q] : 0.0;
-        cg_decide_from(st, cs, r, dc.it, dc.mirror, dc.flag, dc.seq, dc.mask);
+        cg_decide_from(st, cs, r, dc.it, dc.mirror, dc.flag, dc.seq, dc.mask, dc.pack);
     }
 }
 
@@ -1745,14 +1758,23 @@ hipError_t cg_update(int K, int64_t M, const CgVecs& c, double diag, CgState* cs
         nb = (int)std::min<int64_t>(K * cdiv(c.nA, 128), kRedBlocks - mb);
         nb = std::max(nb, 1);
     }
-    hipLaunchKernelGGL(cg_update_kernel, dim3(mb + nb), dim3(kBlock), 0, st, K, M, c, diag, cs, dp_dev, pp_dev,
-                       fuse, ro, dc, mb);
+    switch (K) {
+        case 1: hipLaunchKernelGGL(cg_update_kernel<1>, dim3(mb + nb), dim3(kBlock), 0, st, M, c, diag, cs, dp_dev,
+                                   pp_dev, fuse, ro, dc, mb); break;
+        case 2: hipLaunchKernelGGL(cg_update_kernel<2>, dim3(mb + nb), dim3(kBlock), 0, st, M, c, diag, cs, dp_dev,
+                                   pp_dev, fuse, ro, dc, mb); break;
+        case 3: hipLaunchKernelGGL(cg_update_kernel<3>, dim3(mb + nb), dim3(kBlock), 0, st, M, c, diag, cs, dp_dev,
+                                   pp_dev, fuse, ro, dc, mb); break;
+        case 4: hipLaunchKernelGGL(cg_update_kernel<4>, dim3(mb + nb), dim3(kBlock), 0, st, M, c, diag, cs, dp_dev,
+                                   pp_dev, fuse, ro, dc, mb); break;
+        default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 
 hipError_t cg_decide(CgState* cs, const double* red, int it, CgMirror* mirror, unsigned long long* flag,
-                     unsigned long long seq, hipStream_t st, int mask) {
-    hipLaunchKernelGGL(cg_decide_kernel, dim3(1), dim3(64), 0, st, cs, red, it, mirror, flag, seq, mask);
+                     unsigned long long seq, hipStream_t st, int mask, int pack) {
+    hipLaunchKernelGGL(cg_decide_kernel, dim3(1), dim3(64), 0, st, cs, red, it, mirror, flag, seq, mask, pack);
     return hipGetLastError();
 }
 

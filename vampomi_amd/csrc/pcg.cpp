@@ -30,13 +30,26 @@ static T* field(vk::CgState* cs, size_t off) {
     return reinterpret_cast<T*>(reinterpret_cast<char*>(cs) + off);
 }
 
+// The outcome of a decided CG step as the host reads it.
+struct CgOutcome {
+    int any = 0;
+    int iters[vk::kMaxRhs] = {};
+};
+
+// Flag words (of the context's mapped block) of the packed decisions: step i
+// is published into word kCgPackWord + (i & 1), so step i+1's (queued before
+// the host reads step i's) never overwrites the one the host is waiting for.
+static constexpr int kCgPackWord = 2;
+
 // the host loop shared by both forms: queue step i+1, then wait for step i's
-// decision; a step queued after the last system stopped is dropped from the stats
-// Step i-1's decision is read from its own mirror slot ((i-1) & 1), tagged
-// with its flag value: step i, queued before the wait, writes the other slot.
-// *last: the slot of the last decided step (its iteration counts are final).
+// decision; a step queued after the last system stopped is dropped from the stats.
+// packed (the one-pass form, K <= 2): step i-1's decision is ONE word
+// (vk::cg_pack) in flag word kCgPackWord + ((i-1) & 1); else it is read from
+// its own mirror slot ((i-1) & 1), tagged with its flag value.  Either way
+// step i, queued before the wait, writes the other one.  *last: the last decided step's outcome
+// (its iteration counts are final).
 template <class Enqueue>
-static vampomi_status cg_loop(vampomi_ctx* c, int max_iter, Enqueue&& enqueue, const vk::CgMirror** last) {
+static vampomi_status cg_loop(vampomi_ctx* c, int max_iter, bool packed, Enqueue&& enqueue, CgOutcome* last) {
     unsigned long long prev = 0, cur = 0;
     STCHK(enqueue(0, &prev));
     for (int i = 1;; ++i) {
@@ -44,14 +57,30 @@ static vampomi_status cg_loop(vampomi_ctx* c, int max_iter, Enqueue&& enqueue, c
         const vampomi_stats before = c->stats;
         if (i < max_iter) STCHK(enqueue(i, &cur));
         c->stats.host_syncs++;
-        STCHK(wait_flag(c, prev));  // step i-1 decided
-        STCHK(op_check_err(c));     // (its decision is void if its operator launch timed out)
-        const vk::CgMirror* m = c->h_cgm + ((i - 1) & 1);
-        if (__atomic_load_n(&m->seq, __ATOMIC_ACQUIRE) != prev)
-            return fail(VAMPOMI_ERR_STATE, "CG step " + std::to_string(i - 1) + ": decision slot holds sequence " +
-                                               std::to_string(m->seq) + ", expected " + std::to_string(prev));
-        *last = m;
-        if (!m->any || i >= max_iter) {
+        CgOutcome o;
+        if (packed) {
+            const int word = kCgPackWord + ((i - 1) & 1);
+            STCHK(wait_flag(c, prev << 32, word));  // step i-1 decided and published
+            STCHK(op_check_err(c));                 // (its decision is void if its operator launch timed out)
+            const unsigned long long w = __atomic_load_n(c->h_flag + word, __ATOMIC_ACQUIRE);
+            if ((w >> 32) != (prev & 0xffffffffULL))
+                return fail(VAMPOMI_ERR_STATE, "CG step " + std::to_string(i - 1) + ": decision word holds sequence " +
+                                                   std::to_string(w >> 32) + ", expected " + std::to_string(prev));
+            o.any = (int)((w >> 30) & 1);
+            o.iters[0] = (int)(w & 0x7fff);
+            o.iters[1] = (int)((w >> 15) & 0x7fff);
+        } else {
+            STCHK(wait_flag(c, prev));  // step i-1 decided
+            STCHK(op_check_err(c));     // (its decision is void if its operator launch timed out)
+            const vk::CgMirror* m = c->h_cgm + ((i - 1) & 1);
+            if (__atomic_load_n(&m->seq, __ATOMIC_ACQUIRE) != prev)
+                return fail(VAMPOMI_ERR_STATE, "CG step " + std::to_string(i - 1) + ": decision slot holds sequence " +
+                                                   std::to_string(m->seq) + ", expected " + std::to_string(prev));
+            o.any = m->any;
+            for (int k = 0; k < vk::kMaxRhs; ++k) o.iters[k] = m->iters[k];
+        }
+        *last = o;
+        if (!o.any || i >= max_iter) {
             if (i < max_iter) drop_launches(c, mark, before);  // step i was queued in vain: it did nothing
             break;
         }
@@ -271,6 +300,9 @@ vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double
             }
             hs->used = true;
         }
+        // the decisions travel as one packed word each (cg_loop): one
+        // system-scope store instead of the mirror's six, a drain and the flag
+        const bool packed = K <= 2 && max_iter < vk::kCgPackMaxIter;
         auto enqueue = [&](int i, unsigned long long* seq) -> vampomi_status {
             // the direction updates fused into step i: every system's from step
             // 1 on; at step 0 those of the systems already under way (head start)
@@ -293,26 +325,29 @@ vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double
             const double* dp = c->use_comm ? AD + (int64_t)K * c->ld : c->scal + SL_DP;
             const vk::RedOut ro{c->red_part, c->scal + SL_CG, c->ticket, nullptr, 0, gate};
             *seq = ++c->sync_seq;
+            unsigned long long* flag = packed ? c->d_flag + kCgPackWord + (i & 1) : c->d_flag;
+            vk::CgMirror* mirror = packed ? nullptr : c->d_cgm;
             vk::CgDecide dc{};
             if (!c->use_comm) {
                 dc.on = 1;
                 dc.it = i;
-                dc.mirror = c->d_cgm;
-                dc.flag = c->d_flag;
+                dc.mirror = mirror;
+                dc.flag = flag;
                 dc.seq = *seq;
+                dc.pack = packed ? 1 : 0;
             }
             HIPCHK(vk::cg_update(K, M, cu, diag, c->cgs, dp, nullptr, fuse, ro, dc, c->st));
             if (c->use_comm) {
                 STCHK(allreduce_dev(c, c->scal + SL_CG, (size_t)(3 * K)));
-                HIPCHK(vk::cg_decide(c->cgs, c->scal + SL_CG, i, c->d_cgm, c->d_flag, *seq, c->st));
+                HIPCHK(vk::cg_decide(c->cgs, c->scal + SL_CG, i, mirror, flag, *seq, c->st, 0xf, packed ? 1 : 0));
             }
             return VAMPOMI_OK;
         };
-        const vk::CgMirror* last = nullptr;
-        STCHK(cg_loop(c, max_iter, enqueue, &last));
+        CgOutcome last;
+        STCHK(cg_loop(c, max_iter, packed, enqueue, &last));
         STCHK(op_check_err(c));
         for (int k = 0; k < K; ++k) {
-            sys[k]->iters = last->iters[k];
+            sys[k]->iters = last.iters[k];
             if (ref_passes) *ref_passes += 2 * (int64_t)sys[k]->iters;
         }
         return VAMPOMI_OK;
@@ -419,10 +454,10 @@ vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double
         }
         return VAMPOMI_OK;
     };
-    const vk::CgMirror* last = nullptr;
-    STCHK(cg_loop(c, max_iter, enqueue, &last));
+    CgOutcome last;
+    STCHK(cg_loop(c, max_iter, false, enqueue, &last));
     for (int k = 0; k < K; ++k) {
-        sys[k]->iters = last->iters[k];
+        sys[k]->iters = last.iters[k];
         if (ref_passes) *ref_passes += 2 * (int64_t)sys[k]->iters;
     }
     return VAMPOMI_OK;
