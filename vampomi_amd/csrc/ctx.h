@@ -287,15 +287,18 @@ struct CgSystem {
 // hs->axnext = A xnext (the next solve's abern).  Without hs->abern the first
 // A.x pass carries xnext instead.
 struct HeadStart {
-    const double* abern = nullptr;
+    double* abern = nullptr;  // (the Onsager solve's A r: updated in place)
     const double* xnext = nullptr;
     double* axnext = nullptr;
     bool used = false;  // out: the head start ran
 };
+// pre (may be null; init must be null): the caller's prelude launch, fused
+// with the solve's start (vk::prelude_cg_init)
 vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double tau, double gam2, int max_iter,
                        double tol, double* nscratch, int64_t* ref_passes, DotBatch* init,
                        const double* extra_x = nullptr, double* ex_out = nullptr, bool onepass = false,
-                       const double* const* ar0 = nullptr, HeadStart* hs = nullptr);
+                       const double* const* ar0 = nullptr, HeadStart* hs = nullptr,
+                       const vk::Prelude* pre = nullptr);
 // plans the one-pass operator (c->opp, c->op_ok, c->hs_ok) and allocates its
 // buffers (idempotent until the plan or the head-start switch changes).
 // COLLECTIVE when collective (several ranks): the ranks agree on op_ok and

@@ -1907,7 +1907,7 @@ extern "C" vampomi_status vampomi_dev_mem_plan(int64_t N, int64_t Mt, int nranks
     }
     for (int q = 0; q < 25; ++q) add(Mx, 8);           // VampRun M-vectors (15 + cgw[10])
     add(ld, 8), add((int64_t)vk::kMaxRhs * ld, 8), add((int64_t)vk::kMaxRhs * ld, 8), add(ld, 8);
-    add(ld, 8);                                        // abern (the head start)
+    add(2 * ld, 8);                                    // abern (the head start, two slots)
     if (probit) {
         for (int q = 0; q < 3; ++q) add(ld, 8);
         for (int q = 0; q < 3; ++q) add(Mx, 8);

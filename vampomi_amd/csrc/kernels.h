@@ -225,6 +225,13 @@ struct EmArgs {
     double v[kMaxL];
     double lambda, noise_var, gam1, max_sigma;
     int L;
+    // r1out (may be null): the round also forms r1 = (la*lx - lb*ly)/lc (the
+    // lincomb_div of src/vamp.cpp:348-350, bit for bit) and stores it, instead
+    // of reading r1: one launch where there were two
+    const double* lx;
+    const double* ly;
+    double la, lb, lc;
+    double* r1out;
 };
 // ro.out[q], Q = 1 + 2(L-1): q=0 sum pin; q=j (1..L-1) sum beta_j pin;
 // q=L-1+j sum beta_j (g_j^2 + v_j) pin
@@ -378,6 +385,12 @@ constexpr int kCgMirrorSlots = 2;
 hipError_t cg_start(const CgState& init, CgState* dst, hipStream_t st);
 // *dst = init with rz[k], vv[k] = sums[2k], sums[2k+1] (cg_init's sums, in device memory)
 hipError_t cg_start_from(const CgState& init, const double* sums, CgState* dst, hipStream_t st);
+// prelude() and cg_init() in one launch (cg_init's grid and sums: bitwise the
+// two launches), where cg_init's v_k may be the prelude's v or bern (taken from
+// registers).  start (may be null): the last block also writes *dst = *start
+// with rz[k], vv[k] from the sums (cg_start_from; one rank, the sums final)
+hipError_t prelude_cg_init(int K, int64_t M, const Prelude& p, const CgVecs& c, double diag, const RedOut& ro,
+                           const CgState* start, CgState* dst, hipStream_t st);
 // for active k: [fuse: p = z + beta_k p, stored] alpha_k = rz[k] / dp_dev[k];
 // mu += alpha p; r -= d alpha; z = r/diag; <r,z>, <r,r>, <v,mu> in ro.out (3K
 // values, k-major; zeros for stopped systems); gated on cs->any.  dc.on (one

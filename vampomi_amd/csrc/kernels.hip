@@ -1359,30 +1359,48 @@ __device__ __forceinline__ double em_num(const EmArgs& a, double r, int j) {
            sqrt(a.vars[j] + a.noise_var) / sqrt(2 * M_PI);
 }
 
+// The Q = 1 + 2(L-1) block sums: each wave reduces every value in registers
+// and leaves it in LDS, ONE barrier, then thread q adds the four wave sums in
+// wave order: per value the arithmetic of block_sum (bitwise), with one
+// barrier instead of 2Q.  a.r1out: r1 is formed here (lincomb_div's
+// expression) and stored, not read.
 __global__ __launch_bounds__(kBlock) void em_kernel(int64_t M, const double* __restrict__ r1, EmArgs a, RedOut ro) {
     __shared__ double lds[4];
+    __shared__ double wl[4][1 + 2 * (kMaxL - 1)];
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const bool valid = i < M;
-    const double r = valid ? r1[i] : 0.0;
+    double r = 0.0;
+    if (valid) {
+        if (a.r1out) {
+            r = (a.la * a.lx[i] - a.lb * a.ly[i]) / a.lc;  // lincomb_div_kernel's expression
+            a.r1out[i] = r;
+        } else {
+            r = r1[i];
+        }
+    }
     const int L = a.L, Q = 1 + 2 * (L - 1);
     double sum_of_elems = 0.0;
     for (int j = 1; j < L; ++j) sum_of_elems += em_num(a, r, j);
     const double pin = 1 / (1 + (1 - a.lambda) / sqrt(2 * M_PI * a.noise_var) *
                                     exp(-(r * r) / 2 * a.max_sigma / a.noise_var / (a.noise_var + a.max_sigma)) /
                                     sum_of_elems);
-    double s = block_sum(valid ? pin : 0.0, lds);
-    if (threadIdx.x == 0) red_put(ro, (int64_t)blockIdx.x * Q, s);
+    double s = wave_sum(valid ? pin : 0.0);
+    if (lane == 0) wl[w][0] = s;
     for (int j = 1; j < L; ++j) {
         const double beta = em_num(a, r, j) / sum_of_elems;
         const double g = a.gam1 * r / (1 / a.vars[j] + a.gam1);
         const double gam = beta * (g * g + a.v[j - 1]);
-        const double sb = block_sum(valid ? beta * pin : 0.0, lds);
-        const double sg = block_sum(valid ? gam * pin : 0.0, lds);
-        if (threadIdx.x == 0) {
-            red_put(ro, (int64_t)blockIdx.x * Q + j, sb);
-            red_put(ro, (int64_t)blockIdx.x * Q + (L - 1) + j, sg);
+        const double sb = wave_sum(valid ? beta * pin : 0.0);
+        const double sg = wave_sum(valid ? gam * pin : 0.0);
+        if (lane == 0) {
+            wl[w][j] = sb;
+            wl[w][(L - 1) + j] = sg;
         }
     }
+    __syncthreads();
+    for (int q = threadIdx.x; q < Q; q += kBlock)
+        red_put(ro, (int64_t)blockIdx.x * Q + q, ((wl[0][q] + wl[1][q]) + wl[2][q]) + wl[3][q]);
     red_finish(ro, Q, lds);
 }
 
@@ -1520,6 +1538,93 @@ __global__ __launch_bounds__(kBlock) void cg_init_kernel(int K, int64_t M, CgVec
     }
     block_put_sums<2 * kMaxRhs>(acc, 2 * K, ro, (int64_t)blockIdx.x * 2 * K);
     red_finish(ro, 2 * K, lds);
+}
+
+// prelude_kernel's and cg_init_kernel's work in one launch, on cg_init's grid
+// (the same sums, in the same order); v_k that the prelude forms (v, bern) is
+// used from registers.  Two elements per round (i, i + stride), all of both
+// elements' loads issued before either is used; the sums still run over i,
+// i + stride, ... in order.  start: the last block builds the CgState
+// (cg_start_from)
+__global__ __launch_bounds__(kBlock) void prelude_cg_init_kernel(int K, int64_t M, Prelude p, CgVecs c, double diag,
+                                                                 RedOut ro, CgState start, CgState* dst) {
+    __shared__ double lds[4];
+    __shared__ double fin[2 * kMaxRhs];
+    double acc[2 * kMaxRhs];
+#pragma unroll
+    for (int q = 0; q < 2 * kMaxRhs; ++q) acc[q] = 0.0;
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    for (int64_t i0 = (int64_t)blockIdx.x * kBlock + threadIdx.x; i0 < M; i0 += 2 * stride) {
+        const bool two = i0 + stride < M;
+        double x1v[2], r1v[2], ayv[2], vo[2][kMaxRhs], a0[2][kMaxRhs], muv[2][kMaxRhs], dd[2][kMaxRhs];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int64_t i = i0 + h * stride;
+            if (h == 1 && !two) break;
+            x1v[h] = p.x1[i];
+            r1v[h] = p.r1[i];
+            ayv[h] = p.atxy[i];
+#pragma unroll
+            for (int k = 0; k < kMaxRhs; ++k) {
+                if (k >= K) continue;
+                vo[h][k] = c.v[k] == p.v || c.v[k] == p.bern ? 0.0 : c.v[k][i];
+                a0[h][k] = c.atx0[k] ? c.atx0[k][i] : 0.0;
+                muv[h][k] = c.atx0[k] ? c.mu[k][i] : 0.0;
+                dd[h][k] = !c.atx0[k] && c.d[k] ? c.d[k][i] : 0.0;
+            }
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int64_t i = i0 + h * stride;
+            if (h == 1 && !two) break;
+            // prelude_kernel's expressions
+            const double r2 = (p.eta1 * x1v[h] - p.gam1 * r1v[h]) / p.gam2;  // lincomb_div's expression
+            p.r2[i] = r2;
+            const double vv = p.gamw * ayv[h] + p.gam2 * r2;                  // axpby's
+            p.v[i] = vv;
+            const double bn = (double)(2 * bern_bit(p.seed, p.it, p.S + i) - 1) / p.sqrtMt;
+            p.bern[i] = bn;
+            if (p.bern_next) p.bern_next[i] = (double)(2 * bern_bit(p.seed, p.it + 1, p.S + i) - 1) / p.sqrtMt;
+            if (p.zero[0]) p.zero[0][i] = 0.0;
+            if (p.zero[1]) p.zero[1][i] = 0.0;
+            // cg_init_kernel's
+#pragma unroll
+            for (int k = 0; k < kMaxRhs; ++k) {
+                if (k >= K) continue;
+                const double vi = c.v[k] == p.v ? vv : c.v[k] == p.bern ? bn : vo[h][k];
+                double r;
+                if (c.atx0[k]) {  // lmmse_mult(mu0) from a precomputed A^T(A mu0): res*=tau; res+=gam2*v
+                    double dv = a0[h][k];
+                    dv *= c.tau;
+                    dv += c.gam2 * muv[h][k];
+                    r = vi - dv;
+                } else {
+                    r = c.d[k] ? vi - dd[h][k] : vi - 0.0;  // r = v - lmmse_mult(mu0)
+                }
+                const double z = r / diag;
+                c.r[k][i] = r;
+                c.z[k][i] = z;
+                c.p[k][i] = z;
+                acc[2 * k] += r * z;
+                acc[2 * k + 1] += vi * vi;
+            }
+        }
+    }
+    block_put_sums<2 * kMaxRhs>(acc, 2 * K, ro, (int64_t)blockIdx.x * 2 * K);
+    if (red_finish(ro, 2 * K, lds, fin) && dst && threadIdx.x == 0) {
+        *dst = start;  // then its sums (indexed in place: no stack copy of the state)
+        for (int k = 0; k < K; ++k) {
+            dst->rz[k] = fin[2 * k];
+            dst->vv[k] = fin[2 * k + 1];
+        }
+    }
+}
+
+hipError_t prelude_cg_init(int K, int64_t M, const Prelude& p, const CgVecs& c, double diag, const RedOut& ro,
+                           const CgState* start, CgState* dst, hipStream_t st) {
+    hipLaunchKernelGGL(prelude_cg_init_kernel, dim3(red_blocks(M)), dim3(kBlock), 0, st, K, M, p, c, diag, ro,
+                       start ? *start : CgState{}, start ? dst : nullptr);
+    return hipGetLastError();
 }
 
 hipError_t cg_init(int K, int64_t M, const CgVecs& c, double diag, const RedOut& ro, hipStream_t st) {

@@ -91,7 +91,7 @@ static vampomi_status cg_loop(vampomi_ctx* c, int max_iter, bool packed, Enqueue
 
 vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double tau, double gam2, int max_iter,
                        double tol, double* nscratch, int64_t* ref_passes, DotBatch* init, const double* extra_x,
-                       double* ex_out, bool onepass, const double* const* ar0, HeadStart* hs) {
+                       double* ex_out, bool onepass, const double* const* ar0, HeadStart* hs, const vk::Prelude* pre) {
     const int64_t M = c->M, N = c->N;
     const double diag = tau * (double)(N - 1) / (double)N + gam2;  // :676-677
     const int K = (int)sys.size();
@@ -134,6 +134,8 @@ vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double
             STCHK(lmmse_dev(c, (int)nz.size(), vv, dd, tau, gam2, nscratch));
         }
     }
+    if (onepass && K <= vk::kOpMaxK && c->have_X) STCHK(op_prepare(c));
+    const bool op1 = onepass && K <= vk::kOpMaxK && c->have_X && c->op_ok;  // the one-pass form (below)
     vk::CgVecs cv{};
     cv.tau = tau;
     cv.gam2 = gam2;
@@ -147,7 +149,6 @@ vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double
         cv.atx0[k] = s->mu0_nonzero ? s->atx0 : nullptr;
         cv.d[k] = (s->mu0_nonzero && !s->atx0) ? s->d : nullptr;
     }
-    if (onepass && K <= vk::kOpMaxK && c->have_X) STCHK(op_prepare(c));
     // the head start (ctx.h, HeadStart): system 0's first step rides in the pass
     // that starts the solve; it is then one step ahead (CgState.off)
     const bool head = hs && hs->abern && c->hs_ok && c->op_ok && max_iter > 0;  // hs_ok: agreed, hs_on included
@@ -163,6 +164,7 @@ vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double
         s0.onsager[k] = sys[k]->onsager ? 1 : 0;
         sys[k]->iters = 0;
     }
+    if (pre && init) return fail(VAMPOMI_ERR_ARG, "pcg: the prelude rides only in the device-side start");
     if (init) {  // the caller's reductions resolve together with <r,z>, <v,v> (one host wait)
         std::vector<double> rzvv(2 * K);
         vk::RedOut ro{};
@@ -177,14 +179,20 @@ vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double
         HIPCHK(vk::cg_start(s0, c->cgs, c->st));
     } else {  // <r,z>, <v,v> stay on the device: the CgState is built there, no host wait
         const vk::RedOut ro{c->red_part, c->scal + SL_CGI, c->ticket, nullptr, 0, nullptr};
-        HIPCHK(vk::cg_init(K, M, cv, diag, ro, c->st));
+        // pre: the caller's prelude rides in the same launch, and on one rank
+        // that launch's last block also builds the CgState (three launches in one)
+        const bool own_start = pre && !c->use_comm;
+        if (pre)
+            HIPCHK(vk::prelude_cg_init(K, M, *pre, cv, diag, ro, own_start ? &s0 : nullptr, c->cgs, c->st));
+        else
+            HIPCHK(vk::cg_init(K, M, cv, diag, ro, c->st));
         STCHK(allreduce_dev(c, c->scal + SL_CGI, (size_t)(2 * K)));
         if (max_iter <= 0) return extra_alone();
-        HIPCHK(vk::cg_start_from(s0, c->scal + SL_CGI, c->cgs, c->st));
+        if (!own_start) HIPCHK(vk::cg_start_from(s0, c->scal + SL_CGI, c->cgs, c->st));
     }
     const int* gate = field<int>(c->cgs, offsetof(vk::CgState, any));
     const double* beta = field<double>(c->cgs, offsetof(vk::CgState, beta));
-    if (onepass && K <= vk::kOpMaxK && c->have_X && c->op_ok) {
+    if (op1) {
         // ---- one pass over X per CG step (vk::atax) ----
         // A r0 for every system (and A extra_x) by one A.x pass; then each step
         // forms q = A p = A r/diag + beta*q_old on the fly, streams X once for
@@ -195,10 +203,10 @@ vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double
         bool given = false;
         for (int k = 0; k < K; ++k) given = given || (ar0 && ar0[k]);
         if (head) {
-            // A r0 of system 0 is hs->abern (r0 = v); its first step's launch
-            // (below, once the step's vectors are set up) also forms A r0 of
-            // system 1, A extra_x and A xnext
-            HIPCHK(hipMemcpyAsync(AR, hs->abern, (size_t)N * 8, hipMemcpyDeviceToDevice, c->st));
+            // A r0 of system 0 is hs->abern (r0 = v), used in place as system
+            // 0's A r (cu.AR[0] below); its first step's launch (below, once
+            // the step's vectors are set up) also forms A r0 of system 1,
+            // A extra_x and A xnext
         } else if (!given) {
             const double* px[vk::kMaxRhs];
             for (int k = 0; k < K; ++k) px[k] = sys[k]->r;
@@ -252,7 +260,7 @@ vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double
             cu.S[k] = sys[k]->W ? sys[k]->S : nullptr;
             cu.AW[k] = sys[k]->AW;
             cu.Q[k] = Q + (int64_t)k * c->ld;
-            cu.AR[k] = AR + (int64_t)k * c->ld;
+            cu.AR[k] = head && k == 0 ? hs->abern : AR + (int64_t)k * c->ld;
             cu.AD[k] = AD + (int64_t)k * c->ld;
         }
         if (!c->use_comm) {  // one rank: cg_update sums the operator's A d slots itself

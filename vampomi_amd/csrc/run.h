@@ -57,7 +57,7 @@ struct VampRun {
     // device N-vectors (ld each)
     double *z1buf = nullptr, *nb3 = nullptr /* A.x2, A.invQ, A.x1_next */, *nsc = nullptr;
     double* ax2 = nullptr;  // arec: A x2, carried from iteration to iteration
-    double* abern = nullptr;      // the head start: A.bern of iteration hs_it (ld)
+    double* abern = nullptr;      // the head start: A.bern of iteration hs_it in slot hs_it & 1 (2 x ld)
     double* bern_next = nullptr;  // ... and the next iteration's probe (M)
     const double* z1 = nullptr;
     int64_t passes_ref = 0;
@@ -92,9 +92,18 @@ struct EmState {
     double omegas[VAMPOMI_MAX_L] = {};
     double sums[2 * VAMPOMI_MAX_L] = {};
 };
+// r1from (may be null): round 0 also forms r1 itself (vk::EmArgs.r1out) from
+// these lincomb_div inputs, in the same launch (em_begin queues round 0 only
+// if EM_max_iter >= 1: the caller forms r1 otherwise)
+struct R1From {
+    const double* x2;
+    const double* r2;
+    double eta2, gam2, gam1;
+};
 vampomi_status em_begin(vampomi_ctx* c, const EmParams& P, const Mixture& m, double gam1, const double* r1,
-                        DotBatch& b, EmState& s);
-vampomi_status em_queue(vampomi_ctx* c, const Mixture& m, double gam1, const double* r1, DotBatch& b, EmState& s);
+                        DotBatch& b, EmState& s, const R1From* r1from = nullptr);
+vampomi_status em_queue(vampomi_ctx* c, const Mixture& m, double gam1, const double* r1, DotBatch& b, EmState& s,
+                        const R1From* r1from = nullptr);
 vampomi_status em_finish(vampomi_ctx* c, const EmParams& P, Mixture& m, double gam1, const double* r1, EmState& s);
 vampomi_status denoise_into(vampomi_ctx* c, const Mixture& m, double gam1, const double* r1, double* x1,
                             const double* x1_prev, bool damp, double rho, double* x1d, DotBatch& b, double* sum_out);

@@ -59,18 +59,18 @@ vampomi_ctx::~vampomi_ctx() {
 // into b; after b.flush(), em_finish does its host part, the further rounds
 // (each with its own batch) and the merge.  update_prior runs both.
 vampomi_status em_begin(vampomi_ctx* c, const EmParams& P, const Mixture& m, double gam1, const double* r1,
-                        DotBatch& b, EmState& s) {
+                        DotBatch& b, EmState& s, const R1From* r1from) {
     s.emit = 0;
     s.lambda = 1 - m.probs[0];
     for (int j = 0; j < m.L; ++j) s.omegas[j] = m.probs[j];
     for (int j = 1; j < m.L; ++j) s.omegas[j] /= s.lambda;
     if (P.EM_max_iter < 1) return VAMPOMI_OK;
-    return em_queue(c, m, gam1, r1, b, s);
+    return em_queue(c, m, gam1, r1, b, s, r1from);
 }
 
 // one EM round's per-slab sums (:555-597) into b, on b's current stream
 vampomi_status em_queue(vampomi_ctx* c, const Mixture& m, double gam1, const double* r1, DotBatch& b,
-                        EmState& s) {
+                        EmState& s, const R1From* r1from) {
     const int L = m.L;
     double max_sigma = m.vars[0];
     for (int j = 1; j < L; ++j) max_sigma = smax(max_sigma, m.vars[j]);  // std::max_element
@@ -85,6 +85,14 @@ vampomi_status em_queue(vampomi_ctx* c, const Mixture& m, double gam1, const dou
     a.gam1 = gam1;
     a.max_sigma = max_sigma;
     a.L = L;
+    if (r1from) {
+        a.lx = r1from->x2;
+        a.ly = r1from->r2;
+        a.la = r1from->eta2;
+        a.lb = r1from->gam2;
+        a.lc = r1from->gam1;
+        a.r1out = const_cast<double*>(r1);
+    }
     vk::RedOut ro{};
     STCHK(b.sink(1 + 2 * (L - 1), true, s.sums, &ro));  // :578, :596-597
     HIPCHK(vk::em_sums(c->M, r1, a, ro, b.stream()));
@@ -230,9 +238,9 @@ static vampomi_status vamp_alloc(vampomi_ctx* c, VampRun& R) {
     STCHK(dev_alloc(&R.nb3, vk::kMaxRhs * ld));  // probit: slot 3 carries the next A.bern_vec
     STCHK(dev_alloc(&R.nsc, vk::kMaxRhs * ld));
     STCHK(dev_alloc(&R.ax2, ld));
-    STCHK(dev_alloc(&R.abern, ld));
+    STCHK(dev_alloc(&R.abern, 2 * ld));  // two slots: A.bern of it (consumed in place) and of it + 1
     HIPCHK(hipMemsetAsync(R.ax2, 0, ld * 8, c->st));
-    HIPCHK(hipMemsetAsync(R.abern, 0, ld * 8, c->st));
+    HIPCHK(hipMemsetAsync(R.abern, 0, 2 * ld * 8, c->st));
     HIPCHK(hipMemsetAsync(R.z1buf, 0, ld * 8, c->st));
     HIPCHK(hipMemsetAsync(R.nb3, 0, vk::kMaxRhs * ld * 8, c->st));
     HIPCHK(hipMemsetAsync(R.nsc, 0, vk::kMaxRhs * ld * 8, c->st));
@@ -493,10 +501,12 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
     if (R.fuse && arec && R.onepass) STCHK(headstart_available(c, &hs_av));
     HeadStart hs;
     if (hs_av) {
-        hs.abern = R.hs_it == it ? R.abern : nullptr;
+        // slot it & 1 holds A.bern(it): the Onsager solve's A r, updated in
+        // place by its CG steps; A.bern(it + 1) goes to the other slot
+        hs.abern = R.hs_it == it ? R.abern + (it & 1) * ld : nullptr;
         if (it < R.prm.max_iter) {
             hs.xnext = R.bern_next;  // the probe of it + 1, formed by the prelude below
-            hs.axnext = R.abern;  // (its A.bern was copied out first, in stream order)
+            hs.axnext = R.abern + ((it + 1) & 1) * ld;
         }
     }
     // the iteration's elementwise work before the CG solves, in one launch
@@ -519,14 +529,18 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
     pr.bern_next = hs.xnext ? R.bern_next : nullptr;
     pr.zero[0] = R.invQ;
     pr.zero[1] = rec ? R.tmpM : nullptr;
-    HIPCHK(vk::prelude(M, pr, c->st));
+    // where the solve starts on the device (no caller batch), the prelude rides
+    // in its first launch (pcg_run's pre); else it is a launch of its own
+    const bool pre_in_cg = R.fuse && (hs_av || arec);
+    if (!pre_in_cg) HIPCHK(vk::prelude(M, pr, c->st));
     if (R.fuse && hs_av) {
         STCHK(pcg_run(c, {&so, &sx}, R.gamw, R.gam2, R.prm.CG_max_iter, R.prm.CG_err_tol, R.nsc, &R.passes_ref,
-                      nullptr, R.x1, R.z1buf, true, nullptr, &hs));
+                      nullptr, R.x1, R.z1buf, true, nullptr, &hs, &pr));
         R.hs_it = hs.xnext ? it + 1 : 0;
     } else if (R.fuse) {
         STCHK(pcg_run(c, {&sx, &so}, R.gamw, R.gam2, R.prm.CG_max_iter, R.prm.CG_err_tol, R.nsc, &R.passes_ref,
-                      arec ? nullptr : &e1, arec ? R.x1 : nullptr, arec ? R.z1buf : nullptr, R.onepass));
+                      arec ? nullptr : &e1, arec ? R.x1 : nullptr, arec ? R.z1buf : nullptr, R.onepass, nullptr,
+                      nullptr, arec ? &pr : nullptr));
         R.hs_it = 0;
     } else {
         STCHK(pcg_run(c, {&sx}, R.gamw, R.gam2, R.prm.CG_max_iter, R.prm.CG_err_tol, R.nsc, &R.passes_ref, &e1));
@@ -549,12 +563,16 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
     const double gam1_prev = R.gam1;
     R.gam1 = smin(smax(R.eta2 - R.gam2, 1e-11), 1e11);
     R.gam1 = R.prm.rho * R.gam1 + (1 - R.prm.rho) * gam1_prev;  // :346
-    HIPCHK(vk::lincomb_div(M, R.eta2, R.x2, R.gam2, R.r2, R.gam1, R.r1, c->st));  // r1 (:348-350)
+    // r1 (:348-350): its own launch, or (the side stream's EM round below)
+    // formed by the first EM round's kernel
+    const bool next = R.fuse && it < R.prm.max_iter;
+    const bool em_next = next && it + 1 > R.prm.learn_prior_delay;
+    const bool r1_in_em = next && arec && em_next && R.prm.EM_max_iter >= 1;
+    if (!r1_in_em) HIPCHK(vk::lincomb_div(M, R.eta2, R.x2, R.gam2, R.r2, R.gam1, R.r1, c->st));
+    const R1From r1from{R.x2, R.r2, R.eta2, R.gam2, R.gam1};
 
     // ---- prefetch: denoising of iteration it+1 (discarded if the stop fires) ----
     // (batch_rhs >= 3: on the side stream, beside the reductions below)
-    const bool next = R.fuse && it < R.prm.max_iter;
-    const bool em_next = next && it + 1 > R.prm.learn_prior_delay;
     DotBatch fin(c);
     EmState em;
     if (next) R.mix_next = R.mix;
@@ -562,7 +580,7 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
         STCHK(fin.fork());
         if (em_next) {
             STCHK(fin.side(true));
-            STCHK(em_begin(c, em_params(R), R.mix_next, R.gam1, R.r1, fin, em));
+            STCHK(em_begin(c, em_params(R), R.mix_next, R.gam1, R.r1, fin, em, r1_in_em ? &r1from : nullptr));
             STCHK(fin.side(false));
         }
     }
