@@ -61,7 +61,7 @@ struct TimedLaunch {
 // (SL_CG: the 3K sums of a CG step, decided on the device; SL_CGI: the 2K sums
 // of cg_init, read by cg_start_from)
 enum : int { SL_DP = 0, SL_CG = 4, SL_SYNC = 16, SL_NSYNC = 256, SL_LOCAL = SL_SYNC + SL_NSYNC, SL_NLOCAL = 128,
-             SL_CGI = SL_LOCAL + SL_NLOCAL, SL_CHECK = SL_CGI + 16, SL_AGREE = SL_CHECK + 8, SL_TOTAL = 512, SL_BARRIER = SL_TOTAL - 1 };
+             SL_CGI = SL_LOCAL + SL_NLOCAL, SL_CHECK = SL_CGI + 16, SL_AGREE = SL_CHECK + 8, SL_CHAIN = SL_AGREE + 8, SL_TOTAL = 512, SL_BARRIER = SL_TOTAL - 1 };
 
 struct vampomi_ctx {
     int rank = 0, nranks = 1, device = 0;
@@ -220,6 +220,10 @@ class DotBatch {
     vampomi_status sink(int nq, bool sync, double* out, vk::RedOut* ro);
     vampomi_status flush();
     bool empty() const { return sinks_.empty(); }
+    // one rank: the device address where the result that flush() will copy to
+    // out is written (mapped host memory), for a kernel queued before the
+    // flush; null if out is not a sink of this batch or with a communicator
+    const double* dev_result(const double* out) const;
     // on = true: the following sinks/adds run on the context's side stream
     // (ordered after everything queued on st so far); flush() joins it back.
     // No effect (one stream) when the context's side stream is off

@@ -593,6 +593,13 @@ vampomi_status DotBatch::add_many(int64_t n, const std::vector<Group>& groups) {
     return VAMPOMI_OK;
 }
 
+const double* DotBatch::dev_result(const double* out) const {
+    if (c_->use_comm || !c_->d_hscal) return nullptr;
+    for (const Sink& k : sinks_)
+        if (k.out == out) return c_->d_hscal + k.slot;
+    return nullptr;
+}
+
 hipStream_t DotBatch::stream() const { return on_side_ ? c_->st2 : c_->st; }
 
 vampomi_status DotBatch::fork() {

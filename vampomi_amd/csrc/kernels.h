@@ -232,7 +232,16 @@ struct EmArgs {
     const double* ly;
     double la, lb, lc;
     double* r1out;
+    // dsc (may be null): gam1 = dsc[0] and la = eta2 = dsc[1] come from the
+    // device (vamp_gam1), and noise_var = 1/gam1, v[j-1] = 1/(1/vars[j] + gam1)
+    // are formed here, with the host's expressions (the host fields are unused)
+    const double* dsc;
 };
+// one thread, after the reduction that produced a2 = <bern, invQ> (src/vamp.cpp:
+// 341-346, 498): alpha2 = gam2*a2, eta2 = gam2/alpha2, gam1 = rho*min(max(eta2 -
+// gam2, 1e-11), 1e11) + (1 - rho)*gam1_prev, into out[0] = gam1, out[1] = eta2,
+// out[2] = alpha2: the host's expressions, bit for bit
+hipError_t vamp_gam1(const double* a2, double gam2, double rho, double gam1_prev, double* out, hipStream_t st);
 // ro.out[q], Q = 1 + 2(L-1): q=0 sum pin; q=j (1..L-1) sum beta_j pin;
 // q=L-1+j sum beta_j (g_j^2 + v_j) pin
 hipError_t em_sums(int64_t M, const double* r1, const EmArgs& a, const RedOut& ro, hipStream_t st);

@@ -1353,10 +1353,10 @@ hipError_t denoise(int64_t M, const double* r1, double gam1, const Mix& mix, dou
 // ---------------------------------------------------------------------------
 // EM prior update sums (src/vamp.cpp:554-597), one marker per thread
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ double em_num(const EmArgs& a, double r, int j) {
+__device__ __forceinline__ double em_num(const EmArgs& a, double noise_var, double r, int j) {
     return a.lambda * a.omegas[j] *
-           exp(-(r * r) / 2 * (a.max_sigma - a.vars[j]) / (a.vars[j] + a.noise_var) / (a.max_sigma + a.noise_var)) /
-           sqrt(a.vars[j] + a.noise_var) / sqrt(2 * M_PI);
+           exp(-(r * r) / 2 * (a.max_sigma - a.vars[j]) / (a.vars[j] + noise_var) / (a.max_sigma + noise_var)) /
+           sqrt(a.vars[j] + noise_var) / sqrt(2 * M_PI);
 }
 
 // The Q = 1 + 2(L-1) block sums: each wave reduces every value in registers
@@ -1370,10 +1370,15 @@ __global__ __launch_bounds__(kBlock) void em_kernel(int64_t M, const double* __r
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const bool valid = i < M;
+    // gam1 and eta2 from the device (a.dsc) or the host; the derived scalars
+    // with the host's expressions (vamp.cpp em_queue)
+    const double gam1 = a.dsc ? a.dsc[0] : a.gam1;
+    const double noise_var = a.dsc ? 1 / gam1 : a.noise_var;
     double r = 0.0;
     if (valid) {
         if (a.r1out) {
-            r = (a.la * a.lx[i] - a.lb * a.ly[i]) / a.lc;  // lincomb_div_kernel's expression
+            const double la = a.dsc ? a.dsc[1] : a.la, lc = a.dsc ? gam1 : a.lc;
+            r = (la * a.lx[i] - a.lb * a.ly[i]) / lc;  // lincomb_div_kernel's expression
             a.r1out[i] = r;
         } else {
             r = r1[i];
@@ -1381,16 +1386,17 @@ __global__ __launch_bounds__(kBlock) void em_kernel(int64_t M, const double* __r
     }
     const int L = a.L, Q = 1 + 2 * (L - 1);
     double sum_of_elems = 0.0;
-    for (int j = 1; j < L; ++j) sum_of_elems += em_num(a, r, j);
-    const double pin = 1 / (1 + (1 - a.lambda) / sqrt(2 * M_PI * a.noise_var) *
-                                    exp(-(r * r) / 2 * a.max_sigma / a.noise_var / (a.noise_var + a.max_sigma)) /
+    for (int j = 1; j < L; ++j) sum_of_elems += em_num(a, noise_var, r, j);
+    const double pin = 1 / (1 + (1 - a.lambda) / sqrt(2 * M_PI * noise_var) *
+                                    exp(-(r * r) / 2 * a.max_sigma / noise_var / (noise_var + a.max_sigma)) /
                                     sum_of_elems);
     double s = wave_sum(valid ? pin : 0.0);
     if (lane == 0) wl[w][0] = s;
     for (int j = 1; j < L; ++j) {
-        const double beta = em_num(a, r, j) / sum_of_elems;
-        const double g = a.gam1 * r / (1 / a.vars[j] + a.gam1);
-        const double gam = beta * (g * g + a.v[j - 1]);
+        const double beta = em_num(a, noise_var, r, j) / sum_of_elems;
+        const double g = gam1 * r / (1 / a.vars[j] + gam1);
+        const double vj = a.dsc ? 1.0 / (1.0 / a.vars[j] + gam1) : a.v[j - 1];
+        const double gam = beta * (g * g + vj);
         const double sb = wave_sum(valid ? beta * pin : 0.0);
         const double sg = wave_sum(valid ? gam * pin : 0.0);
         if (lane == 0) {
@@ -1402,6 +1408,24 @@ __global__ __launch_bounds__(kBlock) void em_kernel(int64_t M, const double* __r
     for (int q = threadIdx.x; q < Q; q += kBlock)
         red_put(ro, (int64_t)blockIdx.x * Q + q, ((wl[0][q] + wl[1][q]) + wl[2][q]) + wl[3][q]);
     red_finish(ro, Q, lds);
+}
+
+__global__ void vamp_gam1_kernel(const double* __restrict__ a2, double gam2, double rho, double gam1_prev,
+                                 double* __restrict__ out) {
+    if (threadIdx.x != 0) return;
+    const double alpha2 = gam2 * __hip_atomic_load(a2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);  // :498
+    const double eta2 = gam2 / alpha2;                                                               // :341
+    const double d = eta2 - gam2;
+    double g = d < 1e-11 ? 1e-11 : d;  // std::max(d, 1e-11)
+    g = 1e11 < g ? 1e11 : g;           // std::min(., 1e11)
+    out[0] = rho * g + (1 - rho) * gam1_prev;  // :346
+    out[1] = eta2;
+    out[2] = alpha2;
+}
+
+hipError_t vamp_gam1(const double* a2, double gam2, double rho, double gam1_prev, double* out, hipStream_t st) {
+    hipLaunchKernelGGL(vamp_gam1_kernel, dim3(1), dim3(64), 0, st, a2, gam2, rho, gam1_prev, out);
+    return hipGetLastError();
 }
 
 hipError_t em_sums(int64_t M, const double* r1, const EmArgs& a, const RedOut& ro, hipStream_t st) {

@@ -99,6 +99,7 @@ struct R1From {
     const double* x2;
     const double* r2;
     double eta2, gam2, gam1;
+    const double* dsc = nullptr;  // device: gam1, eta2 (vk::vamp_gam1); then eta2 and gam1 above are unused
 };
 vampomi_status em_begin(vampomi_ctx* c, const EmParams& P, const Mixture& m, double gam1, const double* r1,
                         DotBatch& b, EmState& s, const R1From* r1from = nullptr);

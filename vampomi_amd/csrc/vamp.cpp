@@ -92,6 +92,7 @@ vampomi_status em_queue(vampomi_ctx* c, const Mixture& m, double gam1, const dou
         a.lb = r1from->gam2;
         a.lc = r1from->gam1;
         a.r1out = const_cast<double*>(r1);
+        a.dsc = r1from->dsc;
     }
     vk::RedOut ro{};
     STCHK(b.sink(1 + 2 * (L - 1), true, s.sums, &ro));  // :578, :596-597
@@ -548,32 +549,46 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
     }
     if (res && res->cg_iters) res->cg_iters[it - 1] = sx.iters;
     if (res && res->ons_iters) res->ons_iters[it - 1] = so.iters;
-    {
-        DotBatch b(c);
-        const DotBatch::Group ga2{{T(R.bern, R.invQ)}, true, &R.a2};  // :498
-        if (arec)
-            STCHK(err_queue(c, R, R.x1, R.z1, b, R.e1m, R.e1n, R.e1s, {ga2}));  // :272
-        else
-            STCHK(b.add_many(M, {ga2}));
-        STCHK(b.flush());
-        R.alpha2 = R.gam2 * R.a2;  // :498
-    }
-    err_finish(R, R.e1m, R.e1n, R.e1s, 1);
-    R.eta2 = R.gam2 / R.alpha2;  // :341
-    const double gam1_prev = R.gam1;
-    R.gam1 = smin(smax(R.eta2 - R.gam2, 1e-11), 1e11);
-    R.gam1 = R.prm.rho * R.gam1 + (1 - R.prm.rho) * gam1_prev;  // :346
     // r1 (:348-350): its own launch, or (the side stream's EM round below)
     // formed by the first EM round's kernel
     const bool next = R.fuse && it < R.prm.max_iter;
     const bool em_next = next && it + 1 > R.prm.learn_prior_delay;
     const bool r1_in_em = next && arec && em_next && R.prm.EM_max_iter >= 1;
-    if (!r1_in_em) HIPCHK(vk::lincomb_div(M, R.eta2, R.x2, R.gam2, R.r2, R.gam1, R.r1, c->st));
-    const R1From r1from{R.x2, R.r2, R.eta2, R.gam2, R.gam1};
-
+    // chain (one rank): alpha2 -> eta2 -> gam1 (:341-346) are formed on the
+    // device from the reduction's result (vk::vamp_gam1), so the EM round and
+    // the reductions after it are queued without the host waiting for alpha2;
+    // the host forms the same values from the same sum at the next flush
+    const bool chain = r1_in_em && !c->use_comm;
+    const DotBatch::Group ga2{{T(R.bern, R.invQ)}, true, &R.a2};  // :498
+    const double gam1_prev = R.gam1;
+    auto host_gam1 = [&] {
+        R.alpha2 = R.gam2 * R.a2;  // :498
+        err_finish(R, R.e1m, R.e1n, R.e1s, 1);
+        R.eta2 = R.gam2 / R.alpha2;  // :341
+        R.gam1 = smin(smax(R.eta2 - R.gam2, 1e-11), 1e11);
+        R.gam1 = R.prm.rho * R.gam1 + (1 - R.prm.rho) * gam1_prev;  // :346
+    };
     // ---- prefetch: denoising of iteration it+1 (discarded if the stop fires) ----
     // (batch_rhs >= 3: on the side stream, beside the reductions below)
     DotBatch fin(c);
+    double* dsc = c->scal + SL_CHAIN;
+    if (chain) {
+        STCHK(err_queue(c, R, R.x1, R.z1, fin, R.e1m, R.e1n, R.e1s, {ga2}));  // :272
+        const double* a2dev = fin.dev_result(&R.a2);
+        if (!a2dev) return fail(VAMPOMI_ERR_STATE, "vamp: alpha2's sum has no device address");
+        HIPCHK(vk::vamp_gam1(a2dev, R.gam2, R.prm.rho, gam1_prev, dsc, c->st));
+    } else {
+        DotBatch b(c);
+        if (arec)
+            STCHK(err_queue(c, R, R.x1, R.z1, b, R.e1m, R.e1n, R.e1s, {ga2}));  // :272
+        else
+            STCHK(b.add_many(M, {ga2}));
+        STCHK(b.flush());
+        host_gam1();
+        if (!r1_in_em) HIPCHK(vk::lincomb_div(M, R.eta2, R.x2, R.gam2, R.r2, R.gam1, R.r1, c->st));
+    }
+    R1From r1from{R.x2, R.r2, R.eta2, R.gam2, R.gam1};
+    if (chain) r1from.dsc = dsc;
     EmState em;
     if (next) R.mix_next = R.mix;
     if (next && arec) {  // the side stream starts from r1 and x1; its EM sums are queued before these reductions
@@ -635,6 +650,7 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
     // same (tests/test_gpu_sharded.py::test_side_stream_bitwise)
     if (next && arec && em_next) {
         STCHK(fin.flush());
+        if (chain) host_gam1();  // (the device formed the same values for the EM round)
         STCHK(em_finish(c, em_params(R), R.mix_next, R.gam1, R.r1, em));
     }
     if (next && arec) {
