@@ -258,3 +258,39 @@ def test_c5_full_shard_properties():
         assert np.all(st[:, 0] > 0) and np.all(st[:, 1] > 0)  # methylation values in (0, 1)
         # 3,090 causal markers share h2 = 0.5: they stand out, the null ones are uniform
         assert np.median(p[beta != 0]) < 0.02 and 0.4 < np.median(p[beta == 0]) < 0.6
+
+
+def test_c5_full_shard_vs_oracle():
+    """The WHOLE per-GPU C5 shard (N = 100,000 x 62,500 methylation-like
+    markers, 50 GB; eight of them are configs[4]) against the oracle's
+    assoc_loo on the same matrix (bit-identical generator): every marker's
+    five sums to 1e-12 relative (the oracle's sequential sums carry ~sqrt(N)
+    eps of their own at this N), the p-value function to 1e-12, and every
+    p-value to 1e-10 relative or, where that fails, to 10x the formula's own
+    sensitivity to summation order measured on that marker (the bars above)."""
+    N, Mt, seed = 100000, 62500, 13
+    with va.Data(N, Mt) as d:
+        d.generate(seed, va.GEN_METH)
+        beta = d.simulate_phen(seed + 1, lam=0.05, h2=0.5)
+        y = d.get_phen()
+        est = _estimate(beta, N)
+        p, st = d.assoc_loo(est)
+    X = O.generate_markers(seed, va.GEN_METH, N, 0, Mt)
+    po, sto = O.assoc_loo(X, y, est)
+    for q in range(5):
+        assert relerr(st[:, q], sto[:, q]) < 1e-12, q
+    _check_pfun(p, st, N)
+    bad = np.nonzero(np.abs(p - po) > 1e-10 * po + 1e-300)[0]
+    assert len(bad) < Mt // 100, len(bad)  # the tail p-values only
+    if len(bad):  # the sensitivity on those markers (y_mod over the whole shard)
+        mave, msig = O.marker_stats(X)
+        x1 = est * np.sqrt(N)
+        ymod = y - O.ax(X, mave, msig, x1)
+        Xb = X[bad]
+        ym = ymod[None, :] + Xb / np.sqrt(N) * x1[bad, None]
+        sums = np.stack([Xb.sum(1), (Xb * Xb).sum(1), (Xb * ym).sum(1), ym.sum(1), (ym * ym).sum(1)], axis=1)
+        pp = np.array([O.reg1d_pval(*q, N) for q in sums])
+        spread = np.abs(pp - po[bad]) / np.maximum(po[bad], 1e-300)
+        ok = np.abs(p[bad] - po[bad]) <= np.maximum(1e-10, 10 * spread) * po[bad] + 1e-300
+        assert ok.all(), (bad[~ok][:5], p[bad][~ok][:5], po[bad][~ok][:5])
+    assert np.median(p[beta != 0]) < 0.02 and 0.4 < np.median(p[beta == 0]) < 0.6
