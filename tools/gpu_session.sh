@@ -1,0 +1,120 @@
+#!/bin/bash
+# One GPU call's steps, in order, each under its own time limit; the call ends
+# at the first step that fails (its log under gpurun_out/<tag>/):
+#
+#   gpurun -- bash tools/gpu_session.sh <tag> <step> [<step> ...]
+#
+# steps:
+#   suite        the GPU test suite (durations of the slowest tests)
+#   fullshard    the whole-shard oracle tests alone (C3, C5)
+#   bitwise      12 VAMP iterations (linear and probit) on this build and on
+#                $OLD (default build_old/), compared bit for bit
+#   ab           C2 lines alternating this build and $OLD, $ROUNDS rounds
+#   envab        C2 lines alternating the settings in $ENVAB ("A=1;A=2;...")
+#   trace        rocprofv3 kernel trace of the C2 line + the gap analysis
+#   hiptrace     rocprofv3 HIP API + kernel trace of a short C2 line
+#   timing       the C2 rate at timing period 4 / 16 / none
+#   probit_k     every probit test, the parity bar's gap / spread ratios
+#   launcher     the default C2 line over a 1-rank RCCL communicator, and the
+#                2-rank launcher on a 1-GPU box (one failure line, rc != 0)
+#   bases        rank 0's 1-GPU bases (tools/one_gpu_bases.py)
+#   final        smoke, the default C2 line (both CPU legs), its kernel stats
+#                and PMC traffic; the same for C3; C4 and C5 lines
+set -u
+cd "${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+TAG=$1
+shift
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+OLD=${OLD:-$PWD/build_old/lib/libvampomi.so}
+ROUNDS=${ROUNDS:-3}
+step() {
+    local name=$1 tmo=$2
+    shift 2
+    echo "== $name ($(date +%T))"
+    timeout -k 10 "$tmo" "$@" > "$OUT/$name.log" 2>&1
+    local rc=$?
+    tail -n 2 "$OUT/$name.log" | cut -c1-400
+    [ $rc -eq 0 ] || { echo "stopping after $name (rc=$rc)"; exit $rc; }
+}
+brief() {
+    grep '^{' "$OUT/$1.log" | tail -1 | python -c "import json,sys; d=json.loads(sys.stdin.read()); r=d.get('roofline') or {}; print('$1', d['value'], d['ms_per_step'], r.get('avg_launch_us'), r.get('frac'), d.get('a_kernel_frac_of_step'))" | tee -a "$OUT/ab.txt"
+}
+C2=(python bench.py --steps 20 --warmup 5 --no-cpu-baseline)
+prof() {
+    step "rocprof_$1" 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$1" -o run --output-format csv -- \
+        python bench.py --config "$1" --steps "$2" --warmup 5 --no-cpu-baseline
+}
+for s in "$@"; do
+    case $s in
+    suite)
+        step suite 900 python -u -m pytest tests -m gpu -x -q --durations=12 --timeout 400 --timeout-method thread ;;
+    fullshard)
+        step fullshard 600 python -u -m pytest tests/test_gpu_scale.py::test_c3_full_shard_vs_oracle \
+            tests/test_gpu_assoc.py::test_c5_full_shard_vs_oracle -m gpu -v --durations=0 --timeout 400 \
+            --timeout-method thread ;;
+    bitwise)
+        for m in linear bin_class; do
+            step bw_new_$m 200 python tools/lib_bitwise.py run "$OUT/new_$m.npz" 10000 20000 12 $m
+            step bw_old_$m 200 env VAMPOMI_LIB="$OLD" python tools/lib_bitwise.py run "$OUT/old_$m.npz" 10000 20000 12 $m
+            python tools/lib_bitwise.py cmp "$OUT/new_$m.npz" "$OUT/old_$m.npz" | tee -a "$OUT/bitwise.txt"
+        done ;;
+    ab)
+        for r in $(seq "$ROUNDS"); do
+            step ab_new_$r 200 "${C2[@]}" && brief ab_new_$r
+            step ab_old_$r 200 env VAMPOMI_LIB="$OLD" "${C2[@]}" && brief ab_old_$r
+        done ;;
+    envab)
+        IFS=';' read -r -a settings <<< "${ENVAB:-}"
+        for r in $(seq "$ROUNDS"); do
+            i=0
+            for e in "${settings[@]}"; do
+                i=$((i + 1))
+                step env${i}_$r 200 env $e "${C2[@]}" && brief env${i}_$r
+            done
+        done ;;
+    trace)
+        step trace 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
+            python bench.py --steps 20 --warmup 5 --no-cpu-baseline
+        f=$(find "$OUT/prof" -name 'run_kernel_trace.csv' | head -1)
+        python tools/trace_gaps.py "$f" 0.3 > "$OUT/gaps.txt" && head -34 "$OUT/gaps.txt" ;;
+    hiptrace)
+        step hiptrace 300 rocprofv3 --hip-trace --kernel-trace -d "$OUT/hprof" -o run --output-format csv -- \
+            python bench.py --steps 6 --warmup 2 --no-cpu-baseline ;;
+    timing)
+        for r in $(seq "$ROUNDS"); do
+            step tp4_$r 200 "${C2[@]}" --timing-period 4 && brief tp4_$r
+            step tp16_$r 200 "${C2[@]}" --timing-period 16 && brief tp16_$r
+            step tpnone_$r 200 "${C2[@]}" --no-timing && brief tpnone_$r
+        done ;;
+    probit_k)
+        export VAMPOMI_PROBIT_RATIOS=$PWD/$OUT/ratios.jsonl
+        rm -f "$VAMPOMI_PROBIT_RATIOS"
+        step probit_k 600 python -u -m pytest tests/test_gpu_probit.py tests/test_gpu_options.py \
+            tests/test_gpu_sharded.py -m gpu -q --timeout 300 --timeout-method thread -k "probit or bin_class or c4"
+        python tools/probit_ratios.py "$VAMPOMI_PROBIT_RATIOS" | tee "$OUT/probit_k.txt"
+        unset VAMPOMI_PROBIT_RATIOS ;;
+    launcher)
+        step bench_c2_rccl1 200 env VAMPOMI_FORCE_RCCL=1 python bench.py --steps 20 --warmup 5 --no-cpu-baseline
+        echo "== spawn2_on_one_gpu ($(date +%T))"
+        timeout -k 10 300 python bench.py --gpus 2 --steps 5 --warmup 2 --deadline-s 240 > "$OUT/spawn2.log" 2>&1
+        echo "rc=$?" >> "$OUT/spawn2.log"
+        tail -n 2 "$OUT/spawn2.log" | cut -c1-2500 ;;
+    bases)
+        step bases 200 python tools/one_gpu_bases.py ;;
+    final)
+        step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+        step bench_c2 400 python bench.py --steps 20 --warmup 5
+        prof c2 20
+        step pmc_c2 300 bash tools/pmc.sh c2
+        step bench_c3 400 python bench.py --config c3 --steps 10 --warmup 2
+        prof c3 6
+        step pmc_c3 300 bash tools/pmc.sh c3
+        step bench_c4 300 python bench.py --config c4 --steps 12 --warmup 2 --no-cpu-baseline
+        step bench_c5 300 python bench.py --config c5 --steps 5 --warmup 1 ;;
+    *)
+        echo "unknown step $s"; exit 2 ;;
+    esac
+done
+echo done
