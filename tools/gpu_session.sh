@@ -12,6 +12,7 @@
 #   ab           C2 lines alternating this build and $OLD, $ROUNDS rounds
 #   envab        C2 lines alternating the settings in $ENVAB ("A=1;A=2;...")
 #   trace        rocprofv3 kernel trace of the C2 line + the gap analysis
+#   trace_old    the same for $OLD
 #   hiptrace     rocprofv3 HIP API + kernel trace of a short C2 line
 #   timing       the C2 rate at timing period 4 / 16 / none
 #   probit_k     every probit test, the parity bar's gap / spread ratios
@@ -79,6 +80,11 @@ for s in "$@"; do
             python bench.py --steps 20 --warmup 5 --no-cpu-baseline
         f=$(find "$OUT/prof" -name 'run_kernel_trace.csv' | head -1)
         python tools/trace_gaps.py "$f" 0.3 > "$OUT/gaps.txt" && head -34 "$OUT/gaps.txt" ;;
+    trace_old)
+        VAMPOMI_LIB="$OLD" step trace_old 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_old" -o run \
+            --output-format csv -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline
+        f=$(find "$OUT/prof_old" -name 'run_kernel_trace.csv' | head -1)
+        python tools/trace_gaps.py "$f" 0.3 > "$OUT/gaps_old.txt" && head -34 "$OUT/gaps_old.txt" ;;
     hiptrace)
         step hiptrace 300 rocprofv3 --hip-trace --kernel-trace -d "$OUT/hprof" -o run --output-format csv -- \
             python bench.py --steps 6 --warmup 2 --no-cpu-baseline ;;

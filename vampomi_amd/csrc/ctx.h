@@ -318,7 +318,10 @@ vampomi_status op_check_err(vampomi_ctx* c);
 // summed over ranks with <d_k,p_k> at its tail; one rank: <d_k,p_k> in
 // scal[SL_DP+k]) from one pass over X.  COLLECTIVE.  reduce = false (one
 // rank only): the per-slot A d partials stay in op_part for cg_update to sum
-vampomi_status op_dev(vampomi_ctx* c, int K, const vk::OpArgs& a, const int* gate, bool reduce = true);
+// divide = false (several ranks): A d stays all-reduced but undivided, for a
+// consumer that divides as it reads (cg_update's addiv)
+vampomi_status op_dev(vampomi_ctx* c, int K, const vk::OpArgs& a, const int* gate, bool reduce = true,
+                      bool divide = true);
 // the head-start launch (c->opp_hs): op_dev's work for ONE system (a, K = 1),
 // and out[kp] = A px[kp] (device ld, /sqrt(N), summed over ranks) for the
 // kOpPlain plain right-hand sides, from the same pass over X.  One rank: the

@@ -535,7 +535,7 @@ vampomi_status DotBatch::sink(int nq, bool sync, double* out, vk::RedOut* ro) {
 vampomi_status DotBatch::add(std::initializer_list<vk::DotTerm> terms, int64_t n, bool sync, double* out) {
     vk::DotArgs a{};
     a.nt = (int)terms.size();
-    if (a.nt < 1 || a.nt > vk::kMaxTerms) return fail(VAMPOMI_ERR_ARG, "DotBatch: 1..8 terms");
+    if (a.nt < 1 || a.nt > vk::kMaxTerms) return fail(VAMPOMI_ERR_ARG, "DotBatch: 1.." + std::to_string(vk::kMaxTerms) + " terms");
     int q = 0;
     for (const auto& t : terms) {
         a.t[q] = t;
@@ -555,7 +555,7 @@ vampomi_status DotBatch::add_many(int64_t n, const std::vector<Group>& groups) {
     int nloc = 0, nsyn = 0;
     for (const Group& g : groups) (g.sync ? nsyn : nloc) += (int)g.terms.size();
     a.nt = nloc + nsyn;
-    if (a.nt < 1 || a.nt > vk::kMaxTerms) return fail(VAMPOMI_ERR_ARG, "DotBatch: 1..8 terms");
+    if (a.nt < 1 || a.nt > vk::kMaxTerms) return fail(VAMPOMI_ERR_ARG, "DotBatch: 1.." + std::to_string(vk::kMaxTerms) + " terms");
     if (nloc + nlocal_ > SL_NLOCAL || nsyn + nsync_ > SL_NSYNC) return fail(VAMPOMI_ERR_STATE, "DotBatch overflow");
     double* base = c_->use_comm ? c_->scal : c_->d_hscal;
     int ql = 0, qs = nloc;
@@ -736,7 +736,7 @@ vampomi_status atx_dev(vampomi_ctx* c, int K, const double* const* u, double* co
 // ---------------------------------------------------------------------------
 // doubles of the per-block reduction partials (every reduction kernel's grid)
 static size_t red_capacity(int64_t Mx) {
-    return std::max<size_t>({(size_t)vk::kRedBlocks * 3 * vk::kMaxRhs,
+    return std::max<size_t>({(size_t)vk::kRedBlocks * 3 * vk::kMaxRhs, (size_t)vk::kRedBlocks * vk::kMaxTerms,
                              (size_t)((Mx + 255) / 256) * (1 + 2 * (vk::kMaxL - 1)),
                              (size_t)(Mx / 8 + 1) * vk::kMaxRhs, (size_t)4096});  // ATx partials at G >= 2
 }
@@ -920,7 +920,7 @@ vampomi_status op_check_err(vampomi_ctx* c) {
 // (pass_bytes: X once, K N-vectors, mave/msig, K M-vectors), the work it
 // replaces being two such passes; its other traffic (p, z, d, A r, q_old and
 // the per-slot A d partials, < 1% at C2) is not counted as algorithmic.
-vampomi_status op_dev(vampomi_ctx* c, int K, const vk::OpArgs& a, const int* gate, bool reduce) {
+vampomi_status op_dev(vampomi_ctx* c, int K, const vk::OpArgs& a, const int* gate, bool reduce, bool divide) {
     if (!c->have_X) return fail(VAMPOMI_ERR_STATE, "A before the methylation data was loaded");
     STCHK(op_prepare(c));
     if (!c->op_ok || K < 1 || K > vk::kOpMaxK)
@@ -952,7 +952,7 @@ vampomi_status op_dev(vampomi_ctx* c, int K, const vk::OpArgs& a, const int* gat
     } else {
         HIPCHK(vk::op_reduce(c->opp, K, c->N, c->ld, c->op_part, os, 0.0, c->st, gate));
         STCHK(allreduce_dev(c, ad, (size_t)K * c->ld + K));  // src/data.cpp:367
-        HIPCHK(vk::vec_div(K, c->N, c->ld, os, c->sqrtN, c->st));
+        if (divide) HIPCHK(vk::vec_div(K, c->N, c->ld, os, c->sqrtN, c->st));
     }
     return VAMPOMI_OK;
 }

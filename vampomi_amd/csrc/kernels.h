@@ -10,7 +10,7 @@ namespace vk {
 
 constexpr int kMaxRhs = 4;     // right-hand sides sharing one pass over X
 constexpr int kMaxL = 64;      // mixture components (VAMPOMI_MAX_L)
-constexpr int kMaxTerms = 8;   // dot-product terms per reduction launch
+constexpr int kMaxTerms = 12;  // dot-product terms per reduction launch
 constexpr int kRedBlocks = 1024;  // max partial blocks of a reduction
 
 struct CPtrs { const double* p[kMaxRhs]; };
@@ -213,10 +213,26 @@ struct Mix {
     double vars[kMaxL];
     int L;
 };
+// The mixture words of the device EM update, kMixWords doubles: [0] L,
+// [1, 1 + kMaxL) probs, [1 + kMaxL, 1 + 2 kMaxL) vars, [1 + 2 kMaxL] eta_max
+constexpr int kMixWords = 2 + 2 * kMaxL;
+// one EM round's update of the mixture, formed on the device (denoise's em)
+struct EmUpd {
+    const double* sums = nullptr;  // em_sums' ro.out (mapped host memory: one rank), Q = 1 + 2(L-1)
+    int64_t Mt = 0;
+    int learn_vars = 0;
+    double merge_vars_thr = 0.0;
+    double* mirror = nullptr;      // the updated mixture's words (mapped host memory), for the host's check
+};
 // x1 = g1(r1) (then rho*x1 + (1-rho)*x1_prev if damp), x1d = g1d(r1),
-// sum of x1d in ro.out[0]
+// sum of x1d in ro.out[0].  em / gam1dev (may be null): the mixture is mix
+// after one EM round from em->sums and the merging of close variances
+// (vamp.cpp em_finish with EM_max_iter = 1, src/vamp.cpp:598-642: the host's
+// expressions, bit for bit), formed in the launch, and gam1 is gam1dev[0]
+// (vamp_gam1), instead of mix and gam1.
 hipError_t denoise(int64_t M, const double* r1, double gam1, const Mix& mix, double* x1,
-                   const double* x1_prev, int damp, double rho, double* x1d, const RedOut& ro, hipStream_t st);
+                   const double* x1_prev, int damp, double rho, double* x1d, const RedOut& ro, hipStream_t st,
+                   const EmUpd* em = nullptr, const double* gam1dev = nullptr);
 
 // ---- EM prior update (vamp::updatePrior) per-marker sums --------------------
 struct EmArgs {
@@ -348,7 +364,9 @@ struct CgVecs {
     // one rank, one-pass operator (may be null): AD is not read; A d of
     // sample i is summed here from the operator's per-slot partials
     // adpart[(t*kMaxRhs + k)*adld + i], t < adslots, in op_reduce's order, and
-    // divided by addiv (the separate op_reduce launch folded into this one)
+    // divided by addiv (the separate op_reduce launch folded into this one).
+    // Without adpart, addiv > 0: AD holds the all-reduced sums not yet divided,
+    // and each is divided here as it is read (the vec_div launch folded in)
     const double* adpart;
     int64_t adld;
     int adslots;

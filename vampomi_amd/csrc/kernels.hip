@@ -1244,14 +1244,16 @@ int red_blocks(int64_t n) {
 
 // every term loads both operands unconditionally (a SUM term's b is its a,
 // set on the host) so a thread's loads for all terms are in flight together;
-// the op is a per-launch uniform selected per element
-template <int NT>
+// the op is a per-launch uniform selected per element.  UPD: some term is a
+// PUPD / SQPUPD (its c and beta are loaded); a launch without one does not
+// keep those pointers (up to 12 terms without scalar-register spills)
+template <int NT, bool UPD>
 __global__ __launch_bounds__(kBlock) void dots_kernel(DotArgs a, int64_t n, RedOut ro) {
     if (ro.gate && !*ro.gate) return;
     __shared__ double lds[4];
     double bt[NT];
 #pragma unroll
-    for (int q = 0; q < NT; ++q) bt[q] = (a.t[q].op == PUPD || a.t[q].op == SQPUPD) ? *a.t[q].beta : 0.0;
+    for (int q = 0; q < NT; ++q) bt[q] = UPD && (a.t[q].op == PUPD || a.t[q].op == SQPUPD) ? *a.t[q].beta : 0.0;
     double acc[NT];
 #pragma unroll
     for (int q = 0; q < NT; ++q) acc[q] = 0.0;
@@ -1260,7 +1262,8 @@ __global__ __launch_bounds__(kBlock) void dots_kernel(DotArgs a, int64_t n, RedO
 #pragma unroll
         for (int q = 0; q < NT; ++q) {
             va[q] = a.t[q].a[e];
-            vb[q] = (a.t[q].op == PUPD || a.t[q].op == SQPUPD) ? a.t[q].c[e] + bt[q] * a.t[q].b[e] : a.t[q].b[e];
+            vb[q] = UPD && (a.t[q].op == PUPD || a.t[q].op == SQPUPD) ? a.t[q].c[e] + bt[q] * a.t[q].b[e]
+                                                                     : a.t[q].b[e];
         }
 #pragma unroll
         for (int q = 0; q < NT; ++q) {
@@ -1277,27 +1280,39 @@ __global__ __launch_bounds__(kBlock) void dots_kernel(DotArgs a, int64_t n, RedO
     red_finish(ro, NT, lds);
 }
 
-hipError_t dots(const DotArgs& a, int64_t n, const RedOut& ro, hipStream_t st) {
+template <bool UPD>
+static hipError_t dots_launch(const DotArgs& a, int64_t n, const RedOut& ro, hipStream_t st) {
     const dim3 g(red_blocks(n)), b(kBlock);
     switch (a.nt) {
-        case 1: hipLaunchKernelGGL(dots_kernel<1>, g, b, 0, st, a, n, ro); break;
-        case 2: hipLaunchKernelGGL(dots_kernel<2>, g, b, 0, st, a, n, ro); break;
-        case 3: hipLaunchKernelGGL(dots_kernel<3>, g, b, 0, st, a, n, ro); break;
-        case 4: hipLaunchKernelGGL(dots_kernel<4>, g, b, 0, st, a, n, ro); break;
-        case 5: hipLaunchKernelGGL(dots_kernel<5>, g, b, 0, st, a, n, ro); break;
-        case 6: hipLaunchKernelGGL(dots_kernel<6>, g, b, 0, st, a, n, ro); break;
-        case 7: hipLaunchKernelGGL(dots_kernel<7>, g, b, 0, st, a, n, ro); break;
-        case 8: hipLaunchKernelGGL(dots_kernel<8>, g, b, 0, st, a, n, ro); break;
+        case 1: hipLaunchKernelGGL((dots_kernel<1, UPD>), g, b, 0, st, a, n, ro); break;
+        case 2: hipLaunchKernelGGL((dots_kernel<2, UPD>), g, b, 0, st, a, n, ro); break;
+        case 3: hipLaunchKernelGGL((dots_kernel<3, UPD>), g, b, 0, st, a, n, ro); break;
+        case 4: hipLaunchKernelGGL((dots_kernel<4, UPD>), g, b, 0, st, a, n, ro); break;
+        case 5: hipLaunchKernelGGL((dots_kernel<5, UPD>), g, b, 0, st, a, n, ro); break;
+        case 6: hipLaunchKernelGGL((dots_kernel<6, UPD>), g, b, 0, st, a, n, ro); break;
+        case 7: hipLaunchKernelGGL((dots_kernel<7, UPD>), g, b, 0, st, a, n, ro); break;
+        case 8: hipLaunchKernelGGL((dots_kernel<8, UPD>), g, b, 0, st, a, n, ro); break;
+        case 9: if (!UPD) { hipLaunchKernelGGL((dots_kernel<9, false>), g, b, 0, st, a, n, ro); break; } return hipErrorInvalidValue;
+        case 10: if (!UPD) { hipLaunchKernelGGL((dots_kernel<10, false>), g, b, 0, st, a, n, ro); break; } return hipErrorInvalidValue;
+        case 11: if (!UPD) { hipLaunchKernelGGL((dots_kernel<11, false>), g, b, 0, st, a, n, ro); break; } return hipErrorInvalidValue;
+        case 12: if (!UPD) { hipLaunchKernelGGL((dots_kernel<12, false>), g, b, 0, st, a, n, ro); break; } return hipErrorInvalidValue;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
 }
 
+// (at most 8 terms when one of them is a PUPD / SQPUPD)
+hipError_t dots(const DotArgs& a, int64_t n, const RedOut& ro, hipStream_t st) {
+    bool upd = false;
+    for (int q = 0; q < a.nt && q < kMaxTerms; ++q) upd = upd || a.t[q].op == PUPD || a.t[q].op == SQPUPD;
+    return upd ? dots_launch<true>(a, n, ro, st) : dots_launch<false>(a, n, ro, st);
+}
+
 // ---------------------------------------------------------------------------
 // denoiser: vamp::g1 / vamp::g1d (src/vamp.cpp:440-492)
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void g1_g1d(double y, double gam1, const Mix& mix, double eta_max, double* g,
-                                       double* gd) {
+__device__ __forceinline__ void g1_g1d(double y, double gam1, const double* probs, const double* vars, int L,
+                                       double eta_max, double* g, double* gd) {
     const double sigma = 1 / gam1;
     if (sigma < 1e-10 && sigma > -1e-10) {
         *g = y;
@@ -1305,31 +1320,103 @@ __device__ __forceinline__ void g1_g1d(double y, double gam1, const Mix& mix, do
         return;
     }
     double pk = 0, pkd = 0, pkdd = 0;
-    for (int i = 0; i < mix.L; ++i) {
-        const double vs = mix.vars[i] + sigma;
-        const double expe_sum = -0.5 * (y * y) * (eta_max - mix.vars[i]) / vs / (eta_max + sigma);
+    for (int i = 0; i < L; ++i) {
+        const double vs = vars[i] + sigma;
+        const double expe_sum = -0.5 * (y * y) * (eta_max - vars[i]) / vs / (eta_max + sigma);
         const double ex = exp(expe_sum);
-        double z = mix.probs[i] / sqrt(vs) * ex;
+        double z = probs[i] / sqrt(vs) * ex;
         pk = pk + z;
         z = z / vs * y;
         pkd = pkd - z;
         const double z2 = z / vs * y;
-        pkdd = pkdd - mix.probs[i] / pow_1p5(vs) * ex + z2;
+        pkdd = pkdd - probs[i] / pow_1p5(vs) * ex + z2;
     }
     *g = y + sigma * pkd / pk;
     const double q = pkd / pk;
     *gd = 1 + sigma * (pkdd / pk - q * q);
 }
 
+// One EM round's update of mixture m from its sums q (1 + 2(L-1), in LDS)
+// and the merging of close variances (vamp.cpp em_finish with one round, the
+// host's expressions in the host's order: src/vamp.cpp:598-642), by ONE
+// thread, into the mixture words w (kMixWords, LDS: [0] L, probs, vars, eta_max)
+__device__ void em_update_mix(const double* q, const Mix& m, const EmUpd& u, double* w) {
+    double* pr = w + 1;
+    double* va = w + 1 + kMaxL;
+    int L = m.L;
+    for (int j = 0; j < L; ++j) {
+        pr[j] = m.probs[j];
+        va[j] = m.vars[j];
+    }
+    const double lambda_total = q[0];
+    const double lambda = lambda_total / (double)u.Mt;
+    const double sum_of_pin = lambda_total;
+    for (int j = 0; j < L - 1; ++j) {
+        const double res_total = q[1 + j];
+        const double res_gammas_total = q[L + j];
+        if (u.learn_vars == 1) va[j + 1] = res_gammas_total / res_total;
+        const double omega = res_total / sum_of_pin;
+        pr[j + 1] = lambda * omega;
+    }
+    pr[0] = 1 - lambda;
+    for (int j = 0; j < L; ++j) {  // merging close variances (src/vamp.cpp:626-642)
+        for (int k = j + 1; k < L; ++k) {
+            const double denom = va[j] != 0 ? (va[k] < va[j] ? va[k] : va[j]) : 1e-7;  // std::min
+            if (fabs(va[j] - va[k]) / denom < u.merge_vars_thr) {
+                const double sum2probs = pr[j] + pr[k];
+                for (int r = k; r + 1 < L; ++r) {
+                    va[r] = va[r + 1];
+                    pr[r] = pr[r + 1];
+                }
+                L--;
+                pr[j] = sum2probs;
+                k--;
+            }
+        }
+    }
+    double eta_max = va[0];  // (denoise: the host's loop)
+    for (int i = 1; i < L; ++i)
+        if (va[i] > eta_max) eta_max = va[i];
+    w[0] = (double)L;
+    w[1 + 2 * kMaxL] = eta_max;
+}
+
+// Dev: the EM round's update of the mixture (em_update_mix, every block
+// forms it from the round's sums; block 0 also stores it into u.mirror for the
+// host's check) and gam1 from the device (vamp_gam1); else mix and gam1
+template <bool Dev>
 __global__ __launch_bounds__(kBlock) void denoise_kernel(int64_t M, const double* __restrict__ r1, double gam1,
                                                          Mix mix, double eta_max, double* __restrict__ x1,
                                                          const double* __restrict__ x1_prev, int damp, double rho,
-                                                         double* __restrict__ x1d, RedOut ro) {
+                                                         double* __restrict__ x1d, RedOut ro, EmUpd u,
+                                                         const double* __restrict__ gam1dev) {
     __shared__ double lds[4];
+    __shared__ double sm[Dev ? kMixWords : 1];
+    __shared__ double sq[Dev ? 1 + 2 * (kMaxL - 1) : 1];
+    const double* probs = mix.probs;
+    const double* vars = mix.vars;
+    int L = mix.L;
+    if (Dev) {
+        // the sums in mapped host memory: one round trip, every load in flight
+        for (int q = threadIdx.x; q < 1 + 2 * (mix.L - 1); q += kBlock)
+            sq[q] = __hip_atomic_load(u.sums + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        gam1 = gam1dev[0];
+        __syncthreads();
+        if (threadIdx.x == 0) em_update_mix(sq, mix, u, sm);
+        __syncthreads();
+        L = (int)sm[0];
+        probs = sm + 1;
+        vars = sm + 1 + kMaxL;
+        eta_max = sm[1 + 2 * kMaxL];
+        // (no fence: the host reads the mirror only after a LATER launch has
+        // flagged it, i.e. after this launch's end-of-kernel release)
+        if (blockIdx.x == 0)
+            for (int q = threadIdx.x; q < kMixWords; q += kBlock) u.mirror[q] = sm[q];
+    }
     double acc = 0.0;
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < M; i += (int64_t)gridDim.x * kBlock) {
         double g, gd;
-        g1_g1d(r1[i], gam1, mix, eta_max, &g, &gd);
+        g1_g1d(r1[i], gam1, probs, vars, L, eta_max, &g, &gd);
         if (damp) g = rho * g + (1 - rho) * x1_prev[i];  // src/vamp.cpp:208-211
         x1[i] = g;
         x1d[i] = gd;
@@ -1341,12 +1428,19 @@ __global__ __launch_bounds__(kBlock) void denoise_kernel(int64_t M, const double
 }
 
 hipError_t denoise(int64_t M, const double* r1, double gam1, const Mix& mix, double* x1, const double* x1_prev,
-                   int damp, double rho, double* x1d, const RedOut& ro, hipStream_t st) {
+                   int damp, double rho, double* x1d, const RedOut& ro, hipStream_t st, const EmUpd* em,
+                   const double* gam1dev) {
     double eta_max = mix.vars[0];
     for (int i = 1; i < mix.L; ++i)
         if (mix.vars[i] > eta_max) eta_max = mix.vars[i];
-    hipLaunchKernelGGL(denoise_kernel, dim3(red_blocks(M)), dim3(kBlock), 0, st, M, r1, gam1, mix, eta_max, x1,
-                       x1_prev, damp, rho, x1d, ro);
+    if (em) {
+        if (!gam1dev || !em->sums || !em->mirror || mix.L < 1 || mix.L > kMaxL) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(denoise_kernel<true>, dim3(red_blocks(M)), dim3(kBlock), 0, st, M, r1, gam1, mix, eta_max,
+                           x1, x1_prev, damp, rho, x1d, ro, *em, gam1dev);
+    } else {
+        hipLaunchKernelGGL(denoise_kernel<false>, dim3(red_blocks(M)), dim3(kBlock), 0, st, M, r1, gam1, mix,
+                           eta_max, x1, x1_prev, damp, rho, x1d, ro, EmUpd{}, nullptr);
+    }
     return hipGetLastError();
 }
 
@@ -1839,7 +1933,7 @@ __global__ __launch_bounds__(kBlock) void cg_update_kernel(int64_t M, CgVecs c, 
                 if (on[k]) {
                     ar[k] = c.AR[k][i];
                     qo[k] = fk[k] ? c.Q[k][i] : 0.0;
-                    ad[k] = c.AD[k][i];
+                    ad[k] = c.addiv > 0 ? c.AD[k][i] / c.addiv : c.AD[k][i];  // (vec_div's division)
                     aw[k] = c.AW[k] ? c.AW[k][i] : 0.0;
                 }
 #pragma unroll

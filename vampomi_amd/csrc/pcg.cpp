@@ -267,8 +267,10 @@ vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double
             cu.adpart = c->op_part;
             cu.adld = c->ld;
             cu.adslots = c->opp.nslots;
-            cu.addiv = c->sqrtN;
         }
+        // the division of A d by sqrt(N) happens where cg_update reads it
+        // (several ranks: the all-reduced A d, op_dev(..., divide = false))
+        cu.addiv = c->sqrtN;
         bool rec = false;
         for (int k = 0; k < K; ++k) rec = rec || sys[k]->W;
         if (rec)
@@ -295,6 +297,7 @@ vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double
             STCHK(op_dev_plain(c, a, px, out, gate));
             vk::CgVecs ch = cu;
             if (!c->use_comm) ch.adslots = (int)c->opp_hs.nslots;
+            else ch.addiv = 0.0;  // (op_dev_plain divided its A d already)
             const double* dp = c->use_comm ? AD + (int64_t)(1 + vk::kOpPlain) * c->ld : c->scal + SL_DP;
             const vk::RedOut ro{c->red_part, c->scal + SL_CG, c->ticket, nullptr, 0, gate};
             vk::CgDecide dc{};  // no mirror, no flag: the host does not wait for this step
@@ -329,7 +332,7 @@ vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double
             a.diag = diag;
             a.tau = tau;
             a.gam2 = gam2;
-            STCHK(op_dev(c, K, a, gate, c->use_comm));
+            STCHK(op_dev(c, K, a, gate, c->use_comm, false));
             const double* dp = c->use_comm ? AD + (int64_t)K * c->ld : c->scal + SL_DP;
             const vk::RedOut ro{c->red_part, c->scal + SL_CG, c->ticket, nullptr, 0, gate};
             *seq = ++c->sync_seq;

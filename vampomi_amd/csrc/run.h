@@ -59,6 +59,13 @@ struct VampRun {
     double* ax2 = nullptr;  // arec: A x2, carried from iteration to iteration
     double* abern = nullptr;      // the head start: A.bern of iteration hs_it in slot hs_it & 1 (2 x ld)
     double* bern_next = nullptr;  // ... and the next iteration's probe (M)
+    // the device EM update (vk::denoise's em): the mixture it formed, in
+    // mapped host memory, checked against the host's update (mix_expect) once
+    // a later launch has flagged (check_device_mix)
+    double* mixh = nullptr;
+    double* mixh_dev = nullptr;
+    bool mix_pending = false;
+    Mixture mix_expect;
     const double* z1 = nullptr;
     int64_t passes_ref = 0;
     // probit (src/vamp_probit.cpp) state
@@ -106,8 +113,11 @@ vampomi_status em_begin(vampomi_ctx* c, const EmParams& P, const Mixture& m, dou
 vampomi_status em_queue(vampomi_ctx* c, const Mixture& m, double gam1, const double* r1, DotBatch& b, EmState& s,
                         const R1From* r1from = nullptr);
 vampomi_status em_finish(vampomi_ctx* c, const EmParams& P, Mixture& m, double gam1, const double* r1, EmState& s);
+// em / gam1dev (may be null): m after one EM round, and gam1, formed on the
+// device (vk::denoise)
 vampomi_status denoise_into(vampomi_ctx* c, const Mixture& m, double gam1, const double* r1, double* x1,
-                            const double* x1_prev, bool damp, double rho, double* x1d, DotBatch& b, double* sum_out);
+                            const double* x1_prev, bool damp, double rho, double* x1d, DotBatch& b, double* sum_out,
+                            const vk::EmUpd* em = nullptr, const double* gam1dev = nullptr);
 vampomi_status upload_or_zero(vampomi_ctx* c, double* dst, const double* host, int64_t n);
 // queues this iteration's x1/sqrt(N), r1/sqrt(N) for the _it_K.bin /
 // _r1_it_K.bin files and the x1/r1 history (R.writer)

@@ -43,6 +43,7 @@ VampRun::~VampRun() {
                        &nb3, &nsc, &ax2, &p1, &p2, &z1h, &x1s, &x1sn, &x2s, &abern, &bern_next})
         dev_free(*p);
     for (auto& p : cgw) dev_free(p);
+    if (mixh) (void)hipHostFree(mixh);
 }
 
 vampomi_ctx::vampomi_ctx() = default;
@@ -173,7 +174,7 @@ vampomi_status update_prior(vampomi_ctx* c, const VampRun& R, Mixture& m, double
 // x1 = g1(r1) [damped], x1d = g1d(r1); sum of x1d over ranks queued in b
 vampomi_status denoise_into(vampomi_ctx* c, const Mixture& m, double gam1, const double* r1, double* x1,
                                    const double* x1_prev, bool damp, double rho, double* x1d, DotBatch& b,
-                                   double* sum_out) {
+                                   double* sum_out, const vk::EmUpd* em, const double* gam1dev) {
     vk::Mix mix{};
     mix.L = m.L;
     for (int j = 0; j < m.L; ++j) {
@@ -182,19 +183,24 @@ vampomi_status denoise_into(vampomi_ctx* c, const Mixture& m, double gam1, const
     }
     vk::RedOut ro{};
     STCHK(b.sink(1, true, sum_out, &ro));  // :214-222
-    HIPCHK(vk::denoise(c->M, r1, gam1, mix, x1, x1_prev, damp ? 1 : 0, rho, x1d, ro, b.stream()));
+    HIPCHK(vk::denoise(c->M, r1, gam1, mix, x1, x1_prev, damp ? 1 : 0, rho, x1d, ro, b.stream(), em, gam1dev));
     return VAMPOMI_OK;
 }
 
 // err_measures (src/vamp.cpp:760-852): the reductions (queued) ...  xm / xn:
 // another group of reductions over M / over N that shares the launch (one
 // kernel per vector length instead of one per group)
-static vampomi_status err_queue(vampomi_ctx* c, VampRun& R, const double* xhat, const double* Axest, DotBatch& b,
-                                double* m3, double* n2, double* s3, std::vector<DotBatch::Group> gm = {},
-                                std::vector<DotBatch::Group> gn = {}) {
+static void err_groups(vampomi_ctx* c, VampRun& R, const double* xhat, const double* Axest, double* m3, double* n2,
+                       double* s3, std::vector<DotBatch::Group>& gm, std::vector<DotBatch::Group>& gn) {
     gm.push_back({{T(xhat, R.ts), T(xhat, xhat), T(R.ts, R.ts)}, true, m3});
     gn.push_back({{T(c->y, Axest, vk::DIFF2), T(c->y, c->y)}, false, n2});  // l2_norm2(., 0)
     gn.push_back({{T(Axest, c->y), T(Axest, Axest), T(c->y, c->y)}, true, s3});
+}
+
+static vampomi_status err_queue(vampomi_ctx* c, VampRun& R, const double* xhat, const double* Axest, DotBatch& b,
+                                double* m3, double* n2, double* s3, std::vector<DotBatch::Group> gm = {},
+                                std::vector<DotBatch::Group> gn = {}) {
+    err_groups(c, R, xhat, Axest, m3, n2, s3, gm, gn);
     STCHK(b.add_many(c->M, gm));
     return b.add_many(c->N, gn);
 }
@@ -240,6 +246,8 @@ static vampomi_status vamp_alloc(vampomi_ctx* c, VampRun& R) {
     STCHK(dev_alloc(&R.nsc, vk::kMaxRhs * ld));
     STCHK(dev_alloc(&R.ax2, ld));
     STCHK(dev_alloc(&R.abern, 2 * ld));  // two slots: A.bern of it (consumed in place) and of it + 1
+    HIPCHK(hipHostMalloc((void**)&R.mixh, vk::kMixWords * sizeof(double), hipHostMallocMapped | hipHostMallocCoherent));
+    HIPCHK(hipHostGetDevicePointer((void**)&R.mixh_dev, R.mixh, 0));
     HIPCHK(hipMemsetAsync(R.ax2, 0, ld * 8, c->st));
     HIPCHK(hipMemsetAsync(R.abern, 0, 2 * ld * 8, c->st));
     HIPCHK(hipMemsetAsync(R.z1buf, 0, ld * 8, c->st));
@@ -399,6 +407,21 @@ vampomi_status end_iteration_io(vampomi_ctx* c, VampRun& R) {
     return VAMPOMI_OK;
 }
 
+// The mixture the device denoised with (devem) is the host's, bit for bit.
+// Called once a launch queued after that denoising has flagged the host (its
+// stores are then visible) and before the next denoising overwrites them.
+static vampomi_status check_device_mix(VampRun& R) {
+    if (!R.mix_pending) return VAMPOMI_OK;
+    R.mix_pending = false;
+    const Mixture& m = R.mix_expect;
+    bool same = (double)m.L == R.mixh[0];
+    for (int j = 0; same && j < m.L; ++j)
+        same = std::memcmp(&m.probs[j], &R.mixh[1 + j], 8) == 0 &&
+               std::memcmp(&m.vars[j], &R.mixh[1 + vk::kMaxL + j], 8) == 0;
+    if (!same) return fail(VAMPOMI_ERR_STATE, "vamp: the device's EM update differs from the host's");
+    return VAMPOMI_OK;
+}
+
 // one VAMP iteration (src/vamp.cpp:148-428)
 extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
     CollScope cs_(c);
@@ -547,6 +570,7 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
         STCHK(pcg_run(c, {&sx}, R.gamw, R.gam2, R.prm.CG_max_iter, R.prm.CG_err_tol, R.nsc, &R.passes_ref, &e1));
         STCHK(pcg_run(c, {&so}, R.gamw, R.gam2, R.prm.CG_max_iter, R.prm.CG_err_tol, R.nsc, &R.passes_ref, nullptr));
     }
+    STCHK(check_device_mix(R));  // (the solves' flags came after the previous iteration's denoising)
     if (res && res->cg_iters) res->cg_iters[it - 1] = sx.iters;
     if (res && res->ons_iters) res->ons_iters[it - 1] = so.iters;
     // r1 (:348-350): its own launch, or (the side stream's EM round below)
@@ -572,8 +596,25 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
     // (batch_rhs >= 3: on the side stream, beside the reductions below)
     DotBatch fin(c);
     double* dsc = c->scal + SL_CHAIN;
+    // updateNoisePrec's two sums (:508-521) and the NMSE sums (:409-413); with
+    // arec they ride in err_measures' launches (one per vector length)
+    const DotBatch::Group gtc{{T(R.bern, R.tmpM)}, true, &R.tc};  // <u, A^T A invQ>
+    const DotBatch::Group gtn{{T(R.ax2, c->y, vk::DIFF2)}, false, &R.tn};  // l2_norm2(temp, 0), temp = A x2 - y
+    const DotBatch::Group gnm{{T(R.x1p, R.x1, vk::DIFF2), T(R.x1p, R.x1p)}, true, R.nm};
     if (chain) {
-        STCHK(err_queue(c, R, R.x1, R.z1, fin, R.e1m, R.e1n, R.e1s, {ga2}));  // :272
+        // every reduction of the iteration's tail reads vectors the solves have
+        // just finished: err_measures of x1 (:272) and of x2 (:365, A x2 from
+        // the CG) with the sums above, ONE launch per vector length (10 terms
+        // over M, 11 over N); each term's sum is the same fixed-order reduction
+        // as in its own launch (the launch geometry depends on the length only)
+        std::vector<DotBatch::Group> gm{ga2}, gn;
+        err_groups(c, R, R.x1, R.z1, R.e1m, R.e1n, R.e1s, gm, gn);
+        gm.push_back(gtc);
+        gm.push_back(gnm);
+        gn.push_back(gtn);
+        err_groups(c, R, R.x2, R.ax2, R.e2m, R.e2n, R.e2s, gm, gn);
+        STCHK(fin.add_many(M, gm));
+        STCHK(fin.add_many(N, gn));
         const double* a2dev = fin.dev_result(&R.a2);
         if (!a2dev) return fail(VAMPOMI_ERR_STATE, "vamp: alpha2's sum has no device address");
         HIPCHK(vk::vamp_gam1(a2dev, R.gam2, R.prm.rho, gam1_prev, dsc, c->st));
@@ -589,6 +630,12 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
     }
     R1From r1from{R.x2, R.r2, R.eta2, R.gam2, R.gam1};
     if (chain) r1from.dsc = dsc;
+    // devem (the chain, one EM round): the EM update of the mixture and the
+    // next denoising (one launch: vk::denoise's em) follow the EM round with no
+    // host wait between them; the host forms the same mixture from the same
+    // sums at the iteration's one flush, and checks it against the device's,
+    // bit for bit
+    const bool devem = chain && R.prm.EM_max_iter == 1;
     EmState em;
     if (next) R.mix_next = R.mix;
     if (next && arec) {  // the side stream starts from r1 and x1; its EM sums are queued before these reductions
@@ -596,6 +643,17 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
         if (em_next) {
             STCHK(fin.side(true));
             STCHK(em_begin(c, em_params(R), R.mix_next, R.gam1, R.r1, fin, em, r1_in_em ? &r1from : nullptr));
+            if (devem) {
+                vk::EmUpd eu;
+                eu.sums = fin.dev_result(em.sums);
+                if (!eu.sums) return fail(VAMPOMI_ERR_STATE, "vamp: the EM sums have no device address");
+                eu.Mt = Mt;
+                eu.learn_vars = R.prm.learn_vars;
+                eu.merge_vars_thr = R.prm.merge_vars_thr;
+                eu.mirror = R.mixh_dev;
+                STCHK(denoise_into(c, R.mix_next, R.gam1, R.r1, R.x1n, R.x1, true, R.prm.rho, R.x1d, fin, &R.sum_d,
+                                   &eu, dsc));
+            }
             STCHK(fin.side(false));
         }
     }
@@ -606,13 +664,10 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
 
     // ---- updateNoisePrec (:504-529) + the next z1 in the same pass ----
     const double* ax2 = R.nb3;  // A.x2_hat
-    // updateNoisePrec's two sums ride in err_measures' launches (one per length)
-    DotBatch::Group gtn{{}, false, &R.tn}, gtc{{T(R.bern, R.tmpM)}, true, &R.tc};  // l2_norm2(temp, 0); <u, A^T A invQ>
     bool shared = false;
     if (arec) {  // no pass: A x2 came with the CG, the next z1 comes with the next CG
         ax2 = R.ax2;
         R.passes_ref += 3;  // :508, :518, :519
-        gtn.terms = {T(R.ax2, c->y, vk::DIFF2)};
         shared = true;
     } else if (rec) {  // A.x2 and the next z1 in one pass; the A^T products came with the CG
         const double* xs[2] = {R.x2, R.x1n};
@@ -635,11 +690,10 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
         STCHK(fin.add({T(R.bern, R.tmpM)}, M, true, &R.tc));
     }
     // (shared: the NMSE sums (:409-413) too; they read x1 and x1_prev, which
-    // the prefetched denoising below does not write)
-    const DotBatch::Group gnm{{T(R.x1p, R.x1, vk::DIFF2), T(R.x1p, R.x1p)}, true, R.nm};
-    if (shared)
+    // the prefetched denoising below does not write; chain: queued above)
+    if (shared && !chain)
         STCHK(err_queue(c, R, R.x2, ax2, fin, R.e2m, R.e2n, R.e2s, {gtc, gnm}, {gtn}));  // :365 (A.x2_hat of :826)
-    else
+    else if (!shared)
         STCHK(err_queue(c, R, R.x2, ax2, fin, R.e2m, R.e2n, R.e2s));
     R.passes_ref += 1;
     // Second stream (batch_rhs >= 3, north_star): iteration it+1's EM sums run
@@ -648,18 +702,24 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
     // the NMSE sums, again one all-reduce and one wait. Every reduction is the
     // same fixed-order kernel as on one stream, so the values are bitwise the
     // same (tests/test_gpu_sharded.py::test_side_stream_bitwise)
-    if (next && arec && em_next) {
+    if (next && arec && em_next && !devem) {
         STCHK(fin.flush());
         if (chain) host_gam1();  // (the device formed the same values for the EM round)
         STCHK(em_finish(c, em_params(R), R.mix_next, R.gam1, R.r1, em));
     }
-    if (next && arec) {
+    if (next && arec && !devem) {
         STCHK(fin.side(true));  // forks again after an EM flush
         STCHK(denoise_into(c, R.mix_next, R.gam1, R.r1, R.x1n, R.x1, true, R.prm.rho, R.x1d, fin, &R.sum_d));
         STCHK(fin.side(false));
     }
     if (!shared) STCHK(fin.add_many(M, {gnm}));  // NMSE (:409-413)
     STCHK(fin.flush());
+    if (devem) {
+        host_gam1();  // (the device formed the same values)
+        STCHK(em_finish(c, em_params(R), R.mix_next, R.gam1, R.r1, em));
+        R.mix_expect = R.mix_next;  // checked after the next solves (or at the end)
+        R.mix_pending = true;
+    }
     const double trace_corr = R.tc * (double)Mt;  // :521
     if (R.prm.verbosity >= 1 && c->rank == 0)
         std::printf("l2_norm2(temp) / N = %g\ntrace_correction / N = %g\n", R.tn / (double)N, trace_corr / (double)N);
@@ -703,6 +763,14 @@ extern "C" vampomi_status vampomi_vamp_end(vampomi_ctx* c) {
         if (R.writer->drain(&msg)) {
             c->run.reset();
             return fail(VAMPOMI_ERR_IO, msg);
+        }
+    }
+    if (R.mix_pending) {  // the last device EM update (one rank: a stream sync)
+        STCHK(host_sync(c));
+        const vampomi_status s = check_device_mix(R);
+        if (s != VAMPOMI_OK) {
+            c->run.reset();
+            return s;
         }
     }
     if (res) {
