@@ -216,25 +216,24 @@ struct Mix {
 // The mixture words of the device EM update, kMixWords doubles: [0] L,
 // [1, 1 + kMaxL) probs, [1 + kMaxL, 1 + 2 kMaxL) vars, [1 + 2 kMaxL] eta_max
 constexpr int kMixWords = 2 + 2 * kMaxL;
-// one EM round's update of the mixture, formed on the device (denoise's em)
+// x1 = g1(r1) (then rho*x1 + (1-rho)*x1_prev if damp), x1d = g1d(r1),
+// sum of x1d in ro.out[0].  mixw / gam1dev (may be null): the mixture's words
+// (kMixWords, device: an EM round's update, em_sums' upd) and gam1 (vamp_gam1)
+// from the device instead of mix and gam1.
+hipError_t denoise(int64_t M, const double* r1, double gam1, const Mix& mix, double* x1,
+                   const double* x1_prev, int damp, double rho, double* x1d, const RedOut& ro, hipStream_t st,
+                   const double* mixw = nullptr, const double* gam1dev = nullptr);
+
+// ---- EM prior update (vamp::updatePrior) per-marker sums --------------------
+// the round's update of the mixture, formed on the device by the launch that
+// finishes the round's sums (em_sums): out non-null
 struct EmUpd {
-    const double* sums = nullptr;  // em_sums' ro.out (mapped host memory: one rank), Q = 1 + 2(L-1)
     int64_t Mt = 0;
     int learn_vars = 0;
     double merge_vars_thr = 0.0;
-    double* mirror = nullptr;      // the updated mixture's words (mapped host memory), for the host's check
+    double* out = nullptr;     // the updated mixture's words (kMixWords, device: denoise's mixw)
+    double* mirror = nullptr;  // the same words in mapped host memory, for the host's check
 };
-// x1 = g1(r1) (then rho*x1 + (1-rho)*x1_prev if damp), x1d = g1d(r1),
-// sum of x1d in ro.out[0].  em / gam1dev (may be null): the mixture is mix
-// after one EM round from em->sums and the merging of close variances
-// (vamp.cpp em_finish with EM_max_iter = 1, src/vamp.cpp:598-642: the host's
-// expressions, bit for bit), formed in the launch, and gam1 is gam1dev[0]
-// (vamp_gam1), instead of mix and gam1.
-hipError_t denoise(int64_t M, const double* r1, double gam1, const Mix& mix, double* x1,
-                   const double* x1_prev, int damp, double rho, double* x1d, const RedOut& ro, hipStream_t st,
-                   const EmUpd* em = nullptr, const double* gam1dev = nullptr);
-
-// ---- EM prior update (vamp::updatePrior) per-marker sums --------------------
 struct EmArgs {
     double omegas[kMaxL];
     double vars[kMaxL];
@@ -252,6 +251,11 @@ struct EmArgs {
     // device (vamp_gam1), and noise_var = 1/gam1, v[j-1] = 1/(1/vars[j] + gam1)
     // are formed here, with the host's expressions (the host fields are unused)
     const double* dsc;
+    // upd.out (may be null): the launch's last block also forms this round's
+    // update of the mixture (vars and L here; vamp.cpp em_finish with one
+    // round and the merging of close variances, src/vamp.cpp:598-642: the
+    // host's expressions, bit for bit) into upd.out and upd.mirror
+    EmUpd upd;
 };
 // one thread, after the reduction that produced a2 = <bern, invQ> (src/vamp.cpp:
 // 341-346, 498): alpha2 = gam2*a2, eta2 = gam2/alpha2, gam1 = rho*min(max(eta2 -

@@ -1308,6 +1308,8 @@ hipError_t dots(const DotArgs& a, int64_t n, const RedOut& ro, hipStream_t st) {
     return upd ? dots_launch<true>(a, n, ro, st) : dots_launch<false>(a, n, ro, st);
 }
 
+constexpr int Q_MAX_EM = 1 + 2 * (kMaxL - 1);  // an EM round's sums
+
 // ---------------------------------------------------------------------------
 // denoiser: vamp::g1 / vamp::g1d (src/vamp.cpp:440-492)
 // ---------------------------------------------------------------------------
@@ -1336,18 +1338,15 @@ __device__ __forceinline__ void g1_g1d(double y, double gam1, const double* prob
     *gd = 1 + sigma * (pkdd / pk - q * q);
 }
 
-// One EM round's update of mixture m from its sums q (1 + 2(L-1), in LDS)
-// and the merging of close variances (vamp.cpp em_finish with one round, the
-// host's expressions in the host's order: src/vamp.cpp:598-642), by ONE
-// thread, into the mixture words w (kMixWords, LDS: [0] L, probs, vars, eta_max)
-__device__ void em_update_mix(const double* q, const Mix& m, const EmUpd& u, double* w) {
+// One EM round's update of the mixture (L components, variances vars) from
+// the round's sums q (1 + 2(L-1)) and the merging of close variances
+// (vamp.cpp em_finish with one round, the host's expressions in the host's
+// order: src/vamp.cpp:598-642; every prob is rewritten), by ONE thread, into
+// the mixture words w (kMixWords, LDS: [0] L, probs, vars, eta_max)
+__device__ void em_update_mix(const double* q, int L, const double* vars, const EmUpd& u, double* w) {
     double* pr = w + 1;
     double* va = w + 1 + kMaxL;
-    int L = m.L;
-    for (int j = 0; j < L; ++j) {
-        pr[j] = m.probs[j];
-        va[j] = m.vars[j];
-    }
+    for (int j = 0; j < L; ++j) va[j] = vars[j];
     const double lambda_total = q[0];
     const double lambda = lambda_total / (double)u.Mt;
     const double sum_of_pin = lambda_total;
@@ -1381,37 +1380,28 @@ __device__ void em_update_mix(const double* q, const Mix& m, const EmUpd& u, dou
     w[1 + 2 * kMaxL] = eta_max;
 }
 
-// Dev: the EM round's update of the mixture (em_update_mix, every block
-// forms it from the round's sums; block 0 also stores it into u.mirror for the
-// host's check) and gam1 from the device (vamp_gam1); else mix and gam1
+// Dev: the mixture's words (an EM round's update, em_kernel) and gam1
+// (vamp_gam1) from the device, the words staged in LDS; else mix and gam1
 template <bool Dev>
 __global__ __launch_bounds__(kBlock) void denoise_kernel(int64_t M, const double* __restrict__ r1, double gam1,
                                                          Mix mix, double eta_max, double* __restrict__ x1,
                                                          const double* __restrict__ x1_prev, int damp, double rho,
-                                                         double* __restrict__ x1d, RedOut ro, EmUpd u,
+                                                         double* __restrict__ x1d, RedOut ro,
+                                                         const double* __restrict__ mixw,
                                                          const double* __restrict__ gam1dev) {
     __shared__ double lds[4];
     __shared__ double sm[Dev ? kMixWords : 1];
-    __shared__ double sq[Dev ? 1 + 2 * (kMaxL - 1) : 1];
     const double* probs = mix.probs;
     const double* vars = mix.vars;
     int L = mix.L;
     if (Dev) {
-        // the sums in mapped host memory: one round trip, every load in flight
-        for (int q = threadIdx.x; q < 1 + 2 * (mix.L - 1); q += kBlock)
-            sq[q] = __hip_atomic_load(u.sums + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        for (int q = threadIdx.x; q < kMixWords; q += kBlock) sm[q] = mixw[q];
         gam1 = gam1dev[0];
-        __syncthreads();
-        if (threadIdx.x == 0) em_update_mix(sq, mix, u, sm);
         __syncthreads();
         L = (int)sm[0];
         probs = sm + 1;
         vars = sm + 1 + kMaxL;
         eta_max = sm[1 + 2 * kMaxL];
-        // (no fence: the host reads the mirror only after a LATER launch has
-        // flagged it, i.e. after this launch's end-of-kernel release)
-        if (blockIdx.x == 0)
-            for (int q = threadIdx.x; q < kMixWords; q += kBlock) u.mirror[q] = sm[q];
     }
     double acc = 0.0;
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < M; i += (int64_t)gridDim.x * kBlock) {
@@ -1428,18 +1418,18 @@ __global__ __launch_bounds__(kBlock) void denoise_kernel(int64_t M, const double
 }
 
 hipError_t denoise(int64_t M, const double* r1, double gam1, const Mix& mix, double* x1, const double* x1_prev,
-                   int damp, double rho, double* x1d, const RedOut& ro, hipStream_t st, const EmUpd* em,
+                   int damp, double rho, double* x1d, const RedOut& ro, hipStream_t st, const double* mixw,
                    const double* gam1dev) {
     double eta_max = mix.vars[0];
     for (int i = 1; i < mix.L; ++i)
         if (mix.vars[i] > eta_max) eta_max = mix.vars[i];
-    if (em) {
-        if (!gam1dev || !em->sums || !em->mirror || mix.L < 1 || mix.L > kMaxL) return hipErrorInvalidValue;
+    if (mixw) {
+        if (!gam1dev) return hipErrorInvalidValue;
         hipLaunchKernelGGL(denoise_kernel<true>, dim3(red_blocks(M)), dim3(kBlock), 0, st, M, r1, gam1, mix, eta_max,
-                           x1, x1_prev, damp, rho, x1d, ro, *em, gam1dev);
+                           x1, x1_prev, damp, rho, x1d, ro, mixw, gam1dev);
     } else {
         hipLaunchKernelGGL(denoise_kernel<false>, dim3(red_blocks(M)), dim3(kBlock), 0, st, M, r1, gam1, mix,
-                           eta_max, x1, x1_prev, damp, rho, x1d, ro, EmUpd{}, nullptr);
+                           eta_max, x1, x1_prev, damp, rho, x1d, ro, nullptr, nullptr);
     }
     return hipGetLastError();
 }
@@ -1501,7 +1491,21 @@ __global__ __launch_bounds__(kBlock) void em_kernel(int64_t M, const double* __r
     __syncthreads();
     for (int q = threadIdx.x; q < Q; q += kBlock)
         red_put(ro, (int64_t)blockIdx.x * Q + q, ((wl[0][q] + wl[1][q]) + wl[2][q]) + wl[3][q]);
-    red_finish(ro, Q, lds);
+    __shared__ double fin[Q_MAX_EM];
+    const bool last = red_finish(ro, Q, lds, a.upd.out ? fin : nullptr);
+    if (last && a.upd.out && threadIdx.x == 0) {  // the round's update of the mixture (EmArgs.upd)
+        __shared__ double w[kMixWords];
+        em_update_mix(fin, L, a.vars, a.upd, w);
+        const int Ln = (int)w[0];
+        for (double* o : {a.upd.out, a.upd.mirror}) {
+            o[0] = w[0];
+            for (int j = 0; j < Ln; ++j) {
+                o[1 + j] = w[1 + j];
+                o[1 + kMaxL + j] = w[1 + kMaxL + j];
+            }
+            o[1 + 2 * kMaxL] = w[1 + 2 * kMaxL];
+        }
+    }
 }
 
 __global__ void vamp_gam1_kernel(const double* __restrict__ a2, double gam2, double rho, double gam1_prev,

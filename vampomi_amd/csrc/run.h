@@ -59,9 +59,11 @@ struct VampRun {
     double* ax2 = nullptr;  // arec: A x2, carried from iteration to iteration
     double* abern = nullptr;      // the head start: A.bern of iteration hs_it in slot hs_it & 1 (2 x ld)
     double* bern_next = nullptr;  // ... and the next iteration's probe (M)
-    // the device EM update (vk::denoise's em): the mixture it formed, in
-    // mapped host memory, checked against the host's update (mix_expect) once
-    // a later launch has flagged (check_device_mix)
+    // the device EM update (vk::EmArgs.upd): the mixture it formed (device
+    // words, read by the next denoising) and its mapped host mirror, checked
+    // against the host's update (mix_expect) once a later launch has flagged
+    // (check_device_mix)
+    double* mixw = nullptr;
     double* mixh = nullptr;
     double* mixh_dev = nullptr;
     bool mix_pending = false;
@@ -108,16 +110,18 @@ struct R1From {
     double eta2, gam2, gam1;
     const double* dsc = nullptr;  // device: gam1, eta2 (vk::vamp_gam1); then eta2 and gam1 above are unused
 };
+// upd (may be null, one round): the round's launch also forms the update of
+// the mixture on the device (vk::EmArgs.upd)
 vampomi_status em_begin(vampomi_ctx* c, const EmParams& P, const Mixture& m, double gam1, const double* r1,
-                        DotBatch& b, EmState& s, const R1From* r1from = nullptr);
+                        DotBatch& b, EmState& s, const R1From* r1from = nullptr, const vk::EmUpd* upd = nullptr);
 vampomi_status em_queue(vampomi_ctx* c, const Mixture& m, double gam1, const double* r1, DotBatch& b, EmState& s,
-                        const R1From* r1from = nullptr);
+                        const R1From* r1from = nullptr, const vk::EmUpd* upd = nullptr);
 vampomi_status em_finish(vampomi_ctx* c, const EmParams& P, Mixture& m, double gam1, const double* r1, EmState& s);
-// em / gam1dev (may be null): m after one EM round, and gam1, formed on the
-// device (vk::denoise)
+// mixw / gam1dev (may be null): the mixture's words and gam1 from the device
+// (vk::denoise)
 vampomi_status denoise_into(vampomi_ctx* c, const Mixture& m, double gam1, const double* r1, double* x1,
                             const double* x1_prev, bool damp, double rho, double* x1d, DotBatch& b, double* sum_out,
-                            const vk::EmUpd* em = nullptr, const double* gam1dev = nullptr);
+                            const double* mixw = nullptr, const double* gam1dev = nullptr);
 vampomi_status upload_or_zero(vampomi_ctx* c, double* dst, const double* host, int64_t n);
 // queues this iteration's x1/sqrt(N), r1/sqrt(N) for the _it_K.bin /
 // _r1_it_K.bin files and the x1/r1 history (R.writer)

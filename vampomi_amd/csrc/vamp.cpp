@@ -43,6 +43,7 @@ VampRun::~VampRun() {
                        &nb3, &nsc, &ax2, &p1, &p2, &z1h, &x1s, &x1sn, &x2s, &abern, &bern_next})
         dev_free(*p);
     for (auto& p : cgw) dev_free(p);
+    dev_free(mixw);
     if (mixh) (void)hipHostFree(mixh);
 }
 
@@ -60,18 +61,18 @@ vampomi_ctx::~vampomi_ctx() {
 // into b; after b.flush(), em_finish does its host part, the further rounds
 // (each with its own batch) and the merge.  update_prior runs both.
 vampomi_status em_begin(vampomi_ctx* c, const EmParams& P, const Mixture& m, double gam1, const double* r1,
-                        DotBatch& b, EmState& s, const R1From* r1from) {
+                        DotBatch& b, EmState& s, const R1From* r1from, const vk::EmUpd* upd) {
     s.emit = 0;
     s.lambda = 1 - m.probs[0];
     for (int j = 0; j < m.L; ++j) s.omegas[j] = m.probs[j];
     for (int j = 1; j < m.L; ++j) s.omegas[j] /= s.lambda;
     if (P.EM_max_iter < 1) return VAMPOMI_OK;
-    return em_queue(c, m, gam1, r1, b, s, r1from);
+    return em_queue(c, m, gam1, r1, b, s, r1from, upd);
 }
 
 // one EM round's per-slab sums (:555-597) into b, on b's current stream
 vampomi_status em_queue(vampomi_ctx* c, const Mixture& m, double gam1, const double* r1, DotBatch& b,
-                        EmState& s, const R1From* r1from) {
+                        EmState& s, const R1From* r1from, const vk::EmUpd* upd) {
     const int L = m.L;
     double max_sigma = m.vars[0];
     for (int j = 1; j < L; ++j) max_sigma = smax(max_sigma, m.vars[j]);  // std::max_element
@@ -95,6 +96,7 @@ vampomi_status em_queue(vampomi_ctx* c, const Mixture& m, double gam1, const dou
         a.r1out = const_cast<double*>(r1);
         a.dsc = r1from->dsc;
     }
+    if (upd) a.upd = *upd;
     vk::RedOut ro{};
     STCHK(b.sink(1 + 2 * (L - 1), true, s.sums, &ro));  // :578, :596-597
     HIPCHK(vk::em_sums(c->M, r1, a, ro, b.stream()));
@@ -174,7 +176,7 @@ vampomi_status update_prior(vampomi_ctx* c, const VampRun& R, Mixture& m, double
 // x1 = g1(r1) [damped], x1d = g1d(r1); sum of x1d over ranks queued in b
 vampomi_status denoise_into(vampomi_ctx* c, const Mixture& m, double gam1, const double* r1, double* x1,
                                    const double* x1_prev, bool damp, double rho, double* x1d, DotBatch& b,
-                                   double* sum_out, const vk::EmUpd* em, const double* gam1dev) {
+                                   double* sum_out, const double* mixw, const double* gam1dev) {
     vk::Mix mix{};
     mix.L = m.L;
     for (int j = 0; j < m.L; ++j) {
@@ -183,7 +185,7 @@ vampomi_status denoise_into(vampomi_ctx* c, const Mixture& m, double gam1, const
     }
     vk::RedOut ro{};
     STCHK(b.sink(1, true, sum_out, &ro));  // :214-222
-    HIPCHK(vk::denoise(c->M, r1, gam1, mix, x1, x1_prev, damp ? 1 : 0, rho, x1d, ro, b.stream(), em, gam1dev));
+    HIPCHK(vk::denoise(c->M, r1, gam1, mix, x1, x1_prev, damp ? 1 : 0, rho, x1d, ro, b.stream(), mixw, gam1dev));
     return VAMPOMI_OK;
 }
 
@@ -246,6 +248,7 @@ static vampomi_status vamp_alloc(vampomi_ctx* c, VampRun& R) {
     STCHK(dev_alloc(&R.nsc, vk::kMaxRhs * ld));
     STCHK(dev_alloc(&R.ax2, ld));
     STCHK(dev_alloc(&R.abern, 2 * ld));  // two slots: A.bern of it (consumed in place) and of it + 1
+    STCHK(dev_alloc(&R.mixw, vk::kMixWords));
     HIPCHK(hipHostMalloc((void**)&R.mixh, vk::kMixWords * sizeof(double), hipHostMallocMapped | hipHostMallocCoherent));
     HIPCHK(hipHostGetDevicePointer((void**)&R.mixh_dev, R.mixh, 0));
     HIPCHK(hipMemsetAsync(R.ax2, 0, ld * 8, c->st));
@@ -630,9 +633,9 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
     }
     R1From r1from{R.x2, R.r2, R.eta2, R.gam2, R.gam1};
     if (chain) r1from.dsc = dsc;
-    // devem (the chain, one EM round): the EM update of the mixture and the
-    // next denoising (one launch: vk::denoise's em) follow the EM round with no
-    // host wait between them; the host forms the same mixture from the same
+    // devem (the chain, one EM round): the EM round's launch also forms the
+    // update of the mixture (vk::EmArgs.upd), and the next denoising follows
+    // with no host wait between them; the host forms the same mixture from the same
     // sums at the iteration's one flush, and checks it against the device's,
     // bit for bit
     const bool devem = chain && R.prm.EM_max_iter == 1;
@@ -642,18 +645,17 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
         STCHK(fin.fork());
         if (em_next) {
             STCHK(fin.side(true));
-            STCHK(em_begin(c, em_params(R), R.mix_next, R.gam1, R.r1, fin, em, r1_in_em ? &r1from : nullptr));
-            if (devem) {
-                vk::EmUpd eu;
-                eu.sums = fin.dev_result(em.sums);
-                if (!eu.sums) return fail(VAMPOMI_ERR_STATE, "vamp: the EM sums have no device address");
-                eu.Mt = Mt;
-                eu.learn_vars = R.prm.learn_vars;
-                eu.merge_vars_thr = R.prm.merge_vars_thr;
-                eu.mirror = R.mixh_dev;
+            vk::EmUpd eu;
+            eu.Mt = Mt;
+            eu.learn_vars = R.prm.learn_vars;
+            eu.merge_vars_thr = R.prm.merge_vars_thr;
+            eu.out = R.mixw;
+            eu.mirror = R.mixh_dev;
+            STCHK(em_begin(c, em_params(R), R.mix_next, R.gam1, R.r1, fin, em, r1_in_em ? &r1from : nullptr,
+                           devem ? &eu : nullptr));
+            if (devem)
                 STCHK(denoise_into(c, R.mix_next, R.gam1, R.r1, R.x1n, R.x1, true, R.prm.rho, R.x1d, fin, &R.sum_d,
-                                   &eu, dsc));
-            }
+                                   R.mixw, dsc));
             STCHK(fin.side(false));
         }
     }
