@@ -7,6 +7,7 @@
 #include <initializer_list>
 #include <memory>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "../../include/vampomi.h"
@@ -60,6 +61,8 @@ struct TimedLaunch {
 // synced (summed over ranks) and local halves of a DotBatch
 // (SL_CG: the 3K sums of a CG step, decided on the device; SL_CGI: the 2K sums
 // of cg_init, read by cg_start_from)
+// (SL_CHAIN, device, one rank: [0, 3) gam1, eta2, alpha2 of G1Chain; [3, 8)
+// the next prelude's scalars (vk::PreOut); [8] tn, [9] tc (DotCopy))
 enum : int { SL_DP = 0, SL_CG = 4, SL_SYNC = 16, SL_NSYNC = 256, SL_LOCAL = SL_SYNC + SL_NSYNC, SL_NLOCAL = 128,
              SL_CGI = SL_LOCAL + SL_NLOCAL, SL_CHECK = SL_CGI + 16, SL_AGREE = SL_CHECK + 8, SL_CHAIN = SL_AGREE + 8, SL_TOTAL = 512, SL_BARRIER = SL_TOTAL - 1 };
 
@@ -214,10 +217,18 @@ class DotBatch {
         bool sync;
         double* out;
     };
-    vampomi_status add_many(int64_t n, const std::vector<Group>& groups);
+    // chain (may be null): its arithmetic rides in the launch, on the sum of
+    // the group whose out is chain_of (a one-term group); copies: the result
+    // of each one-term group whose out is .first is also stored at .second
+    // (device memory) by the launch (at most 2)
+    vampomi_status add_many(int64_t n, const std::vector<Group>& groups, const vk::G1Chain* chain = nullptr,
+                            const double* chain_of = nullptr,
+                            const std::vector<std::pair<const double*, double*>>& copies = {});
     // reserves nq result slots for a fused reduction kernel: *ro says where the
     // kernel writes; the values reach out[0..nq) at flush()
     vampomi_status sink(int nq, bool sync, double* out, vk::RedOut* ro);
+    // the main stream continues after the side stream's work (no host wait)
+    vampomi_status join();
     vampomi_status flush();
     bool empty() const { return sinks_.empty(); }
     // one rank: the device address where the result that flush() will copy to
@@ -297,12 +308,16 @@ struct HeadStart {
     bool used = false;  // out: the head start ran
 };
 // pre (may be null; init must be null): the caller's prelude launch, fused
-// with the solve's start (vk::prelude_cg_init)
+// with the solve's start (vk::prelude_cg_init).  pm (one rank, with pre):
+// ahead: queue only that launch, its scalars from the device (pre->dev; tau
+// and gam2 unused), and return; queued: that launch was queued ahead (the same
+// sys, hs and pre): the solve goes on after it
+enum class PreMode { normal, ahead, queued };
 vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double tau, double gam2, int max_iter,
                        double tol, double* nscratch, int64_t* ref_passes, DotBatch* init,
                        const double* extra_x = nullptr, double* ex_out = nullptr, bool onepass = false,
                        const double* const* ar0 = nullptr, HeadStart* hs = nullptr,
-                       const vk::Prelude* pre = nullptr);
+                       const vk::Prelude* pre = nullptr, PreMode pm = PreMode::normal);
 // plans the one-pass operator (c->opp, c->op_ok, c->hs_ok) and allocates its
 // buffers (idempotent until the plan or the head-start switch changes).
 // COLLECTIVE when collective (several ranks): the ranks agree on op_ok and

@@ -548,7 +548,10 @@ vampomi_status DotBatch::add(std::initializer_list<vk::DotTerm> terms, int64_t n
     return VAMPOMI_OK;
 }
 
-vampomi_status DotBatch::add_many(int64_t n, const std::vector<Group>& groups) {
+vampomi_status DotBatch::add_many(int64_t n, const std::vector<Group>& groups, const vk::G1Chain* chain,
+                                  const double* chain_of,
+                                  const std::vector<std::pair<const double*, double*>>& copies) {
+    if (copies.size() > 2) return fail(VAMPOMI_ERR_ARG, "DotBatch: at most 2 device copies per launch");
     // terms in the order [local groups..., synced groups...]: each kind's
     // results land in one contiguous slot range (out, then out2 from split)
     vk::DotArgs a{};
@@ -565,6 +568,15 @@ vampomi_status DotBatch::add_many(int64_t n, const std::vector<Group>& groups) {
             int& q = g.sync ? qs : ql;
             sinks_.push_back(Sink{g.sync ? SL_SYNC + nsync_ + (q - nloc) : SL_LOCAL + nlocal_ + q,
                                   (int)g.terms.size(), g.out});
+            if (chain && g.out == chain_of) {
+                a.g1 = *chain;
+                a.g1.term = q;
+            }
+            for (const auto& cp : copies)
+                if (g.out == cp.first) {
+                    a.copy.term[a.copy.n] = q;
+                    a.copy.dst[a.copy.n++] = cp.second;
+                }
             for (const auto& t : g.terms) {
                 a.t[q] = t;
                 if (t.op == vk::SUM) a.t[q].b = t.a;  // the kernel loads both operands of every term
@@ -572,6 +584,8 @@ vampomi_status DotBatch::add_many(int64_t n, const std::vector<Group>& groups) {
             }
         }
     }
+    if (chain && !a.g1.out) return fail(VAMPOMI_ERR_ARG, "DotBatch: the chained group is not in the launch");
+    if (a.copy.n != (int)copies.size()) return fail(VAMPOMI_ERR_ARG, "DotBatch: a copied group is not in the launch");
     vk::RedOut ro{};
     ro.part = on_side_ ? c_->red_part2 : c_->red_part;
     ro.ticket = on_side_ ? c_->ticket2 : c_->ticket;
@@ -617,15 +631,20 @@ vampomi_status DotBatch::side(bool on) {
     return VAMPOMI_OK;
 }
 
-vampomi_status DotBatch::flush() {
+vampomi_status DotBatch::join() {
     on_side_ = false;
-    const bool had_side = side_seq_ != 0;
-    if (forked_) {  // join: st continues after the side stream's work
+    if (forked_) {  // st continues after the side stream's work
         HIPCHK(hipEventRecord(c_->ev_join, c_->st2));
         HIPCHK(hipStreamWaitEvent(c_->st, c_->ev_join, 0));
         forked_ = false;
         c_->side_open = false;
     }
+    return VAMPOMI_OK;
+}
+
+vampomi_status DotBatch::flush() {
+    const bool had_side = side_seq_ != 0;
+    STCHK(join());
     if (side_seq_) {  // one rank: the host reads the side results when their own kernel flags them
         c_->stats.host_syncs++;
         STCHK(wait_flag(c_, side_seq_, 1));

@@ -201,7 +201,28 @@ struct DotTerm {
     const double* c = nullptr;
     const double* beta = nullptr;
 };
-struct DotArgs { DotTerm t[kMaxTerms]; int nt; };
+// gam1 chain (rides in a reduction launch, after the sum a2 = <bern, invQ>): from
+// the sum of term `term`, a2: alpha2 = gam2*a2, eta2 = gam2/alpha2, gam1 =
+// rho*min(max(eta2 - gam2, 1e-11), 1e11) + (1 - rho)*gam1_prev into out[0] =
+// gam1, out[1] = eta2, out[2] = alpha2 (out null: none)
+struct G1Chain {
+    int term = 0;
+    double gam2 = 0.0, rho = 0.0, gam1_prev = 0.0;
+    double* out = nullptr;
+};
+// device copies of chosen results (the results themselves may land in mapped
+// host memory, which a later kernel reads at a PCIe round trip's cost)
+struct DotCopy {
+    int n = 0;
+    int term[2] = {0, 0};
+    double* dst[2] = {nullptr, nullptr};
+};
+struct DotArgs {
+    DotTerm t[kMaxTerms];
+    int nt;
+    G1Chain g1;    // formed by the launch's last block from its final sums
+    DotCopy copy;  // ... and these copies stored by it
+};
 int red_blocks(int64_t n);
 // ro.out[q] = term q summed over [0, n): per-block partials, then the blocks'
 // sums in block order (fixed geometry: depends on n only)
@@ -218,11 +239,14 @@ struct Mix {
 constexpr int kMixWords = 2 + 2 * kMaxL;
 // x1 = g1(r1) (then rho*x1 + (1-rho)*x1_prev if damp), x1d = g1d(r1),
 // sum of x1d in ro.out[0].  mixw / gam1dev (may be null): the mixture's words
-// (kMixWords, device: an EM round's update, em_sums' upd) and gam1 (vamp_gam1)
+// (kMixWords, device: an EM round's update, em_sums' upd) and gam1 (G1Chain)
 // from the device instead of mix and gam1.
+// po (may be null, with mixw): the launch's last block also forms the next
+// prelude's scalars (PreOut) from the sum of x1d
+struct PreOut;
 hipError_t denoise(int64_t M, const double* r1, double gam1, const Mix& mix, double* x1,
                    const double* x1_prev, int damp, double rho, double* x1d, const RedOut& ro, hipStream_t st,
-                   const double* mixw = nullptr, const double* gam1dev = nullptr);
+                   const double* mixw = nullptr, const double* gam1dev = nullptr, const PreOut* po = nullptr);
 
 // ---- EM prior update (vamp::updatePrior) per-marker sums --------------------
 // the round's update of the mixture, formed on the device by the launch that
@@ -248,7 +272,7 @@ struct EmArgs {
     double la, lb, lc;
     double* r1out;
     // dsc (may be null): gam1 = dsc[0] and la = eta2 = dsc[1] come from the
-    // device (vamp_gam1), and noise_var = 1/gam1, v[j-1] = 1/(1/vars[j] + gam1)
+    // device (G1Chain), and noise_var = 1/gam1, v[j-1] = 1/(1/vars[j] + gam1)
     // are formed here, with the host's expressions (the host fields are unused)
     const double* dsc;
     // upd.out (may be null): the launch's last block also forms this round's
@@ -257,11 +281,6 @@ struct EmArgs {
     // host's expressions, bit for bit) into upd.out and upd.mirror
     EmUpd upd;
 };
-// one thread, after the reduction that produced a2 = <bern, invQ> (src/vamp.cpp:
-// 341-346, 498): alpha2 = gam2*a2, eta2 = gam2/alpha2, gam1 = rho*min(max(eta2 -
-// gam2, 1e-11), 1e11) + (1 - rho)*gam1_prev, into out[0] = gam1, out[1] = eta2,
-// out[2] = alpha2: the host's expressions, bit for bit
-hipError_t vamp_gam1(const double* a2, double gam2, double rho, double gam1_prev, double* out, hipStream_t st);
 // ro.out[q], Q = 1 + 2(L-1): q=0 sum pin; q=j (1..L-1) sum beta_j pin;
 // q=L-1+j sum beta_j (g_j^2 + v_j) pin
 hipError_t em_sums(int64_t M, const double* r1, const EmArgs& a, const RedOut& ro, hipStream_t st);
@@ -282,8 +301,29 @@ hipError_t bernoulli(uint64_t seed, int it, int64_t S, int64_t M, double sqrtMt,
 //   v = gamw*atxy + gam2*r2              (:303-306)
 //   bern = the probe of iteration it     (:295-296, P2); bern_next: of it + 1 (may be null)
 //   zero[z][i] = 0 for the non-null zero[z] (the CG solves' zero starts)
+// The next iteration's prelude scalars, formed on the device by the launch
+// that finishes its last sum (denoise, one rank), so that the prelude can be
+// queued before the host has them: alpha1 = sum_d/Mt, eta1 = gam1/alpha1,
+// gam2 = min(max(eta1 - gam1, 1e-11), 1e11), gamw = N/(tn + tc*Mt) (src/vamp.
+// cpp:223, 230, 255-256, 521-528) and the CG's diag = gamw*(N-1)/N + gam2
+// (:676-677): the host's expressions, bit for bit.  out (device) = {eta1, gam2, gamw, diag,
+// gam1}, mirror (mapped host) = its first four, for the host's check.  tn,
+// tc: device copies (DotCopy) of earlier launches' results
+struct PreOut {
+    const double* tn = nullptr;
+    const double* tc = nullptr;
+    double Mt = 0.0, N = 0.0;
+    double* out = nullptr;
+    double* mirror = nullptr;
+};
+// scal (device, may be null): the prelude's scalars {eta1, gam2, gamw, diag,
+// gam1} from PreOut.out instead of the Prelude's own (prelude_cg_init only)
+struct PreDev {
+    const double* scal = nullptr;
+};
 struct Prelude {
     double eta1, gam1, gam2, gamw;
+    PreDev dev;  // prelude_cg_init only
     const double* x1;
     const double* r1;
     const double* atxy;

@@ -1242,6 +1242,18 @@ int red_blocks(int64_t n) {
     return (int)b;
 }
 
+// src/vamp.cpp:341-346, 498 (G1Chain): the host's expressions
+__device__ __forceinline__ void gam1_chain(double a2, double gam2, double rho, double gam1_prev, double* out) {
+    const double alpha2 = gam2 * a2;    // :498
+    const double eta2 = gam2 / alpha2;  // :341
+    const double d = eta2 - gam2;
+    double g = d < 1e-11 ? 1e-11 : d;  // std::max(d, 1e-11)
+    g = 1e11 < g ? 1e11 : g;           // std::min(., 1e11)
+    out[0] = rho * g + (1 - rho) * gam1_prev;  // :346
+    out[1] = eta2;
+    out[2] = alpha2;
+}
+
 // every term loads both operands unconditionally (a SUM term's b is its a,
 // set on the host) so a thread's loads for all terms are in flight together;
 // the op is a per-launch uniform selected per element.  UPD: some term is a
@@ -1277,7 +1289,12 @@ __global__ __launch_bounds__(kBlock) void dots_kernel(DotArgs a, int64_t n, RedO
         }
     }
     block_put_sums<NT>(acc, NT, ro, (int64_t)blockIdx.x * NT);
-    red_finish(ro, NT, lds);
+    __shared__ double fin[NT];
+    const bool post = a.g1.out || a.copy.n;
+    if (red_finish(ro, NT, lds, post ? fin : nullptr) && post && threadIdx.x == 0) {
+        if (a.g1.out) gam1_chain(fin[a.g1.term], a.g1.gam2, a.g1.rho, a.g1.gam1_prev, a.g1.out);
+        for (int j = 0; j < a.copy.n && j < 2; ++j) a.copy.dst[j][0] = fin[a.copy.term[j]];
+    }
 }
 
 template <bool UPD>
@@ -1381,16 +1398,23 @@ __device__ void em_update_mix(const double* q, int L, const double* vars, const 
 }
 
 // Dev: the mixture's words (an EM round's update, em_kernel) and gam1
-// (vamp_gam1) from the device, the words staged in LDS; else mix and gam1
+// (G1Chain) from the device, the words staged in LDS; else mix and gam1
 template <bool Dev>
 __global__ __launch_bounds__(kBlock) void denoise_kernel(int64_t M, const double* __restrict__ r1, double gam1,
                                                          Mix mix, double eta_max, double* __restrict__ x1,
                                                          const double* __restrict__ x1_prev, int damp, double rho,
                                                          double* __restrict__ x1d, RedOut ro,
                                                          const double* __restrict__ mixw,
-                                                         const double* __restrict__ gam1dev) {
+                                                         const double* __restrict__ gam1dev, PreOut po) {
     __shared__ double lds[4];
     __shared__ double sm[Dev ? kMixWords : 1];
+    // po: tn and tc (device copies) are loaded at the start, their latency
+    // behind the launch's work; the last block uses them
+    double tn = 0.0, tc = 0.0;
+    if (Dev && po.out && threadIdx.x == 0) {
+        tn = po.tn[0];
+        tc = po.tc[0];
+    }
     const double* probs = mix.probs;
     const double* vars = mix.vars;
     int L = mix.L;
@@ -1414,22 +1438,37 @@ __global__ __launch_bounds__(kBlock) void denoise_kernel(int64_t M, const double
     }
     acc = block_sum(acc, lds);
     if (threadIdx.x == 0) red_put(ro, blockIdx.x, acc);
-    red_finish(ro, 1, lds);
+    __shared__ double fin[1];
+    const bool last = red_finish(ro, 1, lds, Dev && po.out ? fin : nullptr);
+    if (Dev && po.out && last && threadIdx.x == 0) {  // the next prelude's scalars (kernels.h PreOut)
+        const double alpha1 = fin[0] / po.Mt;  // :223
+        const double eta1 = gam1 / alpha1;     // :230
+        const double dg = eta1 - gam1;
+        double gam2 = dg < 1e-11 ? 1e-11 : dg;  // std::max(., 1e-11) (:255-256)
+        gam2 = 1e11 < gam2 ? 1e11 : gam2;       // std::min(., 1e11)
+        const double trace_corr = tc * po.Mt;    // :521
+        const double gamw = po.N / (tn + trace_corr);  // :528
+        const double diag = gamw * (po.N - 1) / po.N + gam2;  // :676-677 (pcg_run)
+        const double v[5] = {eta1, gam2, gamw, diag, gam1};
+        for (int q = 0; q < 5; ++q) po.out[q] = v[q];
+        for (int q = 0; q < 4; ++q) po.mirror[q] = v[q];
+    }
 }
 
 hipError_t denoise(int64_t M, const double* r1, double gam1, const Mix& mix, double* x1, const double* x1_prev,
                    int damp, double rho, double* x1d, const RedOut& ro, hipStream_t st, const double* mixw,
-                   const double* gam1dev) {
+                   const double* gam1dev, const PreOut* po) {
     double eta_max = mix.vars[0];
     for (int i = 1; i < mix.L; ++i)
         if (mix.vars[i] > eta_max) eta_max = mix.vars[i];
     if (mixw) {
-        if (!gam1dev) return hipErrorInvalidValue;
+        if (!gam1dev || (po && (!po->out || !po->mirror || !po->tn || !po->tc))) return hipErrorInvalidValue;
         hipLaunchKernelGGL(denoise_kernel<true>, dim3(red_blocks(M)), dim3(kBlock), 0, st, M, r1, gam1, mix, eta_max,
-                           x1, x1_prev, damp, rho, x1d, ro, mixw, gam1dev);
+                           x1, x1_prev, damp, rho, x1d, ro, mixw, gam1dev, po ? *po : PreOut{});
     } else {
+        if (po) return hipErrorInvalidValue;
         hipLaunchKernelGGL(denoise_kernel<false>, dim3(red_blocks(M)), dim3(kBlock), 0, st, M, r1, gam1, mix,
-                           eta_max, x1, x1_prev, damp, rho, x1d, ro, nullptr, nullptr);
+                           eta_max, x1, x1_prev, damp, rho, x1d, ro, nullptr, nullptr, PreOut{});
     }
     return hipGetLastError();
 }
@@ -1506,24 +1545,6 @@ __global__ __launch_bounds__(kBlock) void em_kernel(int64_t M, const double* __r
             o[1 + 2 * kMaxL] = w[1 + 2 * kMaxL];
         }
     }
-}
-
-__global__ void vamp_gam1_kernel(const double* __restrict__ a2, double gam2, double rho, double gam1_prev,
-                                 double* __restrict__ out) {
-    if (threadIdx.x != 0) return;
-    const double alpha2 = gam2 * __hip_atomic_load(a2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);  // :498
-    const double eta2 = gam2 / alpha2;                                                               // :341
-    const double d = eta2 - gam2;
-    double g = d < 1e-11 ? 1e-11 : d;  // std::max(d, 1e-11)
-    g = 1e11 < g ? 1e11 : g;           // std::min(., 1e11)
-    out[0] = rho * g + (1 - rho) * gam1_prev;  // :346
-    out[1] = eta2;
-    out[2] = alpha2;
-}
-
-hipError_t vamp_gam1(const double* a2, double gam2, double rho, double gam1_prev, double* out, hipStream_t st) {
-    hipLaunchKernelGGL(vamp_gam1_kernel, dim3(1), dim3(64), 0, st, a2, gam2, rho, gam1_prev, out);
-    return hipGetLastError();
 }
 
 hipError_t em_sums(int64_t M, const double* r1, const EmArgs& a, const RedOut& ro, hipStream_t st) {
@@ -1672,6 +1693,15 @@ __global__ __launch_bounds__(kBlock) void prelude_cg_init_kernel(int K, int64_t 
                                                                  RedOut ro, CgState start, CgState* dst) {
     __shared__ double lds[4];
     __shared__ double fin[2 * kMaxRhs];
+    double eta1 = p.eta1, gam1 = p.gam1, gam2 = p.gam2, gamw = p.gamw, tau = c.tau, cgam2 = c.gam2;
+    if (p.dev.scal) {  // the scalars from the device (kernels.h PreDev, formed by the denoiser's launch)
+        const double* q = p.dev.scal;
+        eta1 = q[0];
+        gam2 = cgam2 = q[1];
+        gamw = tau = q[2];
+        diag = q[3];
+        gam1 = q[4];
+    }
     double acc[2 * kMaxRhs];
 #pragma unroll
     for (int q = 0; q < 2 * kMaxRhs; ++q) acc[q] = 0.0;
@@ -1700,9 +1730,9 @@ __global__ __launch_bounds__(kBlock) void prelude_cg_init_kernel(int K, int64_t 
             const int64_t i = i0 + h * stride;
             if (h == 1 && !two) break;
             // prelude_kernel's expressions
-            const double r2 = (p.eta1 * x1v[h] - p.gam1 * r1v[h]) / p.gam2;  // lincomb_div's expression
+            const double r2 = (eta1 * x1v[h] - gam1 * r1v[h]) / gam2;  // lincomb_div's expression
             p.r2[i] = r2;
-            const double vv = p.gamw * ayv[h] + p.gam2 * r2;                  // axpby's
+            const double vv = gamw * ayv[h] + gam2 * r2;                  // axpby's
             p.v[i] = vv;
             const double bn = (double)(2 * bern_bit(p.seed, p.it, p.S + i) - 1) / p.sqrtMt;
             p.bern[i] = bn;
@@ -1717,8 +1747,8 @@ __global__ __launch_bounds__(kBlock) void prelude_cg_init_kernel(int K, int64_t 
                 double r;
                 if (c.atx0[k]) {  // lmmse_mult(mu0) from a precomputed A^T(A mu0): res*=tau; res+=gam2*v
                     double dv = a0[h][k];
-                    dv *= c.tau;
-                    dv += c.gam2 * muv[h][k];
+                    dv *= tau;
+                    dv += cgam2 * muv[h][k];
                     r = vi - dv;
                 } else {
                     r = c.d[k] ? vi - dd[h][k] : vi - 0.0;  // r = v - lmmse_mult(mu0)
@@ -1735,6 +1765,7 @@ __global__ __launch_bounds__(kBlock) void prelude_cg_init_kernel(int K, int64_t 
     block_put_sums<2 * kMaxRhs>(acc, 2 * K, ro, (int64_t)blockIdx.x * 2 * K);
     if (red_finish(ro, 2 * K, lds, fin) && dst && threadIdx.x == 0) {
         *dst = start;  // then its sums (indexed in place: no stack copy of the state)
+        dst->gam2 = cgam2;
         for (int k = 0; k < K; ++k) {
             dst->rz[k] = fin[2 * k];
             dst->vv[k] = fin[2 * k + 1];

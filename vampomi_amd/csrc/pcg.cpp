@@ -91,7 +91,8 @@ static vampomi_status cg_loop(vampomi_ctx* c, int max_iter, bool packed, Enqueue
 
 vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double tau, double gam2, int max_iter,
                        double tol, double* nscratch, int64_t* ref_passes, DotBatch* init, const double* extra_x,
-                       double* ex_out, bool onepass, const double* const* ar0, HeadStart* hs, const vk::Prelude* pre) {
+                       double* ex_out, bool onepass, const double* const* ar0, HeadStart* hs, const vk::Prelude* pre,
+                       PreMode pm) {
     const int64_t M = c->M, N = c->N;
     const double diag = tau * (double)(N - 1) / (double)N + gam2;  // :676-677
     const int K = (int)sys.size();
@@ -125,6 +126,7 @@ vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double
             if (s->mu0_nonzero && ref_passes) *ref_passes += 2;
         }
         if (!nz.empty()) {
+            if (pm != PreMode::normal) return fail(VAMPOMI_ERR_ARG, "pcg: a start queued ahead needs no lmmse pass");
             const double* vv[vk::kMaxRhs];
             double* dd[vk::kMaxRhs];
             for (size_t k = 0; k < nz.size(); ++k) {
@@ -165,6 +167,7 @@ vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double
         sys[k]->iters = 0;
     }
     if (pre && init) return fail(VAMPOMI_ERR_ARG, "pcg: the prelude rides only in the device-side start");
+    if (pm != PreMode::normal && !pre) return fail(VAMPOMI_ERR_ARG, "pcg: a start queued ahead is the prelude's");
     if (init) {  // the caller's reductions resolve together with <r,z>, <v,v> (one host wait)
         std::vector<double> rzvv(2 * K);
         vk::RedOut ro{};
@@ -182,10 +185,16 @@ vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double
         // pre: the caller's prelude rides in the same launch, and on one rank
         // that launch's last block also builds the CgState (three launches in one)
         const bool own_start = pre && !c->use_comm;
-        if (pre)
+        if (pm != PreMode::normal && (!own_start || (pm == PreMode::ahead) != (pre->dev.scal != nullptr)))
+            return fail(VAMPOMI_ERR_ARG, "pcg: a start queued ahead needs one rank, the prelude and its device scalars");
+        if (pm == PreMode::queued) {
+            // (queued ahead by the previous iteration, scalars from the device)
+        } else if (pre) {
             HIPCHK(vk::prelude_cg_init(K, M, *pre, cv, diag, ro, own_start ? &s0 : nullptr, c->cgs, c->st));
-        else
+            if (pm == PreMode::ahead) return VAMPOMI_OK;
+        } else {
             HIPCHK(vk::cg_init(K, M, cv, diag, ro, c->st));
+        }
         STCHK(allreduce_dev(c, c->scal + SL_CGI, (size_t)(2 * K)));
         if (max_iter <= 0) return extra_alone();
         if (!own_start) HIPCHK(vk::cg_start_from(s0, c->scal + SL_CGI, c->cgs, c->st));

@@ -68,6 +68,12 @@ struct VampRun {
     double* mixh_dev = nullptr;
     bool mix_pending = false;
     Mixture mix_expect;
+    // the iteration whose prelude and solves' start the previous iteration
+    // queued ahead (0: none), its scalars formed on the device (vk::PreOut);
+    // mixh + kMixWords holds them (eta1, gam2, gamw, diag), checked against
+    // the host's (check_device_values).  VAMPOMI_PRE_AHEAD=0: off
+    int pre_ahead = 0;
+    bool pre_ahead_on = true;
     const double* z1 = nullptr;
     int64_t passes_ref = 0;
     // probit (src/vamp_probit.cpp) state
@@ -108,7 +114,7 @@ struct R1From {
     const double* x2;
     const double* r2;
     double eta2, gam2, gam1;
-    const double* dsc = nullptr;  // device: gam1, eta2 (vk::vamp_gam1); then eta2 and gam1 above are unused
+    const double* dsc = nullptr;  // device: gam1, eta2 (vk::G1Chain); then eta2 and gam1 above are unused
 };
 // upd (may be null, one round): the round's launch also forms the update of
 // the mixture on the device (vk::EmArgs.upd)
@@ -121,7 +127,8 @@ vampomi_status em_finish(vampomi_ctx* c, const EmParams& P, Mixture& m, double g
 // (vk::denoise)
 vampomi_status denoise_into(vampomi_ctx* c, const Mixture& m, double gam1, const double* r1, double* x1,
                             const double* x1_prev, bool damp, double rho, double* x1d, DotBatch& b, double* sum_out,
-                            const double* mixw = nullptr, const double* gam1dev = nullptr);
+                            const double* mixw = nullptr, const double* gam1dev = nullptr,
+                            const vk::PreOut* po = nullptr);
 vampomi_status upload_or_zero(vampomi_ctx* c, double* dst, const double* host, int64_t n);
 // queues this iteration's x1/sqrt(N), r1/sqrt(N) for the _it_K.bin /
 // _r1_it_K.bin files and the x1/r1 history (R.writer)

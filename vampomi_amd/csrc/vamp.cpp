@@ -176,7 +176,8 @@ vampomi_status update_prior(vampomi_ctx* c, const VampRun& R, Mixture& m, double
 // x1 = g1(r1) [damped], x1d = g1d(r1); sum of x1d over ranks queued in b
 vampomi_status denoise_into(vampomi_ctx* c, const Mixture& m, double gam1, const double* r1, double* x1,
                                    const double* x1_prev, bool damp, double rho, double* x1d, DotBatch& b,
-                                   double* sum_out, const double* mixw, const double* gam1dev) {
+                                   double* sum_out, const double* mixw, const double* gam1dev,
+                                   const vk::PreOut* po) {
     vk::Mix mix{};
     mix.L = m.L;
     for (int j = 0; j < m.L; ++j) {
@@ -185,7 +186,7 @@ vampomi_status denoise_into(vampomi_ctx* c, const Mixture& m, double gam1, const
     }
     vk::RedOut ro{};
     STCHK(b.sink(1, true, sum_out, &ro));  // :214-222
-    HIPCHK(vk::denoise(c->M, r1, gam1, mix, x1, x1_prev, damp ? 1 : 0, rho, x1d, ro, b.stream(), mixw, gam1dev));
+    HIPCHK(vk::denoise(c->M, r1, gam1, mix, x1, x1_prev, damp ? 1 : 0, rho, x1d, ro, b.stream(), mixw, gam1dev, po));
     return VAMPOMI_OK;
 }
 
@@ -249,7 +250,12 @@ static vampomi_status vamp_alloc(vampomi_ctx* c, VampRun& R) {
     STCHK(dev_alloc(&R.ax2, ld));
     STCHK(dev_alloc(&R.abern, 2 * ld));  // two slots: A.bern of it (consumed in place) and of it + 1
     STCHK(dev_alloc(&R.mixw, vk::kMixWords));
-    HIPCHK(hipHostMalloc((void**)&R.mixh, vk::kMixWords * sizeof(double), hipHostMallocMapped | hipHostMallocCoherent));
+    HIPCHK(hipHostMalloc((void**)&R.mixh, (vk::kMixWords + 4) * sizeof(double),
+                         hipHostMallocMapped | hipHostMallocCoherent));
+    {
+        const char* e = std::getenv("VAMPOMI_PRE_AHEAD");
+        R.pre_ahead_on = !e || std::atoi(e) != 0;
+    }
     HIPCHK(hipHostGetDevicePointer((void**)&R.mixh_dev, R.mixh, 0));
     HIPCHK(hipMemsetAsync(R.ax2, 0, ld * 8, c->st));
     HIPCHK(hipMemsetAsync(R.abern, 0, 2 * ld * 8, c->st));
@@ -425,6 +431,106 @@ static vampomi_status check_device_mix(VampRun& R) {
     return VAMPOMI_OK;
 }
 
+// The LMMSE half's solves of iteration it (src/vamp.cpp:289-350): their
+// vectors, schedule flags and the prelude (r2, the probe bern, v and the zero
+// starts, :259-261, :295-306, :496), from R's scalars and x1 (iteration it's
+// x1_hat).  No launches: vamp_step queues them, and the previous iteration
+// may queue the prelude and the solves' start ahead (R.pre_ahead).
+struct LmmseSetup {
+    CgSystem sx{}, so{};
+    bool rec = false, arec = false, hs_av = false, pre_in_cg = false;
+    HeadStart hs;
+    vk::Prelude pr{};
+};
+
+static vampomi_status lmmse_setup(vampomi_ctx* c, VampRun& R, int it, const double* x1, LmmseSetup& L) {
+    const int64_t ld = c->ld;
+    CgSystem& sx = L.sx;
+    CgSystem& so = L.so;
+    sx.v = R.v;
+    sx.mu = R.x2;  // mu_CG_last: warm start, updated in place (:308-311, :753-754)
+    sx.mu0_nonzero = it > 1;
+    sx.atx0 = (it > 1 && R.have_next) ? R.atx0 : nullptr;
+    sx.r = R.cgw[0];
+    sx.z = R.cgw[1];
+    sx.p = R.cgw[2];
+    sx.d = R.cgw[3];
+    so.v = R.bern;
+    so.mu = R.invQ;  // g2d_onsager starts from zeros (:496, :664-669)
+    so.onsager = true;
+    so.r = R.cgw[4];
+    so.z = R.cgw[5];
+    so.p = R.cgw[6];
+    so.d = R.cgw[7];
+    // batch_rhs 2: updateNoisePrec's A^T(A x2) (the next warm start, :681) and
+    // A^T(A invQ) (the trace, :519) are carried through the CG steps as
+    // W += alpha * A^T(A p) beside mu += alpha * p, instead of one more pass
+    // over X per iteration (mathematically the same vectors; rounding differs)
+    L.rec = R.recur && R.fuse && (it == 1 || sx.atx0);
+    if (L.rec) {
+        sx.W = R.atx0;  // holds A^T A mu0 on entry (the warm start's product), in place
+        sx.S = R.cgw[8];
+        so.W = R.tmpM;  // invQ starts from zeros
+        so.S = R.cgw[9];
+    }
+    // batch_rhs 3: A x2 (updateNoisePrec :508, err_measures :826, and the next
+    // warm start) is carried as AW += alpha * A p beside mu += alpha * p, from
+    // the previous iteration's A x2; z1 = A x1_hat (:232) is one more
+    // right-hand side of the first CG pass
+    L.arec = R.arec && L.rec;
+    if (L.arec) sx.AW = R.ax2;
+    // the head start (pcg.cpp, ctx.h HeadStart): the Onsager solve (system 0)
+    // takes its first CG step in the pass that starts the x2 solve, from
+    // A.bern computed one iteration early (bern depends on (seed, it, marker)
+    // only, P2); that pass also forms A.bern of the next iteration
+    if (R.fuse && L.arec && R.onepass) STCHK(headstart_available(c, &L.hs_av));
+    if (L.hs_av) {
+        // slot it & 1 holds A.bern(it): the Onsager solve's A r, updated in
+        // place by its CG steps; A.bern(it + 1) goes to the other slot
+        L.hs.abern = R.hs_it == it ? R.abern + (it & 1) * ld : nullptr;
+        if (it < R.prm.max_iter) {
+            L.hs.xnext = R.bern_next;  // the probe of it + 1, formed by the prelude below
+            L.hs.axnext = R.abern + ((it + 1) & 1) * ld;
+        }
+    }
+    // the iteration's elementwise work before the CG solves, in one launch
+    // (it replaces five: r2, bern, v, and the zeroed invQ (:496) and its W)
+    vk::Prelude& pr = L.pr;
+    pr.eta1 = R.eta1;
+    pr.gam1 = R.gam1;
+    pr.gam2 = R.gam2;
+    pr.gamw = R.gamw;
+    pr.x1 = x1;
+    pr.r1 = R.r1;
+    pr.atxy = R.atxy;
+    pr.r2 = R.r2;
+    pr.v = R.v;
+    pr.seed = R.prm.seed;
+    pr.it = it;
+    pr.S = c->S;
+    pr.sqrtMt = std::sqrt((double)c->Mt);
+    pr.bern = R.bern;
+    pr.bern_next = L.hs.xnext ? R.bern_next : nullptr;
+    pr.zero[0] = R.invQ;
+    pr.zero[1] = L.rec ? R.tmpM : nullptr;
+    // where the solve starts on the device (no caller batch), the prelude rides
+    // in its first launch (pcg_run's pre); else it is a launch of its own
+    L.pre_in_cg = R.fuse && (L.hs_av || L.arec);
+    return VAMPOMI_OK;
+}
+
+// ... and the scalars of a prelude queued ahead are the host's, bit for bit
+static vampomi_status check_device_values(vampomi_ctx* c, VampRun& R, int it) {
+    STCHK(check_device_mix(R));
+    if (R.pre_ahead != it) return VAMPOMI_OK;
+    R.pre_ahead = 0;
+    const double diag = R.gamw * (double)(c->N - 1) / (double)c->N + R.gam2;  // pcg_run (:676-677)
+    const double want[4] = {R.eta1, R.gam2, R.gamw, diag};
+    if (std::memcmp(want, R.mixh + vk::kMixWords, sizeof want) != 0)
+        return fail(VAMPOMI_ERR_STATE, "vamp: the prelude queued ahead formed other scalars than the host");
+    return VAMPOMI_OK;
+}
+
 // one VAMP iteration (src/vamp.cpp:148-428)
 extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
     CollScope cs_(c);
@@ -482,87 +588,27 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
     // (r2 (:259-261), the probe bern (:295-296, P2) and v = gamw ATx(y) + gam2 r2
     // (:303-306) are formed by the prelude launch below, with the zero starts)
     R.passes_ref += 1;
-    CgSystem sx{}, so{};
-    sx.v = R.v;
-    sx.mu = R.x2;  // mu_CG_last: warm start, updated in place (:308-311, :753-754)
-    sx.mu0_nonzero = it > 1;
-    sx.atx0 = (it > 1 && R.have_next) ? R.atx0 : nullptr;
-    sx.r = R.cgw[0];
-    sx.z = R.cgw[1];
-    sx.p = R.cgw[2];
-    sx.d = R.cgw[3];
-    so.v = R.bern;
-    so.mu = R.invQ;  // g2d_onsager starts from zeros (:496, :664-669)
-    so.onsager = true;
-    so.r = R.cgw[4];
-    so.z = R.cgw[5];
-    so.p = R.cgw[6];
-    so.d = R.cgw[7];
-    if (it == 1) HIPCHK(hipMemsetAsync(R.x2, 0, (size_t)std::max<int64_t>(M, 1) * 8, c->st));
-    // batch_rhs 2: updateNoisePrec's A^T(A x2) (the next warm start, :681) and
-    // A^T(A invQ) (the trace, :519) are carried through the CG steps as
-    // W += alpha * A^T(A p) beside mu += alpha * p, instead of one more pass
-    // over X per iteration (mathematically the same vectors; rounding differs)
-    const bool rec = R.recur && R.fuse && (it == 1 || sx.atx0);
-    if (rec) {
-        if (it == 1) HIPCHK(hipMemsetAsync(R.atx0, 0, (size_t)std::max<int64_t>(M, 1) * 8, c->st));
-        sx.W = R.atx0;  // holds A^T A mu0 on entry (the warm start's product), in place
-        sx.S = R.cgw[8];
-        so.W = R.tmpM;  // invQ starts from zeros
-        so.S = R.cgw[9];
+    LmmseSetup L;
+    STCHK(lmmse_setup(c, R, it, R.x1, L));
+    CgSystem& sx = L.sx;
+    CgSystem& so = L.so;
+    const bool rec = L.rec, arec = L.arec, hs_av = L.hs_av;
+    HeadStart& hs = L.hs;
+    vk::Prelude& pr = L.pr;
+    if (it == 1) {  // the zero starts of the first iteration
+        HIPCHK(hipMemsetAsync(R.x2, 0, (size_t)std::max<int64_t>(M, 1) * 8, c->st));
+        if (rec) HIPCHK(hipMemsetAsync(R.atx0, 0, (size_t)std::max<int64_t>(M, 1) * 8, c->st));
+        if (arec) HIPCHK(hipMemsetAsync(R.ax2, 0, (size_t)ld * 8, c->st));
     }
-    // batch_rhs 3: A x2 (updateNoisePrec :508, err_measures :826, and the next
-    // warm start) is carried as AW += alpha * A p beside mu += alpha * p, from
-    // the previous iteration's A x2; z1 = A x1_hat (:232) is one more
-    // right-hand side of the first CG pass
-    const bool arec = R.arec && rec;
-    if (arec) {
-        if (it == 1) HIPCHK(hipMemsetAsync(R.ax2, 0, (size_t)ld * 8, c->st));
-        sx.AW = R.ax2;
-    }
-    // the head start (pcg.cpp, ctx.h HeadStart): the Onsager solve (system 0)
-    // takes its first CG step in the pass that starts the x2 solve, from
-    // A.bern computed one iteration early (bern depends on (seed, it, marker)
-    // only, P2); that pass also forms A.bern of the next iteration
-    bool hs_av = false;
-    if (R.fuse && arec && R.onepass) STCHK(headstart_available(c, &hs_av));
-    HeadStart hs;
-    if (hs_av) {
-        // slot it & 1 holds A.bern(it): the Onsager solve's A r, updated in
-        // place by its CG steps; A.bern(it + 1) goes to the other slot
-        hs.abern = R.hs_it == it ? R.abern + (it & 1) * ld : nullptr;
-        if (it < R.prm.max_iter) {
-            hs.xnext = R.bern_next;  // the probe of it + 1, formed by the prelude below
-            hs.axnext = R.abern + ((it + 1) & 1) * ld;
-        }
-    }
-    // the iteration's elementwise work before the CG solves, in one launch
-    // (it replaces five: r2, bern, v, and the zeroed invQ (:496) and its W)
-    vk::Prelude pr{};
-    pr.eta1 = R.eta1;
-    pr.gam1 = R.gam1;
-    pr.gam2 = R.gam2;
-    pr.gamw = R.gamw;
-    pr.x1 = R.x1;
-    pr.r1 = R.r1;
-    pr.atxy = R.atxy;
-    pr.r2 = R.r2;
-    pr.v = R.v;
-    pr.seed = R.prm.seed;
-    pr.it = it;
-    pr.S = c->S;
-    pr.sqrtMt = std::sqrt((double)Mt);
-    pr.bern = R.bern;
-    pr.bern_next = hs.xnext ? R.bern_next : nullptr;
-    pr.zero[0] = R.invQ;
-    pr.zero[1] = rec ? R.tmpM : nullptr;
-    // where the solve starts on the device (no caller batch), the prelude rides
-    // in its first launch (pcg_run's pre); else it is a launch of its own
-    const bool pre_in_cg = R.fuse && (hs_av || arec);
-    if (!pre_in_cg) HIPCHK(vk::prelude(M, pr, c->st));
+    // the prelude and the solves' start of this iteration queued by the
+    // previous one (its scalars from the device, R.pre_ahead)
+    const PreMode pm = R.pre_ahead == it ? PreMode::queued : PreMode::normal;
+    if (pm == PreMode::queued && !(L.pre_in_cg && R.fuse && hs_av))
+        return fail(VAMPOMI_ERR_STATE, "vamp: the start queued ahead does not match this iteration's schedule");
+    if (!L.pre_in_cg) HIPCHK(vk::prelude(M, pr, c->st));
     if (R.fuse && hs_av) {
         STCHK(pcg_run(c, {&so, &sx}, R.gamw, R.gam2, R.prm.CG_max_iter, R.prm.CG_err_tol, R.nsc, &R.passes_ref,
-                      nullptr, R.x1, R.z1buf, true, nullptr, &hs, &pr));
+                      nullptr, R.x1, R.z1buf, true, nullptr, &hs, &pr, pm));
         R.hs_it = hs.xnext ? it + 1 : 0;
     } else if (R.fuse) {
         STCHK(pcg_run(c, {&sx, &so}, R.gamw, R.gam2, R.prm.CG_max_iter, R.prm.CG_err_tol, R.nsc, &R.passes_ref,
@@ -573,7 +619,7 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
         STCHK(pcg_run(c, {&sx}, R.gamw, R.gam2, R.prm.CG_max_iter, R.prm.CG_err_tol, R.nsc, &R.passes_ref, &e1));
         STCHK(pcg_run(c, {&so}, R.gamw, R.gam2, R.prm.CG_max_iter, R.prm.CG_err_tol, R.nsc, &R.passes_ref, nullptr));
     }
-    STCHK(check_device_mix(R));  // (the solves' flags came after the previous iteration's denoising)
+    STCHK(check_device_values(c, R, it));  // (the solves' flags came after the previous iteration's launches)
     if (res && res->cg_iters) res->cg_iters[it - 1] = sx.iters;
     if (res && res->ons_iters) res->ons_iters[it - 1] = so.iters;
     // r1 (:348-350): its own launch, or (the side stream's EM round below)
@@ -582,7 +628,7 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
     const bool em_next = next && it + 1 > R.prm.learn_prior_delay;
     const bool r1_in_em = next && arec && em_next && R.prm.EM_max_iter >= 1;
     // chain (one rank): alpha2 -> eta2 -> gam1 (:341-346) are formed on the
-    // device from the reduction's result (vk::vamp_gam1), so the EM round and
+    // device from the reduction's result (vk::G1Chain), so the EM round and
     // the reductions after it are queued without the host waiting for alpha2;
     // the host forms the same values from the same sum at the next flush
     const bool chain = r1_in_em && !c->use_comm;
@@ -616,11 +662,15 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
         gm.push_back(gnm);
         gn.push_back(gtn);
         err_groups(c, R, R.x2, R.ax2, R.e2m, R.e2n, R.e2s, gm, gn);
-        STCHK(fin.add_many(M, gm));
-        STCHK(fin.add_many(N, gn));
-        const double* a2dev = fin.dev_result(&R.a2);
-        if (!a2dev) return fail(VAMPOMI_ERR_STATE, "vamp: alpha2's sum has no device address");
-        HIPCHK(vk::vamp_gam1(a2dev, R.gam2, R.prm.rho, gam1_prev, dsc, c->st));
+        // alpha2 -> eta2 -> gam1 in the M launch's last block (vk::G1Chain)
+        vk::G1Chain g1;
+        g1.gam2 = R.gam2;
+        g1.rho = R.prm.rho;
+        g1.gam1_prev = gam1_prev;
+        g1.out = dsc;
+        // (tc and tn also into device memory, for the next prelude's scalars: vk::PreOut)
+        STCHK(fin.add_many(M, gm, &g1, &R.a2, {{&R.tc, dsc + 9}}));
+        STCHK(fin.add_many(N, gn, nullptr, nullptr, {{&R.tn, dsc + 8}}));
     } else {
         DotBatch b(c);
         if (arec)
@@ -639,6 +689,31 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
     // sums at the iteration's one flush, and checks it against the device's,
     // bit for bit
     const bool devem = chain && R.prm.EM_max_iter == 1;
+    // ahead (devem): iteration it+1's prelude and solves' start are queued at
+    // the end of this iteration, its scalars formed by the next denoising's
+    // launch (vk::PreOut): the GPU runs it while the host waits for this
+    // iteration's flush, instead of idling from the end of this iteration's
+    // last launch to the host's first launch of the next.  If the stop fires,
+    // it has only written vectors that no later read depends on (r2, v, bern,
+    // the CG start, the zero starts)
+    LmmseSetup A;
+    vk::PreOut po;
+    bool ahead = false;
+    if (devem && R.pre_ahead_on && next) {
+        const bool had = R.have_next;
+        R.have_next = true;  // (it + 1's view: its x1_hat is x1n)
+        const vampomi_status st = lmmse_setup(c, R, it + 1, R.x1n, A);
+        R.have_next = had;
+        STCHK(st);
+        po.tn = dsc + 8;  // (device copies, above)
+        po.tc = dsc + 9;
+        po.Mt = (double)Mt;
+        po.N = (double)N;
+        po.out = dsc + 3;
+        po.mirror = R.mixh_dev + vk::kMixWords;
+        ahead = A.pre_in_cg && R.fuse && A.hs_av && A.sx.atx0 && po.tn && po.tc;
+        A.pr.dev.scal = po.out;
+    }
     EmState em;
     if (next) R.mix_next = R.mix;
     if (next && arec) {  // the side stream starts from r1 and x1; its EM sums are queued before these reductions
@@ -655,7 +730,7 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
                            devem ? &eu : nullptr));
             if (devem)
                 STCHK(denoise_into(c, R.mix_next, R.gam1, R.r1, R.x1n, R.x1, true, R.prm.rho, R.x1d, fin, &R.sum_d,
-                                   R.mixw, dsc));
+                                   R.mixw, dsc, ahead ? &po : nullptr));
             STCHK(fin.side(false));
         }
     }
@@ -715,6 +790,13 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
         STCHK(fin.side(false));
     }
     if (!shared) STCHK(fin.add_many(M, {gnm}));  // NMSE (:409-413)
+    // iteration it+1's prelude and solves' start, queued now (set up above)
+    if (ahead) {
+        STCHK(fin.join());  // (x1n, r1 and the scalars may come from the side stream)
+        STCHK(pcg_run(c, {&A.so, &A.sx}, 0.0, 0.0, R.prm.CG_max_iter, R.prm.CG_err_tol, R.nsc, nullptr, nullptr,
+                      R.x1n, R.z1buf, true, nullptr, &A.hs, &A.pr, PreMode::ahead));
+        R.pre_ahead = it + 1;
+    }
     STCHK(fin.flush());
     if (devem) {
         host_gam1();  // (the device formed the same values)
