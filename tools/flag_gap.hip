@@ -9,6 +9,8 @@
 //   1  release store of a sequence number at system scope (as now)
 //   2  relaxed system-scope stores + s_waitcnt (no L2 writeback)
 //   3  release store at agent scope into device memory (control)
+//   4  a relaxed system-scope LOAD from mapped host memory, its value stored
+//      into device memory (what a kernel's read of a host-side result costs)
 // Prints us per pair.   hipcc --offload-arch=gfx950 -O3 -o flag_gap flag_gap.hip
 #include <hip/hip_runtime.h>
 
@@ -44,6 +46,9 @@ __global__ void w_kernel(double* v, int64_t n, int mode, unsigned long long* hfl
         __hip_atomic_store(hflag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     } else if (mode == 3) {
         __hip_atomic_store(dflag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    } else if (mode == 4) {
+        const double h = __hip_atomic_load(hdata, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(dflag, (unsigned long long)h + seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -74,7 +79,7 @@ int main(int argc, char** argv) {
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
-    for (int mode : {0, 1, 2, 3, 0, 1, 2, 3}) {
+    for (int mode : {0, 1, 2, 3, 4, 0, 1, 2, 3, 4}) {
         for (int withb : {0, 1}) {
             unsigned long long seq = 1;
             auto pair = [&] {
