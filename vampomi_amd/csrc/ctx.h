@@ -224,6 +224,12 @@ class DotBatch {
     vampomi_status add_many(int64_t n, const std::vector<Group>& groups, const vk::G1Chain* chain = nullptr,
                             const double* chain_of = nullptr,
                             const std::vector<std::pair<const double*, double*>>& copies = {});
+    // add_many over [0, na) with ga and over [0, nb) with gb in one launch
+    // where vk::dots2 has the pairing (else two launches): the same results
+    vampomi_status add_pair(int64_t na, const std::vector<Group>& ga, const vk::G1Chain* chain,
+                            const double* chain_of, const std::vector<std::pair<const double*, double*>>& ca,
+                            int64_t nb, const std::vector<Group>& gb,
+                            const std::vector<std::pair<const double*, double*>>& cb);
     // reserves nq result slots for a fused reduction kernel: *ro says where the
     // kernel writes; the values reach out[0..nq) at flush()
     vampomi_status sink(int nq, bool sync, double* out, vk::RedOut* ro);
@@ -246,6 +252,10 @@ class DotBatch {
     hipStream_t stream() const;
 
    private:
+    // a launch's DotArgs and RedOut from its groups (sinks registered, flag sequence taken)
+    vampomi_status build(const std::vector<Group>& groups, const vk::G1Chain* chain, const double* chain_of,
+                         const std::vector<std::pair<const double*, double*>>& copies, vk::DotArgs& a,
+                         vk::RedOut& ro);
     struct Sink {
         int slot, count;
         double* out;

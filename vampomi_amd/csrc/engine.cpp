@@ -551,10 +551,41 @@ vampomi_status DotBatch::add(std::initializer_list<vk::DotTerm> terms, int64_t n
 vampomi_status DotBatch::add_many(int64_t n, const std::vector<Group>& groups, const vk::G1Chain* chain,
                                   const double* chain_of,
                                   const std::vector<std::pair<const double*, double*>>& copies) {
+    vk::DotArgs a{};
+    vk::RedOut ro{};
+    STCHK(build(groups, chain, chain_of, copies, a, ro));
+    HIPCHK(vk::dots(a, n, ro, stream()));
+    return VAMPOMI_OK;
+}
+
+vampomi_status DotBatch::add_pair(int64_t na, const std::vector<Group>& ga, const vk::G1Chain* chain,
+                                  const double* chain_of, const std::vector<std::pair<const double*, double*>>& ca,
+                                  int64_t nb, const std::vector<Group>& gb,
+                                  const std::vector<std::pair<const double*, double*>>& cb) {
+    vk::DotArgs a{}, b{};
+    vk::RedOut roa{}, rob{};
+    STCHK(build(ga, chain, chain_of, ca, a, roa));
+    STCHK(build(gb, nullptr, nullptr, cb, b, rob));
+    const size_t need = (size_t)vk::red_blocks(na) * a.nt + (size_t)vk::red_blocks(nb) * b.nt;
+    if (a.nt == 10 && b.nt == 11 && need <= c_->red_cap) {  // (the pairing vk::dots2 instantiates)
+        roa.flag = nullptr;  // b's flag (the later sequence number) covers both
+        rob.part = roa.part + (int64_t)vk::red_blocks(na) * a.nt;
+        rob.ticket = roa.ticket;
+        HIPCHK(vk::dots2(a, na, roa, b, nb, rob, stream()));
+    } else {
+        HIPCHK(vk::dots(a, na, roa, stream()));
+        HIPCHK(vk::dots(b, nb, rob, stream()));
+    }
+    return VAMPOMI_OK;
+}
+
+vampomi_status DotBatch::build(const std::vector<Group>& groups, const vk::G1Chain* chain, const double* chain_of,
+                               const std::vector<std::pair<const double*, double*>>& copies, vk::DotArgs& a,
+                               vk::RedOut& ro) {
     if (copies.size() > 2) return fail(VAMPOMI_ERR_ARG, "DotBatch: at most 2 device copies per launch");
     // terms in the order [local groups..., synced groups...]: each kind's
     // results land in one contiguous slot range (out, then out2 from split)
-    vk::DotArgs a{};
+    a = vk::DotArgs{};
     int nloc = 0, nsyn = 0;
     for (const Group& g : groups) (g.sync ? nsyn : nloc) += (int)g.terms.size();
     a.nt = nloc + nsyn;
@@ -586,7 +617,7 @@ vampomi_status DotBatch::add_many(int64_t n, const std::vector<Group>& groups, c
     }
     if (chain && !a.g1.out) return fail(VAMPOMI_ERR_ARG, "DotBatch: the chained group is not in the launch");
     if (a.copy.n != (int)copies.size()) return fail(VAMPOMI_ERR_ARG, "DotBatch: a copied group is not in the launch");
-    vk::RedOut ro{};
+    ro = vk::RedOut{};
     ro.part = on_side_ ? c_->red_part2 : c_->red_part;
     ro.ticket = on_side_ ? c_->ticket2 : c_->ticket;
     ro.out = base + SL_LOCAL + nlocal_;
@@ -603,7 +634,6 @@ vampomi_status DotBatch::add_many(int64_t n, const std::vector<Group>& groups, c
     }
     nlocal_ += nloc;
     nsync_ += nsyn;
-    HIPCHK(vk::dots(a, n, ro, stream()));
     return VAMPOMI_OK;
 }
 

@@ -227,6 +227,12 @@ int red_blocks(int64_t n);
 // ro.out[q] = term q summed over [0, n): per-block partials, then the blocks'
 // sums in block order (fixed geometry: depends on n only)
 hipError_t dots(const DotArgs& a, int64_t n, const RedOut& ro, hipStream_t st);
+// a over [0, na) and b over [0, nb) in ONE launch, each bitwise as its own
+// dots launch (its partials at its RedOut's part; one shared ticket; roa
+// without a flag, rob's flag after both).  No PUPD / SQPUPD terms; the term
+// counts of the pairs instantiated (10, 11) only, else hipErrorInvalidValue
+hipError_t dots2(const DotArgs& a, int64_t na, const RedOut& roa, const DotArgs& b, int64_t nb, const RedOut& rob,
+                 hipStream_t st);
 
 // ---- denoiser (vamp::g1 / g1d) ---------------------------------------------
 struct Mix {

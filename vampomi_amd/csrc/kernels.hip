@@ -72,18 +72,26 @@ __device__ __forceinline__ void block_put_sums(double (&v)[NQ], int nq, const Re
 // Returns true in the last block (after out[] is written; thread 0 wrote it).
 // keep (LDS, may be null): thread 0 also leaves the results there (a caller
 // that goes on with them in thread 0 then reads no global memory).
-__device__ bool red_finish(const RedOut& ro, int nq, double* /*lds4*/, double* keep = nullptr) {
+// (red_finish's halves, for a launch that finishes two reductions: dots2)
+// every partial store of this block is acknowledged before the ticket moves;
+// true in the block that brings it to nblocks (block-uniform)
+__device__ bool red_ticket(const RedOut& ro, int nblocks) {
     __shared__ int is_last;
-    __shared__ double lds[4 * 8];
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    __builtin_amdgcn_s_waitcnt(0);  // every partial store of this block is acknowledged ...
+    __builtin_amdgcn_s_waitcnt(0);
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    __syncthreads();                // ... before the ticket moves
-    if (threadIdx.x == 0)
-        is_last = __hip_atomic_fetch_add(ro.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
     __syncthreads();
-    if (!is_last) return false;
-    const int nblk = (int)gridDim.x;
+    if (threadIdx.x == 0)
+        is_last = __hip_atomic_fetch_add(ro.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                  (unsigned)nblocks - 1;
+    __syncthreads();
+    return is_last;
+}
+
+// the last block's sums of the nblk blocks' partials at ro.part, into ro.out
+// (and keep); finish: then re-arm the ticket and store the host flag
+__device__ void red_final(const RedOut& ro, int nq, int nblk, double* keep, bool finish) {
+    __shared__ double lds[4 * 8];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     for (int q0 = 0; q0 < nq; q0 += 8) {
         const int nc = nq - q0 < 8 ? nq - q0 : 8;
@@ -112,14 +120,14 @@ __device__ bool red_finish(const RedOut& ro, int nq, double* /*lds4*/, double* k
                 const double v = ((lds[c] + lds[8 + c]) + lds[16 + c]) + lds[24 + c];
                 const int q = q0 + c;
                 double* dst = ro.out2 && q >= ro.split ? ro.out2 + (q - ro.split) : ro.out + q;
-                if (ro.flag)  // mapped host memory: written through, drained before the flag below
+                if (ro.flag || !finish)  // mapped host memory: written through, drained before the flag below
                     __hip_atomic_store(dst, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 else
                     *dst = v;
                 if (keep) keep[q0 + c] = v;
             }
     }
-    if (threadIdx.x == 0) {
+    if (finish && threadIdx.x == 0) {
         __hip_atomic_store(ro.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         // host completion flag, after the results above have landed (drained
         // write-through stores: no release fence, which would first write back
@@ -129,6 +137,19 @@ __device__ bool red_finish(const RedOut& ro, int nq, double* /*lds4*/, double* k
             __hip_atomic_store(ro.flag, ro.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
+}
+
+// The last block sums up to 8 results per round: each thread adds its
+// blocks' partials of every result (blocks in order), then each result is
+// wave-reduced and the four wave sums added in wave order — per result, the
+// operations of block_sum, so the sums are bitwise those of one block_sum per
+// result, with one barrier round per 8 results instead of one per result.
+// Returns true in the last block (after out[] is written; thread 0 wrote it).
+// keep (LDS, may be null): thread 0 also leaves the results there (a caller
+// that goes on with them in thread 0 then reads no global memory).
+__device__ bool red_finish(const RedOut& ro, int nq, double* /*lds4*/, double* keep = nullptr) {
+    if (!red_ticket(ro, (int)gridDim.x)) return false;
+    red_final(ro, nq, (int)gridDim.x, keep, true);
     return true;
 }
 
@@ -1259,17 +1280,16 @@ __device__ __forceinline__ void gam1_chain(double a2, double gam2, double rho, d
 // the op is a per-launch uniform selected per element.  UPD: some term is a
 // PUPD / SQPUPD (its c and beta are loaded); a launch without one does not
 // keep those pointers (up to 12 terms without scalar-register spills)
+// one reduction's blocks [bid of nblk]: the per-block partials of its NT terms
 template <int NT, bool UPD>
-__global__ __launch_bounds__(kBlock) void dots_kernel(DotArgs a, int64_t n, RedOut ro) {
-    if (ro.gate && !*ro.gate) return;
-    __shared__ double lds[4];
+__device__ __forceinline__ void dots_part(const DotArgs& a, int64_t n, const RedOut& ro, int bid, int nblk) {
     double bt[NT];
 #pragma unroll
     for (int q = 0; q < NT; ++q) bt[q] = UPD && (a.t[q].op == PUPD || a.t[q].op == SQPUPD) ? *a.t[q].beta : 0.0;
     double acc[NT];
 #pragma unroll
     for (int q = 0; q < NT; ++q) acc[q] = 0.0;
-    for (int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x; e < n; e += (int64_t)gridDim.x * kBlock) {
+    for (int64_t e = (int64_t)bid * kBlock + threadIdx.x; e < n; e += (int64_t)nblk * kBlock) {
         double va[NT], vb[NT];
 #pragma unroll
         for (int q = 0; q < NT; ++q) {
@@ -1288,13 +1308,59 @@ __global__ __launch_bounds__(kBlock) void dots_kernel(DotArgs a, int64_t n, RedO
             acc[q] += v;
         }
     }
-    block_put_sums<NT>(acc, NT, ro, (int64_t)blockIdx.x * NT);
+    block_put_sums<NT>(acc, NT, ro, (int64_t)bid * NT);
+}
+
+// the launch's hooks on its final sums (thread 0 of the last block)
+__device__ __forceinline__ void dots_post(const DotArgs& a, const double* fin) {
+    if (a.g1.out) gam1_chain(fin[a.g1.term], a.g1.gam2, a.g1.rho, a.g1.gam1_prev, a.g1.out);
+    for (int j = 0; j < a.copy.n && j < 2; ++j) a.copy.dst[j][0] = fin[a.copy.term[j]];
+}
+
+template <int NT, bool UPD>
+__global__ __launch_bounds__(kBlock) void dots_kernel(DotArgs a, int64_t n, RedOut ro) {
+    if (ro.gate && !*ro.gate) return;
+    __shared__ double lds[4];
+    dots_part<NT, UPD>(a, n, ro, (int)blockIdx.x, (int)gridDim.x);
     __shared__ double fin[NT];
     const bool post = a.g1.out || a.copy.n;
-    if (red_finish(ro, NT, lds, post ? fin : nullptr) && post && threadIdx.x == 0) {
-        if (a.g1.out) gam1_chain(fin[a.g1.term], a.g1.gam2, a.g1.rho, a.g1.gam1_prev, a.g1.out);
-        for (int j = 0; j < a.copy.n && j < 2; ++j) a.copy.dst[j][0] = fin[a.copy.term[j]];
+    if (red_finish(ro, NT, lds, post ? fin : nullptr) && post && threadIdx.x == 0) dots_post(a, fin);
+}
+
+// Two reductions in one launch (dots2): blocks [0, ba) are reduction A's
+// (red_blocks(na) of them), the rest B's; each part's partials, final sums and
+// hooks are those of its own dots launch, bit for bit.  One ticket counts every
+// block; the last one finishes A, then B (B's RedOut carries the flag).
+template <int NA, int NB>
+__global__ __launch_bounds__(kBlock) void dots2_kernel(DotArgs a, int64_t na, RedOut roa, int ba, DotArgs b,
+                                                       int64_t nb, RedOut rob) {
+    if ((int)blockIdx.x < ba)
+        dots_part<NA, false>(a, na, roa, (int)blockIdx.x, ba);
+    else
+        dots_part<NB, false>(b, nb, rob, (int)blockIdx.x - ba, (int)gridDim.x - ba);
+    if (!red_ticket(roa, (int)gridDim.x)) return;
+    __shared__ double fa[NA], fb[NB];
+    red_final(roa, NA, ba, fa, false);
+    red_final(rob, NB, (int)gridDim.x - ba, fb, true);
+    if (threadIdx.x == 0) {
+        dots_post(a, fa);
+        dots_post(b, fb);
     }
+}
+
+hipError_t dots2(const DotArgs& a, int64_t na, const RedOut& roa, const DotArgs& b, int64_t nb, const RedOut& rob,
+                 hipStream_t st) {
+    const int ba = red_blocks(na), bb = red_blocks(nb);
+    if (roa.flag || roa.gate || rob.gate || rob.ticket != roa.ticket) return hipErrorInvalidValue;
+    for (const DotArgs* x : {&a, &b})
+        for (int q = 0; q < x->nt; ++q)
+            if (x->t[q].op == PUPD || x->t[q].op == SQPUPD) return hipErrorInvalidValue;
+    const dim3 g(ba + bb), blk(kBlock);
+    if (a.nt == 10 && b.nt == 11)
+        hipLaunchKernelGGL((dots2_kernel<10, 11>), g, blk, 0, st, a, na, roa, ba, b, nb, rob);
+    else
+        return hipErrorInvalidValue;  // (the one pairing in use: vamp.cpp's iteration tail)
+    return hipGetLastError();
 }
 
 template <bool UPD>

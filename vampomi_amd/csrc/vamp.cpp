@@ -653,9 +653,9 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
     if (chain) {
         // every reduction of the iteration's tail reads vectors the solves have
         // just finished: err_measures of x1 (:272) and of x2 (:365, A x2 from
-        // the CG) with the sums above, ONE launch per vector length (10 terms
-        // over M, 11 over N); each term's sum is the same fixed-order reduction
-        // as in its own launch (the launch geometry depends on the length only)
+        // the CG) with the sums above: 10 terms over M and 11 over N, in ONE
+        // launch (vk::dots2); each term's sum is the same fixed-order reduction
+        // as in its own launch (the geometry depends on the length only)
         std::vector<DotBatch::Group> gm{ga2}, gn;
         err_groups(c, R, R.x1, R.z1, R.e1m, R.e1n, R.e1s, gm, gn);
         gm.push_back(gtc);
@@ -669,8 +669,7 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
         g1.gam1_prev = gam1_prev;
         g1.out = dsc;
         // (tc and tn also into device memory, for the next prelude's scalars: vk::PreOut)
-        STCHK(fin.add_many(M, gm, &g1, &R.a2, {{&R.tc, dsc + 9}}));
-        STCHK(fin.add_many(N, gn, nullptr, nullptr, {{&R.tn, dsc + 8}}));
+        STCHK(fin.add_pair(M, gm, &g1, &R.a2, {{&R.tc, dsc + 9}}, N, gn, {{&R.tn, dsc + 8}}));  // one launch
     } else {
         DotBatch b(c);
         if (arec)
