@@ -1574,15 +1574,26 @@ __global__ __launch_bounds__(kBlock) void em_kernel(int64_t M, const double* __r
         }
     }
     const int L = a.L, Q = 1 + 2 * (L - 1);
+    // em_num of the first kEmC - 1 slabs is formed once and kept in registers
+    // (fixed-bound unrolled loops: no run-time register indexing); the same
+    // values, summed in the same order, as forming it twice
+    constexpr int kEmC = 12;
+    double en[kEmC];
     double sum_of_elems = 0.0;
-    for (int j = 1; j < L; ++j) sum_of_elems += em_num(a, noise_var, r, j);
+#pragma unroll
+    for (int j = 1; j < kEmC; ++j)
+        if (j < L) {
+            en[j] = em_num(a, noise_var, r, j);
+            sum_of_elems += en[j];
+        }
+    for (int j = kEmC; j < L; ++j) sum_of_elems += em_num(a, noise_var, r, j);
     const double pin = 1 / (1 + (1 - a.lambda) / sqrt(2 * M_PI * noise_var) *
                                     exp(-(r * r) / 2 * a.max_sigma / noise_var / (noise_var + a.max_sigma)) /
                                     sum_of_elems);
     double s = wave_sum(valid ? pin : 0.0);
     if (lane == 0) wl[w][0] = s;
-    for (int j = 1; j < L; ++j) {
-        const double beta = em_num(a, noise_var, r, j) / sum_of_elems;
+    auto slab = [&](int j, double num) {
+        const double beta = num / sum_of_elems;
         const double g = gam1 * r / (1 / a.vars[j] + gam1);
         const double vj = a.dsc ? 1.0 / (1.0 / a.vars[j] + gam1) : a.v[j - 1];
         const double gam = beta * (g * g + vj);
@@ -1592,7 +1603,11 @@ __global__ __launch_bounds__(kBlock) void em_kernel(int64_t M, const double* __r
             wl[w][j] = sb;
             wl[w][(L - 1) + j] = sg;
         }
-    }
+    };
+#pragma unroll
+    for (int j = 1; j < kEmC; ++j)
+        if (j < L) slab(j, en[j]);
+    for (int j = kEmC; j < L; ++j) slab(j, em_num(a, noise_var, r, j));
     __syncthreads();
     for (int q = threadIdx.x; q < Q; q += kBlock)
         red_put(ro, (int64_t)blockIdx.x * Q + q, ((wl[0][q] + wl[1][q]) + wl[2][q]) + wl[3][q]);
