@@ -28,6 +28,14 @@
 // batch_rhs=4 (the default) reads X once per CG step: A p is carried as an
 // N-vector recurrence and the one-pass operator (atax_team.hip) forms A^T q
 // and A d from the same column read: 1 + max(k1, k2) passes per iteration.
+// On one rank the iteration's tail after the solves runs without the host
+// (DESIGN.md §4.4 item 5): its reductions in one launch (vk::dots2) whose
+// last block also forms gam1 (vk::G1Chain); the EM round, whose last block
+// forms the mixture update; the next denoising, whose last block forms the
+// next prelude's scalars (vk::PreOut); and the next prelude + CG start
+// (pcg_run's PreMode::ahead).  The host waits once, at the end, forms the
+// same scalars and mixture from the same sums, and checks the device's bit
+// for bit after the next solves (check_device_values).
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
