@@ -307,9 +307,11 @@ vampomi_status vampomi_reset_stats(vampomi_ctx* ctx);
  * prefetched EM/denoiser, 0 off, 1 on (default: on with several ranks).
  * which = 5: the CG head start of the linear model (the Onsager solve's first
  * step in the pass that starts the x2 solve, pcg.cpp), 0 off, 1 on (default
- * on; VAMPOMI_HEADSTART=0 turns it off at vampomi_open).  Several ranks run the
- * head start only if every rank has it on (agreed at the next collective
- * call: it changes the job's collective sequence). */
+ * on; VAMPOMI_HEADSTART=0 turns it off at vampomi_open).  On a context with
+ * several ranks, which = 3 and 5 take effect at the next vampomi_vamp_begin
+ * (or vampomi_infere), where the ranks agree on them: the one-pass operator
+ * runs only if every rank has a plan for it, the head start only if every rank
+ * has it on (both change the job's collective sequence). */
 vampomi_status vampomi_dev_set_variant(vampomi_ctx* ctx, int which, int variant);
 /* average device time (HIP events) of `reps` back-to-back launches, K RHS */
 vampomi_status vampomi_dev_time_pass(vampomi_ctx* ctx, int which, int K, int reps, double* avg_ms);

@@ -72,6 +72,7 @@ def load() -> C.CDLL:
         lib.orc_ax_local.argtypes = [p, i64, i64, i64, p, p, p, p]
         lib.orc_ax.argtypes = [p, i64, i64, i64, p, p, p, p, ALLREDUCE_FN, p]
         lib.orc_atx.argtypes = [p, i64, i64, i64, p, p, p, p]
+        lib.orc_set_atx_block.argtypes = [C.c_int]
         lib.orc_g1.restype = d
         lib.orc_g1.argtypes = [d, d, p, p, C.c_int]
         lib.orc_g1d.restype = d
@@ -152,6 +153,11 @@ def atx(X, mave, msig, u) -> np.ndarray:
     out = np.empty(M)
     load().orc_atx(_p(X), N, N, M, _p(mave), _p(msig), _p(np.ascontiguousarray(u, dtype=np.float64)), _p(out))
     return out
+
+
+def set_atx_block(B: int) -> None:
+    """Sensitivity mode: A^T.u sums samples in blocks of B rows (0 = off)."""
+    load().orc_set_atx_block(int(B))
 
 
 def g1(y: float, gam1: float, probs, vars_scaled) -> float:

@@ -276,15 +276,35 @@ void orc_ax(const double* X, int64_t N, int64_t ld, int64_t M, const double* mav
     for (int64_t j = 0; j < N; ++j) out[j] /= sq; /* src/data.cpp:369-370 */
 }
 
+/* Sensitivity mode (test infrastructure, off by default): with B > 0 the
+ * per-marker sum over samples of orc_atx runs in blocks of B rows whose sums
+ * are combined in block order -- the kind of reassociation every parallel
+ * A^T.u has (the device splits a column's rows over lanes, waves and team
+ * members).  Together with the virtual-shard runs (tests/_data.py, many ranks:
+ * the sums over markers split) it measures how far the reference's own result
+ * moves under a change of summation order (tests/golden/make_c4_window.py). */
+static int g_atx_block = 0;
+void orc_set_atx_block(int B) { g_atx_block = B > 0 ? B : 0; }
+
 /* ATx / dot_product — src/data.cpp:294-333 */
 void orc_atx(const double* X, int64_t N, int64_t ld, int64_t M, const double* mave,
              const double* msig, const double* u, double* out) {
+    const int64_t B = g_atx_block;
 #pragma omp parallel for schedule(static)
     for (int64_t i = 0; i < M; ++i) {
         const double* m = X + i * ld;
         double mu = mave[i];
         double dpa = 0.0;
-        for (int64_t j = 0; j < N; ++j) dpa += (m[j] - mu) * u[j];
+        if (B > 0) {
+            for (int64_t lo = 0; lo < N; lo += B) {
+                const int64_t hi = lo + B < N ? lo + B : N;
+                double b = 0.0;
+                for (int64_t j = lo; j < hi; ++j) b += (m[j] - mu) * u[j];
+                dpa += b;
+            }
+        } else {
+            for (int64_t j = 0; j < N; ++j) dpa += (m[j] - mu) * u[j];
+        }
         out[i] = msig[i] * dpa;
     }
     double scale = 1.0 / sqrt((double)N);

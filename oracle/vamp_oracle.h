@@ -75,6 +75,10 @@ void orc_ax(const double* X, int64_t N, int64_t ld, int64_t M, const double* mav
 void orc_atx(const double* X, int64_t N, int64_t ld, int64_t M, const double* mave,
              const double* msig, const double* u, double* out);
 
+/* sensitivity mode: orc_atx sums samples in blocks of B rows (0 = sequential,
+ * the reference's order); process-wide, test infrastructure only */
+void orc_set_atx_block(int B);
+
 /* ---- denoiser (src/vamp.cpp:440-492) ---- */
 double orc_g1(double y, double gam1, const double* probs, const double* vars, int L);
 double orc_g1d(double y, double gam1, const double* probs, const double* vars, int L);

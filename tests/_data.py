@@ -12,8 +12,15 @@ from oracle import pyoracle as O
 
 def make_problem(N: int, Mt: int, seed: int = 3, kind: int = 0, lam: float = 0.1, h2: float = 0.8):
     """X (Mt, N) marker-major, y (N, standardised like read_phen), beta (Mt)."""
-    lib = O.load()
     X = O.generate_markers(seed, kind, N, 0, Mt)
+    y, beta = phen_from_markers(X, seed, lam, h2)
+    return X, y, beta
+
+
+def phen_from_markers(X, seed: int = 3, lam: float = 0.1, h2: float = 0.8):
+    """make_problem's phenotype for a given design X (Mt, N): (y, beta)."""
+    lib = O.load()
+    Mt, N = X.shape
     mave, msig = O.marker_stats(X)
     beta = np.zeros(Mt)
     causal = np.array([(lib.orc_splitmix64(seed * 7919 + i) >> 11) * 2.0 ** -53 < lam for i in range(Mt)])
@@ -23,7 +30,7 @@ def make_problem(N: int, Mt: int, seed: int = 3, kind: int = 0, lam: float = 0.1
     z = O.ax(X, mave, msig, beta * np.sqrt(N))  # sum_i (X_i - mave_i) msig_i beta_i, fixed order
     noise = np.array([lib.orc_gauss_dyadic(seed + 202, -1, j) for j in range(N)])
     y = O.standardize_phen(z + np.sqrt(1 - h2) * noise)
-    return X, y, beta
+    return y, beta
 
 
 class ThreadComm:
@@ -64,32 +71,51 @@ def sharded_oracle(X, y, beta, Mt, P, **kw):
     return res
 
 
-def oracle_with_spread(X, y, beta, Mt, ranks=(2, 3, 4), **kw):
+def oracle_with_spread(X, y, beta, Mt, ranks=(2, 3, 4), blocks=(), ref=None, per_variant=None, **kw):
     """The single-rank oracle run plus the reference's own sensitivity to the
-    all-reduce order: per iteration, the largest norm-relative change of
-    x1 / r1 (and element-wise of params) when the same problem runs on 2, 3
-    or 4 ranks.  Returns (ref, spread) with spread["x1"], spread["r1"] of
-    shape (iterations,) and spread["params"] like ref["params"]."""
-    ref = O.vamp_infere(X, y, Mt, true_signal=beta, **kw)
+    summation order: per iteration, the largest norm-relative change of
+    x1 / r1 (and element-wise of params, metrics, prior) when the same
+    problem runs
+    * on P ranks for P in `ranks` (the all-reduce order, exactly what
+      `mpirun -np P` changes for the reference; P = 64 or 128 "virtual
+      shards" split the sums over markers as finely as the device's team
+      slots do), and
+    * with orc_atx summing samples in blocks of B rows for (P, B) in `blocks`
+      (the sums over samples, which a rank count never splits).
+    Returns (ref, spread) with spread["x1"], spread["r1"] of shape
+    (iterations,) and spread["params"] like ref["params"].  `ref` may be
+    passed in (the single-rank run, already made); `per_variant` (a dict)
+    receives each variant's own spread."""
+    if ref is None:
+        ref = O.vamp_infere(X, y, Mt, true_signal=beta, **kw)
     kw = {k: v for k, v in kw.items() if k not in ("out_dir", "out_name")}  # files: single-rank run only
     n = ref["iterations"]
     sp = {"x1": np.zeros(n), "r1": np.zeros(n), "params": np.zeros_like(ref["params"]),
           "metrics": np.zeros_like(ref["metrics"])}
-    for P in ranks:
-        res = sharded_oracle(X, y, beta, Mt, P, **kw)
-        assert res[0]["iterations"] == n, "the reference's own iteration count depends on the rank count"
+    for P, B in [(P, 0) for P in ranks] + list(blocks):
+        O.set_atx_block(B)
+        try:
+            res = sharded_oracle(X, y, beta, Mt, P, **kw) if P > 1 else \
+                [O.vamp_infere(X, y, Mt, true_signal=beta, **kw)]
+        finally:
+            O.set_atx_block(0)
+        assert res[0]["iterations"] == n, "the reference's own iteration count depends on the summation order"
+        own = {}
         for key in ("x1", "r1"):
             h = np.concatenate([r[f"{key}_hist"] for r in res], axis=1)
             num = np.linalg.norm(h - ref[f"{key}_hist"], axis=1)
             den = np.maximum(np.linalg.norm(ref[f"{key}_hist"], axis=1), 1e-300)
-            sp[key] = np.maximum(sp[key], num / den)
+            own[key] = num / den
         for key in ("params", "metrics", "prior"):
             if key not in ref:
                 continue
             a, b = res[0][key], ref[key]
             with np.errstate(invalid="ignore", divide="ignore"):
-                e = np.where(np.isnan(a) & np.isnan(b), 0.0, np.abs(a - b) / np.maximum(np.abs(b), 1e-300))
+                own[key] = np.where(np.isnan(a) & np.isnan(b), 0.0, np.abs(a - b) / np.maximum(np.abs(b), 1e-300))
+        for key, e in own.items():
             sp[key] = np.maximum(sp.get(key, np.zeros_like(e)), e)
+        if per_variant is not None:
+            per_variant[(P, B)] = own
     return ref, sp
 
 

@@ -322,3 +322,38 @@ def test_headstart_agreed_over_ranks(monkeypatch):
         assert np.allclose(p["params"], off["params"], rtol=1e-11)
     for k in range(its):
         assert relerr(_cat(parts, "x1_hist")[k], off["x1_hist"][k]) < 1e-12, k
+
+
+def test_rank_local_switches_between_runs(monkeypatch):
+    """a rank-local set_variant(5) (and a one-rank timing hook on
+    the operator) between two runs of a job must not make the ranks issue
+    different collectives.  The choice is agreed at vampomi_vamp_begin, the
+    one point every rank reaches, so the second run -- head start off on
+    rank 1 only -- runs without it on both ranks (bitwise the one-rank run
+    with it off) and the first run with it (bitwise the one-rank default)."""
+    import ctypes as C
+
+    N, Mt, its = 1001, 2003, 6
+    X, y, beta = make_problem(N, Mt)
+    kw = dict(max_iter=its, stop_criteria_thr=0.0)
+    one = {}
+    for hs in (1, 0):
+        with va.Data(N, Mt) as d:
+            d.set_variant(5, hs)
+            one[hs] = _vamp(d, X, y, beta, **kw)
+
+    def fn(r, d):
+        first = _vamp(d, X, y, beta, **kw)
+        if r == 1:
+            d.set_variant(5, 0)
+            ms = C.c_double()
+            va.load().vampomi_dev_time_pass(d.ctx, 3, 1, 1, C.byref(ms))  # plans this rank's operator, no agreement
+        return first, _vamp(d, X, y, beta, **kw)
+
+    parts = run_ranks(monkeypatch, 2, N, Mt, fn)
+    for run, hs in ((0, 1), (1, 0)):
+        ps = [p[run] for p in parts]
+        for p in ps:
+            assert p["cg_iters"] == one[hs]["cg_iters"] and p["ons_iters"] == one[hs]["ons_iters"]
+        for k in range(its):
+            assert relerr(_cat(ps, "x1_hist")[k], one[hs]["x1_hist"][k]) < 1e-12, (run, k)

@@ -97,6 +97,23 @@ def test_pow_minus_one_is_within_one_ulp_of_the_reciprocal(tmp_path):
     assert tot > 3_000_000 and maxulp <= 1 and bad < 0.01 * tot
 
 
+def test_device_exp_is_correctly_rounded(tmp_path):
+    """The probit denoiser's erfcx (src/utilities.cpp:293-363) calls exp; the
+    device evaluates it as exp_cr (vampomi_amd/csrc/exp_cr.h, the same source
+    compiled here): equal to the 113-bit expq rounded to double on every
+    argument tried, and to glibc's exp (the reference's, the oracle's) except
+    where glibc misrounds (~0.08 %, one ulp; profiles/r05_exp_cr_check.txt holds
+    the 1e8-argument run)."""
+    exe = tmp_path / "expcr"
+    subprocess.run(["gcc", "-O2", "-ffp-contract=off", os.path.join(ROOT, "tests", "exp_cr_check.c"),
+                    "-o", str(exe), "-lquadmath", "-lm"], check=True)
+    lines = [ln.split() for ln in run(str(exe), 300000).strip().splitlines()]
+    for name, tried, cr_vs_quad, glibc_vs_quad, cr_vs_glibc, maxulp in lines[:3]:
+        assert int(tried) == 300000 and int(cr_vs_quad) == 0, name
+        assert int(maxulp) <= 1 and int(cr_vs_glibc) == int(glibc_vs_quad) and int(cr_vs_glibc) < 0.002 * int(tried)
+    assert lines[3] == ["special", "0", "0"]
+
+
 def test_cli_rendezvous_never_reads_an_earlier_jobs_file(harness, tmp_path):
     """main_meth.exe's rank rendezvous (vio::rdzv_*): a second job into the same
     out-dir must not pick up the first job's RCCL id, with a run nonce (torchrun

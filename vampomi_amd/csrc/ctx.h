@@ -116,8 +116,14 @@ struct vampomi_ctx {
     // one-pass CG operator (batch_rhs 4; allocated on first use, pcg.cpp)
     vk::OpPlan opp{};
     int op_variant = vk::kOpDefault;  // plan choice (dev hook: vampomi_dev_set_variant(c, 3, v))
-    bool op_ready = false;            // opp planned and its buffers allocated
-    bool op_ok = false;               // a plan exists for this N
+    bool op_ready = false;            // opp planned (locally) and its buffers allocated
+    bool op_ok_mine = false;          // this rank's plan exists and its grid fits the device
+    bool op_ok = false;               // the operator runs: op_ok_mine on one rank; the agreed value on several
+    // several ranks: the one-pass / head-start choice is agreed at one fixed
+    // collective point every rank reaches (op_agree, at vampomi_vamp_begin);
+    // set_variant(3 / 5) requests wait for it (applied at once on one rank)
+    bool op_agreed = false;
+    int op_variant_req = vk::kOpDefault;
     int cus = 0;                // compute units of the device (the operator's grid)
     double* op_part = nullptr;  // opp.nslots x kMaxRhs x ld partial A d
     int64_t op_part_slots = 0;
@@ -128,8 +134,10 @@ struct vampomi_ctx {
     // the head-start launch (pcg.cpp): its plan and whether it runs (default
     // on; VAMPOMI_HEADSTART=0 or vampomi_dev_set_variant(c, 5, 0) turns it off)
     vk::OpPlan opp_hs{};
-    bool hs_ok = false;
+    bool hs_ok_mine = false;  // this rank's head-start plan exists and fits
+    bool hs_ok = false;       // the head start runs (hs_on included; agreed on several ranks)
     bool hs_on = true;
+    bool hs_on_req = true;
     unsigned long long* op_ts = nullptr;  // VAMPOMI_OP_TS=1 (TM_TS builds): the last launch's workgroup times
     double* nbuf = nullptr;     // kMaxRhs * ld scratch N-vectors (API calls)
     double* mbuf = nullptr;     // (2*kMaxRhs) * M scratch M-vectors (API calls)
@@ -328,13 +336,19 @@ vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double
                        const double* extra_x = nullptr, double* ex_out = nullptr, bool onepass = false,
                        const double* const* ar0 = nullptr, HeadStart* hs = nullptr,
                        const vk::Prelude* pre = nullptr, PreMode pm = PreMode::normal);
-// plans the one-pass operator (c->opp, c->op_ok, c->hs_ok) and allocates its
-// buffers (idempotent until the plan or the head-start switch changes).
-// COLLECTIVE when collective (several ranks): the ranks agree on op_ok and
-// hs_ok (both change the collective sequence); false only for one-rank hooks
-vampomi_status op_prepare(vampomi_ctx* c, bool collective = true);
+// plans the one-pass operator on this rank (c->opp, op_ok_mine, hs_ok_mine)
+// and allocates its buffers (idempotent until the plan or the head-start
+// switch changes); never a collective.  Sets op_ok / hs_ok: this rank's plan
+// on one rank; on several the values op_agree agreed (both false before it)
+vampomi_status op_prepare(vampomi_ctx* c);
+// COLLECTIVE (several ranks; nothing on one): applies pending set_variant(3 /
+// 5) requests, plans, and agrees op_ok and hs_ok over the ranks (both change
+// the job's collective sequence; each rank planned from its own shard size,
+// CU count and VAMPOMI_HEADSTART).  Called unconditionally by
+// vampomi_vamp_begin, the one point every rank of a run reaches
+vampomi_status op_agree(vampomi_ctx* c);
 // whether pcg_run's head start can run on this context (plans the operator;
-// the same answer on every rank).  COLLECTIVE
+// the same answer on every rank)
 vampomi_status headstart_available(vampomi_ctx* c, bool* yes);
 // the device word a team launch sets when a hand-off timed out, and its host view
 unsigned* op_err_dev(vampomi_ctx* c);

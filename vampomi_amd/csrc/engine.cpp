@@ -184,14 +184,18 @@ void drop_launches(vampomi_ctx* c, size_t pending_mark, const vampomi_stats& bef
 //
 // With an RCCL communicator the waits also watch the job: a peer that died or
 // a communicator RCCL reports broken (ncclCommGetAsyncError) or a wait longer
-// than VAMPOMI_COLL_TIMEOUT_S (default 600 s; the queued all-reduce waits for
+// than VAMPOMI_COLL_TIMEOUT_S (default 120 s; the queued all-reduce waits for
 // a peer that never comes) aborts this rank's communicator (ncclCommAbort)
-// and fails, instead of blocking forever in a collective.
+// and fails, instead of blocking forever in a collective.  A healthy job's
+// ranks reach each collective within milliseconds of each other; the one
+// legitimate long wait is the first collective after the data load, when the
+// ranks' shards come off a slow shared filesystem at different rates: raise
+// the limit for such jobs.
 static double coll_timeout_s() {
     static const double t = [] {
         const char* e = std::getenv("VAMPOMI_COLL_TIMEOUT_S");
         const double v = e ? std::atof(e) : 0.0;
-        return v > 0 ? v : 600.0;
+        return v > 0 ? v : 120.0;
     }();
     return t;
 }
@@ -796,46 +800,31 @@ static size_t op_xg_words_for(int64_t Mx, const vk::OpPlan& p) {
     return (size_t)(Mx + p.grid) * vk::kOpMaxK * (size_t)p.T * 2 + (size_t)p.grid * (2 * vk::kOpMaxK + 1);
 }
 
-vampomi_status op_prepare(vampomi_ctx* c, bool collective) {
-    if (c->op_ready) return VAMPOMI_OK;
+static vampomi_status op_plan_local(vampomi_ctx* c) {
     if (c->cus <= 0) HIPCHK(hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, c->device));
     const int64_t M = std::max<int64_t>(c->M, 1);
-    c->op_ok = vk::op_plan(c->N, M, c->cus, c->op_variant, &c->opp);
-    if (c->op_ok && c->opp.T >= 1) {
+    bool op_ok = vk::op_plan(c->N, M, c->cus, c->op_variant, &c->opp);
+    if (op_ok && c->opp.T >= 1) {
         // a team launch waits for members that must all be resident at once:
         // the device must hold the whole grid (one workgroup per CU) for every
         // K; a device that cannot (or an occupancy query that failed) runs the
         // CG on the two-pass schedule instead
-        for (int K = 1; K <= vk::kOpMaxK && c->op_ok; ++K) {
+        for (int K = 1; K <= vk::kOpMaxK && op_ok; ++K) {
             const int occ = vk::team_occupancy(c->opp, K);
             if ((int64_t)occ * c->cus < c->opp.grid) {
                 std::fprintf(stderr, "libvampomi: one-pass operator off: %s fits %d workgroup(s) per CU; the plan "
                                      "needs %lld resident on %d CUs (two passes per CG step)\n",
                              vk::team_kernel_name(K, c->opp).c_str(), occ, (long long)c->opp.grid, c->cus);
-                c->op_ok = false;
+                op_ok = false;
             }
         }
     }
     // the head-start plan: optional (no plan, or a grid the device cannot
     // hold, only means the solves start without it)
-    c->hs_ok = c->op_ok && vk::team_plain_plan(c->N, M, c->cus, c->opp, &c->opp_hs);
-    if (c->hs_ok && (int64_t)vk::team_occupancy(c->opp_hs, 1 + vk::kOpPlain) * c->cus < c->opp_hs.grid)
-        c->hs_ok = false;
-    // Both choices change the job's collective sequence (one-pass vs two-pass
-    // CG steps; the head-start launch's all-reduce vs ax_dev's), and each rank
-    // made them from its own shard size, CU count and VAMPOMI_HEADSTART /
-    // set_variant(5).  A job runs a choice only if every rank made it: one
-    // all-reduce of the three refusals, each in its own base-2^10 digit.
-    if (collective && c->use_comm) {
-        const double mine = (c->op_ok ? 0.0 : 1.0) + (c->hs_ok ? 0.0 : 1024.0) + (c->hs_on ? 0.0 : 1048576.0);
-        double all = 0.0;
-        STCHK(sum_over_ranks(c, mine, &all));
-        const int64_t a = (int64_t)all;
-        if (a % 1024 != 0) c->op_ok = false;
-        if ((a / 1024) % 1024 != 0 || a / 1048576 != 0 || !c->op_ok) c->hs_ok = false;
-    } else if (!c->hs_on) {
-        c->hs_ok = false;
-    }
+    bool hs_ok = op_ok && vk::team_plain_plan(c->N, M, c->cus, c->opp, &c->opp_hs);
+    if (hs_ok && (int64_t)vk::team_occupancy(c->opp_hs, 1 + vk::kOpPlain) * c->cus < c->opp_hs.grid) hs_ok = false;
+    c->op_ok_mine = op_ok;
+    c->hs_ok_mine = hs_ok;
     if (!c->op_ts && std::getenv("VAMPOMI_OP_TS") && std::atoi(std::getenv("VAMPOMI_OP_TS"))) {
         HIPCHK(hipMalloc((void**)&c->op_ts, (size_t)4 * 8 * std::max(c->cus, 1) * 2));
         HIPCHK(hipMemsetAsync(c->op_ts, 0, (size_t)4 * 8 * std::max(c->cus, 1) * 2, c->st));
@@ -844,16 +833,16 @@ vampomi_status op_prepare(vampomi_ctx* c, bool collective) {
         STCHK(dev_alloc(&c->op_nvec, (size_t)3 * vk::kMaxRhs * c->ld + 16));
         HIPCHK(hipMemsetAsync(c->op_nvec, 0, ((size_t)3 * vk::kMaxRhs * c->ld + 16) * 8, c->st));
     }
-    if (c->op_ok) {
-        const int64_t slots = std::max<int64_t>(c->opp.nslots, c->hs_ok ? c->opp_hs.nslots : 0);
+    if (op_ok) {
+        const int64_t slots = std::max<int64_t>(c->opp.nslots, hs_ok ? c->opp_hs.nslots : 0);
         if (slots > c->op_part_slots) {
             dev_free(c->op_part);
             STCHK(dev_alloc(&c->op_part, (size_t)slots * vk::kMaxRhs * c->ld));
             c->op_part_slots = slots;
         }
-        if (c->opp.T > 1 || (c->hs_ok && c->opp_hs.T > 1)) {
+        if (c->opp.T > 1 || (hs_ok && c->opp_hs.T > 1)) {
             size_t words = c->opp.T > 1 ? op_xg_words_for(M, c->opp) : 0;
-            if (c->hs_ok && c->opp_hs.T > 1) words = std::max(words, op_xg_words_for(M, c->opp_hs));
+            if (hs_ok && c->opp_hs.T > 1) words = std::max(words, op_xg_words_for(M, c->opp_hs));
             if (words > c->op_xg_words) {
                 if (c->op_xg) (void)hipFree(c->op_xg);
                 c->op_xg = nullptr;
@@ -868,10 +857,45 @@ vampomi_status op_prepare(vampomi_ctx* c, bool collective) {
     return VAMPOMI_OK;
 }
 
+vampomi_status op_prepare(vampomi_ctx* c) {
+    if (!c->op_ready) STCHK(op_plan_local(c));
+    if (!c->use_comm) {
+        c->op_ok = c->op_ok_mine;
+        c->hs_ok = c->hs_ok_mine && c->hs_on;
+    } else if (!c->op_agreed) {  // no agreement yet: the two-pass schedule, the same on every rank
+        c->op_ok = c->hs_ok = false;
+    }
+    return VAMPOMI_OK;
+}
+
+vampomi_status op_agree(vampomi_ctx* c) {
+    if (!c->use_comm) return VAMPOMI_OK;
+    if (c->op_variant_req != c->op_variant || c->hs_on_req != c->hs_on) {
+        c->op_variant = c->op_variant_req;
+        c->hs_on = c->hs_on_req;
+        c->op_ready = false;
+    }
+    bool op = false, hs = false;
+    if (c->have_X) {
+        if (!c->op_ready) STCHK(op_plan_local(c));
+        op = c->op_ok_mine;
+        hs = c->hs_ok_mine;
+    }
+    // one all-reduce of the three refusals, each in its own base-2^10 digit
+    const double mine = (op ? 0.0 : 1.0) + (hs ? 0.0 : 1024.0) + (c->hs_on ? 0.0 : 1048576.0);
+    double all = 0.0;
+    STCHK(sum_over_ranks(c, mine, &all));
+    const int64_t a = (int64_t)all;
+    c->op_ok = a % 1024 == 0;
+    c->hs_ok = c->op_ok && (a / 1024) % 1024 == 0 && a / 1048576 == 0;
+    c->op_agreed = true;
+    return VAMPOMI_OK;
+}
+
 vampomi_status headstart_available(vampomi_ctx* c, bool* yes) {
     *yes = false;
     if (!c->have_X) return VAMPOMI_OK;
-    STCHK(op_prepare(c));  // hs_ok: agreed over the ranks, VAMPOMI_HEADSTART / set_variant(5) included
+    STCHK(op_prepare(c));  // hs_ok: agreed over the ranks at vamp_begin, VAMPOMI_HEADSTART / set_variant(5) included
     *yes = c->op_ok && c->hs_ok;
     return VAMPOMI_OK;
 }
@@ -1108,6 +1132,7 @@ void release_ctx_resources(vampomi_ctx* c) {
     c->op_xg_words = 0;
     c->op_part_slots = 0;
     c->op_ready = false;
+    c->op_agreed = false;
     if (c->h_scal) (void)hipHostFree(c->h_scal);
     c->h_scal = nullptr;
     if (c->ticket) (void)hipFree(c->ticket);
@@ -1208,7 +1233,7 @@ extern "C" vampomi_status vampomi_open(const vampomi_shard_desc* d, vampomi_ctx*
     // cross-queue events cost more than the 5-17 us kernels they overlap)
     c->side_on = c->use_comm;
     if (const char* sv = std::getenv("VAMPOMI_SIDE_STREAM")) c->side_on = std::atoi(sv) != 0;
-    if (const char* hv = std::getenv("VAMPOMI_HEADSTART")) c->hs_on = std::atoi(hv) != 0;
+    if (const char* hv = std::getenv("VAMPOMI_HEADSTART")) c->hs_on = c->hs_on_req = std::atoi(hv) != 0;
     const char* mode = std::getenv("VAMPOMI_COMM");
     if (c->use_comm && mode && std::strcmp(mode, "loopback") == 0) {
         if (!d->comm_id) return fail(VAMPOMI_ERR_ARG, "the loopback communicator needs a communicator id");
@@ -1771,15 +1796,18 @@ extern "C" vampomi_status vampomi_dev_set_variant(vampomi_ctx* c, int which, int
         vk::OpPlan p{};
         if (!vk::op_plan(c->N, std::max<int64_t>(c->M, 1), c->cus > 0 ? c->cus : 256, variant, &p))
             return fail(VAMPOMI_ERR_ARG, "no such one-pass operator plan for this N");
-        c->op_variant = variant;
-        c->op_ready = false;
+        c->op_variant_req = variant;  // several ranks: applied and agreed at the next vampomi_vamp_begin
+        if (!c->use_comm) {
+            c->op_variant = variant;
+            c->op_ready = false;
+        }
     } else if (which == 4) {  // side stream for the prefetched denoiser/EM: 0 off, 1 on
         if (variant != 0 && variant != 1) return fail(VAMPOMI_ERR_ARG, "side stream: 0 or 1");
         c->side_on = variant == 1;
     } else if (which == 5) {  // the CG head start (pcg.cpp): 0 off, 1 on
         if (variant != 0 && variant != 1) return fail(VAMPOMI_ERR_ARG, "head start: 0 or 1");
-        c->hs_on = variant == 1;
-        c->op_ready = false;  // re-planned (and re-agreed over the ranks) at the next collective use
+        c->hs_on_req = variant == 1;  // several ranks: applied and agreed at the next vampomi_vamp_begin
+        if (!c->use_comm) c->hs_on = c->hs_on_req;
     } else {
         if (!vk::loo_variant_ok(variant)) return fail(VAMPOMI_ERR_ARG, "no such association-pass variant");
         c->loo_variant = variant;
@@ -1793,8 +1821,8 @@ extern "C" vampomi_status vampomi_dev_time_pass(vampomi_ctx* c, int which, int K
     if (!c->have_X) return fail(VAMPOMI_ERR_STATE, "no methylation data loaded");
     HIPCHK(hipSetDevice(c->device));
     if (which == 3) {
-        STCHK(op_prepare(c, false));  // a one-rank timing hook: no agreement
-        if (!c->op_ok) return fail(VAMPOMI_ERR_ARG, "no one-pass operator plan for this N");
+        STCHK(op_prepare(c));  // a timing hook: this rank's plan, no agreement
+        if (!c->op_ok_mine) return fail(VAMPOMI_ERR_ARG, "no one-pass operator plan for this N");
     }
     const int64_t Mx = std::max<int64_t>(c->M, 1);
     vk::CPtrs in{};
@@ -1861,7 +1889,7 @@ extern "C" vampomi_status vampomi_dev_op_apply(vampomi_ctx* c, int K, const doub
         return fail(VAMPOMI_ERR_ARG, "bad argument");
     if (c->use_comm) return fail(VAMPOMI_ERR_ARG, "vampomi_dev_op_apply: one rank only");
     HIPCHK(hipSetDevice(c->device));
-    STCHK(op_prepare(c, false));
+    STCHK(op_prepare(c));
     if (!c->op_ok) return fail(VAMPOMI_ERR_ARG, "no one-pass operator plan for this N");
     const int64_t Mx = std::max<int64_t>(c->M, 1);
     double* AR = c->op_nvec;

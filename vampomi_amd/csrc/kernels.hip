@@ -174,6 +174,10 @@ __device__ __forceinline__ double pow_1p5(double x) {
     return t + (t_lo + x * (e / (2.0 * s)));
 }
 
+// exp correctly rounded in practice (the probit denoiser's erfcx; exp_cr.h)
+#define EXPCR_FN __device__ __forceinline__
+#include "exp_cr.h"
+
 __host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
     x += 0x9E3779B97F4A7C15ULL;
     x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
@@ -2123,8 +2127,10 @@ hipError_t cg_decide(CgState* cs, const double* red, int it, CgMirror* mirror, u
 // ---------------------------------------------------------------------------
 // erfcx as the reference evaluates it (src/utilities.cpp:293-363: N. Juffa's
 // published fma approximation, with +inf below -10 and lowest() above 10).
-// Same operations in the same order as the oracle's orc_erfcx; only exp()
-// (OCML vs glibc) may differ in the last bit for x < 0.
+// Same operations in the same order as the oracle's orc_erfcx.  exp() is the
+// correctly rounded exp_cr (exp_cr.h), not OCML's ~1-ulp exp: it equals glibc's
+// (the oracle's, the reference's) except where glibc misrounds, 0.08 % of the
+// arguments (tests/exp_cr_check.c).
 __constant__ double kErfcxPoly[24] = {
     0x1.edcad78fc8044p-31,  0x1.b1548f14735d1p-30,  -0x1.a1ad2e6c4a7a8p-27, -0x1.1985b48f08574p-26,
     0x1.c6a8093ac4f83p-24,  0x1.31c2b2b44b731p-24,  -0x1.b87373facb29fp-21, 0x1.3fef1358803b7p-22,
@@ -2152,7 +2158,7 @@ __device__ __forceinline__ double erfcx_ref(double x) {
     if (x < 0.0) {
         const double s = x * x;
         const double lo = __builtin_fma(x, x, -s);
-        const double e = exp(s);
+        const double e = exp_cr(s);
         r = __builtin_fma(e, lo + lo, e - r) + e;
         if (e > 1.7976931348623157e308) r = e;
     }

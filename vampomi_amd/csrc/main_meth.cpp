@@ -32,11 +32,15 @@ static int env_int(const char* a, const char* b, int dflt) {
 }
 
 // rank 0 publishes the RCCL id (removing any file an earlier job left there),
-// the others wait up to 10 minutes for a file of THIS job (vio::rdzv_*)
+// the others wait for a file of THIS job (vio::rdzv_*) up to
+// VAMPOMI_RDZV_TIMEOUT_S (default 120 s, the bench's collective limit: the
+// ranks of one job start together, so a longer wait means rank 0 is gone)
 static bool exchange_id(const std::string& path, int rank, double not_before, unsigned char* id) {
     const std::string nonce = vio::rdzv_nonce();
     if (rank == 0) return vampomi_comm_unique_id(id) == VAMPOMI_OK && vio::rdzv_publish(path, nonce, id, VAMPOMI_UNIQUE_ID_BYTES);
-    return vio::rdzv_fetch(path, nonce, not_before, id, VAMPOMI_UNIQUE_ID_BYTES, 600000);
+    const char* e = std::getenv("VAMPOMI_RDZV_TIMEOUT_S");
+    const double s = e && std::atof(e) > 0 ? std::atof(e) : 120.0;
+    return vio::rdzv_fetch(path, nonce, not_before, id, VAMPOMI_UNIQUE_ID_BYTES, (int)(s * 1000.0));
 }
 
 static vampomi_ctx* g_ctx = nullptr;  // the open context: die() ends the job's communicator
@@ -263,17 +267,29 @@ int main(int argc, char** argv) {
     vampomi_result r{};
     r.cg_iters = cg.data();
     r.ons_iters = ons.data();
+    // vampomi_infere step by step, so that every iteration reports its time
+    // as the reference does (src/vamp.cpp:396-401, rank 0): one step is one
+    // iteration, and the host waits once per iteration, at its end
     auto t1 = std::chrono::steady_clock::now();
-    if (vampomi_infere(ctx, &p, &r) != VAMPOMI_OK) return die("inference");
+    if (vampomi_vamp_begin(ctx, &p, &r) != VAMPOMI_OK) return die("inference");
+    double total = 0.0;
+    for (int stopped = 0; !stopped;) {
+        const auto ts0 = std::chrono::steady_clock::now();
+        if (vampomi_vamp_step(ctx, &stopped) != VAMPOMI_OK) return die("inference");
+        const double it_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - ts0).count();
+        total += it_s;
+        const int it = r.iterations_run;
+        if (rank == 0 && it >= 1)
+            std::cout << "it " << it << ": CG iterations " << cg[it - 1] << ", onsager CG iterations " << ons[it - 1]
+                      << "\nTotal iteration time = " << it_s << "\nTotal computation time so far = " << total
+                      << std::endl;
+    }
+    if (vampomi_vamp_end(ctx) != VAMPOMI_OK) return die("inference");
     const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count();
-    if (rank == 0) {
+    if (rank == 0)
         std::cout << "iterations run = " << r.iterations_run << ", total computation time = " << secs
                   << " s, A-passes executed = " << r.a_passes_exec << " (reference-equivalent " << r.a_passes_ref
                   << ")" << std::endl;
-        for (int i = 0; i < r.iterations_run; ++i)
-            std::cout << "it " << (i + 1) << ": CG iterations " << cg[i] << ", onsager CG iterations " << ons[i]
-                      << std::endl;
-    }
     vampomi_barrier(ctx);
     vampomi_close(ctx);
     return 0;

@@ -282,6 +282,7 @@ extern "C" vampomi_status vampomi_vamp_begin(vampomi_ctx* c, const vampomi_param
         return fail(VAMPOMI_ERR_MODEL, std::string("Invalid model specification! ('") + p->model + "')");
     if (p->L < 1 || p->L > VAMPOMI_MAX_L) return fail(VAMPOMI_ERR_ARG, "number of mixture components out of range");
     HIPCHK(hipSetDevice(c->device));
+    STCHK(op_agree(c));  // several ranks: the one-pass / head-start choice, agreed here, where every rank is
     c->run.reset(new VampRun());
     VampRun& R = *c->run;
     R.prm = *p;
