@@ -100,7 +100,24 @@ def parse_args(argv=None):
                          "\"error\" and each rank's last stage (keep it under the caller's own limit)")
     ap.add_argument("--no-headline", action="store_true",
                     help="n > 1 with --config auto: skip the configs[2] (c3full) phase and its 1-GPU basis")
+    ap.add_argument("--rehearse", type=int, default=0, metavar="P",
+                    help="rehearsal of the n > 1 flow on ONE GPU: P loopback ranks as threads of this process on "
+                         "GPU 0 (bases, main phase, headline phase, line assembly), every workload's markers "
+                         "scaled by --rehearse-scale; the rate is not a multi-GPU number")
+    ap.add_argument("--rehearse-scale", type=float, default=0.05)
     return ap.parse_args(argv)
+
+
+WORKLOAD_SCALE = 1.0  # --rehearse: markers of every workload scaled by this
+
+
+def get_workload(cfg: str, n: int) -> dict:
+    from vampomi_amd.workloads import workload
+
+    w = workload(cfg, n)
+    if WORKLOAD_SCALE != 1.0:
+        w = dict(w, Mt=max(n, int(round(w["Mt"] * WORKLOAD_SCALE))), rehearsal_scale=WORKLOAD_SCALE)
+    return w
 
 
 # ---------------------------------------------------------------------------
@@ -224,6 +241,7 @@ class Watchdog:
         self.printed = False
         self.finished = False  # this rank's part of the run is complete (teardown only)
         self.partial = None  # rank 0: the finished part of the line, printed if a later phase hangs
+        self.stopped = False
         os.makedirs(self.dir, exist_ok=True)
         self.stage("start")
         threading.Thread(target=self._run, daemon=True).start()
@@ -248,9 +266,17 @@ class Watchdog:
             print(json.dumps(line), flush=True)
             return True
 
+    def stop(self):
+        """The job is over (--rehearse: its rank threads have joined): no deadline action."""
+        self.stopped = True
+
     def _run(self):
         while time.time() < self.deadline:
+            if self.stopped:
+                return
             time.sleep(min(1.0, max(0.05, self.deadline - time.time())))
+        if self.stopped:
+            return
         why = f"deadline of {self.deadline - self.t0:.0f} s passed (rank {self.rank} at stage '{self.cur}')"
         sys.stderr.write(f"bench.py rank {self.rank}: {why}\n")
         sys.stderr.flush()
@@ -470,11 +496,7 @@ def per_rank_times(R, st, el: float) -> list:
             "allreduce_ms_total": round(st.coll.ms_total, 3),
             "allreduce_us_avg": round(st.coll.ms_timed / st.coll.timed * 1e3, 2) if st.coll.timed else None,
             "allreduce_bytes": int(st.coll.bytes_total)}
-    if R.world == 1:
-        return [mine]
-    out = [None] * R.world
-    R.dist.all_gather_object(out, mine)
-    return out
+    return R.gather(mine)
 
 
 def cpu_baseline_assoc(d, w: dict, est, seed: int) -> dict:
@@ -541,6 +563,13 @@ class Ranks:
         self.dist.broadcast_object_list(box, src=0)
         return box[0]
 
+    def gather(self, obj) -> list:
+        if self.world == 1:
+            return [obj]
+        out = [None] * self.world
+        self.dist.all_gather_object(out, obj)
+        return out
+
     def close(self):
         if self.world > 1:
             self.dist.destroy_process_group()
@@ -566,6 +595,9 @@ class Solo:
 
     def bcast(self, obj):
         return obj
+
+    def gather(self, obj) -> list:
+        return [obj]
 
 
 def dry_run(args, R: Ranks, wd: Watchdog):
@@ -649,7 +681,7 @@ def vamp_window(args, R, w: dict, wd: Watchdog, steps: int, warmup: int, tag: st
         res = {"el": el, "st": st, "summ": v.summary(), "ref_passes": (ref1 - ref0) / steps, "setup": t_setup,
                "M": d.M, "nranks": d.nranks, "steps": steps, "warmup": warmup, "model": model, "beta": beta,
                "opts": opts, "barrier": barrier}
-        res["rank_times"] = per_rank_times(R, st, el) if R.world > 1 else per_rank_times(Solo(R.local), st, el)
+        res["rank_times"] = per_rank_times(R, st, el)
         v.end()
         if keep:
             res["d"] = d
@@ -722,9 +754,7 @@ def one_gpu_bases(args, R: Ranks, wd: Watchdog, w: dict, headline: bool) -> dict
                 traceback.print_exc()
                 out["same_problem"] = {"error": repr(e)}
         if headline:
-            from vampomi_amd.workloads import workload
-
-            wb = workload("c3big", 1)
+            wb = get_workload("c3big", 1)
             try:
                 r = vamp_window(args, solo, wb, wd, 4, 1, "basis c3big")
                 rec = summary_of(r, wb, False, 1)
@@ -864,9 +894,7 @@ def run_headline(args, R: Ranks, wd: Watchdog, c3big) -> dict:
     this job's ranks, after the main phase: north_star's headline problem at
     n = 2 / 4 / 8 (it does not fit one GPU).  Fewer timed iterations (at most
     10) keep the job short; errors are recorded, not fatal for the line."""
-    from vampomi_amd.workloads import workload
-
-    w = workload("c3full", R.world)
+    w = get_workload("c3full", R.world)
     steps = min(args.steps, 10)
     try:
         res = vamp_window(args, R, w, wd, steps, args.warmup, "headline", keep=True)
@@ -964,8 +992,100 @@ def bench_assoc(args, R: Ranks, wd: Watchdog, w: dict, t_start):
     return line
 
 
+class ThreadRanks:
+    """Ranks of a --rehearse job: P threads of this process, one loopback rank
+    each, all on GPU 0 (the interface of Ranks: max / sum / barrier / bcast,
+    combined in rank order)."""
+
+    class Shared:
+        def __init__(self, P: int, timeout_s: float):
+            self.P = P
+            self.bar = threading.Barrier(P, timeout=timeout_s)
+            self.vals = [None] * P
+
+    dist = None
+
+    def __init__(self, shared: "ThreadRanks.Shared", rank: int):
+        self.s, self.rank, self.world, self.local = shared, rank, shared.P, 0
+
+    def _combine(self, v, fn):
+        self.s.vals[self.rank] = v
+        self.s.bar.wait()
+        out = fn(list(self.s.vals))
+        self.s.bar.wait()
+        return out
+
+    def max(self, v: float) -> float:
+        return self._combine(v, max)
+
+    def sum(self, v: float) -> float:
+        return self._combine(v, lambda a: float(sum(a)))
+
+    def barrier(self):
+        self.s.bar.wait()
+
+    def bcast(self, obj):
+        return self._combine(obj, lambda a: a[0])
+
+    def gather(self, obj) -> list:
+        return self._combine(obj, list)
+
+    def close(self):
+        pass
+
+
+def rehearse(args) -> int:
+    """--rehearse P: the whole n > 1 flow of `bench.py --gpus P` (rank 0's
+    1-GPU bases, the main phase, the configs[2] headline phase, the line) with
+    P loopback ranks as threads on GPU 0 and every workload's markers scaled
+    by --rehearse-scale, so that the driver's first multi-GPU run is not the
+    first time this code path runs on the device.  Prints rank 0's line with
+    "rehearsal" set; its rates are one GPU's, not a scaling result."""
+    global WORKLOAD_SCALE
+    WORKLOAD_SCALE = args.rehearse_scale
+    os.environ["VAMPOMI_COMM"] = "loopback"
+    os.environ.setdefault("VAMPOMI_RUN_ID", f"rehearse-{os.getpid()}")
+    P = args.rehearse
+    args.gpus = P
+    import torch  # noqa: F401  (before libvampomi: one HIP runtime per process)
+
+    shared = ThreadRanks.Shared(P, args.deadline_s)
+    lines, errs = [None] * P, []
+    t_start = time.perf_counter()
+
+    wds = [None] * P
+
+    def work(r):
+        R = ThreadRanks(shared, r)
+        wd = wds[r] = Watchdog(args, r, P)
+        try:
+            w = get_workload(args.config, P)
+            lines[r] = run_linear(args, R, wd, w, t_start) if w.get("model") != "loo" else \
+                bench_assoc(args, R, wd, w, t_start)
+            wd.finished = True
+        except BaseException as e:  # noqa: BLE001 - reported in the line
+            traceback.print_exc()
+            errs.append((r, repr(e)))
+            shared.bar.abort()  # the other ranks' next barrier fails instead of waiting
+
+    th = [threading.Thread(target=work, args=(r,), daemon=True) for r in range(P)]
+    [t.start() for t in th]
+    [t.join() for t in th]
+    for wd in wds:
+        if wd is not None:
+            wd.stop()
+    line = lines[0] or failure_line(P, sys.argv[1:], f"rehearsal: {errs}", {})
+    line["rehearsal"] = {"loopback_rank_threads_on_one_gpu": P, "markers_scale": args.rehearse_scale,
+                         "errors": errs,
+                         "note": "the n > 1 flow on one GPU; rates are not multi-GPU numbers"}
+    print(json.dumps(line), flush=True)
+    return 0 if (lines[0] is not None and not errs) else 1
+
+
 def main():
     args = parse_args()
+    if args.rehearse > 0:
+        sys.exit(rehearse(args))
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         # start the ranks before this process touches the GPU (or imports torch)
         sys.exit(spawn_ranks(args.gpus, sys.argv[1:], args.deadline_s))
@@ -986,7 +1106,6 @@ def main():
             return dry_run(args, R, wd)
         if args.gpus != R.world:
             raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={R.world}: launch one process per GPU")
-        from vampomi_amd.workloads import workload
 
         if torch.cuda.is_available():
             # one GPU per local rank; more ranks than visible GPUs share them
@@ -994,7 +1113,7 @@ def main():
             # reported in the line like any other failure)
             R.local = R.local % max(1, torch.cuda.device_count())
             torch.cuda.set_device(R.local)  # torch's own context on this rank's GPU, not on GPU 0
-        w = workload(args.config, R.world)
+        w = get_workload(args.config, R.world)
         if w.get("model") == "loo":
             line = bench_assoc(args, R, wd, w, t_start)
         else:

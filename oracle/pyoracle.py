@@ -155,6 +155,20 @@ def atx(X, mave, msig, u) -> np.ndarray:
     return out
 
 
+def set_omp_threads(n: int) -> None:
+    """OpenMP team size of the oracle's parallel loops started from the
+    calling thread (omp_set_num_threads sets the calling thread's ICV)."""
+    global _gomp
+    if _gomp is None:
+        load()
+        _gomp = C.CDLL("libgomp.so.1")
+        _gomp.omp_set_num_threads.argtypes = [C.c_int]
+    _gomp.omp_set_num_threads(int(n))
+
+
+_gomp = None
+
+
 def set_atx_block(B: int) -> None:
     """Sensitivity mode: A^T.u sums samples in blocks of B rows (0 = off)."""
     load().orc_set_atx_block(int(B))

@@ -3,6 +3,7 @@ the oracle's fixed-order arithmetic, so inputs are bit-identical on every host
 (no BLAS, no numpy RNG)."""
 from __future__ import annotations
 
+import os
 import threading
 
 import numpy as np
@@ -61,6 +62,9 @@ def sharded_oracle(X, y, beta, Mt, P, **kw):
     res = [None] * P
 
     def work(r):
+        # OpenMP threads per rank: the host's cores shared out (each rank's
+        # thread has its own OpenMP team; 128 ranks x all cores would thrash)
+        O.set_omp_threads(max(1, (os.cpu_count() or 1) // P))
         M, S, _ = O.divide_work(Mt, P, r)
         res[r] = O.vamp_infere(X[S:S + M], y, Mt, S=S, rank=r, nranks=P,
                                true_signal=None if beta is None else beta[S:S + M], allreduce=comm.make(r), **kw)
@@ -140,5 +144,6 @@ def record_probit_ratio(test: str, key: str, gap, spread, floor: float = 1e-10):
     f = os.environ.get("VAMPOMI_PROBIT_RATIOS")
     if f:
         with open(f, "a") as fh:
-            fh.write(json.dumps({"test": test, "key": key, "max_ratio": r, "n": int(np.sum(m))}) + "\n")
+            fh.write(json.dumps({"test": test, "key": key, "max_ratio": r, "n": int(np.sum(m)),
+                                 "gap": [float(g) for g in gap[:16]], "spread": [float(v) for v in spread[:16]]}) + "\n")
     return r

@@ -127,6 +127,9 @@ class _Ranks:
     def bcast(self, obj):
         return obj
 
+    def gather(self, obj):
+        return [obj] * self.world
+
 
 class _Wd:
     partial = None
@@ -196,16 +199,11 @@ def test_multi_rank_line_assembly(monkeypatch):
     assert line["scaling"] == "strong" and line["one_gpu_equivalent"]["measured_in_this_job"]
 
 
-def test_vamp_window_and_bases_with_a_stub_library(monkeypatch):
-    """bench.py's real vamp_window / one_gpu_bases code over a stub of the
-    library's Python mirror (no GPU): every leg of the n > 1 flow runs without
-    a Python error, so the driver's first multi-GPU run cannot die on one."""
+def _stub_library(monkeypatch):
+    """The library's Python mirror (Data, Vamp) replaced by a stub: no GPU."""
     from types import SimpleNamespace as NS
 
-    sys.path.insert(0, ROOT)
-    import bench
     import vampomi_amd as va
-    from vampomi_amd.workloads import workload
 
     z = NS(ms_total=0.0, ms_timed=0.0, timed=0, launches=0, bytes_total=0.0)
 
@@ -270,6 +268,17 @@ def test_vamp_window_and_bases_with_a_stub_library(monkeypatch):
     monkeypatch.setattr(va, "Data", Data)
     monkeypatch.setattr(va, "Vamp", Vamp)
     monkeypatch.setattr(va, "comm_unique_id", lambda: b"x" * va.UNIQUE_ID_BYTES)
+
+
+def test_vamp_window_and_bases_with_a_stub_library(monkeypatch):
+    """bench.py's real vamp_window / one_gpu_bases code over a stub of the
+    library's Python mirror (no GPU): every leg of the n > 1 flow runs without
+    a Python error, so the driver's first multi-GPU run cannot die on one."""
+    sys.path.insert(0, ROOT)
+    import bench
+    from vampomi_amd.workloads import workload
+
+    _stub_library(monkeypatch)
     args = bench.parse_args(["--gpus", "2", "--steps", "3", "--warmup", "1"])
     out = bench.one_gpu_bases(args, _Ranks(2), _Wd(), workload("auto", 2), True)
     assert set(out) == {"same_problem", "c3big"}, out
@@ -277,3 +286,28 @@ def test_vamp_window_and_bases_with_a_stub_library(monkeypatch):
     line = bench.run_linear(args, _Ranks(2), _Wd(), workload("auto", 2), 0.0)
     json.dumps(line)
     assert "error" not in line["headline_c3full"], line["headline_c3full"]
+
+
+def test_rehearsal_flow_with_a_stub_library(monkeypatch, capsys):
+    """bench.py --rehearse P (the n > 1 flow with P loopback rank threads on one
+    GPU, tests/test_gpu_bench.py runs it on the device) over the stub library:
+    one line, rank 0's bases, the main phase and the headline phase at the
+    scaled marker counts, per-rank records gathered from every thread."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    _stub_library(monkeypatch)
+    monkeypatch.setenv("TMPDIR", os.environ.get("TMPDIR", "/tmp"))
+    args = bench.parse_args(["--rehearse", "3", "--rehearse-scale", "0.1", "--steps", "2", "--warmup", "1",
+                             "--deadline-s", "120"])
+    try:
+        rc = bench.rehearse(args)
+    finally:
+        bench.WORKLOAD_SCALE = 1.0
+    line = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
+    assert rc == 0 and line["rehearsal"]["errors"] == [], line
+    assert line["n_gpus"] == 3 and line["config"]["workload"] == "c2-weak" and line["config"]["Mt"] == 15000
+    assert [r["rank"] for r in line["per_rank"]] == [0, 1, 2]
+    assert "error" not in line["one_gpu"]["same_problem"] and "error" not in line["one_gpu"]["c3big"]
+    h = line["headline_c3full"]
+    assert "error" not in h and h["Mt"] == 50000 and h["n_gpus"] == 3

@@ -84,7 +84,7 @@ def test_sharded_operators(monkeypatch, P):
     assert relerr(np.concatenate([r[5] for r in res]), msig) < 1e-14
 
 
-@pytest.mark.parametrize("P", [2, 3])
+@pytest.mark.parametrize("P", [2, 3, 4, 8])
 def test_sharded_linear_vamp_matches_single_rank(monkeypatch, P):
     N, Mt, its = 1000, 2000, 12
     X, y, beta = make_problem(N, Mt)
@@ -104,25 +104,28 @@ def test_sharded_linear_vamp_matches_single_rank(monkeypatch, P):
     assert parts[0]["cg_iters"] == ref["cg_iters"].tolist()
 
 
-def test_sharded_probit(monkeypatch):
-    N, Mt, its = 1000, 2000, 12
+@pytest.mark.parametrize("P", [2, 4, 8])
+def test_sharded_probit(monkeypatch, P):
+    """Mt = 2003: shards of unequal size at every P (divide_work's remainder)."""
+    N, Mt, its = 1000, 2003, 12
     X, y, beta = make_problem(N, Mt)
     yb = (y > 0).astype(np.float64)
     kw = dict(max_iter=its, stop_criteria_thr=0.0, model="bin_class")
     ref, spread = oracle_with_spread(X, yb, beta, Mt, **kw)
-    parts = run_ranks(monkeypatch, 2, N, Mt, lambda r, d: _vamp(d, X, yb, beta, **kw))
+    parts = run_ranks(monkeypatch, P, N, Mt, lambda r, d: _vamp(d, X, yb, beta, **kw))
     for p in parts:
         assert p["cg_iters"] == ref["cg_iters"].tolist() and p["ons_iters"] == ref["ons_iters"].tolist()
         m = np.array(p["metrics"])
         for o in (0, 6):
             assert np.array_equal(m[:, o:o + 4], ref["metrics"][:, o:o + 4])
     gap = np.array([relerr(_cat(parts, "x1_hist")[k], ref["x1_hist"][k]) for k in range(its)])
-    record_probit_ratio("test_sharded_probit", "x1", gap, spread["x1"][:its])
+    record_probit_ratio(f"test_sharded_probit[{P}]", "x1", gap, spread["x1"][:its])
     for k in range(its):
         assert gap[k] <= max(1e-10, PROBIT_K * spread["x1"][k]), k
 
 
-def test_sharded_association_and_test_mode(monkeypatch):
+@pytest.mark.parametrize("P", [3, 4, 8])
+def test_sharded_association_and_test_mode(monkeypatch, P):
     N, Mt = 900, 1501
     X, y, beta = make_problem(N, Mt, kind=1)
     est = beta * 0.9
@@ -133,7 +136,8 @@ def test_sharded_association_and_test_mode(monkeypatch):
         p, st = d.assoc_loo(est[d.S:d.S + d.M])
         return p, st, d.test_metrics(est[d.S:d.S + d.M]), d.assoc_se(est[d.S:d.S + d.M], 2.0)
 
-    res = run_ranks(monkeypatch, 3, N, Mt, fn)
+    res = run_ranks(monkeypatch, P, N, Mt, fn)
+    assert [r[1].shape[0] for r in res] == [O.divide_work(Mt, P, k)[0] for k in range(P)]
     po, sto = O.assoc_loo(X, y, est)
     st = np.concatenate([r[1] for r in res])
     p = np.concatenate([r[0] for r in res])
@@ -145,6 +149,36 @@ def test_sharded_association_and_test_mode(monkeypatch):
     for r in res:
         assert abs(r[2][0] - ro) <= 1e-12 * abs(ro) and abs(r[2][1] - co) <= 1e-12 * abs(co)
     assert np.allclose(np.concatenate([r[3] for r in res]), O.assoc_se(est, 2.0, N), rtol=1e-14, atol=1e-16)
+
+
+def test_eight_ranks_team_operator_matches_single_rank(monkeypatch):
+    """configs[2]'s rank count at C2's sample count: N = 10,000 (the team
+    operator with teams of 2 on every rank, the head start) and Mt = 16,003
+    (Mt % 8 = 3: three shards one marker longer), 8 loopback ranks against
+    the one-rank run: counts exact, x1_hat / r1 within 1e-12 at every
+    iteration (only the rank-ordered A.x / A d / scalar sums differ)."""
+    N, Mt, its, P = 10000, 16003, 8, 8
+    X, y, beta = make_problem(N, Mt, seed=6)
+    kw = dict(max_iter=its, stop_criteria_thr=0.0)
+    with va.Data(N, Mt) as d:
+        one = _vamp(d, X, y, beta, **kw)
+        assert d.stats().op.launches > 0
+
+    def fn(r, d):
+        s = _vamp(d, X, y, beta, **kw)
+        s["op_launches"] = d.stats().op.launches
+        s["op_name"] = d.kernel_name(3, 2)
+        return s
+
+    parts = run_ranks(monkeypatch, P, N, Mt, fn, timeout=300)
+    assert [p["M"] for p in parts] == [O.divide_work(Mt, P, k)[0] for k in range(P)]
+    for p in parts:
+        assert p["op_launches"] > 0 and "team" in p["op_name"], p["op_name"]
+        assert p["cg_iters"] == one["cg_iters"] and p["ons_iters"] == one["ons_iters"] and p["L"] == one["L"]
+        assert np.allclose(p["params"], one["params"], rtol=1e-11)
+    for k in range(its):
+        assert relerr(_cat(parts, "x1_hist")[k], one["x1_hist"][k]) < 1e-12, k
+        assert relerr(_cat(parts, "r1_hist")[k], one["r1_hist"][k]) < 1e-12, k
 
 
 def test_pcg_warm_start_on_some_ranks_only(monkeypatch):

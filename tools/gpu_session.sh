@@ -6,9 +6,11 @@
 #
 # steps:
 #   suite        the GPU test suite (durations of the slowest tests)
-#   fullshard    the whole-shard oracle tests alone (C3, C5)
+#   fullshard    the whole-shard oracle tests alone (C3, C4, C5)
+#   tests        the GPU tests named in $TESTS (pytest arguments; $TESTK: a -k expression)
+#   rehearse     bench.py's n > 1 flow with 8 loopback rank threads on this GPU
 #   bitwise      12 VAMP iterations (linear and probit) on this build and on
-#                $OLD (default build_old/), compared bit for bit
+#                $OLD (default build_ab/, make -C vampomi_amd/csrc OBJDIR=../../build_ab/obj LIBDIR=../../build_ab/lib BINDIR=../../build_ab/bin at the base commit), compared bit for bit
 #   ab           C2 lines alternating this build and $OLD, $ROUNDS rounds
 #   envab        C2 lines alternating the settings in $ENVAB ("A=1;A=2;...")
 #   trace        rocprofv3 kernel trace of the C2 line + the gap analysis
@@ -28,7 +30,7 @@ shift
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-OLD=${OLD:-$PWD/build_old/lib/libvampomi.so}
+OLD=${OLD:-$PWD/build_ab/lib/libvampomi.so}
 ROUNDS=${ROUNDS:-3}
 step() {
     local name=$1 tmo=$2
@@ -52,9 +54,18 @@ for s in "$@"; do
     suite)
         step suite 900 python -u -m pytest tests -m gpu -x -q --durations=12 --timeout 400 --timeout-method thread ;;
     fullshard)
-        step fullshard 600 python -u -m pytest tests/test_gpu_scale.py::test_c3_full_shard_vs_oracle \
+        step fullshard 900 python -u -m pytest tests/test_gpu_scale.py::test_c3_full_shard_window_vs_oracle_fixture \
+            tests/test_gpu_probit.py::test_c4_full_shard_vs_oracle \
             tests/test_gpu_assoc.py::test_c5_full_shard_vs_oracle -m gpu -v --durations=0 --timeout 400 \
             --timeout-method thread ;;
+    tests)       # TESTS="<pytest args>": a subset, the probit gap / spread ratios recorded
+        export VAMPOMI_PROBIT_RATIOS=$PWD/$OUT/ratios.jsonl
+        step tests 900 python -u -m pytest $TESTS ${TESTK:+-k "$TESTK"} -m gpu -v --durations=8 --timeout 300 \
+            --timeout-method thread
+        [ -f "$VAMPOMI_PROBIT_RATIOS" ] && python tools/probit_ratios.py "$VAMPOMI_PROBIT_RATIOS" | tee "$OUT/probit_k.txt"
+        unset VAMPOMI_PROBIT_RATIOS ;;
+    rehearse)
+        step rehearse 400 python bench.py --rehearse 8 --steps 3 --warmup 1 --deadline-s 380 ;;
     bitwise)
         for m in linear bin_class; do
             step bw_new_$m 200 python tools/lib_bitwise.py run "$OUT/new_$m.npz" 10000 20000 12 $m
@@ -117,7 +128,7 @@ for s in "$@"; do
         step bench_c3 400 python bench.py --config c3 --steps 10 --warmup 2
         prof c3 6
         step pmc_c3 300 bash tools/pmc.sh c3
-        step bench_c4 300 python bench.py --config c4 --steps 12 --warmup 2 --no-cpu-baseline
+        step bench_c4 400 python bench.py --config c4 --steps 12 --warmup 2
         step bench_c5 300 python bench.py --config c5 --steps 5 --warmup 1 ;;
     *)
         echo "unknown step $s"; exit 2 ;;
