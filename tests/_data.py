@@ -48,11 +48,13 @@ class ThreadComm:
             with self.lock:
                 self.buf[rank] = a.copy()
             self.bar.wait()
-            tot = np.zeros_like(a)
-            for r in range(self.P):
-                tot += self.buf[r]
+            if rank == 0:  # one sum, in rank order, for every rank (P ranks summing P buffers each is O(P^2 n))
+                tot = np.zeros_like(a)
+                for r in range(self.P):
+                    tot += self.buf[r]
+                self.tot = tot
             self.bar.wait()
-            a[:] = tot
+            a[:] = self.tot  # (rank 0 replaces self.tot only after every rank reached the next call's barrier)
         return ar
 
 
@@ -144,6 +146,8 @@ def record_probit_ratio(test: str, key: str, gap, spread, floor: float = 1e-10):
     f = os.environ.get("VAMPOMI_PROBIT_RATIOS")
     if f:
         with open(f, "a") as fh:
+            g1 = gap.reshape(len(gap), -1).max(axis=1) if gap.ndim > 1 else gap  # per iteration (params: rows)
+            s1 = spread.reshape(len(spread), -1).max(axis=1) if spread.ndim > 1 else spread
             fh.write(json.dumps({"test": test, "key": key, "max_ratio": r, "n": int(np.sum(m)),
-                                 "gap": [float(g) for g in gap[:16]], "spread": [float(v) for v in spread[:16]]}) + "\n")
+                                 "gap": [float(g) for g in g1[:16]], "spread": [float(v) for v in s1[:16]]}) + "\n")
     return r
