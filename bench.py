@@ -802,7 +802,8 @@ def run_linear(args, R: Ranks, wd: Watchdog, w: dict, t_start: float) -> dict:
                    "design": "gaussian" if w["kind"] == va.GEN_GAUSS else "methylation-like",
                    "iterations_timed": f"{args.warmup + 1}-{args.warmup + args.steps}",
                    "parallelism": f"markers sharded over {n} GPU(s)" + (", RCCL all-reduce" if n > 1 else ""),
-                   "comm": {"backend": "rccl" if n > 1 else "none", "nranks": res["nranks"]}},
+                   "comm": {"backend": ("loopback" if os.environ.get("VAMPOMI_COMM") == "loopback" else "rccl")
+                            if n > 1 else "none", "nranks": res["nranks"]}},
         "roofline": roof,
         "hbm_gbs_all_A_kernels": round(all_bytes / (all_ms * 1e-3) / 1e9, 1) if all_ms > 0 else None,
         "passes_exec_per_step": round(st.a_passes_exec / args.steps, 2),  # stats reset at the timed region

@@ -144,29 +144,3 @@ def test_team_launches_from_two_contexts_on_one_gpu():
         assert relerr(gd, ref[0]) < 1e-12 and relerr(gad, ref[1]) < 1e-12
         assert np.array_equal(gd, outs[0][0]) and np.array_equal(gad, outs[0][1])
 
-
-@pytest.mark.parametrize("xdon", [1, 3, 8])
-@pytest.mark.parametrize("N,Mt", [(10000, 50000), (10000, 999), (50001, 130)])
-def test_xcd_donation_covers_every_column(monkeypatch, N, Mt, xdon):
-    """VAMPOMI_OP_XDON (OpArgs.xdon): each team on an even XCD hands its last
-    xdon columns to its partner on the next XCD.  Every column is still
-    processed exactly once (d, A d and <d,p> match numpy), including shapes
-    where teams hold fewer columns than xdon, and the result is bitwise
-    repeatable."""
-    monkeypatch.setenv("VAMPOMI_OP_XDON", str(xdon))
-    X = O.generate_markers(13, 0, N, 0, Mt)
-    mave, msig = O.marker_stats(X)
-    rng = np.random.default_rng(xdon)
-    ar, qo = rng.normal(size=(2, N)), rng.normal(size=(2, N))
-    p, z = rng.normal(size=(2, Mt)), rng.normal(size=(2, Mt))
-    beta = np.array([0.3, 0.7])
-    rd, rad, rdp = _ref(X, mave, msig, ar, qo, p, z, beta, 1.7, 0.9, 0.35)
-    with va.Data(N, Mt) as d:
-        d.load_meth(X)
-        assert "team" in d.kernel_name(3, 2)
-        a = d.op_apply(ar, p, 1.7, 0.9, 0.35, z=z, qo=qo, beta=beta)
-        b = d.op_apply(ar, p, 1.7, 0.9, 0.35, z=z, qo=qo, beta=beta)
-    assert relerr(a[0], rd) < 1e-12 and relerr(a[1], rad) < 1e-12
-    assert np.allclose(a[2], rdp, rtol=1e-12, atol=0)
-    for x, y in zip(a, b):
-        assert np.array_equal(x, y)

@@ -20,6 +20,7 @@
 #   probit_k     every probit test, the parity bar's gap / spread ratios
 #   launcher     the default C2 line over a 1-rank RCCL communicator, and the
 #                2-rank launcher on a 1-GPU box (one failure line, rc != 0)
+#   rccl         the 1-rank RCCL path against the direct one (rates, timing on/off, traces compared)
 #   bases        rank 0's 1-GPU bases (tools/one_gpu_bases.py)
 #   final        smoke, the default C2 line (both CPU legs), its kernel stats
 #                and PMC traffic; the same for C3; C4 and C5 lines
@@ -118,6 +119,19 @@ for s in "$@"; do
         timeout -k 10 300 python bench.py --gpus 2 --steps 5 --warmup 2 --deadline-s 240 > "$OUT/spawn2.log" 2>&1
         echo "rc=$?" >> "$OUT/spawn2.log"
         tail -n 2 "$OUT/spawn2.log" | cut -c1-2500 ;;
+    rccl)        # the 1-rank RCCL path against the direct one: rates with and without event timing, traces
+        for r in $(seq "$ROUNDS"); do
+            step rc_dir_$r 200 "${C2[@]}" && brief rc_dir_$r
+            step rc_rccl_$r 200 env VAMPOMI_FORCE_RCCL=1 "${C2[@]}" && brief rc_rccl_$r
+            step rc_dir_nt_$r 200 "${C2[@]}" --no-timing && brief rc_dir_nt_$r
+            step rc_rccl_nt_$r 200 env VAMPOMI_FORCE_RCCL=1 "${C2[@]}" --no-timing && brief rc_rccl_nt_$r
+        done
+        step trace_dir 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_dir" -o run --output-format csv -- \
+            python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-timing
+        VAMPOMI_FORCE_RCCL=1 step trace_rccl 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_rccl" -o run \
+            --output-format csv -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-timing
+        python tools/trace_cmp.py "$(find "$OUT/prof_dir" -name 'run_kernel_trace.csv' | head -1)" \
+            "$(find "$OUT/prof_rccl" -name 'run_kernel_trace.csv' | head -1)" | tee "$OUT/trace_cmp.txt" ;;
     bases)
         step bases 200 python tools/one_gpu_bases.py ;;
     final)

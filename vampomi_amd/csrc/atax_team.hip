@@ -251,29 +251,9 @@ __device__ __forceinline__ void atax_team_body(const double* __restrict__ X, int
     // the team's columns: mb + cs*m, m < n (a contiguous range, or every nteams-th)
     const int64_t cs = ilv ? nteams : 1;
     const int64_t mb = ilv ? team : (int64_t)team * M / nteams;
-    int n = (int)(ilv ? (M - team + nteams - 1) / nteams : (int64_t)(team + 1) * M / nteams - mb);
-    // OpArgs.xdon: a team on an even XCD hands its last xdon columns to its
-    // partner on the next XCD, which runs them as steps n1.. after its own:
-    // step m's column is mb + off(m), off(m) = m*cs below n1, else
-    // dext + (m - n1)*cs (the donor's last columns, relative to mb)
-    const int xdon = (ilv && TM_TEAMS_BY_XCD) ? a.xdon : 0;
-    int n1 = n;
-    int dext = 0;
-    if (xdon > 0) {
-        const int tpx = nteams >> 3;
-        if (((blockIdx.x & 7) & 1) == 0) {
-            n -= n < xdon ? n : xdon;
-            n1 = n;
-        } else {
-            const int donor = team - tpx;
-            const int nd = (int)((M - donor + nteams - 1) / nteams);
-            const int dd = nd < xdon ? nd : xdon;
-            dext = (donor - team) + (nd - dd) * nteams;
-            n += dd;
-        }
-    }
-    const int64_t nmax = (M + nteams - 1) / nteams + xdon;  // granule rows per team
-    const int64_t gwords = (M + gridDim.x + (int64_t)nteams * kOpMaxDon) * kOpMaxK * T * 2;  // the granule block (OpArgs.xg)
+    const int n = (int)(ilv ? (M - team + nteams - 1) / nteams : (int64_t)(team + 1) * M / nteams - mb);
+    const int64_t nmax = (M + nteams - 1) / nteams;  // granule rows per team
+    const int64_t gwords = (M + gridDim.x) * kOpMaxK * T * 2;  // the granule block (OpArgs.xg)
     const int64_t r0 = (int64_t)member * TR;
     const int nrows = (int)(N - r0 < TR ? N - r0 : TR);  // >= 1 (op_plan)
     constexpr bool QFULL = tm_qfull(K, S, COMM, E);
@@ -369,8 +349,7 @@ __device__ __forceinline__ void atax_team_body(const double* __restrict__ X, int
                     // the column polled now (finished P steps later), the column finished now
                     const int ci = m - L + P, cf = m - L;
                     const int cic = ci < 0 ? 0 : ci < n ? ci : n - 1;
-                    tm_load8(ps[(i + RING - L + P) % RING],
-                             scp + (cic < n1 ? cic * csi : dext + (cic - n1) * csi));  // offsets < 2^31: 32-bit math
+                    tm_load8(ps[(i + RING - L + P) % RING], scp + cic * csi);  // offsets < 2^31: 32-bit math
                     tm_poll(pl[(i + RING - L + P) % RING], xg + (cic * nq2 + ql2));
                     v4u& g = pl[(i + RING - L) % RING];
                     v2u& sc = ps[(i + RING - L) % RING];
@@ -405,7 +384,7 @@ __device__ __forceinline__ void atax_team_body(const double* __restrict__ X, int
                         const double scv = __builtin_bit_cast(double, ((unsigned long long)sc.y << 32) | sc.x);
                         const double sg = readlane_d(scv, 0);
                         const bool own = (cf & (T - 1)) == member;  // T: a power of two
-                        const int64_t mg = mb + (cf < n1 ? cf * csi : dext + (cf - n1) * csi);  // the shard's column
+                        const int64_t mg = mb + cf * csi;  // the shard's column index
                         // both systems' chains first (independent: interleaved), then the
                         // LDS hand-over, then the owner's stores and <d,p>
                         double tsc[K], dval[K], pdir[K];
@@ -533,7 +512,7 @@ __device__ __forceinline__ void atax_team_body(const double* __restrict__ X, int
     double pk[RING];
     const char* xtile = reinterpret_cast<const char*>(X + mb * ld + r0);
     auto load = [&](int slot, int m) {
-        const int64_t c = m < n1 ? m * cs : dext + (int64_t)(m - n1) * cs;  // offset from mb
+        const int64_t c = m * cs;  // offset from mb
         pk[slot] = *tm_chk(pkp + c, pkp - mb, pkp - mb + M, 1024, a.err);  // older than the column's X loads: it lands first
         const __amdgpu_buffer_rsrc_t rs =
             __builtin_amdgcn_make_buffer_rsrc((void*)(xtile + c * ld * 8), (short)0, nbytes, 0x00020000);
@@ -628,7 +607,7 @@ __device__ __forceinline__ void atax_team_body(const double* __restrict__ X, int
         } else {
             const double sg = readlane_d(pk[slot], 1);
             const bool own = (m % T) == member;
-            const int64_t mg = mb + (m < n1 ? m * cs : dext + (int64_t)(m - n1) * cs);  // the shard's column index
+            const int64_t mg = mb + m * cs;  // the shard's column index
 #pragma unroll
             for (int k = 0; k < K; ++k) {
                 double t = sg * tot[k];  // sigma_inv * dpa

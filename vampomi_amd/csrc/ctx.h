@@ -124,7 +124,6 @@ struct vampomi_ctx {
     // set_variant(3 / 5) requests wait for it (applied at once on one rank)
     bool op_agreed = false;
     int op_variant_req = vk::kOpDefault;
-    int op_xdon = 0;                  // OpArgs.xdon (VAMPOMI_OP_XDON: columns each even-XCD team hands over)
     int cus = 0;                // compute units of the device (the operator's grid)
     double* op_part = nullptr;  // opp.nslots x kMaxRhs x ld partial A d
     int64_t op_part_slots = 0;

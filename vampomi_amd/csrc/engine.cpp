@@ -797,8 +797,7 @@ static size_t red_capacity(int64_t Mx) {
 // 8-byte words of the team hand-off granules: M columns x K x T granule pairs,
 // then a dummy pair per workgroup and K, then one XCD word per workgroup
 static size_t op_xg_words_for(int64_t Mx, const vk::OpPlan& p) {
-    return (size_t)(Mx + p.grid + (int64_t)(p.grid / p.T) * vk::kOpMaxDon) * vk::kOpMaxK * (size_t)p.T * 2 +
-           (size_t)p.grid * (2 * vk::kOpMaxK + 1);
+    return (size_t)(Mx + p.grid) * vk::kOpMaxK * (size_t)p.T * 2 + (size_t)p.grid * (2 * vk::kOpMaxK + 1);
 }
 
 static vampomi_status op_plan_local(vampomi_ctx* c) {
@@ -1012,7 +1011,6 @@ vampomi_status op_dev(vampomi_ctx* c, int K, const vk::OpArgs& a, const int* gat
     static const int dbg = std::getenv("VAMPOMI_OP_DBG") ? std::atoi(std::getenv("VAMPOMI_OP_DBG")) : 0;
     x.dbg = dbg;
     x.ts = c->op_ts;
-    x.xdon = c->op_xdon;
     // <d,p>: one rank into scal[SL_DP+k]; several: behind the A d block, all-reduced with it
     x.ro = vk::RedOut{c->red_part, c->use_comm ? ad + (int64_t)K * c->ld : c->scal + SL_DP, c->ticket, nullptr, 0,
                       gate};
@@ -1050,7 +1048,6 @@ vampomi_status op_dev_plain(vampomi_ctx* c, const vk::OpArgs& a, const double* c
         x.err = op_err_dev(c);
     }
     x.dbg = 0;
-    x.xdon = c->op_xdon;
     x.ro = vk::RedOut{c->red_part, c->use_comm ? ad + (int64_t)KT * c->ld : c->scal + SL_DP, c->ticket, nullptr, 0,
                       gate};
     TimedLaunch t = launch_stat(c, 3, KT, pass_bytes(c, KT), pass_flops(c, 1) + pass_flops(c, KT));
@@ -1237,7 +1234,6 @@ extern "C" vampomi_status vampomi_open(const vampomi_shard_desc* d, vampomi_ctx*
     c->side_on = c->use_comm;
     if (const char* sv = std::getenv("VAMPOMI_SIDE_STREAM")) c->side_on = std::atoi(sv) != 0;
     if (const char* hv = std::getenv("VAMPOMI_HEADSTART")) c->hs_on = c->hs_on_req = std::atoi(hv) != 0;
-    if (const char* xv = std::getenv("VAMPOMI_OP_XDON")) c->op_xdon = std::min(std::max(std::atoi(xv), 0), vk::kOpMaxDon);
     const char* mode = std::getenv("VAMPOMI_COMM");
     if (c->use_comm && mode && std::strcmp(mode, "loopback") == 0) {
         if (!d->comm_id) return fail(VAMPOMI_ERR_ARG, "the loopback communicator needs a communicator id");
@@ -1865,7 +1861,6 @@ extern "C" vampomi_status vampomi_dev_time_pass(vampomi_ctx* c, int which, int K
             x.dbg = std::getenv("VAMPOMI_OP_DBG") ? std::atoi(std::getenv("VAMPOMI_OP_DBG")) : 0;
             if (c->opp.T > 1) x.err = op_err_dev(c);
             x.ts = c->op_ts;
-            x.xdon = c->op_xdon;
             STCHK(team_launch(c, c->opp.T, [&] { return vk::atax(c->shard(), c->opp, K, x, c->st); }));
         }
         else  // association pass: ymod = nbuf slot 0, x1 = mbuf slot 0, sums in mbuf slots 3..7

@@ -142,8 +142,8 @@ struct OpArgs {
                         // partial slots 1 .. kOpPlain
     double* part;       // nslots x kMaxRhs x ld partial A d (before the sum over slots)
     RedOut ro;          // <d_k, p_k> summed over the shard (K values)
-    // team kernel with T > 1: hand-off granules ((M + grid + grid/T x
-    // kOpMaxDon) x kOpMaxK x T x 2 words, then 2 x kOpMaxK dummy words per workgroup, then one XCD word per
+    // team kernel with T > 1: hand-off granules ((M + grid) x kOpMaxK x T x 2
+    // words, then 2 x kOpMaxK dummy words per workgroup, then one XCD word per
     // workgroup; zeroed once), this launch's
     // tag (never 0, new every launch) and a mapped host word set when a
     // hand-off timed out
@@ -154,13 +154,7 @@ struct OpArgs {
     int dbg;  // timing experiments only (VAMPOMI_OP_DBG; results are wrong when set, except bit 5):
               // bit 0 no poll waits, 1 no publishes, 2 no butterfly, 3 no A d accumulation,
               // 5 write-through hand-off even when the team shares an XCD
-    // static XCD balance of interleaved team plans (0..kOpMaxDon): each team on
-    // an even dispatch XCD hands its last xdon columns to the team with the same
-    // local index on the next XCD, which runs them after its own (a fixed
-    // assignment: results stay bitwise repeatable; 0 = every team its own)
-    int xdon;
 };
-constexpr int kOpMaxDon = 8;
 std::string op_kernel_name(int K, const OpPlan& pl);
 std::string team_kernel_name(int K, const OpPlan& pl);
 // workgroups of the team kernel of plan pl (T >= 1) with K right-hand sides one
