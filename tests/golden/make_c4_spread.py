@@ -19,9 +19,10 @@ thresholded at 0.  Stored (tests/golden/oracle_c4_spread.npz):
 
 tests/test_gpu_probit.py::test_c4_full_shard_vs_oracle holds the device to
 PROBIT_K x the largest of these per iteration.  Run in the build container
-(20 GB for X; about 15 min on 8 cores):
+(20 GB for X; about 25 min on 8 cores):
 
     python tests/golden/make_c4_spread.py
+    python tests/golden/make_c4_spread.py --add 256 512 1024   # finer virtual shards
 """
 from __future__ import annotations
 
@@ -51,6 +52,10 @@ def c4_inputs(X):
 
 
 def main():
+    """`make_c4_spread.py` makes the fixture; `make_c4_spread.py --add P ...`
+    adds P-rank variants to the committed one (the single-rank run is redone,
+    the stored variants kept)."""
+    add = [int(a) for a in sys.argv[sys.argv.index("--add") + 1:]] if "--add" in sys.argv else None
     t0 = time.time()
     X = O.generate_markers(SEED, GEN_GAUSS, N, 0, MT)
     y, beta = c4_inputs(X)
@@ -58,7 +63,15 @@ def main():
     ref = O.vamp_infere(X, y, MT, true_signal=beta, **kw)
     print(f"single rank: {time.time() - t0:.0f} s", flush=True)
     pv = {}
-    ref, sp = oracle_with_spread(X, y, beta, MT, ranks=RANKS, blocks=BLOCKS, ref=ref, per_variant=pv, **kw)
+    if add:
+        old = np.load(os.path.join(HERE, "oracle_c4_spread.npz"))
+        assert np.array_equal(old["ref_x1_norm"], np.linalg.norm(ref["x1_hist"], axis=1)), "not the stored run"
+        for i, v in enumerate(old["variants"]):
+            pv[tuple(int(a) for a in v)] = {key: old[f"spread_{key}"][i] for key in ("x1", "r1", "params", "metrics",
+                                                                                    "prior")}
+        oracle_with_spread(X, y, beta, MT, ranks=tuple(add), blocks=(), ref=ref, per_variant=pv, **kw)
+    else:
+        oracle_with_spread(X, y, beta, MT, ranks=RANKS, blocks=BLOCKS, ref=ref, per_variant=pv, **kw)
     variants = sorted(pv)
     out = dict(N=N, Mt=MT, seed=SEED, its=ITS, y=y.astype(np.uint8), beta=beta,
                ref_x1_norm=np.linalg.norm(ref["x1_hist"], axis=1), ref_r1_norm=np.linalg.norm(ref["r1_hist"], axis=1),
