@@ -391,3 +391,38 @@ def test_rank_local_switches_between_runs(monkeypatch):
             assert p["cg_iters"] == one[hs]["cg_iters"] and p["ons_iters"] == one[hs]["ons_iters"]
         for k in range(its):
             assert relerr(_cat(ps, "x1_hist")[k], one[hs]["x1_hist"][k]) < 1e-12, (run, k)
+
+
+@pytest.mark.parametrize("P", [2, 3])
+@pytest.mark.parametrize("kw", [dict(max_iter=10, stop_criteria_thr=0.0), dict(max_iter=30, stop_criteria_thr=0.01),
+                                dict(max_iter=8, stop_criteria_thr=0.0, EM_max_iter=3, EM_err_thr=1e-9),
+                                dict(max_iter=8, stop_criteria_thr=0.0, learn_prior_delay=4)],
+                         ids=["fixed", "stops", "em3", "delay"])
+def test_multi_rank_tail_without_host_waits_bitwise(monkeypatch, P, kw):
+    """Several ranks (VAMPOMI_MR_TAIL, default on): the linear iteration's tail
+    runs without host waits -- gam1, the EM round's mixture update and the next
+    prelude's scalars are formed on the device after the all-reduce of their
+    sums (vk::tail_post), and the next prelude + CG start are queued before
+    the host's one wait.  Bitwise the run with the host waiting at every
+    level (VAMPOMI_MR_TAIL=0), also when the stop criterion fires, with
+    several EM rounds (the host path) and with the prior's learning delayed."""
+    N, Mt = 1001, 2003
+    X, y, beta = make_problem(N, Mt)
+    out = {}
+
+    def fn(r, d):
+        s = _vamp(d, X, y, beta, **kw)
+        s["host_syncs"] = d.stats().host_syncs
+        return s
+
+    for mt in ("0", "1"):
+        monkeypatch.setenv("VAMPOMI_MR_TAIL", mt)
+        out[mt] = run_ranks(monkeypatch, P, N, Mt, fn)
+    if "EM_max_iter" not in kw and "learn_prior_delay" not in kw:  # (the host path of those settings is kept)
+        assert out["1"][0]["host_syncs"] < out["0"][0]["host_syncs"], (out["1"][0]["host_syncs"],
+                                                                      out["0"][0]["host_syncs"])
+    for a, b in zip(out["0"], out["1"]):
+        for k in ("iterations", "cg_iters", "ons_iters", "L"):
+            assert a[k] == b[k], k
+        for k in ("x1_hist", "r1_hist", "params", "metrics"):
+            np.testing.assert_array_equal(np.asarray(a[k]), np.asarray(b[k]), err_msg=k)

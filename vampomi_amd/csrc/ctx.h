@@ -83,6 +83,7 @@ struct vampomi_ctx {
     unsigned* ticket2 = nullptr;
     bool side_open = false;  // the side stream has work st has not joined (DotBatch fork .. flush)
     bool side_on = false;  // default: several ranks; VAMPOMI_SIDE_STREAM=0/1 or vampomi_dev_set_variant(c, 4, 0/1)
+    bool mr_tail = true;   // several ranks: the linear iteration's tail without host waits (vamp.cpp); VAMPOMI_MR_TAIL=0
     bool team_reg = false;           // registered with its device's team gate (engine.cpp)
     hipEvent_t team_ev = nullptr;    // recorded on st when another context must order behind it
     ncclComm_t comm = nullptr;
@@ -249,6 +250,14 @@ class DotBatch {
     // out is written (mapped host memory), for a kernel queued before the
     // flush; null if out is not a sink of this batch or with a communicator
     const double* dev_result(const double* out) const;
+    // several ranks: all-reduces the synced slots filled since the last call,
+    // on the main stream, with no host copy or wait (flush() then publishes
+    // them without reducing them again), so that a kernel queued next can read
+    // the final sums at dev_slot(); nothing on one rank.  COLLECTIVE
+    vampomi_status reduce_now();
+    // several ranks: the device address of the slot whose value flush() will
+    // copy to out (final after reduce_now() for a synced result); else null
+    double* dev_slot(const double* out) const;
     // on = true: the following sinks/adds run on the context's side stream
     // (ordered after everything queued on st so far); flush() joins it back.
     // No effect (one stream) when the context's side stream is off
@@ -270,6 +279,7 @@ class DotBatch {
     };
     vampomi_ctx* c_;
     int nsync_ = 0, nlocal_ = 0;
+    int nred_ = 0;  // synced slots [0, nred_) already all-reduced (reduce_now)
     bool on_side_ = false, forked_ = false;
     unsigned long long last_seq_ = 0;  // one rank: flag value the last reduction kernel stores
     unsigned long long side_seq_ = 0;  // ... and the last side-stream reduction (flag word 1)

@@ -648,6 +648,21 @@ const double* DotBatch::dev_result(const double* out) const {
     return nullptr;
 }
 
+double* DotBatch::dev_slot(const double* out) const {
+    if (!c_->use_comm) return nullptr;
+    for (const Sink& k : sinks_)
+        if (k.out == out) return c_->scal + k.slot;
+    return nullptr;
+}
+
+vampomi_status DotBatch::reduce_now() {
+    if (!c_->use_comm || nsync_ == nred_) return VAMPOMI_OK;
+    if (on_side_ || forked_) return fail(VAMPOMI_ERR_STATE, "DotBatch::reduce_now with the side stream open");
+    STCHK(allreduce_dev(c_, c_->scal + SL_SYNC + nred_, (size_t)(nsync_ - nred_)));
+    nred_ = nsync_;
+    return VAMPOMI_OK;
+}
+
 hipStream_t DotBatch::stream() const { return on_side_ ? c_->st2 : c_->st; }
 
 vampomi_status DotBatch::fork() {
@@ -686,7 +701,7 @@ vampomi_status DotBatch::flush() {
     }
     if (sinks_.empty()) return VAMPOMI_OK;
     if (c_->use_comm) {  // slots in device memory: all-reduce the synced ones, then publish both ranges
-        if (nsync_ > 0) STCHK(allreduce_dev(c_, c_->scal + SL_SYNC, (size_t)nsync_));
+        if (nsync_ > nred_) STCHK(allreduce_dev(c_, c_->scal + SL_SYNC + nred_, (size_t)(nsync_ - nred_)));
         if (c_->h_flag) {
             const unsigned long long seq = ++c_->sync_seq;
             HIPCHK(vk::publish_host(c_->scal + SL_SYNC, nsync_, c_->d_hscal + SL_SYNC, c_->scal + SL_LOCAL, nlocal_,
@@ -711,7 +726,7 @@ vampomi_status DotBatch::flush() {
     for (const Sink& k : sinks_)
         for (int i = 0; i < k.count; ++i) k.out[i] = c_->h_scal[k.slot + i];
     sinks_.clear();
-    nsync_ = nlocal_ = 0;
+    nsync_ = nlocal_ = nred_ = 0;
     last_seq_ = 0;
     return VAMPOMI_OK;
 }
@@ -1233,6 +1248,7 @@ extern "C" vampomi_status vampomi_open(const vampomi_shard_desc* d, vampomi_ctx*
     // cross-queue events cost more than the 5-17 us kernels they overlap)
     c->side_on = c->use_comm;
     if (const char* sv = std::getenv("VAMPOMI_SIDE_STREAM")) c->side_on = std::atoi(sv) != 0;
+    if (const char* mv = std::getenv("VAMPOMI_MR_TAIL")) c->mr_tail = std::atoi(mv) != 0;
     if (const char* hv = std::getenv("VAMPOMI_HEADSTART")) c->hs_on = c->hs_on_req = std::atoi(hv) != 0;
     const char* mode = std::getenv("VAMPOMI_COMM");
     if (c->use_comm && mode && std::strcmp(mode, "loopback") == 0) {

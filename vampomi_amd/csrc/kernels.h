@@ -322,6 +322,26 @@ struct PreOut {
     double* out = nullptr;
     double* mirror = nullptr;
 };
+// Several ranks: what the one-rank launches' last blocks form from their final
+// sums (G1Chain, EmArgs.upd, PreOut), formed by one thread after the sums'
+// all-reduce (vamp.cpp's host-free tail; the same expressions, bit for bit).
+// mode 0: gam1_chain from src[0] = a2 into g1.out, and the device copies
+// cp_dst[i] = *cp_src[i]; 1: one EM round's update of the mixture (L, vars)
+// from src (1 + 2(L-1) sums) into upd.out / upd.mirror; 2: the next prelude's
+// scalars from src[0] = the sum of x1d and gam1 = gam1dev[0] into po
+struct TailPost {
+    int mode = 0;
+    const double* src = nullptr;
+    G1Chain g1;
+    const double* cp_src[2] = {nullptr, nullptr};
+    double* cp_dst[2] = {nullptr, nullptr};
+    int L = 0;
+    double vars[kMaxL] = {};
+    EmUpd upd;
+    PreOut po;
+    const double* gam1dev = nullptr;
+};
+hipError_t tail_post(const TailPost& t, hipStream_t st);
 // scal (device, may be null): the prelude's scalars {eta1, gam2, gamw, diag,
 // gam1} from PreOut.out instead of the Prelude's own (prelude_cg_init only)
 struct PreDev {
@@ -461,7 +481,10 @@ constexpr int kCgMirrorSlots = 2;
 // *dst = init (one thread)
 hipError_t cg_start(const CgState& init, CgState* dst, hipStream_t st);
 // *dst = init with rz[k], vv[k] = sums[2k], sums[2k+1] (cg_init's sums, in device memory)
-hipError_t cg_start_from(const CgState& init, const double* sums, CgState* dst, hipStream_t st);
+// gam2dev (may be null): init.gam2 from the device (a start queued ahead: the
+// next prelude's scalars, PreOut.out + 1)
+hipError_t cg_start_from(const CgState& init, const double* sums, CgState* dst, hipStream_t st,
+                         const double* gam2dev = nullptr);
 // prelude() and cg_init() in one launch (cg_init's grid and sums: bitwise the
 // two launches), where cg_init's v_k may be the prelude's v or bern (taken from
 // registers).  start (may be null): the last block also writes *dst = *start

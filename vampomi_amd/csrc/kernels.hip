@@ -1467,6 +1467,35 @@ __device__ void em_update_mix(const double* q, int L, const double* vars, const 
     w[1 + 2 * kMaxL] = eta_max;
 }
 
+// the next prelude's scalars (kernels.h PreOut) from the sum of x1d, gam1 and
+// the two updateNoisePrec sums: the host's expressions
+__device__ void pre_scalars(double sum_d, double gam1, double tn, double tc, const PreOut& po) {
+    const double alpha1 = sum_d / po.Mt;  // :223
+    const double eta1 = gam1 / alpha1;    // :230
+    const double dg = eta1 - gam1;
+    double gam2 = dg < 1e-11 ? 1e-11 : dg;  // std::max(., 1e-11) (:255-256)
+    gam2 = 1e11 < gam2 ? 1e11 : gam2;       // std::min(., 1e11)
+    const double trace_corr = tc * po.Mt;    // :521
+    const double gamw = po.N / (tn + trace_corr);  // :528
+    const double diag = gamw * (po.N - 1) / po.N + gam2;  // :676-677 (pcg_run)
+    const double v[5] = {eta1, gam2, gamw, diag, gam1};
+    for (int q = 0; q < 5; ++q) po.out[q] = v[q];
+    for (int q = 0; q < 4; ++q) po.mirror[q] = v[q];
+}
+
+// the mixture words w (em_update_mix) into upd.out and upd.mirror
+__device__ void em_write(const double* w, const EmUpd& u) {
+    const int Ln = (int)w[0];
+    for (double* o : {u.out, u.mirror}) {
+        o[0] = w[0];
+        for (int j = 0; j < Ln; ++j) {
+            o[1 + j] = w[1 + j];
+            o[1 + kMaxL + j] = w[1 + kMaxL + j];
+        }
+        o[1 + 2 * kMaxL] = w[1 + 2 * kMaxL];
+    }
+}
+
 // Dev: the mixture's words (an EM round's update, em_kernel) and gam1
 // (G1Chain) from the device, the words staged in LDS; else mix and gam1
 template <bool Dev>
@@ -1510,19 +1539,7 @@ __global__ __launch_bounds__(kBlock) void denoise_kernel(int64_t M, const double
     if (threadIdx.x == 0) red_put(ro, blockIdx.x, acc);
     __shared__ double fin[1];
     const bool last = red_finish(ro, 1, lds, Dev && po.out ? fin : nullptr);
-    if (Dev && po.out && last && threadIdx.x == 0) {  // the next prelude's scalars (kernels.h PreOut)
-        const double alpha1 = fin[0] / po.Mt;  // :223
-        const double eta1 = gam1 / alpha1;     // :230
-        const double dg = eta1 - gam1;
-        double gam2 = dg < 1e-11 ? 1e-11 : dg;  // std::max(., 1e-11) (:255-256)
-        gam2 = 1e11 < gam2 ? 1e11 : gam2;       // std::min(., 1e11)
-        const double trace_corr = tc * po.Mt;    // :521
-        const double gamw = po.N / (tn + trace_corr);  // :528
-        const double diag = gamw * (po.N - 1) / po.N + gam2;  // :676-677 (pcg_run)
-        const double v[5] = {eta1, gam2, gamw, diag, gam1};
-        for (int q = 0; q < 5; ++q) po.out[q] = v[q];
-        for (int q = 0; q < 4; ++q) po.mirror[q] = v[q];
-    }
+    if (Dev && po.out && last && threadIdx.x == 0) pre_scalars(fin[0], gam1, tn, tc, po);
 }
 
 hipError_t denoise(int64_t M, const double* r1, double gam1, const Mix& mix, double* x1, const double* x1_prev,
@@ -1620,16 +1637,34 @@ __global__ __launch_bounds__(kBlock) void em_kernel(int64_t M, const double* __r
     if (last && a.upd.out && threadIdx.x == 0) {  // the round's update of the mixture (EmArgs.upd)
         __shared__ double w[kMixWords];
         em_update_mix(fin, L, a.vars, a.upd, w);
-        const int Ln = (int)w[0];
-        for (double* o : {a.upd.out, a.upd.mirror}) {
-            o[0] = w[0];
-            for (int j = 0; j < Ln; ++j) {
-                o[1 + j] = w[1 + j];
-                o[1 + kMaxL + j] = w[1 + kMaxL + j];
-            }
-            o[1 + 2 * kMaxL] = w[1 + 2 * kMaxL];
-        }
+        em_write(w, a.upd);
     }
+}
+
+// kernels.h TailPost: the one-rank last blocks' work, after the all-reduce
+__global__ void tail_post_kernel(TailPost t) {
+    if (threadIdx.x != 0) return;
+    if (t.mode == 0) {
+        gam1_chain(t.src[0], t.g1.gam2, t.g1.rho, t.g1.gam1_prev, t.g1.out);
+        for (int i = 0; i < 2; ++i)
+            if (t.cp_dst[i]) *t.cp_dst[i] = *t.cp_src[i];
+    } else if (t.mode == 1) {
+        __shared__ double w[kMixWords];
+        em_update_mix(t.src, t.L, t.vars, t.upd, w);
+        em_write(w, t.upd);
+    } else {
+        pre_scalars(t.src[0], t.gam1dev[0], t.po.tn[0], t.po.tc[0], t.po);
+    }
+}
+
+hipError_t tail_post(const TailPost& t, hipStream_t st) {
+    if (!t.src || t.mode < 0 || t.mode > 2 || (t.mode == 0 && !t.g1.out) || (t.mode == 1 && (!t.upd.out || !t.upd.mirror)) ||
+        (t.mode == 2 && (!t.gam1dev || !t.po.out || !t.po.mirror || !t.po.tn || !t.po.tc)))
+        return hipErrorInvalidValue;
+    for (int i = 0; i < 2; ++i)
+        if (t.cp_dst[i] && !t.cp_src[i]) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(tail_post_kernel, dim3(1), dim3(64), 0, st, t);
+    return hipGetLastError();
 }
 
 hipError_t em_sums(int64_t M, const double* r1, const EmArgs& a, const RedOut& ro, hipStream_t st) {
@@ -1879,17 +1914,20 @@ hipError_t cg_start(const CgState& init, CgState* dst, hipStream_t st) {
     return hipGetLastError();
 }
 
-__global__ void cg_start_from_kernel(CgState init, const double* __restrict__ sums, CgState* dst) {
+__global__ void cg_start_from_kernel(CgState init, const double* __restrict__ sums, CgState* dst,
+                                     const double* __restrict__ gam2dev) {
     if (threadIdx.x != 0) return;
     for (int k = 0; k < init.K; ++k) {
         init.rz[k] = sums[2 * k];
         init.vv[k] = sums[2 * k + 1];
     }
+    if (gam2dev) init.gam2 = gam2dev[0];
     *dst = init;
 }
 
-hipError_t cg_start_from(const CgState& init, const double* sums, CgState* dst, hipStream_t st) {
-    hipLaunchKernelGGL(cg_start_from_kernel, dim3(1), dim3(64), 0, st, init, sums, dst);
+hipError_t cg_start_from(const CgState& init, const double* sums, CgState* dst, hipStream_t st,
+                         const double* gam2dev) {
+    hipLaunchKernelGGL(cg_start_from_kernel, dim3(1), dim3(64), 0, st, init, sums, dst, gam2dev);
     return hipGetLastError();
 }
 

@@ -185,19 +185,26 @@ vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double
         // pre: the caller's prelude rides in the same launch, and on one rank
         // that launch's last block also builds the CgState (three launches in one)
         const bool own_start = pre && !c->use_comm;
-        if (pm != PreMode::normal && (!own_start || (pm == PreMode::ahead) != (pre->dev.scal != nullptr)))
-            return fail(VAMPOMI_ERR_ARG, "pcg: a start queued ahead needs one rank, the prelude and its device scalars");
+        if (pm != PreMode::normal && (!pre || (pm == PreMode::ahead) != (pre->dev.scal != nullptr)))
+            return fail(VAMPOMI_ERR_ARG, "pcg: a start queued ahead needs the prelude and its device scalars");
         if (pm == PreMode::queued) {
-            // (queued ahead by the previous iteration, scalars from the device)
-        } else if (pre) {
-            HIPCHK(vk::prelude_cg_init(K, M, *pre, cv, diag, ro, own_start ? &s0 : nullptr, c->cgs, c->st));
-            if (pm == PreMode::ahead) return VAMPOMI_OK;
+            // (queued ahead by the previous iteration, scalars from the device:
+            // the prelude, and on several ranks the sums' all-reduce and the CgState)
         } else {
-            HIPCHK(vk::cg_init(K, M, cv, diag, ro, c->st));
+            if (pre)
+                HIPCHK(vk::prelude_cg_init(K, M, *pre, cv, diag, ro, own_start ? &s0 : nullptr, c->cgs, c->st));
+            else
+                HIPCHK(vk::cg_init(K, M, cv, diag, ro, c->st));
+            if (!own_start) {
+                STCHK(allreduce_dev(c, c->scal + SL_CGI, (size_t)(2 * K)));
+                // (ahead: gam2 from the device, the prelude's scalars {eta1, gam2, ...})
+                if (max_iter > 0)
+                    HIPCHK(vk::cg_start_from(s0, c->scal + SL_CGI, c->cgs, c->st,
+                                             pm == PreMode::ahead ? pre->dev.scal + 1 : nullptr));
+            }
+            if (pm == PreMode::ahead) return VAMPOMI_OK;
         }
-        STCHK(allreduce_dev(c, c->scal + SL_CGI, (size_t)(2 * K)));
         if (max_iter <= 0) return extra_alone();
-        if (!own_start) HIPCHK(vk::cg_start_from(s0, c->scal + SL_CGI, c->cgs, c->st));
     }
     const int* gate = field<int>(c->cgs, offsetof(vk::CgState, any));
     const double* beta = field<double>(c->cgs, offsetof(vk::CgState, beta));

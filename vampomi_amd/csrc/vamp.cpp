@@ -636,11 +636,16 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
     const bool next = R.fuse && it < R.prm.max_iter;
     const bool em_next = next && it + 1 > R.prm.learn_prior_delay;
     const bool r1_in_em = next && arec && em_next && R.prm.EM_max_iter >= 1;
-    // chain (one rank): alpha2 -> eta2 -> gam1 (:341-346) are formed on the
-    // device from the reduction's result (vk::G1Chain), so the EM round and
-    // the reductions after it are queued without the host waiting for alpha2;
-    // the host forms the same values from the same sum at the next flush
-    const bool chain = r1_in_em && !c->use_comm;
+    // chain: alpha2 -> eta2 -> gam1 (:341-346) are formed on the device from
+    // the reduction's result (vk::G1Chain), so the EM round and the reductions
+    // after it are queued without the host waiting for alpha2; the host forms
+    // the same values from the same sum at the next flush.  Several ranks
+    // (mr): the sums are final only after their all-reduce, so each value the
+    // one-rank launches' last blocks form is formed by a one-thread launch
+    // after it (vk::tail_post), all on the main stream (DotBatch::reduce_now);
+    // VAMPOMI_MR_TAIL=0: the host waits at each level instead (round 4)
+    const bool chain = r1_in_em && (!c->use_comm || c->mr_tail);
+    const bool mr = chain && c->use_comm;
     const DotBatch::Group ga2{{T(R.bern, R.invQ)}, true, &R.a2};  // :498
     const double gam1_prev = R.gam1;
     auto host_gam1 = [&] {
@@ -678,7 +683,21 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
         g1.gam1_prev = gam1_prev;
         g1.out = dsc;
         // (tc and tn also into device memory, for the next prelude's scalars: vk::PreOut)
-        STCHK(fin.add_pair(M, gm, &g1, &R.a2, {{&R.tc, dsc + 9}}, N, gn, {{&R.tn, dsc + 8}}));  // one launch
+        if (!mr) {
+            STCHK(fin.add_pair(M, gm, &g1, &R.a2, {{&R.tc, dsc + 9}}, N, gn, {{&R.tn, dsc + 8}}));  // one launch
+        } else {
+            STCHK(fin.add_pair(M, gm, nullptr, nullptr, {}, N, gn, {}));
+            STCHK(fin.reduce_now());
+            vk::TailPost t;
+            t.mode = 0;
+            t.src = fin.dev_slot(&R.a2);
+            t.g1 = g1;
+            t.cp_src[0] = fin.dev_slot(&R.tc);
+            t.cp_dst[0] = dsc + 9;
+            t.cp_src[1] = fin.dev_slot(&R.tn);
+            t.cp_dst[1] = dsc + 8;
+            HIPCHK(vk::tail_post(t, c->st));
+        }
     } else {
         DotBatch b(c);
         if (arec)
@@ -725,9 +744,9 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
     EmState em;
     if (next) R.mix_next = R.mix;
     if (next && arec) {  // the side stream starts from r1 and x1; its EM sums are queued before these reductions
-        STCHK(fin.fork());
+        if (!mr) STCHK(fin.fork());  // (mr: one stream, the all-reduces between the launches)
         if (em_next) {
-            STCHK(fin.side(true));
+            if (!mr) STCHK(fin.side(true));
             vk::EmUpd eu;
             eu.Mt = Mt;
             eu.learn_vars = R.prm.learn_vars;
@@ -735,11 +754,31 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
             eu.out = R.mixw;
             eu.mirror = R.mixh_dev;
             STCHK(em_begin(c, em_params(R), R.mix_next, R.gam1, R.r1, fin, em, r1_in_em ? &r1from : nullptr,
-                           devem ? &eu : nullptr));
-            if (devem)
+                           devem && !mr ? &eu : nullptr));
+            if (devem && mr) {  // the round's update of the mixture, from its all-reduced sums
+                STCHK(fin.reduce_now());
+                vk::TailPost t;
+                t.mode = 1;
+                t.src = fin.dev_slot(em.sums);
+                t.L = R.mix_next.L;
+                for (int j = 0; j < R.mix_next.L; ++j) t.vars[j] = R.mix_next.vars[j];
+                t.upd = eu;
+                HIPCHK(vk::tail_post(t, c->st));
+            }
+            if (devem) {
                 STCHK(denoise_into(c, R.mix_next, R.gam1, R.r1, R.x1n, R.x1, true, R.prm.rho, R.x1d, fin, &R.sum_d,
-                                   R.mixw, dsc, ahead ? &po : nullptr));
-            STCHK(fin.side(false));
+                                   R.mixw, dsc, ahead && !mr ? &po : nullptr));
+                if (ahead && mr) {  // the next prelude's scalars, from the all-reduced sum of x1d
+                    STCHK(fin.reduce_now());
+                    vk::TailPost t;
+                    t.mode = 2;
+                    t.src = fin.dev_slot(&R.sum_d);
+                    t.po = po;
+                    t.gam1dev = dsc;
+                    HIPCHK(vk::tail_post(t, c->st));
+                }
+            }
+            if (!mr) STCHK(fin.side(false));
         }
     }
     if (next && !arec) {  // the pass below carries the next z1 = A x1_hat: denoise first
