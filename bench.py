@@ -314,6 +314,27 @@ def pmc_traffic(kernel: str, workload: str):
     return None, None
 
 
+CEILING_FILES = [os.path.join(ROOT, "profiles", f) for f in ("r05_hbm_read_ceiling.json", "r01h_hbm_read_ceiling.json")]
+
+
+def read_ceiling(xbytes: float):
+    """The measured HBM read ceiling of one MI355X (tools/hbm_ceiling: every
+    byte of a buffer of about this size read once, 16-B nontemporal loads, the
+    best variant's median), newest profile first: (GB/s, source) or (None, None)."""
+    for f in CEILING_FILES:
+        try:
+            d = json.load(open(f))
+        except Exception:
+            continue
+        sizes = {float(k[:-2]): v for k, v in d.items() if k.endswith("GB") and isinstance(v, list)}
+        if not sizes:
+            continue
+        gb = min(sizes, key=lambda g: abs(g - xbytes / 1e9))
+        best = min(sizes[gb], key=lambda v: v["us_med"])
+        return best["GBs_med"], f"{os.path.relpath(f, ROOT)} ({gb:g} GB buffer, {best['variant']}, median)"
+    return None, None
+
+
 def roofline(ks, kname: str, workload: str, period: int) -> dict:
     """The dominant kernel's achieved GB/s: algorithmic bytes per launch (exact
     count) over its average launch time (HIP events recorded in
@@ -322,7 +343,11 @@ def roofline(ks, kname: str, workload: str, period: int) -> dict:
     bytes_per = ks.bytes_total / ks.launches
     achieved = bytes_per / (avg_ms * 1e-3) / 1e9
     traffic, tfile = pmc_traffic(kname, workload)
+    ceil, cfile = read_ceiling(bytes_per)
     return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            # the same achieved rate against what a pure read stream of the same size reaches on this hardware
+            "read_ceiling_measured": round(ceil, 1) if ceil else None,
+            "frac_of_read_ceiling": round(achieved / ceil, 4) if ceil else None, "read_ceiling_source": cfile,
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": int(traffic) if traffic else None,
             "traffic_unit": f"HBM bytes per launch (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, {tfile})"
             if tfile else None,

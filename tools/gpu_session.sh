@@ -21,6 +21,7 @@
 #   launcher     the default C2 line over a 1-rank RCCL communicator, and the
 #                2-rank launcher on a 1-GPU box (one failure line, rc != 0)
 #   rccl         the 1-rank RCCL path against the direct one (rates, timing on/off, traces compared)
+#   ceiling      the HBM read ceiling of this box (tools/hbm_ceiling, 4 GB and 50 GB buffers)
 #   bases        rank 0's 1-GPU bases (tools/one_gpu_bases.py)
 #   final        smoke, the default C2 line (both CPU legs), its kernel stats
 #                and PMC traffic; the same for C3; C4 and C5 lines
@@ -132,6 +133,9 @@ for s in "$@"; do
             --output-format csv -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-timing
         python tools/trace_cmp.py "$(find "$OUT/prof_dir" -name 'run_kernel_trace.csv' | head -1)" \
             "$(find "$OUT/prof_rccl" -name 'run_kernel_trace.csv' | head -1)" | tee "$OUT/trace_cmp.txt" ;;
+    ceiling)     # the HBM read ceiling (tools/hbm_ceiling: every byte of a 4 GB / 50 GB buffer read once)
+        step ceiling_4 200 tools/hbm_ceiling 4 15
+        step ceiling_50 300 tools/hbm_ceiling 50 5 ;;
     bases)
         step bases 200 python tools/one_gpu_bases.py ;;
     final)

@@ -1083,10 +1083,10 @@ vampomi_status op_dev_plain(vampomi_ctx* c, const vk::OpArgs& a, const double* c
         for (int k = 0; k < KT; ++k) os.p[k] = ad + (int64_t)k * c->ld;
         HIPCHK(vk::op_reduce(c->opp_hs, KT, c->N, c->ld, c->op_part, os, 0.0, c->st, gate));
         STCHK(allreduce_dev(c, ad, (size_t)KT * c->ld + 1));  // src/data.cpp:367
-        HIPCHK(vk::vec_div(KT, c->N, c->ld, os, c->sqrtN, c->st));
-        for (int k = 0; k < vk::kOpPlain; ++k)
-            HIPCHK(hipMemcpyAsync(out[k], ad + (int64_t)(1 + k) * c->ld, (size_t)c->N * 8, hipMemcpyDeviceToDevice,
-                                  c->st));
+        // the system's A d divided in place, the plain products divided into their destinations (one launch)
+        vk::Ptrs dst = os;
+        for (int k = 0; k < vk::kOpPlain; ++k) dst.p[1 + k] = out[k];
+        HIPCHK(vk::vec_div(KT, c->N, c->ld, os, c->sqrtN, c->st, &dst));
     }
     return VAMPOMI_OK;
 }

@@ -87,7 +87,8 @@ hipError_t ax_partial(const Shard& s, const AxPlan& pl, int K, CPtrs x, double* 
 hipError_t ax_reduce(const AxPlan& pl, int K, int64_t N, int64_t ld, const double* part, Ptrs out,
                      double div, hipStream_t st, const int* gate = nullptr);
 // out_k[j] /= div (after the cross-rank all-reduce)
-hipError_t vec_div(int K, int64_t n, int64_t ld, Ptrs v, double div, hipStream_t st);
+// v_k / div into dst_k (dst null: in place)
+hipError_t vec_div(int K, int64_t n, int64_t ld, Ptrs v, double div, hipStream_t st, const Ptrs* dst = nullptr);
 
 // ---- A^T.u : one wave per group of markers --------------------------------
 // mode 0: out_k[i] = (msig_i * dot_k(i)) * scale

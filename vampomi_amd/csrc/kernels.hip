@@ -550,17 +550,17 @@ hipError_t ax_reduce(const AxPlan& pl, int K, int64_t N, int64_t ld, const doubl
     return hipGetLastError();
 }
 
-__global__ void vec_div_kernel(int K, int64_t n, Ptrs v, double div) {
+__global__ void vec_div_kernel(int K, int64_t n, Ptrs v, double div, Ptrs dst) {
     const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (e >= (int64_t)K * n) return;
     const int k = (int)(e / n);
     const int64_t j = e - (int64_t)k * n;
-    v.p[k][j] /= div;
+    dst.p[k][j] = v.p[k][j] / div;
 }
 
-hipError_t vec_div(int K, int64_t n, int64_t /*ld*/, Ptrs v, double div, hipStream_t st) {
+hipError_t vec_div(int K, int64_t n, int64_t /*ld*/, Ptrs v, double div, hipStream_t st, const Ptrs* dst) {
     hipLaunchKernelGGL(vec_div_kernel, dim3((unsigned)cdiv((int64_t)K * n, kBlock)), dim3(kBlock), 0, st, K, n, v,
-                       div);
+                       div, dst ? *dst : v);
     return hipGetLastError();
 }
 
