@@ -189,6 +189,11 @@ def test_cli_on_reference_written_files(tmp_path):
                                                      r.stdout)]
     assert [c[0] for c in counts] == z["cg_iters"].tolist()
     assert [c[1] for c in counts] == z["ons_iters"].tolist()
+    # per iteration, as the reference prints them (src/vamp.cpp:396-401)
+    times = [float(t) for t in re.findall(r"Total iteration time = ([0-9.eE+-]+)", r.stdout)]
+    so_far = [float(t) for t in re.findall(r"Total computation time so far = ([0-9.eE+-]+)", r.stdout)]
+    assert len(times) == its and len(so_far) == its and all(t > 0 for t in times)
+    assert np.allclose(np.cumsum(times), so_far, rtol=1e-4)
     for q, k in enumerate(z["keep_its"]):
         x1 = np.fromfile(tmp_path / f"g_it_{k}.bin", dtype="<f8")
         r1 = np.fromfile(tmp_path / f"g_r1_it_{k}.bin", dtype="<f8")

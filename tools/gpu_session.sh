@@ -146,7 +146,7 @@ for s in "$@"; do
         step bench_c3 400 python bench.py --config c3 --steps 10 --warmup 2
         prof c3 6
         step pmc_c3 300 bash tools/pmc.sh c3
-        step bench_c4 400 python bench.py --config c4 --steps 12 --warmup 2
+        step bench_c4 400 python bench.py --config c4 --steps 6 --warmup 2   # iterations 3-8: inside test_c4_full_shard_vs_oracle
         step bench_c5 300 python bench.py --config c5 --steps 5 --warmup 1 ;;
     *)
         echo "unknown step $s"; exit 2 ;;
