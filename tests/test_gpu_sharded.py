@@ -426,3 +426,34 @@ def test_multi_rank_tail_without_host_waits_bitwise(monkeypatch, P, kw):
             assert a[k] == b[k], k
         for k in ("x1_hist", "r1_hist", "params", "metrics"):
             np.testing.assert_array_equal(np.asarray(a[k]), np.asarray(b[k]), err_msg=k)
+
+
+@pytest.mark.parametrize("P", [2, 3])
+@pytest.mark.parametrize("kw", [dict(), dict(CG_max_iter=2), dict(CG_max_iter=1), dict(hs=0)],
+                         ids=["default", "cg_max2", "cg_max1", "no_headstart"])
+def test_folded_cg_decisions_bitwise(monkeypatch, P, kw):
+    """Several ranks (VAMPOMI_CG_FOLD, default on): each CG step's decision is
+    formed by the next step's operator launch from the all-reduced sums
+    (vk::OpFold; the two CgStates alternate), and by a decision launch only
+    when no step follows (CG_max_iter reached).  Bitwise the run with a
+    decision launch after every step (VAMPOMI_CG_FOLD=0), with and without
+    the head start, and with the solve cut at 1 and 2 steps; the team
+    operator (N = 12,000) and the whole-column plan (N = 1,001)."""
+    kw = dict(kw)
+    hs = kw.pop("hs", 1)
+    for N, Mt, its in ((1001, 2003, 6), (12000, 3001, 4)):
+        X, y, beta = make_problem(N, Mt, seed=8)
+        out = {}
+
+        def fn(r, d):
+            d.set_variant(5, hs)
+            return _vamp(d, X, y, beta, max_iter=its, stop_criteria_thr=0.0, **kw)
+
+        for fo in ("0", "1"):
+            monkeypatch.setenv("VAMPOMI_CG_FOLD", fo)
+            out[fo] = run_ranks(monkeypatch, P, N, Mt, fn, timeout=300)
+        for a, b in zip(out["0"], out["1"]):
+            for k in ("iterations", "cg_iters", "ons_iters", "L"):
+                assert a[k] == b[k], (N, k)
+            for k in ("x1_hist", "r1_hist", "params"):
+                np.testing.assert_array_equal(np.asarray(a[k]), np.asarray(b[k]), err_msg=f"{N} {k}")

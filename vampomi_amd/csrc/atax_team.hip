@@ -216,7 +216,31 @@ __device__ __forceinline__ void atax_team_body(const double* __restrict__ X, int
                                                const double* __restrict__ mave, const double* __restrict__ msig,
                                                const OpArgs& a, int T, int TR, int ilv,
                                                const int* __restrict__ gate) {
-    if (gate && !*gate) return;
+    // beta_k of the fused direction updates: from the previous step's decision
+    // when this launch forms it (OpArgs.fold), else a.beta
+    __shared__ double s_beta[kOpMaxK];
+    if (a.fold.on) {
+        __shared__ int s_go;
+        if (threadIdx.x == 0) {
+            CgState cs = *a.fold.src;
+            double r[3 * kMaxRhs];
+#pragma unroll
+            for (int q = 0; q < 3 * kMaxRhs; ++q) r[q] = q < 3 * cs.K ? a.fold.red[q] : 0.0;
+            const bool ran = cg_decide_into(cs, r, a.fold.it, a.fold.mask);
+            if (blockIdx.x == 0) {
+                *a.fold.dst = cs;
+                cg_publish(cs, ran, a.fold.it, a.fold.mirror, a.fold.flag, a.fold.seq, a.fold.pack);
+            }
+            s_go = cs.any;
+#pragma unroll
+            for (int k = 0; k < kOpMaxK; ++k) s_beta[k] = cs.beta[k];
+        }
+        __syncthreads();
+        if (!s_go) return;
+    } else if (gate && !*gate) {
+        return;
+    }
+    const double* beta = a.fold.on ? s_beta : a.beta;
     static_assert(K + KP <= kMaxRhs, "partial slots per team");
 #if TM_TS
     const unsigned long long ts0 = __builtin_amdgcn_s_memrealtime();
@@ -304,7 +328,7 @@ __device__ __forceinline__ void atax_team_body(const double* __restrict__ X, int
         double bk[K], dpacc[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            bk[k] = ((a.fuse >> k) & 1) ? a.beta[k] : 0.0;
+            bk[k] = ((a.fuse >> k) & 1) ? beta[k] : 0.0;
             dpacc[k] = 0.0;
         }
         v4u pl[RING];
@@ -464,7 +488,7 @@ __device__ __forceinline__ void atax_team_body(const double* __restrict__ X, int
                 if (jl + h < nrows) {
                     const int64_t j = r0 + jl + h;
                     q = a.ar.p[k][j] / a.diag;
-                    if ((a.fuse >> k) & 1) q = q + a.beta[k] * a.qo.p[k][j];
+                    if ((a.fuse >> k) & 1) q = q + beta[k] * a.qo.p[k][j];
                 }
                 q_lds[k * QS + jl + h] = q;
             }
@@ -472,7 +496,7 @@ __device__ __forceinline__ void atax_team_body(const double* __restrict__ X, int
     }
     double bk[K];
 #pragma unroll
-    for (int k = 0; k < K; ++k) bk[k] = ((a.fuse >> k) & 1) ? a.beta[k] : 0.0;
+    for (int k = 0; k < K; ++k) bk[k] = ((a.fuse >> k) & 1) ? beta[k] : 0.0;
     // per-lane source of the column's scalars: lane 0 mave, 1 msig, 2.. p_k,
     // 2+K.. z_k, 2+2K.. the plain right-hand sides x_kp
     const double* pkp = mave;

@@ -84,6 +84,7 @@ struct vampomi_ctx {
     bool side_open = false;  // the side stream has work st has not joined (DotBatch fork .. flush)
     bool side_on = false;  // default: several ranks; VAMPOMI_SIDE_STREAM=0/1 or vampomi_dev_set_variant(c, 4, 0/1)
     bool mr_tail = true;   // several ranks: the linear iteration's tail without host waits (vamp.cpp); VAMPOMI_MR_TAIL=0
+    bool cg_fold = true;   // several ranks: each CG decision formed by the next operator launch (pcg.cpp); VAMPOMI_CG_FOLD=0
     bool team_reg = false;           // registered with its device's team gate (engine.cpp)
     hipEvent_t team_ev = nullptr;    // recorded on st when another context must order behind it
     ncclComm_t comm = nullptr;
@@ -111,7 +112,7 @@ struct vampomi_ctx {
     unsigned long long* h_flag = nullptr;  // mapped host word the stream stores sync sequence numbers into
     unsigned long long* d_flag = nullptr;
     unsigned long long sync_seq = 0, side_seq = 0;
-    vk::CgState* cgs = nullptr;     // device-side CG control (pcg.cpp)
+    vk::CgState* cgs = nullptr;     // device-side CG control (pcg.cpp), two states (the folded decisions alternate)
     vk::CgMirror* h_cgm = nullptr;  // its mapped host mirror, and the mirror's device address
     vk::CgMirror* d_cgm = nullptr;
     // one-pass CG operator (batch_rhs 4; allocated on first use, pcg.cpp)

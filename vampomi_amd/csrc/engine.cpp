@@ -1235,8 +1235,8 @@ extern "C" vampomi_status vampomi_open(const vampomi_shard_desc* d, vampomi_ctx*
     STCHK(dev_alloc(&c->nbuf, (size_t)vk::kMaxRhs * c->ld));
     HIPCHK(hipMemsetAsync(c->nbuf, 0, (size_t)vk::kMaxRhs * c->ld * 8, c->st));
     STCHK(dev_alloc(&c->mbuf, (size_t)2 * vk::kMaxRhs * Mx));
-    HIPCHK(hipMalloc((void**)&c->cgs, sizeof(vk::CgState)));
-    HIPCHK(hipMemsetAsync(c->cgs, 0, sizeof(vk::CgState), c->st));
+    HIPCHK(hipMalloc((void**)&c->cgs, 2 * sizeof(vk::CgState)));  // [1]: the folded decisions' second state (pcg.cpp)
+    HIPCHK(hipMemsetAsync(c->cgs, 0, 2 * sizeof(vk::CgState), c->st));
     HIPCHK(hipHostMalloc((void**)&c->h_cgm, vk::kCgMirrorSlots * sizeof(vk::CgMirror),
                          hipHostMallocMapped | hipHostMallocCoherent));
     std::memset(c->h_cgm, 0, vk::kCgMirrorSlots * sizeof(vk::CgMirror));
@@ -1253,6 +1253,7 @@ extern "C" vampomi_status vampomi_open(const vampomi_shard_desc* d, vampomi_ctx*
     c->side_on = c->use_comm;
     if (const char* sv = std::getenv("VAMPOMI_SIDE_STREAM")) c->side_on = std::atoi(sv) != 0;
     if (const char* mv = std::getenv("VAMPOMI_MR_TAIL")) c->mr_tail = std::atoi(mv) != 0;
+    if (const char* fv = std::getenv("VAMPOMI_CG_FOLD")) c->cg_fold = std::atoi(fv) != 0;
     if (const char* hv = std::getenv("VAMPOMI_HEADSTART")) c->hs_on = c->hs_on_req = std::atoi(hv) != 0;
     const char* mode = std::getenv("VAMPOMI_COMM");
     if (c->use_comm && mode && std::strcmp(mode, "loopback") == 0) {

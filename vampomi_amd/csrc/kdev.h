@@ -56,15 +56,12 @@ __device__ __forceinline__ void ticket_sum_blocks(const RedOut& ro) {
 }
 
 // one thread: the host loop of vamp::precondCG_solver after each step's sums
-// red[3k..3k+2] = <r,z>, <r,r>, <v,mu> of system k.  s: the state as *cs holds
-// it (read by the caller in one burst); it is written back once (a chain of
-// dependent device loads and stores otherwise: this runs at the end of every
-// CG step).
-// pack: *flag receives the decision as one word (cg_pack), no mirror.
-__device__ inline void cg_decide_from(CgState s, CgState* cs, const double* red, int it, CgMirror* mirror,
-                                      unsigned long long* flag, unsigned long long seq, int mask, int pack = 0) {
+// red[3k..3k+2] = <r,z>, <r,r>, <v,mu> of system k, applied to the state s
+// (in place; nothing if the solve had stopped: s.any == 0).  Returns whether
+// the step ran (s.any on entry).
+__device__ inline bool cg_decide_into(CgState& s, const double* red, int it, int mask) {
     const bool ran = s.any != 0;  // a step queued after the solve stopped decides (and publishes) nothing
-    if (s.any) {
+    if (ran) {
         int any = 0;
 #pragma unroll
         for (int k = 0; k < kMaxRhs; ++k) {
@@ -102,8 +99,14 @@ __device__ inline void cg_decide_from(CgState s, CgState* cs, const double* red,
             any = 1;
         }
         s.any = any;
-        *cs = s;
     }
+    return ran;
+}
+
+// the decided state s to the host: pack: *flag receives the decision as one
+// word (cg_pack), no mirror; else the mirror slot (it & 1) then the flag
+__device__ inline void cg_publish(const CgState& s, bool ran, int it, CgMirror* mirror, unsigned long long* flag,
+                                  unsigned long long seq, int pack) {
     if (pack) {  // one word, one system-scope store: nothing to order
         if (flag && ran)
             __hip_atomic_store(flag, cg_pack(seq, s.any, s.iters[0], s.iters[1]), __ATOMIC_RELAXED,
@@ -125,6 +128,16 @@ __device__ inline void cg_decide_from(CgState s, CgState* cs, const double* red,
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __hip_atomic_store(flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
+}
+
+// s: the state as *cs holds it (read by the caller in one burst); it is
+// written back once (a chain of dependent device loads and stores otherwise:
+// this runs at the end of every CG step), then published
+__device__ inline void cg_decide_from(CgState s, CgState* cs, const double* red, int it, CgMirror* mirror,
+                                      unsigned long long* flag, unsigned long long seq, int mask, int pack = 0) {
+    const bool ran = cg_decide_into(s, red, it, mask);
+    if (ran) *cs = s;
+    cg_publish(s, ran, it, mirror, flag, seq, pack);
 }
 
 __device__ inline void cg_decide_body(CgState* cs, const double* red, int it, CgMirror* mirror, unsigned long long* flag,

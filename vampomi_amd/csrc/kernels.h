@@ -132,6 +132,24 @@ constexpr int kOpDefault = -1;
 bool op_plan(int64_t N, int64_t M, int cus, int variant, OpPlan* out);
 bool op_supported(int64_t N, int K);
 bool team_plan(int64_t N, int64_t M, int cus, int T, int cfg, OpPlan* out);
+struct CgState;
+struct CgMirror;
+// Several ranks (pcg.cpp): the previous CG step's decision (cg_decide on its
+// all-reduced sums red) formed by the operator launch that needs its beta,
+// instead of by a launch of its own between the all-reduce and this one: every
+// workgroup decides from src (the same arithmetic, the same bits), workgroup 0
+// stores the new state to dst (a second state: src is still being read) and
+// publishes it (mirror / flag, as cg_decide); the launch then runs on the new
+// beta, gated on its "any".  on = 0: a.beta and the gate as given
+struct OpFold {
+    const CgState* src = nullptr;
+    CgState* dst = nullptr;
+    const double* red = nullptr;
+    int on = 0, it = 0, mask = 0xf, pack = 0;
+    CgMirror* mirror = nullptr;
+    unsigned long long* flag = nullptr;
+    unsigned long long seq = 0;
+};
 struct OpArgs {
     CPtrs ar, qo;       // q_k = ar_k/diag [+ beta_k*qo_k when fuse] (N-space, replicated)
     CPtrs p, z;         // p_k [= z_k + beta_k*p_k when fuse] (M-space)
@@ -155,6 +173,7 @@ struct OpArgs {
     int dbg;  // timing experiments only (VAMPOMI_OP_DBG; results are wrong when set, except bit 5):
               // bit 0 no poll waits, 1 no publishes, 2 no butterfly, 3 no A d accumulation,
               // 5 write-through hand-off even when the team shares an XCD
+    OpFold fold;  // team kernels only (atax_team.hip)
 };
 std::string op_kernel_name(int K, const OpPlan& pl);
 std::string team_kernel_name(int K, const OpPlan& pl);

@@ -48,14 +48,21 @@ static constexpr int kCgPackWord = 2;
 // its own mirror slot ((i-1) & 1), tagged with its flag value.  Either way
 // step i, queued before the wait, writes the other one.  *last: the last decided step's outcome
 // (its iteration counts are final).
-template <class Enqueue>
-static vampomi_status cg_loop(vampomi_ctx* c, int max_iter, bool packed, Enqueue&& enqueue, CgOutcome* last) {
+// settle (may be null): called instead of enqueue(i) when no step i is
+// queued (i = max_iter), for a decision of step i-1 that step i's launch
+// would have formed (folded decisions)
+template <class Enqueue, class Settle>
+static vampomi_status cg_loop(vampomi_ctx* c, int max_iter, bool packed, Enqueue&& enqueue, CgOutcome* last,
+                              Settle&& settle) {
     unsigned long long prev = 0, cur = 0;
     STCHK(enqueue(0, &prev));
     for (int i = 1;; ++i) {
         const size_t mark = c->pending.size();
         const vampomi_stats before = c->stats;
-        if (i < max_iter) STCHK(enqueue(i, &cur));
+        if (i < max_iter)
+            STCHK(enqueue(i, &cur));
+        else
+            STCHK(settle());
         c->stats.host_syncs++;
         CgOutcome o;
         if (packed) {
@@ -209,6 +216,21 @@ vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double
     const int* gate = field<int>(c->cgs, offsetof(vk::CgState, any));
     const double* beta = field<double>(c->cgs, offsetof(vk::CgState, beta));
     if (op1) {
+        // several ranks, team plans: each step's decision is formed by the next
+        // operator launch (vk::OpFold) from the all-reduced sums, instead of
+        // by a decision launch of its own; the two CgStates alternate (the
+        // launch reads one while its workgroup 0 writes the other).  cur: the
+        // state the next launches use; pend: the decision not yet formed
+        const bool fold = c->use_comm && c->cg_fold && c->opp.T >= 1 && (!head || c->opp_hs.T >= 1);
+        int cur = 0;
+        struct Pending {
+            bool on = false;
+            int it = 0, mask = 0xf, pack = 0;
+            vk::CgMirror* mirror = nullptr;
+            unsigned long long* flag = nullptr;
+            unsigned long long seq = 0;
+        } pend;
+        auto state = [&](int s) { return c->cgs + s; };
         // ---- one pass over X per CG step (vk::atax) ----
         // A r0 for every system (and A extra_x) by one A.x pass; then each step
         // forms q = A p = A r/diag + beta*q_old on the fly, streams X once for
@@ -323,7 +345,13 @@ vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double
             HIPCHK(vk::cg_update(1, M, ch, diag, c->cgs, dp, nullptr, 0, ro, dc, c->st));
             if (c->use_comm) {
                 STCHK(allreduce_dev(c, c->scal + SL_CG, 3));
-                HIPCHK(vk::cg_decide(c->cgs, c->scal + SL_CG, -1, nullptr, nullptr, 0, c->st, 1));
+                if (fold) {  // formed by step 0's operator launch
+                    pend.on = true;
+                    pend.it = -1;
+                    pend.mask = 1;
+                } else {
+                    HIPCHK(vk::cg_decide(c->cgs, c->scal + SL_CG, -1, nullptr, nullptr, 0, c->st, 1));
+                }
             }
             hs->used = true;
         }
@@ -343,14 +371,35 @@ vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double
                 a.d.p[k] = sys[k]->d;
                 a.sraw.p[k] = rec ? sys[k]->S : nullptr;
             }
-            a.beta = beta;
+            a.beta = fold ? nullptr : beta;
             a.fuse = fuse;
             a.diag = diag;
             a.tau = tau;
             a.gam2 = gam2;
-            STCHK(op_dev(c, K, a, gate, c->use_comm, false));
+            const int* g = gate;
+            vk::CgState* cs = c->cgs;
+            if (fold) {
+                if (pend.on) {  // the previous step's decision, formed by this launch into the other state
+                    a.fold.on = 1;
+                    a.fold.src = state(cur);
+                    a.fold.dst = state(cur ^ 1);
+                    a.fold.red = c->scal + SL_CG;
+                    a.fold.it = pend.it;
+                    a.fold.mask = pend.mask;
+                    a.fold.pack = pend.pack;
+                    a.fold.mirror = pend.mirror;
+                    a.fold.flag = pend.flag;
+                    a.fold.seq = pend.seq;
+                    cur ^= 1;
+                    pend.on = false;
+                }
+                cs = state(cur);
+                g = field<int>(cs, offsetof(vk::CgState, any));
+                if (!a.fold.on) a.beta = field<double>(cs, offsetof(vk::CgState, beta));
+            }
+            STCHK(op_dev(c, K, a, g, c->use_comm, false));
             const double* dp = c->use_comm ? AD + (int64_t)K * c->ld : c->scal + SL_DP;
-            const vk::RedOut ro{c->red_part, c->scal + SL_CG, c->ticket, nullptr, 0, gate};
+            const vk::RedOut ro{c->red_part, c->scal + SL_CG, c->ticket, nullptr, 0, g};
             *seq = ++c->sync_seq;
             unsigned long long* flag = packed ? c->d_flag + kCgPackWord + (i & 1) : c->d_flag;
             vk::CgMirror* mirror = packed ? nullptr : c->d_cgm;
@@ -363,15 +412,33 @@ vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double
                 dc.seq = *seq;
                 dc.pack = packed ? 1 : 0;
             }
-            HIPCHK(vk::cg_update(K, M, cu, diag, c->cgs, dp, nullptr, fuse, ro, dc, c->st));
+            HIPCHK(vk::cg_update(K, M, cu, diag, cs, dp, nullptr, fuse, ro, dc, c->st));
             if (c->use_comm) {
                 STCHK(allreduce_dev(c, c->scal + SL_CG, (size_t)(3 * K)));
-                HIPCHK(vk::cg_decide(c->cgs, c->scal + SL_CG, i, mirror, flag, *seq, c->st, 0xf, packed ? 1 : 0));
+                if (fold) {  // formed by the next step's operator launch (or settle)
+                    pend.on = true;
+                    pend.it = i;
+                    pend.mask = 0xf;
+                    pend.pack = packed ? 1 : 0;
+                    pend.mirror = mirror;
+                    pend.flag = flag;
+                    pend.seq = *seq;
+                } else {
+                    HIPCHK(vk::cg_decide(c->cgs, c->scal + SL_CG, i, mirror, flag, *seq, c->st, 0xf, packed ? 1 : 0));
+                }
             }
             return VAMPOMI_OK;
         };
+        // the last step's decision when no step follows to form it
+        auto settle = [&]() -> vampomi_status {
+            if (!pend.on) return VAMPOMI_OK;
+            HIPCHK(vk::cg_decide(state(cur), c->scal + SL_CG, pend.it, pend.mirror, pend.flag, pend.seq, c->st,
+                                 pend.mask, pend.pack));
+            pend.on = false;
+            return VAMPOMI_OK;
+        };
         CgOutcome last;
-        STCHK(cg_loop(c, max_iter, packed, enqueue, &last));
+        STCHK(cg_loop(c, max_iter, packed, enqueue, &last, settle));
         STCHK(op_check_err(c));
         for (int k = 0; k < K; ++k) {
             sys[k]->iters = last.iters[k];
@@ -482,7 +549,7 @@ vampomi_status pcg_run(vampomi_ctx* c, const std::vector<CgSystem*>& sys, double
         return VAMPOMI_OK;
     };
     CgOutcome last;
-    STCHK(cg_loop(c, max_iter, false, enqueue, &last));
+    STCHK(cg_loop(c, max_iter, false, enqueue, &last, [] { return VAMPOMI_OK; }));
     for (int k = 0; k < K; ++k) {
         sys[k]->iters = last.iters[k];
         if (ref_passes) *ref_passes += 2 * (int64_t)sys[k]->iters;
