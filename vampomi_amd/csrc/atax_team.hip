@@ -62,6 +62,7 @@ typedef unsigned int v2u __attribute__((ext_vector_type(2)));
 #define TM_DBG 0  // 1: honour OpArgs.dbg (timing experiments); 0: its branches compile out
 #endif
 static constexpr int kTmThreads = 512;        // 8 waves, 2 per SIMD: <= 256 VGPRs per lane
+static constexpr int kTmLdsHead = 4;          // dynamic LDS words before q: the folded decision (team_plan's +4)
 static constexpr int kTmMaxT = 32;            // members per team (one XCD under round-robin dealing)
 static constexpr unsigned kTmMaxSpins = 1u << 21;  // ~2 s of polling, then the launch gives up (err)
 
@@ -216,11 +217,15 @@ __device__ __forceinline__ void atax_team_body(const double* __restrict__ X, int
                                                const double* __restrict__ mave, const double* __restrict__ msig,
                                                const OpArgs& a, int T, int TR, int ilv,
                                                const int* __restrict__ gate) {
+    // the dynamic LDS: kTmLdsHead words for the folded decision (beta_k, go),
+    // then q and the partials.  (No static __shared__ in this kernel: its
+    // launches set the dynamic limit to the whole 160 KiB.)
+    extern __shared__ __attribute__((aligned(16))) double lds[];
     // beta_k of the fused direction updates: from the previous step's decision
     // when this launch forms it (OpArgs.fold), else a.beta
-    __shared__ double s_beta[kOpMaxK];
+    double* s_beta = lds;
     if (a.fold.on) {
-        __shared__ int s_go;
+        double& s_go = lds[kOpMaxK];
         if (threadIdx.x == 0) {
             CgState cs = *a.fold.src;
             double r[3 * kMaxRhs];
@@ -231,12 +236,12 @@ __device__ __forceinline__ void atax_team_body(const double* __restrict__ X, int
                 *a.fold.dst = cs;
                 cg_publish(cs, ran, a.fold.it, a.fold.mirror, a.fold.flag, a.fold.seq, a.fold.pack);
             }
-            s_go = cs.any;
+            s_go = cs.any ? 1.0 : 0.0;
 #pragma unroll
             for (int k = 0; k < kOpMaxK; ++k) s_beta[k] = cs.beta[k];
         }
         __syncthreads();
-        if (!s_go) return;
+        if (s_go == 0.0) return;
     } else if (gate && !*gate) {
         return;
     }
@@ -257,7 +262,6 @@ __device__ __forceinline__ void atax_team_body(const double* __restrict__ X, int
     static_assert(COMM || L == 0, "without a hand-off the column is finished in its own step");
     static_assert(!COMM || (P >= 1 && P <= L), "polls in flight");
     static_assert(!COMM || P < RING, "a poll's slot is consumed before it is reissued");
-    extern __shared__ __attribute__((aligned(16))) double lds[];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int g = blockIdx.x >> 3;
     const int member = g % T;
@@ -282,7 +286,7 @@ __device__ __forceinline__ void atax_team_body(const double* __restrict__ X, int
     const int nrows = (int)(N - r0 < TR ? N - r0 : TR);  // >= 1 (op_plan)
     constexpr bool QFULL = tm_qfull(K, S, COMM, E);
     const int QS = (int)tm_qstride(K, S, COMM, E, TR < N ? TR : N);  // q stride
-    double* q_lds = lds;                                  // K x QS
+    double* q_lds = lds + kTmLdsHead;                     // K x QS
     double* s_part = lds + K * QS;                        // [2][CW][K] wave partials of a column's dot
     double* s_tot = s_part + 2 * CW * K;                  // [2][K] team totals (hand-off)
     const int jb = 64 * E * wave + E * lane;              // row of this lane in step s: RS*s + jb
@@ -787,7 +791,7 @@ bool team_plan(int64_t N, int64_t M, int cus, int T, int cfg, OpPlan* out) {
     const int S = tm_S(TR, c.comm, c.E);
     if (S > c.maxS) return false;
     const int64_t QS = tm_qstride(kOpMaxK, S, c.comm, c.E, std::min<int64_t>(TR, N));
-    const int64_t lds = (QS * kOpMaxK + 2 * 8 * kOpMaxK + 2 * kOpMaxK + 4) * 8;
+    const int64_t lds = (QS * kOpMaxK + 2 * 8 * kOpMaxK + 2 * kOpMaxK + kTmLdsHead) * 8;
     if (lds > 160 * 1024) return false;
     OpPlan p{};
     p.grid = grid;
@@ -817,11 +821,14 @@ static void launch_tm(const Shard& s, const OpPlan& pl, const OpArgs& a, hipStre
     else
         kern = atax_team_kernel<K, S, c.F, c.L, c.P, c.comm, c.E, (bool)TM_FMA>;
     const int64_t QS = tm_qstride(K, S, c.comm, c.E, std::min<int64_t>(pl.TR, s.N));
-    const size_t lds = (size_t)(K * QS + 2 * CW * K + 2 * K) * sizeof(double);
+    const size_t lds = (size_t)(kTmLdsHead + K * QS + 2 * CW * K + 2 * K) * sizeof(double);
     static std::once_flag once;  // more than 64 KiB of dynamic LDS must be allowed explicitly
     std::call_once(once, [&] {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  160 * 1024);
+        // (a failure must not linger as the thread's last error: the next
+        // launch checked with hipGetLastError would report it as its own)
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                160 * 1024) != hipSuccess)
+            (void)hipGetLastError();
     });
     if (occ) {
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, kern, kTmThreads, lds) != hipSuccess) *occ = 0;
