@@ -287,7 +287,7 @@ __device__ __forceinline__ void atax_team_body(const double* __restrict__ X, int
     constexpr bool QFULL = tm_qfull(K, S, COMM, E);
     const int QS = (int)tm_qstride(K, S, COMM, E, TR < N ? TR : N);  // q stride
     double* q_lds = lds + kTmLdsHead;                     // K x QS
-    double* s_part = lds + K * QS;                        // [2][CW][K] wave partials of a column's dot
+    double* s_part = q_lds + K * QS;                      // [2][CW][K] wave partials of a column's dot
     double* s_tot = s_part + 2 * CW * K;                  // [2][K] team totals (hand-off)
     const int jb = 64 * E * wave + E * lane;              // row of this lane in step s: RS*s + jb
     // the tile of a column (E = 2: + the zero pad row for odd N)
