@@ -261,7 +261,8 @@ vampomi_status vampomi_test_metrics(vampomi_ctx* ctx, const double* est, double*
 /* ---- measurement ---- */
 typedef struct {
     int64_t launches;             /* kernel launches of this class that did work (exact) */
-    double ms_total;              /* their device time: ms_timed / timed x launches */
+    double ms_total;              /* their device time: ms_timed / timed x launches (per K; a
+                                     class's is the sum over its K) */
     double bytes_total;           /* algorithmic HBM bytes of those launches */
     double flops_total;
     int64_t timed;                /* launches timed with HIP events (vampomi_set_timing) */
@@ -286,8 +287,9 @@ typedef struct {
 
 /* HIP-event timing of the A/A^T kernels: on = 0 off, 1 every launch, n > 1 one
  * launch in n of each (kernel class, K) (each timed launch carries an event
- * pair in its dispatch, a few microseconds).  Launch counts and bytes in the
- * stats are always exact; ms_total extrapolates the timed average to them. */
+ * pair in its dispatch, a few microseconds; the first launch of each (class, K)
+ * after a reset is always timed).  Launch counts and bytes in the stats are
+ * always exact; ms_total extrapolates the timed average to them. */
 vampomi_status vampomi_set_timing(vampomi_ctx* ctx, int on);
 vampomi_status vampomi_get_stats(vampomi_ctx* ctx, vampomi_stats* out);
 vampomi_status vampomi_reset_stats(vampomi_ctx* ctx);

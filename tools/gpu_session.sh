@@ -22,6 +22,7 @@
 #                2-rank launcher on a 1-GPU box (one failure line, rc != 0)
 #   rccl         the 1-rank RCCL path against the direct one (rates, timing on/off, traces compared)
 #   ceiling      the HBM read ceiling of this box (tools/hbm_ceiling, 4 GB and 50 GB buffers)
+#   c4           the probit shard's line and its per-iteration kernel trace
 #   bases        rank 0's 1-GPU bases (tools/one_gpu_bases.py)
 #   final        smoke, the default C2 line (both CPU legs), its kernel stats
 #                and PMC traffic; the same for C3; C4 and C5 lines
@@ -136,6 +137,12 @@ for s in "$@"; do
     ceiling)     # the HBM read ceiling (tools/hbm_ceiling: every byte of a 4 GB / 50 GB buffer read once)
         step ceiling_4 200 tools/hbm_ceiling 4 15
         step ceiling_50 300 tools/hbm_ceiling 50 5 ;;
+    c4)          # the probit shard: its line, and a kernel trace of 10 iterations (A passes against the rest)
+        step bench_c4 400 python bench.py --config c4 --steps 6 --warmup 2 --no-cpu-baseline
+        step trace_c4 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_c4" -o run --output-format csv -- \
+            python bench.py --config c4 --steps 10 --warmup 2 --no-cpu-baseline --no-timing
+        python tools/trace_cmp.py "$(find "$OUT/prof_c4" -name 'run_kernel_trace.csv' | head -1)" --skip 2 \
+            --mark probit_denoise_kernel | tee "$OUT/trace_c4.txt" ;;
     bases)
         step bases 200 python tools/one_gpu_bases.py ;;
     final)

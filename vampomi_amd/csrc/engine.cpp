@@ -120,7 +120,12 @@ TimedLaunch launch_stat(vampomi_ctx* c, int cls, int K, double bytes, double flo
     // own (no dispatch packet to carry them), each a few us of idle queue:
     // sampled 8x more sparsely (the 1-rank RCCL line lost 1 % to them, r05c)
     const uint64_t period = (uint64_t)std::max(c->tperiod, 1) * (cls == 4 ? 8 : 1);
-    if (period > 1 && h % period != 0) return t;
+    // the first launch of each (class, K) since the stats were reset is always
+    // sampled: a (class, K) with launches and no sample would count its bytes
+    // and no time (c4's one K = 4 A.x pass per iteration, r05j)
+    const vampomi_kernel_stat* xk = stat_k_of(c, cls, K);
+    const bool first = (xk ? xk : stat_of(c, cls))->launches == 1;
+    if (period > 1 && h % period != 0 && !first) return t;
     t.a = ev_get(c);
     t.b = ev_get(c);
     t.cls = cls;
@@ -1781,9 +1786,23 @@ extern "C" vampomi_status vampomi_get_stats(vampomi_ctx* c, vampomi_stats* out) 
     auto fill = [](vampomi_kernel_stat& x) {
         x.ms_total = x.timed > 0 ? x.ms_timed / (double)x.timed * (double)x.launches : 0.0;
     };
-    for (vampomi_kernel_stat* x : {&out->ax, &out->atx, &out->loo, &out->op, &out->coll}) fill(*x);
+    for (vampomi_kernel_stat* x : {&out->loo, &out->coll}) fill(*x);
+    // a class's time is the sum of its per-K estimates (launches of different K
+    // take different times: one average over the mix would weigh them by where
+    // the samples fell)
     for (int k = 0; k < 4; ++k)
         for (vampomi_kernel_stat* x : {&out->ax_k[k], &out->atx_k[k], &out->op_k[k]}) fill(*x);
+    for (auto pr : {std::make_pair(&out->ax, out->ax_k), std::make_pair(&out->atx, out->atx_k),
+                    std::make_pair(&out->op, out->op_k)}) {
+        int64_t n = 0;
+        double ms = 0.0;
+        for (int k = 0; k < 4; ++k) {
+            n += pr.second[k].launches;
+            ms += pr.second[k].ms_total;
+        }
+        if (n == pr.first->launches) pr.first->ms_total = ms;
+        else fill(*pr.first);
+    }
     return VAMPOMI_OK;
 }
 
