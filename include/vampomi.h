@@ -236,6 +236,14 @@ vampomi_status vampomi_infere(vampomi_ctx* ctx, const vampomi_params* p, vampomi
 vampomi_status vampomi_vamp_begin(vampomi_ctx* ctx, const vampomi_params* p, vampomi_result* r);
 vampomi_status vampomi_vamp_step(vampomi_ctx* ctx, int* stopped);
 vampomi_status vampomi_vamp_end(vampomi_ctx* ctx);
+/* the last step's phase times as the host sees them (rank-local wall clock),
+ * replacing the reference's per-iteration stopwatches "CG took" / "onsager
+ * took" (src/vamp.cpp:313-316, :326-333; one interval here: both solves share
+ * every pass) and "Total iteration time" (:396-401): *solve_s from the start
+ * of the step's CG solves to their stop (the linear model queues their start
+ * at the end of the previous step, so the device begins a little earlier),
+ * *step_s the whole vampomi_vamp_step.  Either pointer may be NULL. */
+vampomi_status vampomi_step_phases(vampomi_ctx* ctx, double* solve_s, double* step_s);
 
 /* ---- association tests (--run-mode association_test) ----
  * loo: src/main_meth.cpp:245-264 + data::pvals_loo src/data.cpp:385-417.

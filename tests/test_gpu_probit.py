@@ -141,6 +141,41 @@ def test_probit_batched_bitwise_equal_to_sequential():
     assert a["a_passes_ref"] == 1 + sum(4 + 2 * (k1 + k2) for k1, k2 in zip(a["cg_iters"], a["ons_iters"]))
 
 
+def test_probit_every_pass_class_timed():
+    """Sampled event timing (one launch in 4 of each kernel class and K) times
+    the first launch of every (class, K) after a reset, so a class launched once
+    per iteration (the probit iteration's K = 4 A.x pass) has time beside its
+    bytes, and a class's time is the sum over its K (engine.cpp launch_stat,
+    vampomi_get_stats); and the step phases (vampomi_step_phases) bracket."""
+    N, Mt = 1000, 2000
+    X, y, beta = _binary_problem(N, Mt)
+    with va.Data(N, Mt) as d:
+        d.load_meth(X)
+        d.set_phen(y, standardize=False)
+        v = va.Vamp(d, va.VampOptions(model="bin_class", max_iter=6, stop_criteria_thr=0.0), true_signal=beta)
+        v.begin()
+        v.step()
+        v.step()
+        d.set_timing(True, period=4)
+        d.reset_stats()
+        for _ in range(3):
+            v.step()
+            solve, step = v.step_phases()
+            assert 0 < solve <= step
+        st = d.stats()
+        v.end()
+    assert st.ax.launches >= 3  # one A.x pass per iteration (+ its right-hand sides)
+    for cls in ("ax", "atx", "op"):
+        per_k = getattr(st, cls + "_k")
+        for k in range(4):
+            if per_k[k].launches:
+                assert per_k[k].timed >= 1, (cls, k + 1)
+        total = sum(per_k[k].ms_total for k in range(4))
+        assert abs(getattr(st, cls).ms_total - total) <= 1e-9 * max(1.0, total), cls
+        if getattr(st, cls).launches:
+            assert getattr(st, cls).ms_total > 0, cls
+
+
 def test_cli_bin_class_files(tmp_path):
     N, Mt, its = 400, 900, 6
     X, y, beta = _binary_problem(N, Mt)

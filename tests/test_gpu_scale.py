@@ -194,6 +194,10 @@ def test_cli_on_reference_written_files(tmp_path):
     so_far = [float(t) for t in re.findall(r"Total computation time so far = ([0-9.eE+-]+)", r.stdout)]
     assert len(times) == its and len(so_far) == its and all(t > 0 for t in times)
     assert np.allclose(np.cumsum(times), so_far, rtol=1e-4)
+    # and the solves' share of it ("CG took", "onsager took", src/vamp.cpp:313-316, :326-333)
+    solves = [float(t) for t in re.findall(r"CG and onsager \(one pass over the markers per step for both\) took "
+                                           r"([0-9.eE+-]+) seconds", r.stdout)]
+    assert len(solves) == its and all(0 < s <= t for s, t in zip(solves, times))
     for q, k in enumerate(z["keep_its"]):
         x1 = np.fromfile(tmp_path / f"g_it_{k}.bin", dtype="<f8")
         r1 = np.fromfile(tmp_path / f"g_r1_it_{k}.bin", dtype="<f8")

@@ -415,6 +415,13 @@ class Vamp:
         check(load().vampomi_vamp_step(self.data.ctx, C.byref(s)))
         return bool(s.value)
 
+    def step_phases(self):
+        """The last step's (solves, whole step) seconds as the host sees them
+        (vampomi_step_phases; the reference's "CG took" / "Total iteration time")."""
+        a, b = C.c_double(), C.c_double()
+        check(load().vampomi_step_phases(self.data.ctx, C.byref(a), C.byref(b)))
+        return a.value, b.value
+
     def end(self) -> np.ndarray:
         check(load().vampomi_vamp_end(self.data.ctx))
         self._active = False

@@ -130,6 +130,7 @@ SIGNATURES = {
     "vampomi_infere": (C.c_int, [_P, C.POINTER(Params), C.POINTER(Result)]),
     "vampomi_vamp_begin": (C.c_int, [_P, C.POINTER(Params), C.POINTER(Result)]),
     "vampomi_vamp_step": (C.c_int, [_P, C.POINTER(C.c_int)]),
+    "vampomi_step_phases": (C.c_int, [_P, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     "vampomi_vamp_end": (C.c_int, [_P]),
     "vampomi_set_timing": (C.c_int, [_P, C.c_int]),
     "vampomi_get_stats": (C.c_int, [_P, C.POINTER(Stats)]),

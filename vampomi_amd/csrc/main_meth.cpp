@@ -279,9 +279,12 @@ int main(int argc, char** argv) {
         const double it_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - ts0).count();
         total += it_s;
         const int it = r.iterations_run;
+        double solve_s = 0.0;
+        if (vampomi_step_phases(ctx, &solve_s, nullptr) != VAMPOMI_OK) return die("inference");
         if (rank == 0 && it >= 1)
             std::cout << "it " << it << ": CG iterations " << cg[it - 1] << ", onsager CG iterations " << ons[it - 1]
-                      << "\nTotal iteration time = " << it_s << "\nTotal computation time so far = " << total
+                      << "\nCG and onsager (one pass over the markers per step for both) took " << solve_s
+                      << " seconds.\nTotal iteration time = " << it_s << "\nTotal computation time so far = " << total
                       << std::endl;
     }
     if (vampomi_vamp_end(ctx) != VAMPOMI_OK) return die("inference");

@@ -16,6 +16,7 @@
 // true_g = A.(true_signal*sqrtN) (:46) is never read; it is counted in
 // a_passes_ref and not computed.
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -180,6 +181,7 @@ vampomi_status probit_step(vampomi_ctx* c, VampRun& R) {
     const size_t Mb = (size_t)std::max<int64_t>(M, 1) * 8;
     HIPCHK(hipMemsetAsync(R.x2, 0, Mb, c->st));
     HIPCHK(hipMemsetAsync(R.invQ, 0, Mb, c->st));
+    const auto t_solve = std::chrono::steady_clock::now();
     if (R.fuse) {
         STCHK(pcg_run(c, {&sx, &so}, R.tau2, R.gam2, R.prm.CG_max_iter, R.prm.CG_err_tol, R.nsc, &R.passes_ref,
                       nullptr, nullptr, nullptr, R.onepass, merged ? ar0 : nullptr));
@@ -187,6 +189,7 @@ vampomi_status probit_step(vampomi_ctx* c, VampRun& R) {
         STCHK(pcg_run(c, {&sx}, R.tau2, R.gam2, R.prm.CG_max_iter, R.prm.CG_err_tol, R.nsc, &R.passes_ref, nullptr));
         STCHK(pcg_run(c, {&so}, R.tau2, R.gam2, R.prm.CG_max_iter, R.prm.CG_err_tol, R.nsc, &R.passes_ref, nullptr));
     }
+    R.ph_solve_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_solve).count();
     if (res && res->cg_iters) res->cg_iters[it - 1] = sx.iters;
     if (res && res->ons_iters) res->ons_iters[it - 1] = so.iters;
     double xc2[3] = {};

@@ -85,6 +85,11 @@ struct VampRun {
     double* x1sn = nullptr; // M: next iteration's x1_hat / sqrt(N)
     double* x2s = nullptr;  // M: x2_hat / sqrt(N)
     double* prior_row = nullptr;  // host staging, unused by the linear model
+    // the last step's phases as the host sees them (vampomi_step_phases): the
+    // solves (entering pcg_run to its return: the device's CG and Onsager
+    // steps, with the linear model's start queued ahead running a little
+    // earlier) and the whole step
+    double ph_solve_s = 0, ph_step_s = 0;
 
     ~VampRun();
 };

@@ -37,6 +37,7 @@
 // same scalars and mixture from the same sums, and checks the device's bit
 // for bit after the next solves (check_device_values).
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -551,8 +552,10 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
         return VAMPOMI_OK;
     }
     HIPCHK(hipSetDevice(c->device));
+    const auto t_step = std::chrono::steady_clock::now();
     if (R.probit) {
         STCHK(probit_step(c, R));
+        R.ph_step_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_step).count();
         if (c->timing) resolve_timing(c);
         if (stopped) *stopped = R.stopped ? 1 : 0;
         return VAMPOMI_OK;
@@ -615,6 +618,7 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
     if (pm == PreMode::queued && !(L.pre_in_cg && R.fuse && hs_av))
         return fail(VAMPOMI_ERR_STATE, "vamp: the start queued ahead does not match this iteration's schedule");
     if (!L.pre_in_cg) HIPCHK(vk::prelude(M, pr, c->st));
+    const auto t_solve = std::chrono::steady_clock::now();
     if (R.fuse && hs_av) {
         STCHK(pcg_run(c, {&so, &sx}, R.gamw, R.gam2, R.prm.CG_max_iter, R.prm.CG_err_tol, R.nsc, &R.passes_ref,
                       nullptr, R.x1, R.z1buf, true, nullptr, &hs, &pr, pm));
@@ -628,6 +632,7 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
         STCHK(pcg_run(c, {&sx}, R.gamw, R.gam2, R.prm.CG_max_iter, R.prm.CG_err_tol, R.nsc, &R.passes_ref, &e1));
         STCHK(pcg_run(c, {&so}, R.gamw, R.gam2, R.prm.CG_max_iter, R.prm.CG_err_tol, R.nsc, &R.passes_ref, nullptr));
     }
+    R.ph_solve_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_solve).count();
     STCHK(check_device_values(c, R, it));  // (the solves' flags came after the previous iteration's launches)
     if (res && res->cg_iters) res->cg_iters[it - 1] = sx.iters;
     if (res && res->ons_iters) res->ons_iters[it - 1] = so.iters;
@@ -882,6 +887,14 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
     }
     if (c->timing) resolve_timing(c);
     if (stopped) *stopped = R.stopped ? 1 : 0;
+    R.ph_step_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_step).count();
+    return VAMPOMI_OK;
+}
+
+extern "C" vampomi_status vampomi_step_phases(vampomi_ctx* c, double* solve_s, double* step_s) {
+    if (!c || !c->run) return fail(VAMPOMI_ERR_STATE, "vampomi_vamp_begin not called");
+    if (solve_s) *solve_s = c->run->ph_solve_s;
+    if (step_s) *step_s = c->run->ph_step_s;
     return VAMPOMI_OK;
 }
 
