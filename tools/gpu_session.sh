@@ -9,7 +9,7 @@
 #   fullshard    the whole-shard oracle tests alone (C3, C4, C5)
 #   tests        the GPU tests named in $TESTS (pytest arguments; $TESTK: a -k expression)
 #   rehearse     bench.py's n > 1 flow with 8 loopback rank threads on this GPU
-#   bitwise      12 VAMP iterations (linear and probit) on this build and on
+#   bitwise      12 VAMP iterations (linear and probit; N x Mt = $BWN x $BWM, default 10000 x 20000) on this build and on
 #                $OLD (default build_ab/, make -C vampomi_amd/csrc OBJDIR=../../build_ab/obj LIBDIR=../../build_ab/lib BINDIR=../../build_ab/bin at the base commit), compared bit for bit
 #   ab           C2 lines alternating this build and $OLD, $ROUNDS rounds
 #   envab        C2 lines alternating the settings in $ENVAB ("A=1;A=2;...")
@@ -72,8 +72,9 @@ for s in "$@"; do
         step rehearse 400 python bench.py --rehearse 8 --steps 3 --warmup 1 --deadline-s 380 ;;
     bitwise)
         for m in linear bin_class; do
-            step bw_new_$m 200 python tools/lib_bitwise.py run "$OUT/new_$m.npz" 10000 20000 12 $m
-            step bw_old_$m 200 env VAMPOMI_LIB="$OLD" python tools/lib_bitwise.py run "$OUT/old_$m.npz" 10000 20000 12 $m
+            step bw_new_$m 200 python tools/lib_bitwise.py run "$OUT/new_$m.npz" "${BWN:-10000}" "${BWM:-20000}" 12 $m
+            step bw_old_$m 200 env VAMPOMI_LIB="$OLD" python tools/lib_bitwise.py run "$OUT/old_$m.npz" \
+                "${BWN:-10000}" "${BWM:-20000}" 12 $m
             python tools/lib_bitwise.py cmp "$OUT/new_$m.npz" "$OUT/old_$m.npz" | tee -a "$OUT/bitwise.txt"
         done ;;
     ab)

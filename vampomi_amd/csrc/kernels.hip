@@ -1080,17 +1080,21 @@ hipError_t atax(const Shard& s, const OpPlan& pl, int K, const OpArgs& a, hipStr
 // c.adpart) sums in exactly this order, so the two paths agree bit for bit.
 // (Every load of a round is issued before the first add: the adds stay in
 // slot order, so the round size changes the latency, not the bits.)
+// W: the largest round (32: 128 VGPRs of loads in flight; 8 for the few slots
+// of the large-N plans, so that cg_update's workgroups are not held to one per
+// CU by a round they never run)
+template <int W = 32>
 __device__ __forceinline__ v2d slot_sum(const double* src, int64_t ss, int t0, int t1) {
     v2d acc = {0.0, 0.0};
     int t = t0;
-    for (; t + 32 <= t1; t += 32) {  // (C2, team of 2: 128 slots, 32 per wave, one round trip)
+    for (; W >= 32 && t + 32 <= t1; t += 32) {  // (C2, team of 2: 128 slots, 32 per wave, one round trip)
         v2d x[32];
 #pragma unroll
         for (int u = 0; u < 32; ++u) x[u] = *reinterpret_cast<const v2d*>(src + (t + u) * ss);
 #pragma unroll
         for (int u = 0; u < 32; ++u) acc += x[u];
     }
-    for (; t + 16 <= t1; t += 16) {
+    for (; W >= 16 && t + 16 <= t1; t += 16) {
         v2d x[16];
 #pragma unroll
         for (int u = 0; u < 16; ++u) x[u] = *reinterpret_cast<const v2d*>(src + (t + u) * ss);
@@ -1945,7 +1949,7 @@ __global__ void cg_decide_kernel(CgState* cs, const double* __restrict__ red, in
 // K systems, not kMaxRhs (at K = 2: a quarter of the live registers, no
 // spills, and only the K systems' vector pointers loaded from the arguments);
 // every per-element operation and every sum is the same, in the same order.
-template <int K>
+template <int K, int W>
 __global__ __launch_bounds__(kBlock) void cg_update_kernel(int64_t M, CgVecs c, double diag,
                                                            CgState* cs, const double* __restrict__ dp_dev,
                                                            const double* __restrict__ pp_dev, int fuse, RedOut ro,
@@ -2064,8 +2068,8 @@ __global__ __launch_bounds__(kBlock) void cg_update_kernel(int64_t M, CgVecs c, 
                 if (fuk) qov = *reinterpret_cast<const v2d*>(c.Q[k] + i);
                 if (c.AW[k]) awv = *reinterpret_cast<const v2d*>(c.AW[k] + i);
             }
-            wsum[w][lane] = ok ? slot_sum(c.adpart + (int64_t)k * c.adld + i, (int64_t)kMaxRhs * c.adld, w * ns / 4,
-                                          (w + 1) * ns / 4)
+            wsum[w][lane] = ok ? slot_sum<W>(c.adpart + (int64_t)k * c.adld + i, (int64_t)kMaxRhs * c.adld,
+                                             w * ns / 4, (w + 1) * ns / 4)
                                : v2d{0.0, 0.0};
             __syncthreads();
             if (upd) {
@@ -2139,17 +2143,26 @@ hipError_t cg_update(int K, int64_t M, const CgVecs& c, double diag, CgState* cs
         nb = (int)std::min<int64_t>(K * cdiv(c.nA, 128), kRedBlocks - mb);
         nb = std::max(nb, 1);
     }
+    // the 32-load slot rounds only where a wave sums >= 32 slots (C2's team of
+    // 2); else rounds of <= 8 loads and the registers of more workgroups per CU
+    const bool wide = c.adpart && c.adslots >= 4 * 32;
+#define VAMPOMI_CGU(KK)                                                                                          \
+    case KK:                                                                                                     \
+        if (wide)                                                                                                \
+            hipLaunchKernelGGL((cg_update_kernel<KK, 32>), dim3(mb + nb), dim3(kBlock), 0, st, M, c, diag, cs,   \
+                               dp_dev, pp_dev, fuse, ro, dc, mb);                                                \
+        else                                                                                                     \
+            hipLaunchKernelGGL((cg_update_kernel<KK, 8>), dim3(mb + nb), dim3(kBlock), 0, st, M, c, diag, cs,    \
+                               dp_dev, pp_dev, fuse, ro, dc, mb);                                                \
+        break;
     switch (K) {
-        case 1: hipLaunchKernelGGL(cg_update_kernel<1>, dim3(mb + nb), dim3(kBlock), 0, st, M, c, diag, cs, dp_dev,
-                                   pp_dev, fuse, ro, dc, mb); break;
-        case 2: hipLaunchKernelGGL(cg_update_kernel<2>, dim3(mb + nb), dim3(kBlock), 0, st, M, c, diag, cs, dp_dev,
-                                   pp_dev, fuse, ro, dc, mb); break;
-        case 3: hipLaunchKernelGGL(cg_update_kernel<3>, dim3(mb + nb), dim3(kBlock), 0, st, M, c, diag, cs, dp_dev,
-                                   pp_dev, fuse, ro, dc, mb); break;
-        case 4: hipLaunchKernelGGL(cg_update_kernel<4>, dim3(mb + nb), dim3(kBlock), 0, st, M, c, diag, cs, dp_dev,
-                                   pp_dev, fuse, ro, dc, mb); break;
+        VAMPOMI_CGU(1)
+        VAMPOMI_CGU(2)
+        VAMPOMI_CGU(3)
+        VAMPOMI_CGU(4)
         default: return hipErrorInvalidValue;
     }
+#undef VAMPOMI_CGU
     return hipGetLastError();
 }
 
