@@ -144,3 +144,27 @@ def test_team_launches_from_two_contexts_on_one_gpu():
         assert relerr(gd, ref[0]) < 1e-12 and relerr(gad, ref[1]) < 1e-12
         assert np.array_equal(gd, outs[0][0]) and np.array_equal(gad, outs[0][1])
 
+
+
+@pytest.mark.parametrize("N,Mt", [(20000, 2000), (50001, 300), (100000, 600), (50001, 7), (33000, 1000)])
+def test_ax_team_plan_vs_numpy(N, Mt):
+    """data::Ax (src/data.cpp:340-373) on the team plan (ax_team_kernel, the
+    default above ~16k samples) against numpy on the explicit matrix and
+    against the tile plan (variant 0): odd N (the zero pad row), fewer markers
+    than teams (empty teams write zero slots), every team size the plan picks;
+    bitwise repeatable."""
+    X = O.generate_markers(7, 1, N, 0, Mt)
+    mave, msig = O.marker_stats(X)
+    x = np.random.default_rng(5).normal(size=Mt)
+    ref = ((X - mave[:, None]) * (msig * x)[:, None]).sum(axis=0) / np.sqrt(N)
+    with va.Data(N, Mt) as d:
+        d.load_meth(X)
+        assert d.kernel_name(0, 1).startswith("ax_team_kernel<")
+        a = d.Ax(x)
+        b = d.Ax(x)
+        d.set_variant(0, 0)
+        assert d.kernel_name(0, 1).startswith("ax_partial_kernel<")
+        tile = d.Ax(x)
+    assert relerr(a, ref) < 1e-13
+    assert relerr(a, tile) < 1e-13
+    assert np.array_equal(a, b)

@@ -767,6 +767,122 @@ __global__ __launch_bounds__(kTmThreads) void atax_team_plain_kernel(const doubl
 }
 
 // ---------------------------------------------------------------------------
+// A.x alone (data::Ax, src/data.cpp:340-373) at large N: the team layout
+// without the operator system.  A plain product needs no column dot, so the T
+// members of a team need no hand-off: each holds rows [r*TR, (r+1)*TR) of the
+// team's interleaved columns (team t: t, t + nteams, ...) and accumulates
+//   acc_k[j] += (X_ij - mave_i) * (msig_i * x_k[i])
+// in registers over all of them (8 streaming waves, 16-byte buffer loads,
+// F columns prefetched), then writes its rows of the team's slot
+// part[team][k][ld]; ax_reduce sums the nteams slots in order.  The tile
+// plans (ax_partial_kernel) cut each column into 4 KB pieces over 512-row
+// tiles; here a member reads TR rows (25 KB at N = 100,000) of every column
+// it takes.  FU: x_k = z_k + beta_k * p_k (AxFuse), as ax_partial_kernel forms it.
+static constexpr int kAxTmF = 4;       // columns prefetched
+static constexpr int kAxTmMaxS = 4;    // loads per lane per column (1024-row steps)
+template <int S, int KP, bool FU>
+__global__ __launch_bounds__(kTmThreads) void ax_team_kernel(const double* __restrict__ X, int64_t ld, int64_t N,
+                                                             int64_t M, const double* __restrict__ mave,
+                                                             const double* __restrict__ msig, CPtrs xs,
+                                                             double* __restrict__ part, AxFuse fu, int T, int TR) {
+    if (fu.gate && !*fu.gate) return;
+    constexpr int E = 2, F = kAxTmF, RING = F + 1;
+    constexpr int RS = tm_rows_per_step(false, E);  // 1024
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int g = blockIdx.x >> 3;
+    const int member = g % T;
+    const int nteams = gridDim.x / T;  // a multiple of 8 (ax_team_plan)
+    const int team = g / T + (nteams >> 3) * (int)(blockIdx.x & 7);  // teams of one XCD numbered together
+    const int n = team < M ? (int)((M - team + nteams - 1) / nteams) : 0;
+    const int64_t r0 = (int64_t)member * TR;
+    const int nrows = (int)(N - r0 < TR ? N - r0 : TR);  // >= 1 (ax_team_plan)
+    const int nbytes = ((nrows + 1) & ~1) * 8;            // the tile (+ the zero pad row for odd N)
+    const int jb = 64 * E * wave + E * lane;              // row of this lane in step s: RS*s + jb
+    double bk[KP];
+#pragma unroll
+    for (int k = 0; k < KP; ++k) bk[k] = FU ? fu.beta[k] : 0.0;
+    // per-lane source of a column's scalars: lane 0 mave, 1 msig, 2.. x_k, 2+KP.. z_k
+    const double* pkp = mave;
+    if (lane == 1) pkp = msig;
+#pragma unroll
+    for (int k = 0; k < KP; ++k) {
+        if (lane == 2 + k) pkp = xs.p[k];
+        if (FU && lane == 2 + KP + k) pkp = fu.z.p[k];
+    }
+    pkp += team;  // column m of the team is pkp[m * nteams]
+    double acc[KP][S][E];
+#pragma unroll
+    for (int k = 0; k < KP; ++k)
+#pragma unroll
+        for (int s = 0; s < S; ++s)
+#pragma unroll
+            for (int e = 0; e < E; ++e) acc[k][s][e] = 0.0;
+    double xr[RING][S][E];
+    double pk[RING];
+    const char* xtile = reinterpret_cast<const char*>(X + (int64_t)team * ld + r0);
+    auto load = [&](int slot, int m) {
+        const int64_t c = (int64_t)m * nteams;
+        pk[slot] = pkp[c];  // older than the column's X loads: it lands first
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc((void*)(xtile + c * ld * 8), (short)0, nbytes, 0x00020000);
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+            const v2d x = __builtin_bit_cast(v2d, __builtin_amdgcn_raw_buffer_load_b128(rs, (RS * s + jb) * 8, 0, 2));
+            xr[slot][s][0] = x.x;
+            xr[slot][s][1] = x.y;
+        }
+    };
+    if (n > 0) {
+        // steps m = -F .. in whole rounds of RING (the first F only load);
+        // column c lives in ring slot (c + F) % RING, every step issues one
+        // load (clamped to the last column: fixed vmcnt counts)
+        for (int base = -F; base < n; base += RING) {
+#pragma unroll
+            for (int i = 0; i < RING; ++i) {
+                const int m = base + i;
+                load((i + F) % RING, m + F < n ? m + F : n - 1);
+                if (m >= 0 && m < n) {
+                    const double mu = readlane_d(pk[i], 0);
+                    const double sg = readlane_d(pk[i], 1);
+                    double cp[KP];  // msig_i * x_k[i]
+#pragma unroll
+                    for (int k = 0; k < KP; ++k) {
+                        double xk = readlane_d(pk[i], 2 + k);
+                        if (FU) xk = readlane_d(pk[i], 2 + KP + k) + bk[k] * xk;
+                        cp[k] = sg * xk;
+                    }
+#pragma unroll
+                    for (int s = 0; s < S; ++s)
+#pragma unroll
+                        for (int e = 0; e < E; ++e) {
+                            const double dx = xr[i][s][e] - mu;  // rows past the tile: never stored
+#pragma unroll
+                            for (int k = 0; k < KP; ++k) {
+                                if constexpr (TM_FMA)
+                                    acc[k][s][e] = __builtin_fma(dx, cp[k], acc[k][s][e]);
+                                else
+                                    acc[k][s][e] += dx * cp[k];
+                            }
+                        }
+                }
+            }
+        }
+    }
+    // this member's rows of the team's slot (zeros for a team without columns)
+    double* dst = part + (int64_t)team * KP * ld + r0;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+        const int jl = RS * s + jb;
+        if (jl >= nrows) continue;
+#pragma unroll
+        for (int k = 0; k < KP; ++k)
+#pragma unroll
+            for (int e = 0; e < E; ++e)
+                if (jl + e < nrows) dst[(int64_t)k * ld + jl + e] = acc[k][s][e];
+    }
+}
+
+// ---------------------------------------------------------------------------
 // host side: plans, instantiations, launch
 // ---------------------------------------------------------------------------
 static int tm_S(int64_t rows, bool comm, int E) {
@@ -922,6 +1038,86 @@ hipError_t atax_team_plain(const Shard& s, const OpPlan& pl, const OpArgs& a, hi
     if (s.M <= 0) return hipSuccess;
     if (!launch_tm_c<1, true>(s, pl, a, st, tm, gate)) return hipErrorInvalidValue;
     return hipGetLastError();
+}
+
+bool ax_team_plan(int64_t N, int64_t M, int cus, AxPlan* out) {
+    if (N < 1 || cus < 8) return false;
+    constexpr int RS = tm_rows_per_step(false, 2);
+    for (int T = 1; T <= kTmMaxT; T *= 2) {
+        if (cus / (8 * T) < 1) break;
+        const int grid = (cus / (8 * T)) * 8 * T;
+        const int64_t TR = T == 1 ? N : ((N + T - 1) / T + 127) / 128 * 128;
+        if ((int64_t)(T - 1) * TR >= N) continue;  // every member holds rows
+        const int S = (int)((TR + RS - 1) / RS);
+        if (S > kAxTmMaxS) continue;
+        AxPlan p{};
+        p.variant = kAxTeam;
+        p.T = T;
+        p.TR = (int)TR;
+        p.S = S;
+        p.groups = grid;
+        p.nslots = grid / T;
+        p.rows = N;  // one tile: every row sums the nslots team slots
+        p.tiles = 1;
+        p.total = M;
+        p.sa = p.nslots;
+        p.sb = 1;
+        *out = p;
+        return true;
+    }
+    return false;
+}
+
+template <int S, int K, bool FU>
+static void launch_axt(const Shard& s, const AxPlan& pl, CPtrs x, double* part, hipStream_t st, const Timing& tm,
+                       const AxFuse& fu) {
+    hipExtLaunchKernelGGL((ax_team_kernel<S, K, FU>), dim3(pl.groups), dim3(kTmThreads), 0, st, tm.start, tm.stop, 0,
+                          s.X, s.ld, s.N, s.M, s.mave, s.msig, x, part, fu, pl.T, pl.TR);
+}
+
+template <int S>
+static bool launch_axt_k(int K, bool fused, const Shard& s, const AxPlan& pl, CPtrs x, double* part,
+                         hipStream_t st, const Timing& tm, const AxFuse& fu) {
+    switch (K * 2 + (fused ? 1 : 0)) {
+        case 2: launch_axt<S, 1, false>(s, pl, x, part, st, tm, fu); return true;
+        case 3: launch_axt<S, 1, true>(s, pl, x, part, st, tm, fu); return true;
+        case 4: launch_axt<S, 2, false>(s, pl, x, part, st, tm, fu); return true;
+        case 5: launch_axt<S, 2, true>(s, pl, x, part, st, tm, fu); return true;
+        case 6: launch_axt<S, 3, false>(s, pl, x, part, st, tm, fu); return true;
+        case 7: launch_axt<S, 3, true>(s, pl, x, part, st, tm, fu); return true;
+        case 8: launch_axt<S, 4, false>(s, pl, x, part, st, tm, fu); return true;
+        case 9: launch_axt<S, 4, true>(s, pl, x, part, st, tm, fu); return true;
+        default: return false;
+    }
+}
+
+hipError_t ax_team(const Shard& s, const AxPlan& pl, int K, CPtrs x, double* part, hipStream_t st, const Timing& tm,
+                   const AxFuse& fu) {
+    // the plan must be this shard's: every member holds rows, S loads cover them
+    if (pl.T < 1 || pl.groups % (8 * pl.T) || pl.nslots != pl.groups / pl.T || pl.S < 1 || pl.S > kAxTmMaxS ||
+        (int64_t)(pl.T - 1) * pl.TR >= s.N || (int64_t)pl.T * pl.TR < s.N ||
+        (int64_t)pl.S * tm_rows_per_step(false, 2) < std::min<int64_t>(pl.TR, s.N) || pl.rows < s.N)
+        return hipErrorInvalidValue;
+    if (s.M <= 0) return hipSuccess;
+    const bool fused = fu.z.p[0] != nullptr;
+    if (fused && !fu.beta) return hipErrorInvalidValue;
+    bool ok = false;
+    switch (pl.S) {
+        case 1: ok = launch_axt_k<1>(K, fused, s, pl, x, part, st, tm, fu); break;
+        case 2: ok = launch_axt_k<2>(K, fused, s, pl, x, part, st, tm, fu); break;
+        case 3: ok = launch_axt_k<3>(K, fused, s, pl, x, part, st, tm, fu); break;
+        case 4: ok = launch_axt_k<4>(K, fused, s, pl, x, part, st, tm, fu); break;
+        default: break;
+    }
+    if (!ok) return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
+std::string ax_kernel_name(int K, bool fused, const AxPlan& pl) {
+    if (pl.T <= 0) return kernel_name(0, K, fused ? 1 : 0, pl.variant);
+    char b[96];
+    std::snprintf(b, sizeof b, "ax_team_kernel<%d, %d, %s>", pl.S, K, fused ? "true" : "false");
+    return b;
 }
 
 bool team_plain_plan(int64_t N, int64_t M, int cus, const OpPlan& main, OpPlan* out) {

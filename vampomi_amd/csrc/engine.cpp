@@ -2061,7 +2061,7 @@ extern "C" vampomi_status vampomi_dev_kernel_name(const vampomi_ctx* c, int whic
     // which = 3: mode carries N (the operator's instantiation depends on it)
     const std::string n = which == 2   ? vk::loo_kernel_name(c->loo_variant)
                           : which == 3 ? op_name(c, K)
-                          : which == 0 ? vk::kernel_name(0, K, mode, c->axp.variant)
+                          : which == 0 ? vk::ax_kernel_name(K, mode == 1, c->axp)
                                        : vk::kernel_name(1, K, mode, c->atx_variant);
     std::snprintf(out, (size_t)cap, "%s", n.c_str());
     return VAMPOMI_OK;

@@ -60,13 +60,21 @@ struct AxPlan {
     int64_t sa, sb;   // tile t's first slot-owning workgroup is t*sa/sb
     int groups;       // workgroups (grid)
     int nslots;       // partial slots of the busiest tile (part holds nslots x kMaxRhs x ld)
+    // team plan (variant kAxTeam, ax_team_kernel): T workgroups per team split
+    // the rows (TR each, S loads per lane per column), every team a full
+    // N-vector slot over its interleaved columns; one tile of N rows (sa =
+    // nslots teams, sb = 1).  T = 0: the tile plans above
+    int T = 0, TR = 0, S = 0;
 };
 // partial slots tile t uses: the workgroups whose share meets it
 inline int64_t ax_slots(const AxPlan& p, int64_t t) { return ((t + 1) * p.sa - 1) / p.sb - (t * p.sa) / p.sb + 1; }
 // Kernel variants (tuning tables in kernels.hip) are per-context launch
 // settings: the defaults are the measured winners, other values are
 // development hooks (tools/kbench.py, vampomi_dev_set_variant).
-constexpr int kAxDefault = 0, kAtxDefault = -1 /* per-K choice */, kLooDefault = 16;
+// kAxDefault: the team plan where it has teams of >= kAxTeamMinT (N above
+// ~16k rows: C3/C4/C5, 4-9 % faster than the tile plans there,
+// profiles/r05q_ax_sweep_c4.txt, r05j_c3_kernel_stats_real.csv), else variant 0
+constexpr int kAxDefault = -1, kAxTeam = 7, kAxTeamMinT = 8, kAtxDefault = -1 /* per-K choice */, kLooDefault = 16;
 AxPlan ax_plan(int64_t N, int64_t M, int variant = kAxDefault);
 int ax_variant_count();
 bool ax_variant_ok(int v);
@@ -83,6 +91,12 @@ struct AxFuse {
 };
 hipError_t ax_partial(const Shard& s, const AxPlan& pl, int K, CPtrs x, double* part, hipStream_t st,
                       const Timing& tm = Timing{}, const AxFuse& fu = AxFuse{});
+// the team plan (atax_team.hip): false if N has none (rows per member past 4
+// loads per lane of 1024-row steps at every team size)
+bool ax_team_plan(int64_t N, int64_t M, int cus, AxPlan* out);
+hipError_t ax_team(const Shard& s, const AxPlan& pl, int K, CPtrs x, double* part, hipStream_t st, const Timing& tm,
+                   const AxFuse& fu);
+std::string ax_kernel_name(int K, bool fused, const AxPlan& pl);  // as rocprofv3 prints it
 // out_k[j] = sum_c part[c][k][j]; if div > 0 then out_k[j] /= div
 hipError_t ax_reduce(const AxPlan& pl, int K, int64_t N, int64_t ld, const double* part, Ptrs out,
                      double div, hipStream_t st, const int* gate = nullptr);

@@ -406,8 +406,9 @@ static constexpr AxVariant kAxVariants[] = {
 static constexpr int kNumAxVariants = sizeof(kAxVariants) / sizeof(kAxVariants[0]);
 // default 0: R=2, U=8, nontemporal (tools/kbench.py)
 
-int ax_variant_count() { return kNumAxVariants; }
-bool ax_variant_ok(int v) { return v >= 0 && v < kNumAxVariants; }
+int ax_variant_count() { return kNumAxVariants + 1; }  // + kAxTeam
+bool ax_variant_ok(int v) { return v == kAxDefault || (v >= 0 && v < kNumAxVariants) || v == kAxTeam; }
+static_assert(kAxTeam == kNumAxVariants, "the team plan numbers after the tile variants");
 
 static int device_cus() {
     int dev = 0, cus = 0;
@@ -419,7 +420,11 @@ static int device_cus() {
 
 AxPlan ax_plan(int64_t N, int64_t M, int variant) {
     AxPlan p;
-    p.variant = ax_variant_ok(variant) ? variant : 0;
+    if (variant == kAxDefault || variant == kAxTeam) {
+        if (ax_team_plan(N, M, device_cus(), &p) && (variant == kAxTeam || p.T >= kAxTeamMinT)) return p;
+        p = AxPlan{};
+    }
+    p.variant = variant >= 0 && variant < kNumAxVariants ? variant : 0;
     p.rows = (int64_t)kBlock * kAxVariants[p.variant].R;
     p.tiles = cdiv(N, p.rows);
     p.total = p.tiles * M;
@@ -480,6 +485,7 @@ static bool launch_ax_v(int v, const Shard& s, const AxPlan& pl, CPtrs x, double
 
 hipError_t ax_partial(const Shard& s, const AxPlan& pl, int K, CPtrs x, double* part, hipStream_t st,
                       const Timing& tm, const AxFuse& fu) {
+    if (pl.T > 0) return ax_team(s, pl, K, x, part, st, tm, fu);
     if (pl.rows != (int64_t)kBlock * kAxVariants[pl.variant].R || pl.total != pl.tiles * s.M ||
         pl.tiles * pl.rows < s.N)
         return hipErrorInvalidValue;  // plan made for another shape
@@ -672,7 +678,7 @@ bool atx_variant_ok(int v) { return v >= -1 && v < kNumAtxVariants; }
 std::string kernel_name(int which, int K, int mode, int variant) {
     char b[160];
     if (which == 0) {
-        const AxVariant& v = kAxVariants[ax_variant_ok(variant) ? variant : 0];
+        const AxVariant& v = kAxVariants[variant >= 0 && variant < kNumAxVariants ? variant : 0];
         std::snprintf(b, sizeof b, "ax_partial_kernel<%d, %d, %d, %s, %s>", K, v.R, v.U, v.NT ? "true" : "false",
                       mode == 1 ? "true" : "false");
     } else {
