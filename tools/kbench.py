@@ -28,7 +28,7 @@ x, u = rng.normal(size=Mt), rng.normal(size=N)
 only = sys.argv[4].split(",") if len(sys.argv) > 4 else ["ax", "atx", "loo"]
 res = {"N": N, "Mt": Mt, "reps": reps, "ax": {}, "atx": {}, "loo": {}}
 ref_ax, ref_atx = None, None
-for which, name, Ks, nvar in ((0, "ax", tuple(int(k) for k in os.environ.get("AX_KS", "1,2,3").split(",")), 7), (1, "atx", (1, 2), 8)):
+for which, name, Ks, nvar in ((0, "ax", tuple(int(k) for k in os.environ.get("AX_KS", "1,2,3").split(",")), 8), (1, "atx", (1, 2), 8)):
     if name not in only:
         continue
     for v in range(nvar):
