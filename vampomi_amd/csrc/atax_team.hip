@@ -778,6 +778,9 @@ __global__ __launch_bounds__(kTmThreads) void atax_team_plain_kernel(const doubl
 // plans (ax_partial_kernel) cut each column into 4 KB pieces over 512-row
 // tiles; here a member reads TR rows (25 KB at N = 100,000) of every column
 // it takes.  FU: x_k = z_k + beta_k * p_k (AxFuse), as ax_partial_kernel forms it.
+#ifndef AX_TEAM_SYNC
+#define AX_TEAM_SYNC 1
+#endif
 static constexpr int kAxTmF = 4;       // columns prefetched
 static constexpr int kAxTmMaxS = 4;    // loads per lane per column (1024-row steps)
 template <int S, int KP, bool FU>
@@ -865,6 +868,10 @@ __global__ __launch_bounds__(kTmThreads) void ax_team_kernel(const double* __res
                             }
                         }
                 }
+                // the waves stay on one column together (as the operator's
+                // per-column barrier keeps them): one column's rows are read
+                // as one stream, not 8 drifting ones
+                if (AX_TEAM_SYNC) __syncthreads();
             }
         }
     }
