@@ -2385,7 +2385,7 @@ __global__ __launch_bounds__(kBlock) void loo_kernel(const double* __restrict__ 
 // reads W KiB contiguous of each column (the wave-per-marker form above reads
 // 1 KiB per wave from columns all over the shard); the W wave sums meet in
 // LDS and are added in wave order.
-template <int G, int UJ, int W, bool SY = false>
+template <int G, int UJ, int W>
 __global__ __launch_bounds__(64 * W) void loo_wg_kernel(const double* __restrict__ X, int64_t ld, int64_t N, int64_t M,
                                                         const double* __restrict__ ymod, const double* __restrict__ x1,
                                                         double sqrtN, double* __restrict__ stats) {
@@ -2431,9 +2431,6 @@ __global__ __launch_bounds__(64 * W) void loo_wg_kernel(const double* __restrict
                 add(g, xx[t][g].x, yy[t].x);
                 add(g, xx[t][g].y, yy[t].y);
             }
-        // SY: the waves stay on one load round together, so each round reads
-        // W KiB of every column as one stream (ax_team_kernel: 3.7 % at C4/C5)
-        if constexpr (SY) __syncthreads();
     }
     for (; j < N; j += RS) {  // (N even or the pad row: ld-padded columns, zero pads)
         v2d xx[G];
@@ -2462,12 +2459,11 @@ __global__ __launch_bounds__(64 * W) void loo_wg_kernel(const double* __restrict
     }
 }
 
-struct LooVariant { int G, UJ; bool FD; int W = 0; bool SY = false; };  // W > 0: loo_wg_kernel (SY: lockstep rounds)
+struct LooVariant { int G, UJ; bool FD; int W = 0; };  // W > 0: loo_wg_kernel
 static constexpr LooVariant kLooVariants[] = {
     {4, 2, true}, {4, 2, false}, {2, 2, true}, {8, 1, true}, {4, 1, true}, {4, 4, true}, {2, 4, true}, {8, 2, true},
     {1, 2, true, 8}, {2, 2, true, 8}, {1, 4, true, 8}, {2, 4, true, 8}, {2, 2, true, 4}, {4, 2, true, 4},
     {4, 1, true, 4}, {8, 1, true, 4}, {4, 2, true, 8}, {4, 2, true, 2}, {8, 2, true, 2}, {4, 4, true, 2},
-    {4, 2, true, 8, true}, {4, 1, true, 8, true}, {2, 2, true, 8, true}, {4, 2, true, 4, true},
 };
 static constexpr int kNumLooVariants = sizeof(kLooVariants) / sizeof(kLooVariants[0]);
 // default (round 3): 16, loo_wg_kernel<4, 2, 8>: 7.00 TB/s at the c5 shard (N=100,000 x 62,500) on
@@ -2481,7 +2477,7 @@ std::string loo_kernel_name(int variant) {
     const LooVariant& v = kLooVariants[loo_variant_ok(variant) ? variant : kLooDefault];
     char b[64];
     if (v.W > 0)
-        std::snprintf(b, sizeof b, "loo_wg_kernel<%d, %d, %d, %s>", v.G, v.UJ, v.W, v.SY ? "true" : "false");
+        std::snprintf(b, sizeof b, "loo_wg_kernel<%d, %d, %d>", v.G, v.UJ, v.W);
     else
         std::snprintf(b, sizeof b, "loo_kernel<%d, %d, %s>", v.G, v.UJ, v.FD ? "true" : "false");
     return b;
@@ -2497,10 +2493,10 @@ static void launch_loo(const Shard& s, const double* ymod, const double* x1, dou
                           tm.stop, 0, s.X, s.ld, s.N, s.M, ymod, x1, sqrtN, stats);
 }
 
-template <int G, int UJ, int W, bool SY = false>
+template <int G, int UJ, int W>
 static void launch_loo_wg(const Shard& s, const double* ymod, const double* x1, double sqrtN, double* stats,
                           hipStream_t st, const Timing& tm) {
-    hipExtLaunchKernelGGL((loo_wg_kernel<G, UJ, W, SY>), dim3((unsigned)cdiv(s.M, G)), dim3(64 * W), 0, st, tm.start,
+    hipExtLaunchKernelGGL((loo_wg_kernel<G, UJ, W>), dim3((unsigned)cdiv(s.M, G)), dim3(64 * W), 0, st, tm.start,
                           tm.stop, 0, s.X, s.ld, s.N, s.M, ymod, x1, sqrtN, stats);
 }
 
@@ -2520,10 +2516,6 @@ hipError_t loo_sums(const Shard& s, const double* ymod, const double* x1, double
         case 17: launch_loo_wg<4, 2, 2>(s, ymod, x1, sqrtN, stats, st, tm); break;
         case 18: launch_loo_wg<8, 2, 2>(s, ymod, x1, sqrtN, stats, st, tm); break;
         case 19: launch_loo_wg<4, 4, 2>(s, ymod, x1, sqrtN, stats, st, tm); break;
-        case 20: launch_loo_wg<4, 2, 8, true>(s, ymod, x1, sqrtN, stats, st, tm); break;
-        case 21: launch_loo_wg<4, 1, 8, true>(s, ymod, x1, sqrtN, stats, st, tm); break;
-        case 22: launch_loo_wg<2, 2, 8, true>(s, ymod, x1, sqrtN, stats, st, tm); break;
-        case 23: launch_loo_wg<4, 2, 4, true>(s, ymod, x1, sqrtN, stats, st, tm); break;
         case 0: launch_loo<4, 2, true>(s, ymod, x1, sqrtN, stats, st, tm); break;
         case 1: launch_loo<4, 2, false>(s, ymod, x1, sqrtN, stats, st, tm); break;
         case 2: launch_loo<2, 2, true>(s, ymod, x1, sqrtN, stats, st, tm); break;
