@@ -72,8 +72,8 @@ inline int64_t ax_slots(const AxPlan& p, int64_t t) { return ((t + 1) * p.sa - 1
 // settings: the defaults are the measured winners, other values are
 // development hooks (tools/kbench.py, vampomi_dev_set_variant).
 // kAxDefault: the team plan where it has teams of >= kAxTeamMinT (N above
-// ~16k rows: C3/C4/C5, 4-9 % faster than the tile plans there,
-// profiles/r05q_ax_sweep_c4.txt, r05j_c3_kernel_stats_real.csv), else variant 0
+// ~16k rows: C3/C4/C5; 3.7-3.8 % faster than the best tile plan there,
+// profiles/r05s_lockstep_ab.txt), else variant 0 (C2 keeps its bits)
 constexpr int kAxDefault = -1, kAxTeam = 7, kAxTeamMinT = 8, kAtxDefault = -1 /* per-K choice */, kLooDefault = 16;
 AxPlan ax_plan(int64_t N, int64_t M, int variant = kAxDefault);
 int ax_variant_count();
