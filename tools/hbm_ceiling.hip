@@ -7,6 +7,7 @@
 //   chunk<U,NT>   a wave reads one contiguous chunk of `chunk` bytes, U loads in
 //                 flight per lane; one chunk per wave, in-order dispatch
 //   persist<U,NT> grid = CUs * wgs_per_cu, every wave an equal contiguous share
+//   lock<U,NT,SYNC> 8-wave workgroups, one contiguous stream each (barrier per round)
 //   cols<G,U,NT>  like atx_kernel: a wave walks G columns of `col` bytes at once
 #include <hip/hip_runtime.h>
 
@@ -88,6 +89,36 @@ __global__ __launch_bounds__(256) void persist_kernel(const double* __restrict__
     }
     const double s = wsum(a0 + a1);
     if (lane == 0) out[w] = s;
+}
+
+// lockstep: 8-wave workgroups (one or two per CU), each a contiguous share;
+// per round the 8 waves read 8U consecutive KiB, then (SYNC) meet at a barrier,
+// so a workgroup reads one stream as the team kernels do (a barrier per column)
+template <int U, bool NT, bool SYNC>
+__global__ __launch_bounds__(512) void lock_kernel(const double* __restrict__ x, int64_t n, double* __restrict__ out) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t units = n / 1024;  // 8 KiB units
+    const int64_t b = units * blockIdx.x / gridDim.x * 1024, e = units * (blockIdx.x + 1) / gridDim.x * 1024;
+    double a0 = 0, a1 = 0;
+    int64_t j = b + 128 * wave + 2 * lane;
+    for (; j + 1024 * (U - 1) < e; j += 1024 * U) {
+        v2d v[U];
+#pragma unroll
+        for (int t = 0; t < U; ++t) v[t] = ldv<NT>(x + j + 1024 * t);
+#pragma unroll
+        for (int t = 0; t < U; ++t) {
+            a0 += v[t].x;
+            a1 += v[t].y;
+        }
+        if (SYNC) __syncthreads();
+    }
+    for (; j < e; j += 1024) {
+        v2d v = ldv<NT>(x + j);
+        a0 += v.x;
+        a1 += v.y;
+    }
+    const double s = wsum(a0 + a1);
+    if (lane == 0) out[(int64_t)blockIdx.x * 8 + wave] = s;
 }
 
 // atx shape: a wave owns G columns of ld doubles, walks them together
@@ -192,6 +223,23 @@ int main(int argc, char** argv) {
         timeit(nm, bytes, reps, [&] { hipLaunchKernelGGL((persist_kernel<8, true>), dim3(blocks), dim3(256), 0, 0, x, n, out); });
         std::snprintf(nm, sizeof nm, "persist_wg%d_U4", wpc);
         timeit(nm, bytes, reps, [&] { hipLaunchKernelGGL((persist_kernel<4, false>), dim3(blocks), dim3(256), 0, 0, x, n, out); });
+    }
+    // lockstep workgroups (the team kernels' access)
+    for (int wpc : {1, 2}) {
+        const unsigned blocks = (unsigned)(cus * wpc);
+        std::snprintf(nm, sizeof nm, "lock_wg%d_U4_nt_sync", wpc);
+        timeit(nm, bytes, reps, [&] { hipLaunchKernelGGL((lock_kernel<4, true, true>), dim3(blocks), dim3(512), 0, 0, x, n, out); });
+        std::snprintf(nm, sizeof nm, "lock_wg%d_U8_nt_sync", wpc);
+        timeit(nm, bytes, reps, [&] { hipLaunchKernelGGL((lock_kernel<8, true, true>), dim3(blocks), dim3(512), 0, 0, x, n, out); });
+        std::snprintf(nm, sizeof nm, "lock_wg%d_U4_sync", wpc);
+        timeit(nm, bytes, reps, [&] { hipLaunchKernelGGL((lock_kernel<4, false, true>), dim3(blocks), dim3(512), 0, 0, x, n, out); });
+        std::snprintf(nm, sizeof nm, "lock_wg%d_U4_nt_nosync", wpc);
+        timeit(nm, bytes, reps, [&] { hipLaunchKernelGGL((lock_kernel<4, true, false>), dim3(blocks), dim3(512), 0, 0, x, n, out); });
+    }
+    if (argc > 3 && std::atoi(argv[3]) == 1) {  // lockstep and persistent only
+        CK(hipFree(x));
+        CK(hipFree(out));
+        return 0;
     }
     // atx shape: N=10,000 (ld 10,000) and 100,000 columns
     for (int64_t ld : {(int64_t)10000, (int64_t)100000}) {
