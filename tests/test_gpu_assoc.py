@@ -166,34 +166,6 @@ def test_workgroup_loo_variants(N, Mt, kind):
         _lib.check(lib.vampomi_dev_set_variant(d.ctx, 2, 16))  # the default
 
 
-@pytest.mark.parametrize("N,Mt,kind", [(4099, 301, 1), (20000, 64, 0), (50001, 300, 1), (100000, 40, 1), (5, 7, 0),
-                                      (257, 5, 1)])
-def test_team_loo_variants(N, Mt, kind):
-    """Variants 20 and 21 (loo_team_kernel: the team layout, member partials
-    summed in member order by a second launch) against the oracle with the LOO
-    bars: odd N, fewer markers than teams (empty teams), every team size up to
-    32; bitwise repeatable."""
-    from vampomi_amd import _lib
-
-    X, y, beta = make_problem(N, Mt, kind=kind)
-    est = _estimate(beta, N)
-    po, sto = O.assoc_loo(X, y, est)
-    spread = _order_spread(X, y, est, po)
-    lib = va.load()
-    with va.Data(N, Mt) as d:
-        d.load_meth(X)
-        d.set_phen(y, standardize=False)
-        for v in (20, 21):
-            _lib.check(lib.vampomi_dev_set_variant(d.ctx, 2, v))
-            assert d.kernel_name(2, 1).startswith("loo_team_kernel<"), d.kernel_name(2, 1)
-            p, st = d.assoc_loo(est)
-            p2, st2 = d.assoc_loo(est)
-            _check_pfun(p, st, N)
-            _check_loo(p, st, po, sto, spread)
-            assert np.array_equal(st, st2) and np.array_equal(p, p2), v
-        _lib.check(lib.vampomi_dev_set_variant(d.ctx, 2, 16))  # the default
-
-
 def test_se_parity():
     N, Mt = 1000, 2000
     X, y, beta = make_problem(N, Mt)

@@ -890,109 +890,6 @@ __global__ __launch_bounds__(kTmThreads) void ax_team_kernel(const double* __res
 }
 
 // ---------------------------------------------------------------------------
-// The association pass (data::pvals_loo, src/data.cpp:385-417) on the same
-// team layout: per marker j the five sums over samples of raw X, X^2, X*ym,
-// ym, ym^2 with ym = ymod + X/sqrtN * x1[j] (loo_wg_kernel's per-element
-// arithmetic, bit for bit).  A member holds its rows' ymod in registers for
-// the whole launch, sums its rows of each column (wave butterflies, the 8
-// waves in order through LDS, a barrier per column: lockstep as
-// ax_team_kernel) and stores the five member partials of the column; a
-// second launch adds the T members in order (loo_team_reduce_kernel).
-template <int S>
-__global__ __launch_bounds__(kTmThreads) void loo_team_kernel(const double* __restrict__ X, int64_t ld, int64_t N,
-                                                              int64_t M, const double* __restrict__ ymod,
-                                                              const double* __restrict__ x1, double sqrtN,
-                                                              double* __restrict__ part, int T, int TR) {
-    constexpr int E = 2, F = kAxTmF, RING = F + 1, CW = 8;
-    constexpr int RS = tm_rows_per_step(false, E);  // 1024
-    __shared__ double s_part[2][CW][5];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int g = blockIdx.x >> 3;
-    const int member = g % T;
-    const int nteams = gridDim.x / T;
-    const int team = g / T + (nteams >> 3) * (int)(blockIdx.x & 7);
-    const int n = team < M ? (int)((M - team + nteams - 1) / nteams) : 0;
-    const int64_t r0 = (int64_t)member * TR;
-    const int nrows = (int)(N - r0 < TR ? N - r0 : TR);
-    const int nbytes = ((nrows + 1) & ~1) * 8;
-    const int jb = 64 * E * wave + E * lane;
-    const double rinv = 1.0 / sqrtN;
-    double y[S][E];  // this lane's rows of ymod (0 past the tile: those rows add nothing)
-#pragma unroll
-    for (int s = 0; s < S; ++s)
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-            const int jl = RS * s + jb + e;
-            y[s][e] = jl < nrows ? ymod[r0 + jl] : 0.0;
-        }
-    double xr[RING][S][E];
-    double pk[RING];
-    const double* xjp = x1 + team;
-    const char* xtile = reinterpret_cast<const char*>(X + (int64_t)team * ld + r0);
-    auto load = [&](int slot, int m) {
-        const int64_t c = (int64_t)m * nteams;
-        pk[slot] = xjp[c];
-        const __amdgpu_buffer_rsrc_t rs =
-            __builtin_amdgcn_make_buffer_rsrc((void*)(xtile + c * ld * 8), (short)0, nbytes, 0x00020000);
-#pragma unroll
-        for (int s = 0; s < S; ++s) {
-            const v2d x = __builtin_bit_cast(v2d, __builtin_amdgcn_raw_buffer_load_b128(rs, (RS * s + jb) * 8, 0, 2));
-            xr[slot][s][0] = x.x;
-            xr[slot][s][1] = x.y;
-        }
-    };
-    if (n > 0) {
-        for (int base = -F; base < n; base += RING) {
-#pragma unroll
-            for (int i = 0; i < RING; ++i) {
-                const int m = base + i;
-                load((i + F) % RING, m + F < n ? m + F : n - 1);
-                const bool real = m >= 0 && m < n;
-                if (real) {
-                    const double xj = pk[i];
-                    double v[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-                    for (int s = 0; s < S; ++s)
-#pragma unroll
-                        for (int e = 0; e < E; ++e) {
-                            const double mv = xr[i][s][e];
-                            const double q0 = mv * rinv;  // loo_wg_kernel's fma-corrected division
-                            const double q = __builtin_fma(__builtin_fma(-q0, sqrtN, mv), rinv, q0);
-                            const double ym = y[s][e] + q * xj;
-                            v[0] += mv;
-                            v[1] += mv * mv;
-                            v[2] += mv * ym;
-                            v[3] += ym;
-                            v[4] += ym * ym;
-                        }
-#pragma unroll
-                    for (int q = 0; q < 5; ++q) {
-                        const double t = group_sum<64>(v[q]);
-                        if (lane == 0) s_part[m & 1][wave][q] = t;
-                    }
-                }
-                __syncthreads();  // the column's wave sums are in; the waves stay in lockstep
-                if (real && wave == 0 && lane < 5) {
-                    double t = 0.0;
-#pragma unroll
-                    for (int w = 0; w < CW; ++w) t += s_part[m & 1][w][lane];
-                    part[((int64_t)member * M + team + (int64_t)m * nteams) * 5 + lane] = t;
-                }
-            }
-        }
-    }
-}
-
-__global__ __launch_bounds__(256) void loo_team_reduce_kernel(int64_t n5, int T, const double* __restrict__ part,
-                                                              double* __restrict__ stats) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= n5) return;
-    double s = 0.0;
-    for (int r = 0; r < T; ++r) s += part[(int64_t)r * n5 + i];  // members in order
-    stats[i] = s;
-}
-
-// ---------------------------------------------------------------------------
 // host side: plans, instantiations, launch
 // ---------------------------------------------------------------------------
 static int tm_S(int64_t rows, bool comm, int E) {
@@ -1150,9 +1047,7 @@ hipError_t atax_team_plain(const Shard& s, const OpPlan& pl, const OpArgs& a, hi
     return hipGetLastError();
 }
 
-// the smallest team size whose members' rows fit maxS loads per lane of
-// 1024-row steps (TR on 128-row boundaries, every member holding rows)
-static bool team_rows_plan(int64_t N, int cus, int maxS, int* T_, int* TR_, int* S_, int* grid_) {
+bool ax_team_plan(int64_t N, int64_t M, int cus, AxPlan* out) {
     if (N < 1 || cus < 8) return false;
     constexpr int RS = tm_rows_per_step(false, 2);
     for (int T = 1; T <= kTmMaxT; T *= 2) {
@@ -1161,20 +1056,7 @@ static bool team_rows_plan(int64_t N, int cus, int maxS, int* T_, int* TR_, int*
         const int64_t TR = T == 1 ? N : ((N + T - 1) / T + 127) / 128 * 128;
         if ((int64_t)(T - 1) * TR >= N) continue;  // every member holds rows
         const int S = (int)((TR + RS - 1) / RS);
-        if (S > maxS) continue;
-        *T_ = T;
-        *TR_ = (int)TR;
-        *S_ = S;
-        *grid_ = grid;
-        return true;
-    }
-    return false;
-}
-
-bool ax_team_plan(int64_t N, int64_t M, int cus, AxPlan* out) {
-    int T = 0, TR = 0, S = 0, grid = 0;
-    if (!team_rows_plan(N, cus, kAxTmMaxS, &T, &TR, &S, &grid)) return false;
-    {
+        if (S > kAxTmMaxS) continue;
         AxPlan p{};
         p.variant = kAxTeam;
         p.T = T;
@@ -1190,47 +1072,7 @@ bool ax_team_plan(int64_t N, int64_t M, int cus, AxPlan* out) {
         *out = p;
         return true;
     }
-}
-
-// the association pass on the team layout (variants kLooTeam..: at most 4 or
-// 8 loads per lane per column)
-bool loo_team_plan(int64_t N, int cus, int variant, LooTeamPlan* out) {
-    if (variant < kLooTeam || variant > kLooTeam + 1) return false;
-    LooTeamPlan p{};
-    if (!team_rows_plan(N, cus, variant == kLooTeam ? 4 : 8, &p.T, &p.TR, &p.S, &p.grid)) return false;
-    *out = p;
-    return true;
-}
-
-template <int S>
-static void launch_loo_team(const Shard& s, const LooTeamPlan& pl, const double* ymod, const double* x1, double sqrtN,
-                            double* part, hipStream_t st, hipEvent_t start) {
-    hipExtLaunchKernelGGL((loo_team_kernel<S>), dim3(pl.grid), dim3(kTmThreads), 0, st, start, nullptr, 0, s.X, s.ld,
-                          s.N, s.M, ymod, x1, sqrtN, part, pl.T, pl.TR);
-}
-
-hipError_t loo_team_sums(const Shard& s, const LooTeamPlan& pl, const double* ymod, const double* x1, double sqrtN,
-                         double* part, double* stats, hipStream_t st, const Timing& tm) {
-    if (pl.T < 1 || pl.grid % (8 * pl.T) || pl.S < 1 || pl.S > 8 || (int64_t)(pl.T - 1) * pl.TR >= s.N ||
-        (int64_t)pl.T * pl.TR < s.N || (int64_t)pl.S * tm_rows_per_step(false, 2) < std::min<int64_t>(pl.TR, s.N) ||
-        !part)
-        return hipErrorInvalidValue;
-    if (s.M <= 0) return hipSuccess;
-    switch (pl.S) {
-        case 1: launch_loo_team<1>(s, pl, ymod, x1, sqrtN, part, st, tm.start); break;
-        case 2: launch_loo_team<2>(s, pl, ymod, x1, sqrtN, part, st, tm.start); break;
-        case 3: launch_loo_team<3>(s, pl, ymod, x1, sqrtN, part, st, tm.start); break;
-        case 4: launch_loo_team<4>(s, pl, ymod, x1, sqrtN, part, st, tm.start); break;
-        case 5: launch_loo_team<5>(s, pl, ymod, x1, sqrtN, part, st, tm.start); break;
-        case 6: launch_loo_team<6>(s, pl, ymod, x1, sqrtN, part, st, tm.start); break;
-        case 7: launch_loo_team<7>(s, pl, ymod, x1, sqrtN, part, st, tm.start); break;
-        case 8: launch_loo_team<8>(s, pl, ymod, x1, sqrtN, part, st, tm.start); break;
-        default: return hipErrorInvalidValue;
-    }
-    const int64_t n5 = 5 * s.M;
-    hipExtLaunchKernelGGL(loo_team_reduce_kernel, dim3((unsigned)((n5 + 255) / 256)), dim3(256), 0, st, nullptr,
-                          tm.stop, 0, n5, pl.T, part, stats);
-    return hipGetLastError();
+    return false;
 }
 
 template <int S, int K, bool FU>

@@ -129,8 +129,6 @@ struct vampomi_ctx {
     int cus = 0;                // compute units of the device (the operator's grid)
     double* op_part = nullptr;  // opp.nslots x kMaxRhs x ld partial A d
     int64_t op_part_slots = 0;
-    double* loo_part = nullptr;  // the team association pass: T x M x 5 member partials
-    size_t loo_part_n = 0;
     double* op_nvec = nullptr;  // 3 x kMaxRhs x ld + 16: A r, q = A p, A d (+ <d,p> tail)
     unsigned long long* op_xg = nullptr;  // team hand-off granules (M x kOpMaxK x T x 2), zeroed once
     size_t op_xg_words = 0;

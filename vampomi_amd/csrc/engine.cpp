@@ -1147,9 +1147,8 @@ void release_ctx_resources(vampomi_ctx* c) {
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
     c->ev_pool.clear();
     for (double** p : {&c->X, &c->mave, &c->msig, &c->y, &c->ax_part, &c->red_part, &c->red_part2, &c->scal, &c->nbuf, &c->mbuf,
-                       &c->op_part, &c->op_nvec, &c->loo_part})
+                       &c->op_part, &c->op_nvec})
         dev_free(*p);
-    c->loo_part_n = 0;
     if (c->op_xg) (void)hipFree(c->op_xg);
     c->op_xg = nullptr;
     if (c->op_ts) (void)hipFree(c->op_ts);
@@ -1693,29 +1692,6 @@ extern "C" vampomi_status vampomi_denoise_bin(vampomi_ctx* c, const double* p1, 
     return VAMPOMI_OK;
 }
 
-// the association pass of the context's variant: the tile/wave kernels
-// (loo_sums), or the team layout with its member partials (vk::loo_team_sums)
-static vampomi_status loo_pass(vampomi_ctx* c, const double* ymod, const double* x1, double* stats,
-                               const vk::Timing& tm) {
-    if (c->loo_variant < vk::kLooTeam) {
-        HIPCHK(vk::loo_sums(c->shard(), ymod, x1, c->sqrtN, stats, c->st, c->loo_variant, tm));
-        return VAMPOMI_OK;
-    }
-    if (c->cus <= 0) HIPCHK(hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, c->device));
-    vk::LooTeamPlan pl{};
-    if (!vk::loo_team_plan(c->N, c->cus, c->loo_variant, &pl))
-        return fail(VAMPOMI_ERR_ARG, "no team plan of the association pass for this N");
-    const size_t need = (size_t)pl.T * (size_t)std::max<int64_t>(c->M, 1) * 5;
-    if (need > c->loo_part_n) {
-        dev_free(c->loo_part);
-        c->loo_part_n = 0;
-        STCHK(dev_alloc(&c->loo_part, need));
-        c->loo_part_n = need;
-    }
-    HIPCHK(vk::loo_team_sums(c->shard(), pl, ymod, x1, c->sqrtN, c->loo_part, stats, c->st, tm));
-    return VAMPOMI_OK;
-}
-
 // --run-mode association_test --pval-method loo (src/main_meth.cpp:245-264,
 // data::pvals_loo src/data.cpp:385-417).  COLLECTIVE (one A.x).
 extern "C" vampomi_status vampomi_assoc_loo(vampomi_ctx* c, const double* est, double* pvals, double* stats,
@@ -1741,7 +1717,7 @@ extern "C" vampomi_status vampomi_assoc_loo(vampomi_ctx* c, const double* est, d
     // for ym, 5 accumulations (3 of them products)
     TimedLaunch t = launch_stat(c, 2, 1, 8.0 * (double)N * (double)M + 8.0 * (double)N + 8.0 * 6.0 * (double)M,
                                 11.0 * (double)N * (double)M);
-    STCHK(loo_pass(c, ymod, x1, st, vk::Timing{t.a, t.b}));  // :393-416
+    HIPCHK(vk::loo_sums(c->shard(), ymod, x1, std::sqrt((double)N), st, c->st, c->loo_variant, vk::Timing{t.a, t.b}));  // :393-416
     c->stats.a_passes_exec++;
     HIPCHK(vk::loo_pvals(M, st, (int)N, pv, c->st));
     if (stats) STCHK(stage_out(c, st, 5 * M, mem, stats));
@@ -1928,7 +1904,7 @@ extern "C" vampomi_status vampomi_dev_time_pass(vampomi_ctx* c, int which, int K
             STCHK(team_launch(c, c->opp.T, [&] { return vk::atax(c->shard(), c->opp, K, x, c->st); }));
         }
         else  // association pass: ymod = nbuf slot 0, x1 = mbuf slot 0, sums in mbuf slots 3..7
-            STCHK(loo_pass(c, c->nbuf, c->mbuf, c->mbuf + 3 * Mx, vk::Timing{}));
+            HIPCHK(vk::loo_sums(c->shard(), c->nbuf, c->mbuf, c->sqrtN, c->mbuf + 3 * Mx, c->st, c->loo_variant));
     }
     HIPCHK(hipEventRecord(b, c->st));
     HIPCHK(hipEventSynchronize(b));
@@ -2083,11 +2059,7 @@ extern "C" vampomi_status vampomi_dev_kernel_name(const vampomi_ctx* c, int whic
                                                   int cap) {
     if (!c || !out || cap < 1) return fail(VAMPOMI_ERR_ARG, "bad argument");
     // which = 3: mode carries N (the operator's instantiation depends on it)
-    vk::LooTeamPlan lp{};
-    const bool loo_team = which == 2 && c->loo_variant >= vk::kLooTeam &&
-                          vk::loo_team_plan(c->N, c->cus > 0 ? c->cus : 256, c->loo_variant, &lp);
-    const std::string n = loo_team       ? "loo_team_kernel<" + std::to_string(lp.S) + ">"
-                          : which == 2   ? vk::loo_kernel_name(c->loo_variant)
+    const std::string n = which == 2   ? vk::loo_kernel_name(c->loo_variant)
                           : which == 3 ? op_name(c, K)
                           : which == 0 ? vk::ax_kernel_name(K, mode == 1, c->axp)
                                        : vk::kernel_name(1, K, mode, c->atx_variant);

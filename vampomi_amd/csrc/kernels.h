@@ -423,18 +423,6 @@ hipError_t loo_sums(const Shard& s, const double* ymod, const double* x1, double
 std::string loo_kernel_name(int variant);
 int loo_variant_count();
 bool loo_variant_ok(int v);
-// The pass on the team layout (atax_team.hip, variants kLooTeam (<= 4 loads
-// per lane per column) and kLooTeam + 1 (<= 8)): loo_team_kernel writes T
-// member partials per marker into part (T x M x 5 doubles), a second launch
-// sums them in member order into stats.  Timing: start on the first launch,
-// stop on the second.
-constexpr int kLooTeam = 20;
-struct LooTeamPlan {
-    int T = 0, TR = 0, S = 0, grid = 0;
-};
-bool loo_team_plan(int64_t N, int cus, int variant, LooTeamPlan* out);
-hipError_t loo_team_sums(const Shard& s, const LooTeamPlan& pl, const double* ymod, const double* x1, double sqrtN,
-                         double* part, double* stats, hipStream_t st, const Timing& tm);
 // pvals[j] = linear_reg1d_pvals(stats[5j..5j+4], n)  (src/utilities.cpp:269-282)
 hipError_t loo_pvals(int64_t M, const double* stats, int n, double* pvals, hipStream_t st);
 // pvals[j] = P(N(r1_j, 1/(gam1 N)) <= 0), flipped for r1_j <= 0 (src/main_meth.cpp:231-236)

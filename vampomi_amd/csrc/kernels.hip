@@ -2470,12 +2470,10 @@ static constexpr int kNumLooVariants = sizeof(kLooVariants) / sizeof(kLooVariant
 // MI355X against 6.81 TB/s for the round-1 default 2 (loo_kernel<2, 2, true>, fma-corrected division,
 // itself 6.80 against 5.63 TB/s with the IEEE division sequence); tools/kbench.py,
 // profiles/r03l_kbench_loo.txt, profiles/r01_kbench_loo.json
-int loo_variant_count() { return kNumLooVariants + 2; }  // + kLooTeam, kLooTeam + 1 (atax_team.hip)
-bool loo_variant_ok(int v) { return v >= 0 && v < kNumLooVariants + 2; }
-static_assert(kLooTeam == kNumLooVariants, "the team variants number after the others");
+int loo_variant_count() { return kNumLooVariants; }
+bool loo_variant_ok(int v) { return v >= 0 && v < kNumLooVariants; }
 
 std::string loo_kernel_name(int variant) {
-    if (variant >= kLooTeam && variant < kNumLooVariants + 2) return "loo_team_kernel";  // <S>: the plan's (engine.cpp)
     const LooVariant& v = kLooVariants[loo_variant_ok(variant) ? variant : kLooDefault];
     char b[64];
     if (v.W > 0)
