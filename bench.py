@@ -81,6 +81,9 @@ def parse_args(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=45.0, help="seconds of host time for the CPU baseline")
     ap.add_argument("--no-timing", action="store_true", help="skip the HIP-event kernel timing")
+    ap.add_argument("--no-read-ceiling", action="store_true",
+                    help="skip the same-run HBM read ceiling (a pure read stream of the resident matrix, after the "
+                         "timed region, n = 1)")
     ap.add_argument("--timing-period", type=int, default=4,
                     help="time one A/A^T launch in this many of each (kernel, K) with HIP events (positions chosen "
                          "by a hash of the launch index; every launch timed costs 1-2.6 %% of a C2 iteration, "
@@ -333,6 +336,22 @@ def read_ceiling(xbytes: float):
         best = min(sizes[gb], key=lambda v: v["us_med"])
         return best["GBs_med"], f"{os.path.relpath(f, ROOT)} ({gb:g} GB buffer, {best['variant']}, median)"
     return None, None
+
+
+def same_run_ceiling(args, d, roof, n: int):
+    """After the timed region, on this device: a pure read stream of the
+    resident matrix (vampomi_dev_read_ceiling), the roofline's achieved rate
+    against it (the same box, the same buffer; n = 1 only)."""
+    if roof is None or n != 1 or args.no_read_ceiling:
+        return
+    try:
+        c = d.read_ceiling(9)
+    except Exception as e:  # noqa: BLE001  (a measurement aid: never fails the line)
+        roof["read_ceiling_same_run"] = {"error": repr(e)}
+        return
+    roof["read_ceiling_same_run"] = {"GBs": round(c["GBs"], 1), "us_med": round(c["us_med"], 2),
+                                     "bytes": int(c["bytes"]), "variant": c["variant"]}
+    roof["frac_of_read_ceiling_same_run"] = round(roof["achieved"] / c["GBs"], 4)
 
 
 def roofline(ks, kname: str, workload: str, period: int) -> dict:
@@ -807,6 +826,7 @@ def run_linear(args, R: Ranks, wd: Watchdog, w: dict, t_start: float) -> dict:
     d, st, el, model = res["d"], res["st"], res["el"], res["model"]
     try:
         roof = dominant_roofline(args, res, w, d.kernel_name)
+        same_run_ceiling(args, d, roof, n)
         y = d.get_phen() if (R.rank == 0 and n == 1 and not args.no_cpu_baseline) else None
         with_writes = (write_rate(args, d, R, res["opts"], res["beta"], res["barrier"], el) if args.write else None)
     finally:
@@ -989,6 +1009,7 @@ def bench_assoc(args, R: Ranks, wd: Watchdog, w: dict, t_start):
     if st.loo.timed:
         roof = roofline(st.loo, d.kernel_name(2, 1, 0), w["workload"], args.timing_period)
         roof["ax_avg_launch_us"] = round(st.ax.ms_timed / max(st.ax.timed, 1) * 1e3, 2)
+        same_run_ceiling(args, d, roof, R.world)
     line = {
         "metric": "LOO association test: markers tested/s (+ achieved HBM GB/s of the per-marker pass)",
         "value": round(Mt * args.steps / el, 1),

@@ -325,6 +325,13 @@ vampomi_status vampomi_reset_stats(vampomi_ctx* ctx);
 vampomi_status vampomi_dev_set_variant(vampomi_ctx* ctx, int which, int variant);
 /* average device time (HIP events) of `reps` back-to-back launches, K RHS */
 vampomi_status vampomi_dev_time_pass(vampomi_ctx* ctx, int which, int K, int reps, double* avg_ms);
+/* The HBM read ceiling of this device for this shard: a pure read stream of
+ * the resident matrix (every byte once, 16-byte nontemporal loads; variant 0
+ * lockstep 8-wave workgroups, one per CU, variant 1 a 1 MiB contiguous chunk
+ * per wave), `reps` timed launches of each; the faster variant's median launch
+ * time in *us_med, the bytes it read in *bytes, the variant in *variant.  No
+ * effect on the run's state or statistics. */
+vampomi_status vampomi_dev_read_ceiling(vampomi_ctx* ctx, int reps, double* us_med, double* bytes, int* variant);
 /* the kernel (as rocprofv3 names it) that pass `which` with K RHS launches now
  * (mode 1: the CG form, i.e. A^T.u with the lmmse_mult epilogue, A.x with the
  * fused direction update; which = 2: the association-test pass of

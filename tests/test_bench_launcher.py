@@ -242,6 +242,10 @@ def _stub_library(monkeypatch):
         def get_phen(self):
             return None
 
+        def read_ceiling(self, reps=9):
+            return {"us_med": 500.0, "bytes": 8.0 * self.N * self.M, "GBs": 8.0 * self.N * self.M / 500e-6 / 1e9,
+                    "variant": "stub"}
+
         def close(self):
             pass
 
@@ -311,3 +315,34 @@ def test_rehearsal_flow_with_a_stub_library(monkeypatch, capsys):
     assert "error" not in line["one_gpu"]["same_problem"] and "error" not in line["one_gpu"]["c3big"]
     h = line["headline_c3full"]
     assert "error" not in h and h["Mt"] == 50000 and h["n_gpus"] == 3
+
+
+def test_same_run_ceiling_fields():
+    """The n = 1 line's roofline carries the read ceiling measured on the same
+    device after the timed region, and its fraction; not at n > 1, not with
+    --no-read-ceiling, and a failing measurement never fails the line."""
+    from types import SimpleNamespace as NS
+
+    sys.path.insert(0, ROOT)
+    import bench
+
+    class D:
+        def read_ceiling(self, reps):
+            return {"us_med": 571.4, "bytes": 4.0e9, "GBs": 7000.0, "variant": "v"}
+
+    class Bad:
+        def read_ceiling(self, reps):
+            raise RuntimeError("no")
+
+    roof = {"achieved": 6500.0}
+    bench.same_run_ceiling(NS(no_read_ceiling=False), D(), roof, 1)
+    assert roof["frac_of_read_ceiling_same_run"] == round(6500.0 / 7000.0, 4)
+    assert roof["read_ceiling_same_run"]["GBs"] == 7000.0
+    for args, n in ((NS(no_read_ceiling=False), 2), (NS(no_read_ceiling=True), 1)):
+        r = {"achieved": 1.0}
+        bench.same_run_ceiling(args, D(), r, n)
+        assert "read_ceiling_same_run" not in r
+    r = {"achieved": 1.0}
+    bench.same_run_ceiling(NS(no_read_ceiling=False), Bad(), r, 1)
+    assert "error" in r["read_ceiling_same_run"] and "frac_of_read_ceiling_same_run" not in r
+    bench.same_run_ceiling(NS(no_read_ceiling=False), D(), None, 1)  # no roofline: nothing to do

@@ -282,6 +282,14 @@ class Data:
                                              _dp(d), _dp(ad), _dp(dp)))
         return d[:, : self.M], ad, dp
 
+    def read_ceiling(self, reps: int = 9) -> dict:
+        """The HBM read ceiling on this device for this shard (vampomi_dev_read_ceiling):
+        a pure read stream of the resident matrix, the faster variant's median."""
+        us, nb, var = C.c_double(), C.c_double(), C.c_int()
+        check(self._lib.vampomi_dev_read_ceiling(self.ctx, int(reps), C.byref(us), C.byref(nb), C.byref(var)))
+        return {"us_med": us.value, "bytes": nb.value, "GBs": nb.value / (us.value * 1e-6) / 1e9,
+                "variant": ("lockstep 8-wave workgroups, one per CU", "1 MiB chunk per wave")[var.value]}
+
     def set_variant(self, which: int, variant: int):
         """Development hook: this context's kernel variant for pass ``which``."""
         check(self._lib.vampomi_dev_set_variant(self.ctx, which, variant))

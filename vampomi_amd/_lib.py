@@ -137,6 +137,8 @@ SIGNATURES = {
     "vampomi_reset_stats": (C.c_int, [_P]),
     "vampomi_dev_set_variant": (C.c_int, [_P, C.c_int, C.c_int]),
     "vampomi_dev_time_pass": (C.c_int, [_P, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_double)]),
+    "vampomi_dev_read_ceiling": (C.c_int, [_P, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double),
+                                           C.POINTER(C.c_int)]),
     "vampomi_dev_kernel_name": (C.c_int, [_P, C.c_int, C.c_int, C.c_int, C.c_char_p, C.c_int]),
     "vampomi_dev_mem_plan": (C.c_int, [C.c_int64, C.c_int64, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _P]),
     "vampomi_dev_op_plan": (C.c_int, [C.c_int64, C.c_int64, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P, _P, C.c_char_p,

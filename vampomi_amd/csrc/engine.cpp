@@ -2055,6 +2055,48 @@ static std::string op_name(const vampomi_ctx* c, int K) {
     return vk::op_kernel_name(K, p);
 }
 
+extern "C" vampomi_status vampomi_dev_read_ceiling(vampomi_ctx* c, int reps, double* us_med, double* bytes,
+                                                   int* variant) {
+    if (!c || reps < 1 || !us_med) return fail(VAMPOMI_ERR_ARG, "bad argument");
+    if (!c->have_X) return fail(VAMPOMI_ERR_STATE, "no methylation data loaded");
+    HIPCHK(hipSetDevice(c->device));
+    if (c->cus <= 0) HIPCHK(hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, c->device));
+    STCHK(sync_stream(c, c->st));
+    const int64_t n = std::max<int64_t>(c->M, 1) * c->ld;
+    hipEvent_t a, b;
+    HIPCHK(hipEventCreate(&a));
+    HIPCHK(hipEventCreate(&b));
+    double best = -1.0, best_bytes = 0.0;
+    int best_kind = -1;
+    for (int kind = 0; kind < 2; ++kind) {
+        double nb = 0.0;
+        if (vk::stream_read(c->X, n, kind, c->cus, c->st, vk::Timing{}, c->red_part, &nb) != hipSuccess) {
+            (void)hipGetLastError();
+            continue;  // the buffer is too small for this shape
+        }
+        std::vector<float> ms((size_t)reps);
+        for (int r = 0; r < reps; ++r) {
+            HIPCHK(vk::stream_read(c->X, n, kind, c->cus, c->st, vk::Timing{a, b}, c->red_part, &nb));
+            HIPCHK(hipEventSynchronize(b));
+            HIPCHK(hipEventElapsedTime(&ms[(size_t)r], a, b));
+        }
+        std::sort(ms.begin(), ms.end());
+        const double med = 1e3 * (double)ms[(size_t)reps / 2];
+        if (best < 0.0 || nb / med > best_bytes / best) {
+            best = med;
+            best_bytes = nb;
+            best_kind = kind;
+        }
+    }
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    if (best_kind < 0) return fail(VAMPOMI_ERR_ARG, "the matrix is too small for a read-ceiling stream");
+    *us_med = best;
+    if (bytes) *bytes = best_bytes;
+    if (variant) *variant = best_kind;
+    return VAMPOMI_OK;
+}
+
 extern "C" vampomi_status vampomi_dev_kernel_name(const vampomi_ctx* c, int which, int K, int mode, char* out,
                                                   int cap) {
     if (!c || !out || cap < 1) return fail(VAMPOMI_ERR_ARG, "bad argument");

@@ -91,6 +91,11 @@ struct AxFuse {
 };
 hipError_t ax_partial(const Shard& s, const AxPlan& pl, int K, CPtrs x, double* part, hipStream_t st,
                       const Timing& tm = Timing{}, const AxFuse& fu = AxFuse{});
+// A pure read stream of x[0, n) (the read ceiling, vampomi_dev_read_ceiling):
+// kind 0 lockstep 8-wave workgroups (cus of them), kind 1 a 1 MiB chunk per
+// wave; returns the bytes read in *bytes (whole 8 KiB / 1 MiB units)
+hipError_t stream_read(const double* x, int64_t n, int kind, int cus, hipStream_t st, const Timing& tm,
+                       double* sink, double* bytes);
 // the team plan (atax_team.hip): false if N has none (rows per member past 4
 // loads per lane of 1024-row steps at every team size)
 bool ax_team_plan(int64_t N, int64_t M, int cus, AxPlan* out);

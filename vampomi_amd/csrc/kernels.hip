@@ -556,6 +556,76 @@ hipError_t ax_reduce(const AxPlan& pl, int K, int64_t N, int64_t ld, const doubl
     return hipGetLastError();
 }
 
+// A pure read stream (the read ceiling of vampomi_dev_read_ceiling; the same
+// shapes as tools/hbm_ceiling's lock and chunk variants).  The sums feed a
+// store that never happens (the comparison with the NaN `never`), so no load
+// is dead.
+__global__ __launch_bounds__(512) void stream_lock_kernel(const double* __restrict__ x, int64_t units,
+                                                          double never, double* __restrict__ sink) {
+    constexpr int U = 8;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t b = units * blockIdx.x / gridDim.x * 1024, e = units * (blockIdx.x + 1) / gridDim.x * 1024;
+    double a0 = 0.0, a1 = 0.0;
+    int64_t j = b + 128 * wave + 2 * lane;
+    for (; j + 1024 * (U - 1) < e; j += 1024 * U) {
+        v2d v[U];
+#pragma unroll
+        for (int t = 0; t < U; ++t) v[t] = __builtin_nontemporal_load(reinterpret_cast<const v2d*>(x + j + 1024 * t));
+#pragma unroll
+        for (int t = 0; t < U; ++t) {
+            a0 += v[t].x;
+            a1 += v[t].y;
+        }
+        __syncthreads();
+    }
+    for (; j < e; j += 1024) {
+        const v2d v = __builtin_nontemporal_load(reinterpret_cast<const v2d*>(x + j));
+        a0 += v.x;
+        a1 += v.y;
+    }
+    if (a0 + a1 == never) sink[0] = a0;
+}
+
+__global__ __launch_bounds__(256) void stream_chunk_kernel(const double* __restrict__ x, int64_t nchunks,
+                                                           double never, double* __restrict__ sink) {
+    constexpr int U = 8;
+    constexpr int64_t CW = 1 << 17;  // 1 MiB of doubles per wave
+    const int lane = threadIdx.x & 63;
+    const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (w >= nchunks) return;
+    double a0 = 0.0, a1 = 0.0;
+    for (int64_t j = w * CW + 2 * lane; j < (w + 1) * CW; j += 128 * U) {
+        v2d v[U];
+#pragma unroll
+        for (int t = 0; t < U; ++t) v[t] = __builtin_nontemporal_load(reinterpret_cast<const v2d*>(x + j + 128 * t));
+#pragma unroll
+        for (int t = 0; t < U; ++t) {
+            a0 += v[t].x;
+            a1 += v[t].y;
+        }
+    }
+    if (a0 + a1 == never) sink[0] = a0;
+}
+
+hipError_t stream_read(const double* x, int64_t n, int kind, int cus, hipStream_t st, const Timing& tm,
+                       double* sink, double* bytes) {
+    const double never = __builtin_nan("");
+    if (kind == 0) {
+        const int64_t units = n / 1024;
+        if (units < cus) return hipErrorInvalidValue;
+        *bytes = 8.0 * (double)(units * 1024);
+        hipExtLaunchKernelGGL(stream_lock_kernel, dim3(cus), dim3(512), 0, st, tm.start, tm.stop, 0, x, units, never,
+                              sink);
+    } else {
+        const int64_t nch = n / (1 << 17);
+        if (nch < 1) return hipErrorInvalidValue;
+        *bytes = 8.0 * (double)(nch << 17);
+        hipExtLaunchKernelGGL(stream_chunk_kernel, dim3((unsigned)((nch + 3) / 4)), dim3(256), 0, st, tm.start,
+                              tm.stop, 0, x, nch, never, sink);
+    }
+    return hipGetLastError();
+}
+
 __global__ void vec_div_kernel(int K, int64_t n, Ptrs v, double div, Ptrs dst) {
     const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (e >= (int64_t)K * n) return;
