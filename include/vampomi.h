@@ -343,6 +343,13 @@ vampomi_status vampomi_dev_kernel_name(const vampomi_ctx* ctx, int which, int K,
  * column S, rows per team member TR, workgroups grid, partial-sum slots
  * nslots, and the kernel name for K right-hand sides.  VAMPOMI_ERR_ARG if
  * no such plan exists. */
+/* The A.x plan for N samples, M markers and `cus` compute units under
+ * `variant` (-1 the default, 0-6 the tile plans, 7 the team plan), no device
+ * needed: team size T (0: a tile plan), rows per member TR, loads per lane S,
+ * workgroups grid, partial slots nslots, and the kernel name for K
+ * right-hand sides. */
+vampomi_status vampomi_dev_ax_plan(int64_t N, int64_t M, int cus, int variant, int K, int* T, int* TR, int* S,
+                                   int* grid, int* nslots, char* name, int cap);
 vampomi_status vampomi_dev_op_plan(int64_t N, int64_t M, int cus, int variant, int K, int* T, int* S, int* TR,
                                    int* grid, int64_t* nslots, char* name, int cap);
 /* Experiment builds only (atax_team.hip compiled with TM_TS=1, and

@@ -103,3 +103,40 @@ def test_bench_workloads_fit_one_mi355x():
     assert mem_plan(100000, 300000, 1, writer=1) + RUNTIME_MARGIN < HBM_BYTES
     assert mem_plan(50000, 200000, 1, probit=1, writer=1) + RUNTIME_MARGIN < HBM_BYTES  # c4full
     assert mem_plan(100000, 500000, 1) > HBM_BYTES
+
+
+def ax_plan(N, M=62500, cus=256, variant=-1, K=1):
+    T, TR, S, grid, ns = (C.c_int() for _ in range(5))
+    name = C.create_string_buffer(128)
+    assert lib.vampomi_dev_ax_plan(N, M, cus, variant, K, C.byref(T), C.byref(TR), C.byref(S), C.byref(grid),
+                                   C.byref(ns), name, 128) == 0
+    return dict(T=T.value, TR=TR.value, S=S.value, grid=grid.value, nslots=ns.value, name=name.value.decode())
+
+
+def test_ax_plans_of_the_baseline_shapes():
+    """The team A.x plan (ax_team_kernel) where it has teams of >= 8 (C3, C4,
+    C5: N above ~16k); the tile plan below, C2 included (its bits unchanged)."""
+    c2, c4, c5 = ax_plan(10000, 50000), ax_plan(50000, 50000, K=4), ax_plan(100000, 62500)
+    assert c2["T"] == 0 and c2["name"].startswith("ax_partial_kernel<1, 2, 8")
+    assert c4["T"] == 16 and c4["S"] == 4 and c4["nslots"] == 16 and c4["name"] == "ax_team_kernel<4, 4, false>"
+    assert c5["T"] == 32 and c5["TR"] == 3200 and c5["nslots"] == 8
+    assert ax_plan(10000, variant=7)["T"] == 4  # the team plan on request (kbench)
+    assert ax_plan(50000, variant=0)["T"] == 0
+
+
+@pytest.mark.parametrize("N", [1, 2, 7, 1024, 1025, 4096, 4097, 8192, 16384, 16385, 20000, 32768, 33000, 50001,
+                               65536, 99999, 100000, 114688, 131072, 131073])
+@pytest.mark.parametrize("cus", [256, 304, 80])
+def test_ax_team_plan_invariants(N, cus):
+    """Every member holds rows, S <= 4 1024-row steps cover them, teams fill
+    whole groups of 8 workgroups on the device, one slot per team."""
+    p = ax_plan(N, cus=cus, variant=7)
+    if p["T"] == 0:  # no team plan: rows past the largest team (<= 32, a group of 8 teams on the device) x 4 steps
+        tmax = max(t for t in (1, 2, 4, 8, 16, 32) if 8 * t <= cus)
+        assert N > tmax * 4096 - 127 * (tmax - 1)
+        assert ax_plan(N, cus=cus)["name"].startswith("ax_partial_kernel")  # the default falls back to a tile plan
+        return
+    T, TR, S = p["T"], p["TR"], p["S"]
+    assert (T - 1) * TR < N <= T * TR
+    assert S <= 4 and S * 1024 >= min(TR, N)
+    assert p["grid"] % (8 * T) == 0 and p["grid"] <= cus and p["nslots"] == p["grid"] // T

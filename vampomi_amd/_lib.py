@@ -141,6 +141,8 @@ SIGNATURES = {
                                            C.POINTER(C.c_int)]),
     "vampomi_dev_kernel_name": (C.c_int, [_P, C.c_int, C.c_int, C.c_int, C.c_char_p, C.c_int]),
     "vampomi_dev_mem_plan": (C.c_int, [C.c_int64, C.c_int64, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _P]),
+    "vampomi_dev_ax_plan": (C.c_int, [C.c_int64, C.c_int64, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P, _P, C.c_char_p,
+                                      C.c_int]),
     "vampomi_dev_op_plan": (C.c_int, [C.c_int64, C.c_int64, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P, _P, C.c_char_p,
                                       C.c_int]),
     "vampomi_dev_op_apply": (C.c_int, [_P, C.c_int, _P, _P, _P, _P, _P, C.c_double, C.c_double, C.c_double, _P, _P,

@@ -1980,6 +1980,20 @@ extern "C" vampomi_status vampomi_dev_op_timestamps(vampomi_ctx* c, unsigned lon
     return VAMPOMI_OK;
 }
 
+extern "C" vampomi_status vampomi_dev_ax_plan(int64_t N, int64_t M, int cus, int variant, int K, int* T, int* TR,
+                                              int* S, int* grid, int* nslots, char* name, int cap) {
+    if (N < 1 || M < 1 || cus < 1 || K < 1 || K > vk::kMaxRhs || !vk::ax_variant_ok(variant))
+        return fail(VAMPOMI_ERR_ARG, "bad argument");
+    const vk::AxPlan p = vk::ax_plan_for(N, M, cus, variant);
+    if (T) *T = p.T;
+    if (TR) *TR = p.TR;
+    if (S) *S = p.S;
+    if (grid) *grid = p.groups;
+    if (nslots) *nslots = p.nslots;
+    if (name && cap > 0) std::snprintf(name, (size_t)cap, "%s", vk::ax_kernel_name(K, false, p).c_str());
+    return VAMPOMI_OK;
+}
+
 extern "C" vampomi_status vampomi_dev_op_plan(int64_t N, int64_t M, int cus, int variant, int K, int* T, int* S,
                                               int* TR, int* grid, int64_t* nslots, char* name, int cap) {
     vk::OpPlan p{};

@@ -76,6 +76,7 @@ inline int64_t ax_slots(const AxPlan& p, int64_t t) { return ((t + 1) * p.sa - 1
 // profiles/r05s_lockstep_ab.txt), else variant 0 (C2 keeps its bits)
 constexpr int kAxDefault = -1, kAxTeam = 7, kAxTeamMinT = 8, kAtxDefault = -1 /* per-K choice */, kLooDefault = 16;
 AxPlan ax_plan(int64_t N, int64_t M, int variant = kAxDefault);
+AxPlan ax_plan_for(int64_t N, int64_t M, int cus, int variant);  // (ax_plan on `cus` compute units)
 int ax_variant_count();
 bool ax_variant_ok(int v);
 int atx_variant_count();

@@ -418,10 +418,12 @@ static int device_cus() {
     return cus;
 }
 
-AxPlan ax_plan(int64_t N, int64_t M, int variant) {
+AxPlan ax_plan(int64_t N, int64_t M, int variant) { return ax_plan_for(N, M, device_cus(), variant); }
+
+AxPlan ax_plan_for(int64_t N, int64_t M, int cus, int variant) {
     AxPlan p;
     if (variant == kAxDefault || variant == kAxTeam) {
-        if (ax_team_plan(N, M, device_cus(), &p) && (variant == kAxTeam || p.T >= kAxTeamMinT)) return p;
+        if (ax_team_plan(N, M, cus, &p) && (variant == kAxTeam || p.T >= kAxTeamMinT)) return p;
         p = AxPlan{};
     }
     p.variant = variant >= 0 && variant < kNumAxVariants ? variant : 0;
@@ -433,7 +435,7 @@ AxPlan ax_plan(int64_t N, int64_t M, int variant) {
     int64_t wpc = 2, bandseg = 32;
     if (const char* f = std::getenv("VAMPOMI_AX_WPC")) wpc = std::max(1, std::atoi(f));
     if (const char* f = std::getenv("VAMPOMI_AX_BANDSEG")) bandseg = std::max(0, std::atoi(f));
-    int64_t G = std::min<int64_t>(wpc * device_cus(), cdiv(p.total, 64));  // >= 64 segments per workgroup
+    int64_t G = std::min<int64_t>(wpc * cus, cdiv(p.total, 64));  // >= 64 segments per workgroup
     if (G < 1) G = 1;
     p.span = cdiv(p.total, G);
     if (p.tiles <= G && bandseg > 0 && M >= (int64_t)kAxVariants[p.variant].U) {
