@@ -13,7 +13,7 @@ import csv
 import sys
 from collections import defaultdict
 
-OPS = ("atax_team_kernel", "atax_team_plain_kernel", "ax_partial_kernel", "atx_kernel")  # the passes over X
+OPS = ("atax_team_kernel", "atax_team_plain_kernel", "ax_partial_kernel", "ax_team_kernel", "atx_kernel")  # the passes over X
 
 
 def short(name):

@@ -2068,11 +2068,14 @@ __global__ __launch_bounds__(kBlock) void cg_update_kernel(int64_t M, CgVecs c, 
     // a store would wait for it); the sums still run over i, i + stride, ...
     // in order, as one element per round would
     const int64_t mstride = (int64_t)mblocks * kBlock;
-    for (int64_t i0 = (int64_t)blockIdx.x * kBlock + threadIdx.x; mpart && i0 < M; i0 += 2 * mstride) {
-        double pv[2][K], zv[2][K], muv[2][K], rv[2][K], dv[2][K], vv[2][K], wv[2][K], sv[2][K];
-        const bool two = i0 + mstride < M;
+    // (W < 32, the large-N plans: one element per round, fewer registers and
+    // more workgroups per CU; the same sums in the same order)
+    constexpr int H = W >= 32 || K >= 3 ? 2 : 1;  // (K >= 3 keeps two: one would spill to scratch)
+    for (int64_t i0 = (int64_t)blockIdx.x * kBlock + threadIdx.x; mpart && i0 < M; i0 += H * mstride) {
+        double pv[H][K], zv[H][K], muv[H][K], rv[H][K], dv[H][K], vv[H][K], wv[H][K], sv[H][K];
+        const bool two = H == 2 && i0 + mstride < M;
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
+        for (int h = 0; h < H; ++h) {
             const int64_t i = i0 + h * mstride;
             if (h == 1 && !two) break;
 #pragma unroll
@@ -2090,7 +2093,7 @@ __global__ __launch_bounds__(kBlock) void cg_update_kernel(int64_t M, CgVecs c, 
             }
         }
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
+        for (int h = 0; h < H; ++h) {
             const int64_t i = i0 + h * mstride;
             if (h == 1 && !two) break;
 #pragma unroll
