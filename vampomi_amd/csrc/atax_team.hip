@@ -781,7 +781,10 @@ __global__ __launch_bounds__(kTmThreads) void atax_team_plain_kernel(const doubl
 #ifndef AX_TEAM_SYNC
 #define AX_TEAM_SYNC 1
 #endif
-static constexpr int kAxTmF = 4;       // columns prefetched
+#ifndef AX_TEAM_F
+#define AX_TEAM_F 4
+#endif
+static constexpr int kAxTmF = AX_TEAM_F;  // columns prefetched (AX_TEAM_F: experiment builds)
 static constexpr int kAxTmMaxS = 4;    // loads per lane per column (1024-row steps)
 template <int S, int KP, bool FU>
 __global__ __launch_bounds__(kTmThreads) void ax_team_kernel(const double* __restrict__ X, int64_t ld, int64_t N,
