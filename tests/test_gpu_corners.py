@@ -129,3 +129,24 @@ def test_device_memory_plan_matches_the_allocations(tmp_path):
     assert va.load().vampomi_dev_mem_plan(N, Mt, 1, 0, cus, 0, 1, C.byref(b)) == 0
     used = free0 - free1
     assert abs(used - b.value) <= 256 * 2**20 + 0.02 * b.value, (used / 2**20, b.value / 2**20)
+
+
+def test_read_ceiling_hook():
+    """vampomi_dev_read_ceiling (the same-run roofline of bench.py): a pure read
+    stream of the resident matrix, the faster of its two shapes; plausible
+    rates, bytes within the matrix, no effect on the operators' results; a
+    matrix too small for either shape is an argument error, not a launch."""
+    N, Mt = 10000, 5000
+    X = O.generate_markers(3, 0, N, 0, Mt)
+    x = np.random.default_rng(1).normal(size=Mt)
+    with va.Data(N, Mt) as d:
+        d.load_meth(X)
+        before = d.Ax(x)
+        c = d.read_ceiling(5)
+        assert 0 < c["bytes"] <= 8.0 * Mt * ((N + 15) // 16 * 16)
+        assert 1000.0 < c["GBs"] < 10000.0, c
+        assert np.array_equal(d.Ax(x), before)
+    with va.Data(100, 10) as d:
+        d.load_meth(O.generate_markers(3, 0, 100, 0, 10))
+        with pytest.raises(va.VampomiError):
+            d.read_ceiling(3)
