@@ -779,7 +779,7 @@ __global__ __launch_bounds__(kTmThreads) void atax_team_plain_kernel(const doubl
 // tiles; here a member reads TR rows (25 KB at N = 100,000) of every column
 // it takes.  FU: x_k = z_k + beta_k * p_k (AxFuse), as ax_partial_kernel forms it.
 #ifndef AX_TEAM_SYNC
-#define AX_TEAM_SYNC 1
+#define AX_TEAM_SYNC 1  // 0: experiment builds without the per-column barrier (3.7 % slower, r05s)
 #endif
 #ifndef AX_TEAM_F
 #define AX_TEAM_F 4
