@@ -84,6 +84,28 @@ def test_sharded_operators(monkeypatch, P):
     assert relerr(np.concatenate([r[5] for r in res]), msig) < 1e-14
 
 
+@pytest.mark.parametrize("P", [2, 4])
+def test_sharded_team_ax(monkeypatch, P):
+    """A.x on the team plan (N above ~16k: ax_team_kernel) on P ranks: each
+    rank's team slots, its reduction, the all-reduce and /sqrt(N); odd N, and
+    fewer markers per rank than teams (empty teams write zero slots)."""
+    N, Mt = 20001, 403
+    X = O.generate_markers(11, 1, N, 0, Mt)
+    mave, msig = O.marker_stats(X)
+    x = np.random.default_rng(9).normal(size=Mt)
+
+    def fn(r, d):
+        d.load_meth(X[d.S:d.S + d.M])
+        return d.kernel_name(0, 1), d.Ax(x[d.S:d.S + d.M])
+
+    res = run_ranks(monkeypatch, P, N, Mt, fn)
+    ref = O.ax(X, mave, msig, x)
+    for name, ax in res:
+        assert name.startswith("ax_team_kernel<"), name
+        assert relerr(ax, ref) < 1e-13
+        assert np.array_equal(ax, res[0][1])  # the same all-reduced vector on every rank
+
+
 @pytest.mark.parametrize("P", [2, 3, 4, 8])
 def test_sharded_linear_vamp_matches_single_rank(monkeypatch, P):
     N, Mt, its = 1000, 2000, 12
