@@ -1,7 +1,14 @@
 """bench.py — VAMP iterations/s + HBM GB/s on MI355X (BASELINE.json metric).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config auto|c2|c3full|c3|c3big|c4|c4full|c5]
-                    [--no-cpu-baseline]
+                    [--no-cpu-baseline] [--no-read-ceiling] [--no-timing | --timing-period P]
+                    [--rehearse P]   (the n > 1 flow with P loopback rank threads on one GPU)
+
+The line's `roofline` is the dominant kernel's algorithmic bytes per launch
+over its HIP-event launch time, against the 8 TB/s spec (`frac`), against the
+pool's measured read ceiling (`frac_of_read_ceiling`, profiles/) and, at
+n = 1, against a pure read stream of the same resident matrix measured by this
+process right after the timed region (`frac_of_read_ceiling_same_run`).
 
 A "step" is one VAMP iteration (src/vamp.cpp:148-428) of the linear model
 (or src/vamp_probit.cpp:68-463 of the probit model for c4) over the whole
