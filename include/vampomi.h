@@ -337,12 +337,6 @@ vampomi_status vampomi_dev_read_ceiling(vampomi_ctx* ctx, int reps, double* us_m
  * fused direction update; which = 2: the association-test pass of
  * vampomi_assoc_loo) */
 vampomi_status vampomi_dev_kernel_name(const vampomi_ctx* ctx, int which, int K, int mode, char* out, int cap);
-/* The one-pass operator's plan for N samples, M markers and `cus` compute
- * units under `variant` (as vampomi_dev_set_variant(ctx, 3, variant)), no
- * device needed: team size T (0: the whole-column kernel), loads per lane per
- * column S, rows per team member TR, workgroups grid, partial-sum slots
- * nslots, and the kernel name for K right-hand sides.  VAMPOMI_ERR_ARG if
- * no such plan exists. */
 /* The A.x plan for N samples, M markers and `cus` compute units under
  * `variant` (-1 the default, 0-6 the tile plans, 7 the team plan), no device
  * needed: team size T (0: a tile plan), rows per member TR, loads per lane S,
@@ -350,8 +344,22 @@ vampomi_status vampomi_dev_kernel_name(const vampomi_ctx* ctx, int which, int K,
  * right-hand sides. */
 vampomi_status vampomi_dev_ax_plan(int64_t N, int64_t M, int cus, int variant, int K, int* T, int* TR, int* S,
                                    int* grid, int* nslots, char* name, int cap);
+/* The one-pass operator's plan for N samples, M markers and `cus` compute
+ * units under `variant` (as vampomi_dev_set_variant(ctx, 3, variant)), no
+ * device needed: team size T (0: the whole-column kernel), loads per lane per
+ * column S, rows per team member TR, workgroups grid, partial-sum slots
+ * nslots, and the kernel name for K right-hand sides.  VAMPOMI_ERR_ARG if
+ * no such plan exists. */
 vampomi_status vampomi_dev_op_plan(int64_t N, int64_t M, int cus, int variant, int K, int* T, int* S, int* TR,
                                    int* grid, int64_t* nslots, char* name, int cap);
+/* The dynamic LDS layout (in doubles) a team-plan operator launch with K
+ * systems uses for that plan, no device needed: out[0] head words (the folded
+ * CG decision), [1] q offset, [2] q stride, [3] wave partials offset, [4]
+ * hand-off totals offset, [5] total words.  The kernel's pointers, the plan's
+ * feasibility check and the launch size all come from this one layout.
+ * VAMPOMI_ERR_ARG if there is no such team plan (or it is the whole-column
+ * kernel's). */
+vampomi_status vampomi_dev_op_lds(int64_t N, int64_t M, int cus, int variant, int K, int64_t* out);
 /* Experiment builds only (atax_team.hip compiled with TM_TS=1, and
  * VAMPOMI_OP_TS=1 set before the context's first operator use): the last
  * operator launch's per-workgroup {start, end, XCC id, HW_ID} (s_memrealtime

@@ -140,3 +140,47 @@ def test_ax_team_plan_invariants(N, cus):
     assert (T - 1) * TR < N <= T * TR
     assert S <= 4 and S * 1024 >= min(TR, N)
     assert p["grid"] % (8 * T) == 0 and p["grid"] <= cus and p["nslots"] == p["grid"] // T
+
+
+def op_lds(N, variant, K, M=62500, cus=256):
+    out = (C.c_int64 * 6)()
+    if lib.vampomi_dev_op_lds(N, M, cus, variant, K, out) != 0:
+        return None
+    return dict(zip(("head", "q", "qs", "part", "tot", "words"), list(out)))
+
+
+# the operator kernels' LDS: gfx950 allows 160 KiB per workgroup; the head holds
+# beta_k of the folded CG decision (k < kOpMaxK = 2) and its go word
+LDS_MAX_DOUBLES = 160 * 1024 // 8
+K_MAX = 2
+
+
+def test_team_lds_layout_one_source_every_selectable_plan():
+    """Every team plan any variant selects (configurations 0-6, T = 1..32, N
+    across the plan boundaries) has one LDS layout for each system count K it
+    may launch with (the head-start kernel is K = 1): the head before q, q's
+    K strides, then the [2][CW][K] wave partials, then the [2][K] totals,
+    disjoint, in that order, inside 160 KiB (team_plan refuses any plan whose
+    layout does not fit, the launch refuses a size over the limit).  The
+    layout the kernel addresses and the size the launch requests are this same
+    function (atax_team.hip tm_lds)."""
+    seen = 0
+    for v in [T * 10 + c for T in (1, 2, 4, 8, 16, 32) for c in range(7)] + [-1]:
+        for N in (1, 7, 1000, 4097, 9216, 9217, 10000, 10752, 10753, 20000, 50000, 50001, 100000, 143360):
+            p = plan(N, variant=v)
+            if p is None or p["T"] == 0:
+                assert op_lds(N, v, 1) is None
+                continue
+            for K in range(1, K_MAX + 1):
+                lay = op_lds(N, v, K)
+                assert lay is not None, (N, v, K)
+                seen += 1
+                assert lay["head"] >= K_MAX + 1 and lay["q"] == lay["head"]
+                assert lay["qs"] >= min(p["TR"], N) and lay["qs"] % 2 == 0  # every row of the tile; 16-byte pairs
+                cw = 8 if p["T"] == 1 else 7
+                assert lay["part"] == lay["q"] + K * lay["qs"]
+                assert lay["tot"] == lay["part"] + 2 * cw * K
+                assert lay["words"] == lay["tot"] + 2 * K <= LDS_MAX_DOUBLES, (N, v, K, lay)
+            assert op_lds(N, v, K_MAX + 1) is None
+    assert seen > 100
+    assert op_lds(10000, 0, 1) is None  # the whole-column kernel has its own layout

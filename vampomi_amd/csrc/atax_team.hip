@@ -105,6 +105,27 @@ __host__ __device__ constexpr int64_t tm_qstride(int K, int S, bool comm, int E,
     return tm_qfull(K, S, comm, E) ? (int64_t)S * tm_rows_per_step(comm, E) : (tile_rows + 1) & ~(int64_t)1;
 }
 
+// The dynamic LDS of a team-kernel launch, in doubles from its start: the
+// head (the folded CG decision: beta_k, then go), q (K x qs), the streaming
+// waves' partials of a column's dot ([2][CW][K]) and the hand-off totals
+// ([2][K]).  The ONE description of it: the kernel's pointers, team_plan's
+// feasibility check and launch_tm's launch size all come from here.
+struct TmLds {
+    int64_t qs;    // q stride (doubles per system)
+    int64_t q;     // offsets
+    int64_t part;
+    int64_t tot;
+    int64_t words;  // total
+};
+static_assert(kOpMaxK + 1 <= kTmLdsHead, "the head holds beta_k (k < kOpMaxK) and the go word after them");
+__host__ __device__ constexpr TmLds tm_lds(int K, int S, bool comm, int E, int64_t tile_rows) {
+    const int64_t qs = tm_qstride(K, S, comm, E, tile_rows);
+    const int cw = comm ? 7 : 8;  // streaming waves
+    const int64_t q = kTmLdsHead, part = q + (int64_t)K * qs, tot = part + 2 * (int64_t)cw * K;
+    return TmLds{qs, q, part, tot, tot + 2 * (int64_t)K};
+}
+static constexpr int64_t kTmLdsMaxBytes = 160 * 1024;  // gfx950: LDS per workgroup
+
 __device__ __forceinline__ double readlane_d(double v, int l) {
     const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
     const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)u, l);
@@ -285,10 +306,11 @@ __device__ __forceinline__ void atax_team_body(const double* __restrict__ X, int
     const int64_t r0 = (int64_t)member * TR;
     const int nrows = (int)(N - r0 < TR ? N - r0 : TR);  // >= 1 (op_plan)
     constexpr bool QFULL = tm_qfull(K, S, COMM, E);
-    const int QS = (int)tm_qstride(K, S, COMM, E, TR < N ? TR : N);  // q stride
-    double* q_lds = lds + kTmLdsHead;                     // K x QS
-    double* s_part = q_lds + K * QS;                      // [2][CW][K] wave partials of a column's dot
-    double* s_tot = s_part + 2 * CW * K;                  // [2][K] team totals (hand-off)
+    const TmLds lay = tm_lds(K, S, COMM, E, TR < N ? TR : N);  // (launch_tm sized the launch from the same)
+    const int QS = (int)lay.qs;                           // q stride
+    double* q_lds = lds + lay.q;                          // K x QS
+    double* s_part = lds + lay.part;                      // [2][CW][K] wave partials of a column's dot
+    double* s_tot = lds + lay.tot;                        // [2][K] team totals (hand-off)
     const int jb = 64 * E * wave + E * lane;              // row of this lane in step s: RS*s + jb
     // the tile of a column (E = 2: + the zero pad row for odd N)
     const int nbytes = (E == 2 ? (nrows + 1) & ~1 : nrows) * 8;
@@ -916,9 +938,9 @@ bool team_plan(int64_t N, int64_t M, int cus, int T, int cfg, OpPlan* out) {
     }
     const int S = tm_S(TR, c.comm, c.E);
     if (S > c.maxS) return false;
-    const int64_t QS = tm_qstride(kOpMaxK, S, c.comm, c.E, std::min<int64_t>(TR, N));
-    const int64_t lds = (QS * kOpMaxK + 2 * 8 * kOpMaxK + 2 * kOpMaxK + kTmLdsHead) * 8;
-    if (lds > 160 * 1024) return false;
+    // every system count the plan may launch with (the head-start kernel is K = 1)
+    for (int K = 1; K <= kOpMaxK; ++K)
+        if (tm_lds(K, S, c.comm, c.E, std::min<int64_t>(TR, N)).words * 8 > kTmLdsMaxBytes) return false;
     OpPlan p{};
     p.grid = grid;
     p.S = S;
@@ -931,14 +953,26 @@ bool team_plan(int64_t N, int64_t M, int cus, int T, int cfg, OpPlan* out) {
     return true;
 }
 
+bool team_lds_layout(const OpPlan& pl, int64_t N, int K, int64_t out[6]) {
+    if (pl.T < 1 || pl.cfg < 0 || pl.cfg >= kTmNCfg || K < 1 || K > kOpMaxK || N < 1) return false;
+    const TmCfg& c = kTmCfg[pl.cfg];
+    const TmLds l = tm_lds(K, pl.S, c.comm, c.E, std::min<int64_t>(pl.TR, N));
+    out[0] = kTmLdsHead;
+    out[1] = l.q;
+    out[2] = l.qs;
+    out[3] = l.part;
+    out[4] = l.tot;
+    out[5] = l.words;
+    return true;
+}
+
 // occ != null: no launch, *occ = the workgroups of this instantiation one CU
 // holds at once (hipOccupancyMaxActiveBlocksPerMultiprocessor).  PL: the
 // head-start kernel (K = 1 operator system + kTmPlain plain right-hand sides)
 template <int K, int S, int C, bool PL>
-static void launch_tm(const Shard& s, const OpPlan& pl, const OpArgs& a, hipStream_t st, const Timing& tm,
-                      const int* gate, int* occ) {
+static hipError_t launch_tm(const Shard& s, const OpPlan& pl, const OpArgs& a, hipStream_t st, const Timing& tm,
+                            const int* gate, int* occ) {
     constexpr TmCfg c = kTmCfg[C];
-    constexpr int CW = c.comm ? 7 : 8;
     static_assert(!PL || K == 1, "the head-start kernel has one operator system");
     void (*kern)(const double*, int64_t, int64_t, int64_t, const double*, const double*, OpArgs, int, int, int,
                  const int*);
@@ -946,22 +980,20 @@ static void launch_tm(const Shard& s, const OpPlan& pl, const OpArgs& a, hipStre
         kern = atax_team_plain_kernel<S, c.F, c.L, c.P, c.comm, c.E, (bool)TM_FMA>;
     else
         kern = atax_team_kernel<K, S, c.F, c.L, c.P, c.comm, c.E, (bool)TM_FMA>;
-    const int64_t QS = tm_qstride(K, S, c.comm, c.E, std::min<int64_t>(pl.TR, s.N));
-    const size_t lds = (size_t)(kTmLdsHead + K * QS + 2 * CW * K + 2 * K) * sizeof(double);
-    static std::once_flag once;  // more than 64 KiB of dynamic LDS must be allowed explicitly
-    std::call_once(once, [&] {
-        // (a failure must not linger as the thread's last error: the next
-        // launch checked with hipGetLastError would report it as its own)
-        if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                160 * 1024) != hipSuccess)
-            (void)hipGetLastError();
-    });
+    const size_t lds = (size_t)tm_lds(K, S, c.comm, c.E, std::min<int64_t>(pl.TR, s.N)).words * sizeof(double);
+    if (lds > (size_t)kTmLdsMaxBytes) return hipErrorInvalidValue;  // (team_plan refuses such plans)
+    // more than 64 KiB of dynamic LDS must be allowed explicitly, once per
+    // instantiation and device
+    static std::atomic<unsigned long long> allowed{0};  // bit d: done on device d
+    if (const hipError_t e = lds_allow(reinterpret_cast<const void*>(kern), allowed, (int)kTmLdsMaxBytes))
+        return e;
     if (occ) {
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, kern, kTmThreads, lds) != hipSuccess) *occ = 0;
-        return;
+        return hipSuccess;
     }
     hipExtLaunchKernelGGL(kern, dim3(pl.grid), dim3(kTmThreads), lds, st, tm.start, tm.stop, 0, s.X, s.ld, s.N, s.M,
                           s.mave, s.msig, a, pl.T, pl.TR, c.ilv ? 1 : 0, gate);
+    return hipSuccess;
 }
 
 // the most loads per lane per column the head-start kernel is instantiated
@@ -972,18 +1004,17 @@ static constexpr int tm_plain_maxS(int cfg) {
     return cfg == 0 ? 8 : cfg == 2 ? 3 : cfg == 3 ? 4 : cfg == 4 ? 5 : 0;
 }
 
+// hipErrorInvalidValue: no such instantiation (or an LDS size over the limit)
 template <int K, int C, int S, bool PL>
-static bool launch_tm_if(const Shard& s, const OpPlan& pl, const OpArgs& a, hipStream_t st, const Timing& tm,
-                         const int* gate, int* occ) {
-    if constexpr (S <= (PL ? tm_plain_maxS(C) : kTmCfg[C].maxS)) {
-        launch_tm<K, S, C, PL>(s, pl, a, st, tm, gate, occ);
-        return true;
-    }
-    return false;
+static hipError_t launch_tm_if(const Shard& s, const OpPlan& pl, const OpArgs& a, hipStream_t st, const Timing& tm,
+                               const int* gate, int* occ) {
+    if constexpr (S <= (PL ? tm_plain_maxS(C) : kTmCfg[C].maxS))
+        return launch_tm<K, S, C, PL>(s, pl, a, st, tm, gate, occ);
+    return hipErrorInvalidValue;
 }
 
 template <int K, int C, bool PL>
-static bool launch_tm_s(int S, const Shard& s, const OpPlan& pl, const OpArgs& a, hipStream_t st,
+static hipError_t launch_tm_s(int S, const Shard& s, const OpPlan& pl, const OpArgs& a, hipStream_t st,
                         const Timing& tm, const int* gate, int* occ) {
     switch (S) {
         case 1: return launch_tm_if<K, C, 1, PL>(s, pl, a, st, tm, gate, occ);
@@ -996,12 +1027,12 @@ static bool launch_tm_s(int S, const Shard& s, const OpPlan& pl, const OpArgs& a
         case 8: return launch_tm_if<K, C, 8, PL>(s, pl, a, st, tm, gate, occ);
         case 9: return launch_tm_if<K, C, 9, PL>(s, pl, a, st, tm, gate, occ);
         case 10: return launch_tm_if<K, C, 10, PL>(s, pl, a, st, tm, gate, occ);
-        default: return false;
+        default: return hipErrorInvalidValue;
     }
 }
 
 template <int K, bool PL = false>
-static bool launch_tm_c(const Shard& s, const OpPlan& pl, const OpArgs& a, hipStream_t st, const Timing& tm,
+static hipError_t launch_tm_c(const Shard& s, const OpPlan& pl, const OpArgs& a, hipStream_t st, const Timing& tm,
                         const int* gate, int* occ = nullptr) {
     if constexpr (PL) {
         switch (pl.cfg) {
@@ -1009,7 +1040,7 @@ static bool launch_tm_c(const Shard& s, const OpPlan& pl, const OpArgs& a, hipSt
             case 2: return launch_tm_s<1, 2, true>(pl.S, s, pl, a, st, tm, gate, occ);
             case 3: return launch_tm_s<1, 3, true>(pl.S, s, pl, a, st, tm, gate, occ);
             case 4: return launch_tm_s<1, 4, true>(pl.S, s, pl, a, st, tm, gate, occ);
-            default: return false;
+            default: return hipErrorInvalidValue;
         }
     }
     switch (pl.cfg) {
@@ -1020,7 +1051,7 @@ static bool launch_tm_c(const Shard& s, const OpPlan& pl, const OpArgs& a, hipSt
         case 4: return launch_tm_s<K, 4, false>(pl.S, s, pl, a, st, tm, gate, occ);
         case 5: return launch_tm_s<K, 5, false>(pl.S, s, pl, a, st, tm, gate, occ);
         case 6: return launch_tm_s<K, 6, false>(pl.S, s, pl, a, st, tm, gate, occ);
-        default: return false;
+        default: return hipErrorInvalidValue;
     }
 }
 
@@ -1029,13 +1060,13 @@ hipError_t atax_team(const Shard& s, const OpPlan& pl, int K, const OpArgs& a, h
     if (pl.T < 1 || pl.grid < pl.T || pl.grid % pl.T) return hipErrorInvalidValue;
     if (pl.T > 1 && (!a.xg || !a.err || a.tag == 0)) return hipErrorInvalidValue;
     if (s.M <= 0) return hipSuccess;
-    bool ok = false;
+    hipError_t e = hipErrorInvalidValue;
     switch (K) {
-        case 1: ok = launch_tm_c<1>(s, pl, a, st, tm, gate); break;
-        case 2: ok = launch_tm_c<2>(s, pl, a, st, tm, gate); break;
+        case 1: e = launch_tm_c<1>(s, pl, a, st, tm, gate); break;
+        case 2: e = launch_tm_c<2>(s, pl, a, st, tm, gate); break;
         default: break;
     }
-    if (!ok) return hipErrorInvalidValue;
+    if (e != hipSuccess) return e;
     return hipGetLastError();
 }
 
@@ -1046,7 +1077,7 @@ hipError_t atax_team_plain(const Shard& s, const OpPlan& pl, const OpArgs& a, hi
     for (int k = 0; k < kTmPlain; ++k)
         if (!a.px.p[k]) return hipErrorInvalidValue;
     if (s.M <= 0) return hipSuccess;
-    if (!launch_tm_c<1, true>(s, pl, a, st, tm, gate)) return hipErrorInvalidValue;
+    if (const hipError_t e = launch_tm_c<1, true>(s, pl, a, st, tm, gate)) return e;
     return hipGetLastError();
 }
 
@@ -1152,14 +1183,14 @@ int team_occupancy(const OpPlan& pl, int K) {
     int occ = 0;
     const Shard s{nullptr, 0, (int64_t)pl.TR * pl.T, 1, nullptr, nullptr};  // the LDS size needs TR and N only
     const OpArgs a{};
-    bool ok = false;
+    hipError_t e = hipErrorInvalidValue;
     switch (K) {
-        case 1: ok = launch_tm_c<1>(s, pl, a, nullptr, Timing{}, nullptr, &occ); break;
-        case 2: ok = launch_tm_c<2>(s, pl, a, nullptr, Timing{}, nullptr, &occ); break;
-        case 1 + kTmPlain: ok = launch_tm_c<1, true>(s, pl, a, nullptr, Timing{}, nullptr, &occ); break;
+        case 1: e = launch_tm_c<1>(s, pl, a, nullptr, Timing{}, nullptr, &occ); break;
+        case 2: e = launch_tm_c<2>(s, pl, a, nullptr, Timing{}, nullptr, &occ); break;
+        case 1 + kTmPlain: e = launch_tm_c<1, true>(s, pl, a, nullptr, Timing{}, nullptr, &occ); break;
         default: break;
     }
-    return ok ? occ : 0;
+    return e == hipSuccess ? occ : 0;
 }
 
 std::string team_kernel_name(int K, const OpPlan& pl) {

@@ -2008,6 +2008,13 @@ extern "C" vampomi_status vampomi_dev_op_plan(int64_t N, int64_t M, int cus, int
     return VAMPOMI_OK;
 }
 
+extern "C" vampomi_status vampomi_dev_op_lds(int64_t N, int64_t M, int cus, int variant, int K, int64_t* out) {
+    vk::OpPlan p{};
+    if (!out || !vk::op_plan(N, std::max<int64_t>(M, 1), cus, variant, &p) || !vk::team_lds_layout(p, N, K, out))
+        return fail(VAMPOMI_ERR_ARG, "no team plan with that system count");
+    return VAMPOMI_OK;
+}
+
 // Device bytes one rank's context allocates for a VAMP run: the same sizes
 // vampomi_open, the data load, op_prepare (the one-pass operator's buffers,
 // batch_rhs 4), vamp_alloc / probit_begin and the iteration writer allocate,

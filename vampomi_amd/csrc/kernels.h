@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdint>
 #include <string>
 
@@ -152,6 +153,14 @@ constexpr int kOpDefault = -1;
 bool op_plan(int64_t N, int64_t M, int cus, int variant, OpPlan* out);
 bool op_supported(int64_t N, int K);
 bool team_plan(int64_t N, int64_t M, int cus, int T, int cfg, OpPlan* out);
+// the team kernel's dynamic LDS for plan pl with K operator systems (the one
+// layout its launches and team_plan use, atax_team.hip tm_lds), in doubles:
+// out[0] head words, [1] q offset, [2] q stride, [3] partials offset,
+// [4] totals offset, [5] total words; false: pl is not a team plan
+bool team_lds_layout(const OpPlan& pl, int64_t N, int K, int64_t out[6]);
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device):
+// bit d of done is device d; a failure is returned, never left pending
+hipError_t lds_allow(const void* kern, std::atomic<unsigned long long>& done, int bytes);
 struct CgState;
 struct CgMirror;
 // Several ranks (pcg.cpp): the previous CG step's decision (cg_decide on its

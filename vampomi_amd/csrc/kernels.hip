@@ -1103,34 +1103,52 @@ std::string op_kernel_name(int K, const OpPlan& pl) {
     return b;
 }
 
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize, bytes) for `kern` on the
+// current device, once per (kernel, device): bit d of `done` is device d.  A
+// failure is returned (and not left behind as the thread's last error, which
+// the next launch's hipGetLastError would report as its own).
+hipError_t lds_allow(const void* kern, std::atomic<unsigned long long>& done, int bytes) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    const unsigned long long bit = dev >= 0 && dev < 64 ? 1ull << dev : 0ull;
+    if (bit && (done.load(std::memory_order_acquire) & bit)) return hipSuccess;
+    e = hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return e;
+    }
+    done.fetch_or(bit, std::memory_order_acq_rel);
+    return hipSuccess;
+}
+
 template <int K, int S>
-static void launch_op(const Shard& s, const OpPlan& pl, const OpArgs& a, hipStream_t st, const Timing& tm,
-                      const int* gate) {
+static hipError_t launch_op(const Shard& s, const OpPlan& pl, const OpArgs& a, hipStream_t st, const Timing& tm,
+                            const int* gate) {
     const size_t lds = ((size_t)K * (s.N + 1 + (s.N & 1)) + 2 + 2 * kOpWaves * K) * sizeof(double);
-    static std::once_flag once;  // more than 64 KiB of dynamic LDS must be allowed explicitly
-    std::call_once(once, [] {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&atax_kernel<K, S>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    });
+    static std::atomic<unsigned long long> allowed{0};  // more than 64 KiB of dynamic LDS must be allowed explicitly
+    if (const hipError_t e = lds_allow(reinterpret_cast<const void*>(&atax_kernel<K, S>), allowed, 160 * 1024))
+        return e;
     hipExtLaunchKernelGGL((atax_kernel<K, S>), dim3(pl.grid), dim3(kOpThreads), lds, st, tm.start, tm.stop, 0, s.X,
                           s.ld, s.N, s.M, s.mave, s.msig, a, gate);
+    return hipSuccess;
 }
 
 template <int K>
-static bool launch_op_s(int S, const Shard& s, const OpPlan& pl, const OpArgs& a, hipStream_t st, const Timing& tm,
-                        const int* gate) {
+static hipError_t launch_op_s(int S, const Shard& s, const OpPlan& pl, const OpArgs& a, hipStream_t st,
+                              const Timing& tm, const int* gate) {
     switch (S) {
-        case 1: launch_op<K, 1>(s, pl, a, st, tm, gate); return true;
-        case 2: launch_op<K, 2>(s, pl, a, st, tm, gate); return true;
-        case 3: launch_op<K, 3>(s, pl, a, st, tm, gate); return true;
-        case 4: launch_op<K, 4>(s, pl, a, st, tm, gate); return true;
-        case 5: launch_op<K, 5>(s, pl, a, st, tm, gate); return true;
-        case 6: launch_op<K, 6>(s, pl, a, st, tm, gate); return true;
-        case 7: launch_op<K, 7>(s, pl, a, st, tm, gate); return true;
-        case 8: launch_op<K, 8>(s, pl, a, st, tm, gate); return true;
-        case 9: launch_op<K, 9>(s, pl, a, st, tm, gate); return true;
-        case 10: launch_op<K, 10>(s, pl, a, st, tm, gate); return true;
-        default: return false;
+        case 1: return launch_op<K, 1>(s, pl, a, st, tm, gate);
+        case 2: return launch_op<K, 2>(s, pl, a, st, tm, gate);
+        case 3: return launch_op<K, 3>(s, pl, a, st, tm, gate);
+        case 4: return launch_op<K, 4>(s, pl, a, st, tm, gate);
+        case 5: return launch_op<K, 5>(s, pl, a, st, tm, gate);
+        case 6: return launch_op<K, 6>(s, pl, a, st, tm, gate);
+        case 7: return launch_op<K, 7>(s, pl, a, st, tm, gate);
+        case 8: return launch_op<K, 8>(s, pl, a, st, tm, gate);
+        case 9: return launch_op<K, 9>(s, pl, a, st, tm, gate);
+        case 10: return launch_op<K, 10>(s, pl, a, st, tm, gate);
+        default: return hipErrorInvalidValue;
     }
 }
 
@@ -1141,13 +1159,13 @@ hipError_t atax(const Shard& s, const OpPlan& pl, int K, const OpArgs& a, hipStr
         pl.S != (int)std::max<int64_t>(1, (s.N + kOpRows - 1) / kOpRows))
         return hipErrorInvalidValue;
     if (s.M <= 0) return hipSuccess;
-    bool ok = false;
+    hipError_t e = hipErrorInvalidValue;
     switch (K) {
-        case 1: ok = launch_op_s<1>(pl.S, s, pl, a, st, tm, gate); break;
-        case 2: ok = launch_op_s<2>(pl.S, s, pl, a, st, tm, gate); break;
+        case 1: e = launch_op_s<1>(pl.S, s, pl, a, st, tm, gate); break;
+        case 2: e = launch_op_s<2>(pl.S, s, pl, a, st, tm, gate); break;
         default: break;
     }
-    if (!ok) return hipErrorInvalidValue;
+    if (e != hipSuccess) return e;
     return hipGetLastError();
 }
 
