@@ -145,6 +145,7 @@ SIGNATURES = {
                                       C.c_int]),
     "vampomi_dev_op_plan": (C.c_int, [C.c_int64, C.c_int64, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P, _P, C.c_char_p,
                                       C.c_int]),
+    "vampomi_dev_op_lds": (C.c_int, [C.c_int64, C.c_int64, C.c_int, C.c_int, C.c_int, _P]),
     "vampomi_dev_op_apply": (C.c_int, [_P, C.c_int, _P, _P, _P, _P, _P, C.c_double, C.c_double, C.c_double, _P, _P,
                                        _P]),
     "vampomi_dev_op_timestamps": (C.c_int, [_P, _P, C.c_int, C.POINTER(C.c_int)]),
