@@ -97,6 +97,12 @@ void vampomi_close(vampomi_ctx* ctx);
 vampomi_status vampomi_shard_info(const vampomi_ctx* ctx, int64_t* M, int64_t* S, int64_t* ld);
 vampomi_status vampomi_sync(vampomi_ctx* ctx);          /* drain the context's stream */
 vampomi_status vampomi_barrier(vampomi_ctx* ctx);       /* COLLECTIVE: RCCL barrier + drain */
+/* COLLECTIVE: vampomi_barrier with its own wait limit instead of
+ * VAMPOMI_COLL_TIMEOUT_S: the barrier after a rank-local phase of uneven
+ * length, e.g. the shard load, where the ranks' files come off storage at
+ * different rates (there is no MPI_Barrier in the reference's data::data,
+ * src/data.cpp:23-46; its first collective simply waits). */
+vampomi_status vampomi_barrier_timeout(vampomi_ctx* ctx, double seconds);
 /* COLLECTIVE: *all_ok = 1 iff local_ok != 0 on every rank.  How ranks agree on
    a rank-local outcome (a file read) before the next collective; the
    reference's rank-local exits (exit(1), throw) leave the other MPI ranks
@@ -317,11 +323,14 @@ vampomi_status vampomi_reset_stats(vampomi_ctx* ctx);
  * prefetched EM/denoiser, 0 off, 1 on (default: on with several ranks).
  * which = 5: the CG head start of the linear model (the Onsager solve's first
  * step in the pass that starts the x2 solve, pcg.cpp), 0 off, 1 on (default
- * on; VAMPOMI_HEADSTART=0 turns it off at vampomi_open).  On a context with
- * several ranks, which = 3 and 5 take effect at the next vampomi_vamp_begin
- * (or vampomi_infere), where the ranks agree on them: the one-pass operator
- * runs only if every rank has a plan for it, the head start only if every rank
- * has it on (both change the job's collective sequence). */
+ * on; VAMPOMI_HEADSTART=0 turns it off at vampomi_open).  which = 6: the
+ * linear iteration's tail without host waits on several ranks, 0 off, 1 on
+ * (default on; VAMPOMI_MR_TAIL=0 turns it off at vampomi_open).  On a context
+ * with several ranks, which = 3, 5 and 6 take effect at the next
+ * vampomi_vamp_begin (or vampomi_infere), where the ranks agree on them: the
+ * one-pass operator runs only if every rank has a plan for it, the head start
+ * and the host-free tail only if every rank has them on (each changes the
+ * job's collective sequence). */
 vampomi_status vampomi_dev_set_variant(vampomi_ctx* ctx, int which, int variant);
 /* average device time (HIP events) of `reps` back-to-back launches, K RHS */
 vampomi_status vampomi_dev_time_pass(vampomi_ctx* ctx, int which, int K, int reps, double* avg_ms);

@@ -415,6 +415,38 @@ def test_rank_local_switches_between_runs(monkeypatch):
             assert relerr(_cat(ps, "x1_hist")[k], one[hs]["x1_hist"][k]) < 1e-12, (run, k)
 
 
+def test_multi_rank_tail_switch_agreed_over_ranks(monkeypatch):
+    """the host-free tail (VAMPOMI_MR_TAIL, set_variant(6)) changes
+    the tail's collective sequence, so a rank-local choice must not reach the
+    collectives: op_agree agrees it at vampomi_vamp_begin with the operator and
+    head-start choices.  Rank 1 alone turns it off: both ranks run the
+    host-waiting tail (no divergent all-reduce: the loopback communicator would
+    fail the job on one), the same host waits on both, bitwise the run with it
+    off everywhere."""
+    N, Mt = 1001, 2003
+    X, y, beta = make_problem(N, Mt)
+    kw = dict(max_iter=8, stop_criteria_thr=0.0)
+
+    def fn_off_on_one(r, d):
+        if r == 1:
+            d.set_variant(6, 0)
+        s = _vamp(d, X, y, beta, **kw)
+        s["host_syncs"] = d.stats().host_syncs
+        return s
+
+    mixed = run_ranks(monkeypatch, 2, N, Mt, fn_off_on_one)
+    monkeypatch.setenv("VAMPOMI_MR_TAIL", "0")
+    off = run_ranks(monkeypatch, 2, N, Mt, lambda r, d: dict(_vamp(d, X, y, beta, **kw),
+                                                             host_syncs=d.stats().host_syncs))
+    monkeypatch.delenv("VAMPOMI_MR_TAIL")
+    on = run_ranks(monkeypatch, 2, N, Mt, lambda r, d: dict(_vamp(d, X, y, beta, **kw),
+                                                            host_syncs=d.stats().host_syncs))
+    assert mixed[0]["host_syncs"] == mixed[1]["host_syncs"] == off[0]["host_syncs"] > on[0]["host_syncs"]
+    for k in range(kw["max_iter"]):
+        assert np.array_equal(_cat(mixed, "x1_hist")[k], _cat(off, "x1_hist")[k]), k
+    assert mixed[0]["cg_iters"] == off[0]["cg_iters"]
+
+
 @pytest.mark.parametrize("P", [2, 3])
 @pytest.mark.parametrize("kw", [dict(max_iter=10, stop_criteria_thr=0.0), dict(max_iter=30, stop_criteria_thr=0.01),
                                 dict(max_iter=8, stop_criteria_thr=0.0, EM_max_iter=3, EM_err_thr=1e-9),

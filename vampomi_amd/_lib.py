@@ -104,6 +104,7 @@ SIGNATURES = {
     "vampomi_shard_info": (C.c_int, [_P, C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
     "vampomi_sync": (C.c_int, [_P]),
     "vampomi_barrier": (C.c_int, [_P]),
+    "vampomi_barrier_timeout": (C.c_int, [_P, C.c_double]),
     "vampomi_load_meth_file": (C.c_int, [_P, C.c_char_p]),
     "vampomi_load_meth_host": (C.c_int, [_P, _P, C.c_int64]),
     "vampomi_generate_meth": (C.c_int, [_P, C.c_uint64, C.c_int]),

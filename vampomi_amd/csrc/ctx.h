@@ -83,7 +83,9 @@ struct vampomi_ctx {
     unsigned* ticket2 = nullptr;
     bool side_open = false;  // the side stream has work st has not joined (DotBatch fork .. flush)
     bool side_on = false;  // default: several ranks; VAMPOMI_SIDE_STREAM=0/1 or vampomi_dev_set_variant(c, 4, 0/1)
-    bool mr_tail = true;   // several ranks: the linear iteration's tail without host waits (vamp.cpp); VAMPOMI_MR_TAIL=0
+    bool mr_tail = true;   // several ranks: the linear iteration's tail without host waits (vamp.cpp), as agreed
+    double coll_limit_s = 0.0;  // > 0: the limit of the collective in progress (vampomi_barrier_timeout)
+    bool mr_tail_req = true;  // this rank's VAMPOMI_MR_TAIL (0: off), agreed over the ranks by op_agree
     bool cg_fold = true;   // several ranks: each CG decision formed by the next operator launch (pcg.cpp); VAMPOMI_CG_FOLD=0
     bool team_reg = false;           // registered with its device's team gate (engine.cpp)
     hipEvent_t team_ev = nullptr;    // recorded on st when another context must order behind it

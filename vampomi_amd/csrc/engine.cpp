@@ -198,8 +198,9 @@ void drop_launches(vampomi_ctx* c, size_t pending_mark, const vampomi_stats& bef
 // and fails, instead of blocking forever in a collective.  A healthy job's
 // ranks reach each collective within milliseconds of each other; the one
 // legitimate long wait is the first collective after the data load, when the
-// ranks' shards come off a slow shared filesystem at different rates: raise
-// the limit for such jobs.
+// ranks' shards come off a slow shared filesystem at different rates: that
+// one is vampomi_barrier_timeout's, with its own limit (main_meth.exe: after
+// the shard load, VAMPOMI_LOAD_TIMEOUT_S, default one hour).
 static double coll_timeout_s() {
     static const double t = [] {
         const char* e = std::getenv("VAMPOMI_COLL_TIMEOUT_S");
@@ -209,6 +210,9 @@ static double coll_timeout_s() {
     return t;
 }
 
+// this context's limit for the collective in progress
+static double coll_limit_s(const vampomi_ctx* c) { return c->coll_limit_s > 0 ? c->coll_limit_s : coll_timeout_s(); }
+
 // nullptr while the job is healthy, else why it is not
 static const char* job_broken(vampomi_ctx* c, std::chrono::steady_clock::time_point t0) {
     if (c->comm && !c->loopback) {
@@ -216,7 +220,7 @@ static const char* job_broken(vampomi_ctx* c, std::chrono::steady_clock::time_po
         if (ncclCommGetAsyncError(c->comm, &r) == ncclSuccess && r != ncclSuccess && r != ncclInProgress)
             return "RCCL communicator error";
     }
-    const double lim = c->use_comm ? coll_timeout_s() : 600.0;
+    const double lim = c->use_comm ? coll_limit_s(c) : 600.0;
     if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > lim)
         return c->use_comm ? "no completion within VAMPOMI_COLL_TIMEOUT_S (a peer rank stopped?)"
                            : "device did not signal completion within 10 minutes";
@@ -417,12 +421,12 @@ static vampomi_status loopback_allreduce(vampomi_ctx* c, double* buf, size_t n, 
                 lb.arrived = 0;
                 ++lb.gen;
                 lb.cv.notify_all();
-            } else if (!lb.cv.wait_for(g, std::chrono::seconds(60),
+            } else if (!lb.cv.wait_for(g, std::chrono::duration<double>(c->coll_limit_s > 0 ? c->coll_limit_s : 60.0),
                                        [&] { return lb.gen != my_gen || !lb.poison.empty(); })) {
                 // a rank that failed without aborting never arrives: end this
                 // rank with an error instead of waiting forever
                 --lb.arrived;
-                lb.poison = "not every rank arrived within 60 s at " + coll_desc(c->rank, me);
+                lb.poison = "not every rank arrived in time at " + coll_desc(c->rank, me);
                 lb.cv.notify_all();
             }
             if (!lb.poison.empty())
@@ -450,7 +454,7 @@ static vampomi_status rccl_check(vampomi_ctx* c, size_t n, const char* site, int
     double h[6] = {v[0], v[1], v[2], -v[0], -v[1], -v[2]};
     HIPCHK(hipMemcpyAsync(d, h, sizeof h, hipMemcpyHostToDevice, c->st));
     STCHK(nccl_settle(c, ncclAllReduce(d, d, 6, ncclDouble, ncclMax, c->comm, c->st), "ncclAllReduce (check)",
-                      coll_timeout_s()));
+                      coll_limit_s(c)));
     HIPCHK(hipMemcpyAsync(h, d, sizeof h, hipMemcpyDeviceToHost, c->st));
     STCHK(sync_stream(c, c->st));
     for (int q = 0; q < 3; ++q)
@@ -469,7 +473,7 @@ vampomi_status allreduce_dev(vampomi_ctx* c, double* buf, size_t n, const char* 
     const TimedLaunch t = launch_stat(c, 4, 1, 8.0 * (double)n, 0.0);
     if (t.a) HIPCHK(hipEventRecord(t.a, c->st));
     STCHK(nccl_settle(c, ncclAllReduce(buf, buf, n, ncclDouble, ncclSum, c->comm, c->st), "ncclAllReduce",
-                      coll_timeout_s()));
+                      coll_limit_s(c)));
     if (t.b) HIPCHK(hipEventRecord(t.b, c->st));
     return VAMPOMI_OK;
 }
@@ -905,13 +909,18 @@ vampomi_status op_agree(vampomi_ctx* c) {
         op = c->op_ok_mine;
         hs = c->hs_ok_mine;
     }
-    // one all-reduce of the three refusals, each in its own base-2^10 digit
-    const double mine = (op ? 0.0 : 1.0) + (hs ? 0.0 : 1024.0) + (c->hs_on ? 0.0 : 1048576.0);
+    // one all-reduce of the four refusals, each in its own base-2^10 digit (a
+    // digit counts the ranks that refuse: up to 1023 ranks); VAMPOMI_MR_TAIL
+    // changes the tail's collective sequence too (vamp.cpp), so it is agreed
+    // here with the others: the host-free tail only if every rank has it on
+    const double mine = (op ? 0.0 : 1.0) + (hs ? 0.0 : 1024.0) + (c->hs_on ? 0.0 : 1048576.0) +
+                        (c->mr_tail_req ? 0.0 : 1073741824.0);
     double all = 0.0;
     STCHK(sum_over_ranks(c, mine, &all));
     const int64_t a = (int64_t)all;
     c->op_ok = a % 1024 == 0;
-    c->hs_ok = c->op_ok && (a / 1024) % 1024 == 0 && a / 1048576 == 0;
+    c->hs_ok = c->op_ok && (a / 1024) % 1024 == 0 && (a / 1048576) % 1024 == 0;
+    c->mr_tail = a / 1073741824 == 0;
     c->op_agreed = true;
     return VAMPOMI_OK;
 }
@@ -1257,7 +1266,7 @@ extern "C" vampomi_status vampomi_open(const vampomi_shard_desc* d, vampomi_ctx*
     // cross-queue events cost more than the 5-17 us kernels they overlap)
     c->side_on = c->use_comm;
     if (const char* sv = std::getenv("VAMPOMI_SIDE_STREAM")) c->side_on = std::atoi(sv) != 0;
-    if (const char* mv = std::getenv("VAMPOMI_MR_TAIL")) c->mr_tail = std::atoi(mv) != 0;
+    if (const char* mv = std::getenv("VAMPOMI_MR_TAIL")) c->mr_tail = c->mr_tail_req = std::atoi(mv) != 0;
     if (const char* fv = std::getenv("VAMPOMI_CG_FOLD")) c->cg_fold = std::atoi(fv) != 0;
     if (const char* hv = std::getenv("VAMPOMI_HEADSTART")) c->hs_on = c->hs_on_req = std::atoi(hv) != 0;
     const char* mode = std::getenv("VAMPOMI_COMM");
@@ -1304,6 +1313,14 @@ extern "C" vampomi_status vampomi_barrier(vampomi_ctx* c) {
     if (c->use_comm) STCHK(allreduce_dev(c, c->scal + SL_BARRIER, 1));
     STCHK(sync_stream(c, c->st));
     return VAMPOMI_OK;
+}
+
+extern "C" vampomi_status vampomi_barrier_timeout(vampomi_ctx* c, double seconds) {
+    if (!c || !(seconds > 0)) return fail(VAMPOMI_ERR_ARG, "null context or no limit");
+    c->coll_limit_s = seconds;
+    const vampomi_status st = vampomi_barrier(c);
+    c->coll_limit_s = 0.0;
+    return st;
 }
 
 // ---------------------------------------------------------------------------
@@ -1848,6 +1865,10 @@ extern "C" vampomi_status vampomi_dev_set_variant(vampomi_ctx* c, int which, int
         if (variant != 0 && variant != 1) return fail(VAMPOMI_ERR_ARG, "head start: 0 or 1");
         c->hs_on_req = variant == 1;  // several ranks: applied and agreed at the next vampomi_vamp_begin
         if (!c->use_comm) c->hs_on = c->hs_on_req;
+    } else if (which == 6) {  // several ranks: the host-free iteration tail (vamp.cpp, VAMPOMI_MR_TAIL): 0 off, 1 on
+        if (variant != 0 && variant != 1) return fail(VAMPOMI_ERR_ARG, "multi-rank tail: 0 or 1");
+        c->mr_tail_req = variant == 1;  // agreed at the next vampomi_vamp_begin (it changes the collectives)
+        if (!c->use_comm) c->mr_tail = c->mr_tail_req;
     } else {
         if (!vk::loo_variant_ok(variant)) return fail(VAMPOMI_ERR_ARG, "no such association-pass variant");
         c->loo_variant = variant;

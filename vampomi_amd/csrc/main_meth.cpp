@@ -208,6 +208,15 @@ int main(int argc, char** argv) {
     if (vampomi_read_phen(ctx, phen.c_str(), standardize) != VAMPOMI_OK) return die("phenotype");
     if (rank == 0) std::cout << "meth file name = " << meth << std::endl;
     if (vampomi_load_meth_file(ctx, meth.c_str()) != VAMPOMI_OK) return die("methylation data");
+    // the ranks' shards load at their own pace (one rank's file may come off
+    // slower storage): they meet here under a limit of their own, so the
+    // first collective of the run is not the one that waits for the slowest
+    // load under VAMPOMI_COLL_TIMEOUT_S
+    if (nranks > 1) {
+        const char* lt = std::getenv("VAMPOMI_LOAD_TIMEOUT_S");
+        const double lim = lt && std::atof(lt) > 0 ? std::atof(lt) : 3600.0;
+        if (vampomi_barrier_timeout(ctx, lim) != VAMPOMI_OK) return die("waiting for the other ranks' shards");
+    }
     if (rank == 0)
         std::cout << "reading methylation data took "
                   << std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() << " seconds."
