@@ -421,72 +421,154 @@ def cpu_baseline(y, w: dict, beta, seed: int, warmup: int, steps: int, gpu_ref_p
 INT_MAX = 2**31 - 1
 
 
+MPIEXEC = "/opt/conda/bin/mpiexec"  # the image's MPICH (hydra), which oracle/_ref/ref_data links
+
+
+def ref_layouts(threads: int) -> list:
+    """The reference's own decompositions of `threads` host cores: np MPI
+    ranks x OMP_NUM_THREADS per rank (README.md:36-38: `mpirun -np {ranks}`
+    with OMP threads per rank), np a power of two dividing `threads`."""
+    out, P = [], 1
+    while P <= threads:
+        if threads % P == 0:
+            out.append((P, threads // P))
+        P *= 2
+    return out
+
+
 def ref_ops_time(w: dict, seed: int, threads: int) -> dict:
     """The reference's OWN data::Ax / data::ATx (src/data.cpp:294-373,
     compiled from its sources into oracle/_ref/ref_data in the build
-    container) timed on a generated N x Ms matrix on `threads` host threads:
-    ms per call at the workload's full marker count.  The reference indexes
-    the matrix with a 32-bit int (`i*N`, src/data.cpp:297,351),
-    which overflows once M*N > 2^31 - 1 (it crashed with SIGSEGV at the C3
-    shard), so a larger shard is timed on its first floor((2^31-1)/N)
-    markers and projected linearly per marker (both kernels loop over markers
-    with per-marker work of N)."""
+    container) timed on a generated N x Ms matrix on `threads` host cores, in
+    each of its own decompositions np x OMP (ref_layouts): np = 1 in-process,
+    np > 1 under the image's MPICH `mpiexec -np`, every rank on its divide_work
+    share with data::Ax's MPI_Allreduce (the job's time: the slowest rank's,
+    after a barrier).  data::Ax forks an OpenMP team per marker
+    (src/data.cpp:349-361), so one rank x many threads is its slowest layout.
+    Returns the fastest layout's ms per call at the workload's full marker
+    count (best = the smallest (5 + k) Ax + (3 + k) ATx for the caller's k, or
+    the smallest Ax; chosen by the caller) with every layout's numbers.  The
+    reference indexes the matrix with a 32-bit int (`i*N`, src/data.cpp:297,
+    351), which overflows once a rank's M*N > 2^31 - 1 (it
+    crashed with SIGSEGV at the C3 shard on one rank), so a layout whose rank
+    shard would overflow is timed on the first np x floor((2^31-1)/N) markers
+    and projected linearly per marker (both kernels loop over markers with
+    per-marker work of N)."""
     exe = os.path.join(ROOT, "oracle", "_ref", "ref_data")
     if not os.path.exists(exe):
         return {"skipped": "oracle/_ref/ref_data not built (needs /root/reference in the build container)"}
     N, Mt = w["N"], w["Mt"]
-    Ms = Mt if N * Mt <= INT_MAX else INT_MAX // N
-    env = dict(os.environ, OMP_NUM_THREADS=str(threads))
-    out = subprocess.run([exe, "time", str(N), str(Ms), "2", str(seed)], env=env, capture_output=True, text=True,
-                         timeout=300)
-    if out.returncode != 0:
-        return {"error": f"ref_data exit {out.returncode}: {out.stderr[-300:]}"}
-    r = json.loads(out.stdout.strip().splitlines()[-1])
-    scale = Mt / Ms
-    res = {"threads": r["threads"], "ax_ms": r["ax_ms"] * scale, "atx_ms": r["atx_ms"] * scale, "Ms": Ms}
-    if Ms < Mt:
-        res["projected_from"] = (f"{N} x {Ms} (the largest shard whose M*N fits the reference's 32-bit int index, "
-                                 f"src/data.cpp:297,351; it overflows at the full {N} x {Mt} shard), "
-                                 f"x {scale:.3f} per marker: Ax {r['ax_ms']:.1f} ms, ATx {r['atx_ms']:.1f} ms measured")
+    layouts, errors = [], []
+    for P, omp in ref_layouts(threads):
+        Ms = min(Mt, P * (INT_MAX // N))
+        env = dict(os.environ, OMP_NUM_THREADS=str(omp))
+        cmd = [exe, "time", str(N), str(Ms), "2", str(seed)]
+        if P > 1:
+            if not os.path.exists(MPIEXEC):
+                errors.append(f"np={P}: {MPIEXEC} not found")
+                continue
+            cmd = [MPIEXEC, "-np", str(P)] + cmd
+        try:
+            out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+        except subprocess.TimeoutExpired:
+            errors.append(f"np={P}: timed out")
+            continue
+        lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+        if out.returncode != 0 or not lines:
+            errors.append(f"np={P}: exit {out.returncode}: {out.stderr[-200:]}")
+            continue
+        r = json.loads(lines[-1])
+        scale = Mt / Ms
+        lay = {"np": P, "omp": r["threads"], "ax_ms": round(r["ax_ms"] * scale, 3),
+               "atx_ms": round(r["atx_ms"] * scale, 3), "Ms": Ms}
+        if Ms < Mt:
+            lay["projected_from"] = (f"{N} x {Ms} ({P} x the largest rank shard whose M*N fits the reference's "
+                                     f"32-bit int index, src/data.cpp:297,351), x {scale:.3f} per marker: Ax "
+                                     f"{r['ax_ms']:.1f} ms, ATx {r['atx_ms']:.1f} ms measured")
+        layouts.append(lay)
+    if not layouts:
+        return {"error": "; ".join(errors)}
+    res = {"threads": threads, "layouts": layouts}
+    if errors:
+        res["layout_errors"] = errors
     return res
+
+
+def _best_layout(r: dict, cost) -> dict:
+    """The layout of ref_ops_time's result with the smallest cost(layout)."""
+    return min(r["layouts"], key=cost)
 
 
 def cpu_reference_ops(w: dict, seed: int, threads: int, k_cg: float):
     """The reference's own Ax / ATx (ref_ops_time) and its projected iteration
     rate from its own call counts per iteration (it > 1): 5 + k Ax and 3 + k
     ATx with k = k1 + k2 CG steps (src/vamp.cpp:232,303,508,518-519,653-654,
-    681,826), k from the GPU window.  The denoiser/EM (< 1 % of
-    its CPU time) is left out."""
+    681,826), k from the GPU window, in its fastest np x OMP
+    decomposition of the same host cores (every layout reported).  The
+    denoiser/EM (< 1 % of its CPU time) is left out."""
     r = ref_ops_time(w, seed, threads)
-    if "ax_ms" not in r:
+    if "layouts" not in r:
         return r
-    t_it = ((5 + k_cg) * r["ax_ms"] + (3 + k_cg) * r["atx_ms"]) * 1e-3
-    out = {"value": 1.0 / t_it, "unit": "VAMP iterations/s", "kind": "reference", "projected": True,
-           "cores": r["threads"], "ax_ms": round(r["ax_ms"], 3), "atx_ms": round(r["atx_ms"], 3),
-           "sample": f"Ax and ATx (mean of 2 calls each) of the reference's src/data.cpp (oracle/_ref) on a generated "
-                     f"{w['N']} x {r['Ms']} matrix, {r['threads']} OpenMP threads; iteration = (5 + k) Ax + (3 + k) "
-                     f"ATx, k = {k_cg:.2f} (the GPU window's mean CG + Onsager steps)"}
-    if "projected_from" in r:
-        out["projected_from"] = r["projected_from"]
+
+    def t_it(lay):
+        return ((5 + k_cg) * lay["ax_ms"] + (3 + k_cg) * lay["atx_ms"]) * 1e-3
+
+    b = _best_layout(r, t_it)
+    one = next((lay for lay in r["layouts"] if lay["np"] == 1), None)
+    out = {"value": 1.0 / t_it(b), "unit": "VAMP iterations/s", "kind": "reference", "projected": True,
+           "cores": threads, "np": b["np"], "omp": b["omp"], "ax_ms": b["ax_ms"], "atx_ms": b["atx_ms"],
+           "layouts": [dict(lay, it_per_s=round(1.0 / t_it(lay), 5)) for lay in r["layouts"]],
+           "sample": f"Ax and ATx (mean of 2 calls each, the slowest rank's) of the reference's src/data.cpp "
+                     f"(oracle/_ref) on a generated {w['N']} x {w['Mt']} matrix, {threads} host cores as np MPI "
+                     f"ranks (MPICH mpiexec) x OMP threads; value = the fastest layout (np={b['np']} x "
+                     f"omp={b['omp']}); iteration = (5 + k) Ax + (3 + k) ATx, k = {k_cg:.2f} (the GPU window's mean "
+                     f"CG + Onsager steps)"}
+    if one is not None:
+        out["value_np1"] = 1.0 / t_it(one)
+    for key in ("layout_errors",):
+        if key in r:
+            out[key] = r[key]
+    if "projected_from" in b:
+        out["projected_from"] = b["projected_from"]
     return out
+
+
+def stated_cpu_baseline(line: dict) -> dict:
+    """`cpu_baseline` states the FASTER of the two CPU measurements of the
+    same host cores: the oracle port's measured iterations (one process,
+    OpenMP over samples in A.x, no per-marker fork) and the reference's own
+    operators in their fastest np x OMP decomposition (cpu_reference_ops);
+    the other stays in the line (`cpu_port` when the reference is faster)."""
+    port, ref = line.get("cpu_baseline"), line.get("cpu_reference_ops")
+    if (isinstance(port, dict) and isinstance(ref, dict) and port.get("value") and ref.get("value")
+            and ref["value"] > port["value"]):
+        line["cpu_port"] = port
+        line["cpu_baseline"] = {k: ref[k] for k in ("value", "unit", "cores", "kind", "sample", "np", "omp",
+                                                     "projected", "upper_bound") if k in ref}
+        line["cpu_baseline"]["why"] = "the faster of the port and the reference's own operators (cpu_reference_ops)"
+    return line
 
 
 def cpu_reference_ops_assoc(w: dict, seed: int, threads: int):
     """c5: of one LOO test (src/main_meth.cpp:245-264) only the reference's
     z1 = A x1_hat (data::Ax) builds here; data::pvals_loo (src/data.cpp:385-417)
     calls linear_reg1d_pvals from the Boost-dependent src/utilities.cpp.  So
-    this times the reference's Ax and reports the rate a test could at most
-    reach if its per-marker pass were free: an UPPER bound on the reference."""
+    this times the reference's Ax (its fastest np x OMP layout, ref_ops_time)
+    and reports the rate a test could at most reach if its per-marker pass
+    were free: an UPPER bound on the reference."""
     r = ref_ops_time(w, seed, threads)
-    if "ax_ms" not in r:
+    if "layouts" not in r:
         return r
-    out = {"value": w["Mt"] / (r["ax_ms"] * 1e-3), "unit": "markers/s", "kind": "reference", "projected": True,
-           "upper_bound": True, "cores": r["threads"], "ax_ms": round(r["ax_ms"], 3),
+    b = _best_layout(r, lambda lay: lay["ax_ms"])
+    out = {"value": w["Mt"] / (b["ax_ms"] * 1e-3), "unit": "markers/s", "kind": "reference", "projected": True,
+           "upper_bound": True, "cores": threads, "np": b["np"], "omp": b["omp"], "ax_ms": b["ax_ms"],
+           "layouts": r["layouts"],
            "sample": f"the reference's data::Ax (src/data.cpp:340-373, oracle/_ref) on a generated {w['N']} x "
-                     f"{r['Ms']} matrix, {r['threads']} OpenMP threads: the test's A x1_hat only (pvals_loo needs "
-                     "Boost, absent), so markers / Ax time bounds the reference's rate from above"}
-    if "projected_from" in r:
-        out["projected_from"] = r["projected_from"]
+                     f"{w['Mt']} matrix, {threads} host cores as np MPI ranks x OMP threads, the fastest (np="
+                     f"{b['np']} x omp={b['omp']}): the test's A x1_hat only (pvals_loo needs Boost, absent), so "
+                     "markers / Ax time bounds the reference's rate from above"}
+    if "projected_from" in b:
+        out["projected_from"] = b["projected_from"]
     return out
 
 
@@ -926,6 +1008,7 @@ def run_linear(args, R: Ranks, wd: Watchdog, w: dict, t_start: float) -> dict:
                 line["cpu_reference_ops"] = cpu_reference_ops(w, args.seed, threads, k_cg)
             except Exception as e:
                 line["cpu_reference_ops"] = {"error": repr(e)}
+            line = stated_cpu_baseline(line)
     line["wall_s_since_start"] = round(time.perf_counter() - t_start, 1)
     return line
 
@@ -1042,6 +1125,7 @@ def bench_assoc(args, R: Ranks, wd: Watchdog, w: dict, t_start):
             line["cpu_reference_ops"] = cpu_reference_ops_assoc(w, args.seed, threads)
         except Exception as e:
             line["cpu_reference_ops"] = {"error": repr(e)}
+        line = stated_cpu_baseline(line)
     d.close()
     return line
 

@@ -18,8 +18,9 @@
 //   ref_data ax    <X.bin> <N> <M> <x.bin> <out.bin>     (statistics first, as data::data does)
 //   ref_data atx   <X.bin> <N> <M> <u.bin> <out.bin>
 //   ref_data phen  <phen> <N> <standardize 0|1> <out.bin>
-//   ref_data time  <N> <M> <reps> <seed>   (bench.py's CPU leg: the reference's own Ax / ATx
-//                  on a generated N x M matrix, OpenMP threads as set; prints one JSON line)
+//   ref_data time  <N> <Mt> <reps> <seed>  (bench.py's CPU leg: the reference's own Ax / ATx
+//                  on a generated N x Mt matrix, OpenMP threads as set, one rank or its
+//                  marker shard under `mpiexec -np P`; prints one JSON line)
 #include <mpi.h>
 #include <omp.h>
 
@@ -86,37 +87,61 @@ static uint64_t splitmix(uint64_t x) {
     return x ^ (x >> 31);
 }
 
-// times the reference's Ax and ATx (src/data.cpp:294-373) on an N x M
-// marker-major matrix of uniform values (timing only; the values do not matter)
-static int time_ops(int N, int M, int reps, uint64_t seed) {
-    const size_t n = size_t(N) * size_t(M);
+// Times the reference's Ax and ATx (src/data.cpp:294-373) as the reference
+// runs them: under `mpiexec -np P` every rank owns its divide_work share of
+// the Mt markers (src/utilities.cpp:207-239: the first Mt % P ranks one
+// more), generates only those columns of an N x Mt marker-major matrix of
+// uniform values (timing only; the values do not matter, and they are the
+// same for every P: indexed by the GLOBAL marker), and runs data::Ax -- its
+// per-marker OpenMP loop and its MPI_Allreduce of the N-vector (:349-367) --
+// and data::ATx on its shard.  Each call starts after an MPI_Barrier; its
+// time is the slowest rank's (MPI_MAX), i.e. the job's.  Rank 0 prints one
+// JSON line: np, OpenMP threads per rank, ms per call.
+static int time_ops(int N, int Mt, int reps, uint64_t seed) {
+    int rank = 0, np = 1;
+    MPI_Comm_rank(MPI_COMM_WORLD, &rank);
+    MPI_Comm_size(MPI_COMM_WORLD, &np);
+    const int M = Mt / np + (rank < Mt % np ? 1 : 0);
+    const int S = rank * (Mt / np) + (rank < Mt % np ? rank : Mt % np);
+    const size_t n = size_t(N) * size_t(M > 0 ? M : 1);
     double* X = (double*)_mm_malloc(n * sizeof(double), 64);  // as data::read_methylation_data (:129)
     if (!X) return 5;
 #pragma omp parallel for schedule(static)
     for (long long m = 0; m < M; ++m)
         for (int j = 0; j < N; ++j)
-            X[size_t(m) * N + j] = double(splitmix(seed ^ (size_t(m) * N + j)) >> 11) * 0x1.0p-53 * 3.4 - 1.7;
-    Obj o(N, M, 1.0);
+            X[size_t(m) * N + j] =
+                double(splitmix(seed ^ (size_t(S + m) * N + j)) >> 11) * 0x1.0p-53 * 3.4 - 1.7;
+    Obj o(N, M > 0 ? M : 1, 1.0);
+    o.d->M = M;
+    o.d->Mt = Mt;
+    o.d->S = S;
+    o.d->rank = rank;
     o.d->meth_data = X;
     o.d->compute_markers_statistics();
-    std::vector<double> x(M), u(N);
-    for (int i = 0; i < M; ++i) x[i] = double(splitmix(seed + 1 + i) >> 11) * 0x1.0p-53 - 0.5;
+    std::vector<double> x(M > 0 ? M : 1), u(N);
+    for (int i = 0; i < M; ++i) x[i] = double(splitmix(seed + 1 + S + i) >> 11) * 0x1.0p-53 - 0.5;
     for (int j = 0; j < N; ++j) u[j] = double(splitmix(seed + 7 + j) >> 11) * 0x1.0p-53 - 0.5;
     using clk = std::chrono::steady_clock;
     double ax = 0, atx = 0, chk = 0;
     for (int r = 0; r < reps; ++r) {
+        MPI_Barrier(MPI_COMM_WORLD);
         auto t0 = clk::now();
         std::vector<double> a = o.d->Ax(x.data());
         auto t1 = clk::now();
-        std::vector<double> b = o.d->ATx(u.data());
+        MPI_Barrier(MPI_COMM_WORLD);
         auto t2 = clk::now();
-        ax += std::chrono::duration<double>(t1 - t0).count();
-        atx += std::chrono::duration<double>(t2 - t1).count();
-        chk += a[0] + b[0];
+        std::vector<double> b = o.d->ATx(u.data());
+        auto t3 = clk::now();
+        double t[2] = {std::chrono::duration<double>(t1 - t0).count(), std::chrono::duration<double>(t3 - t2).count()};
+        MPI_Allreduce(MPI_IN_PLACE, t, 2, MPI_DOUBLE, MPI_MAX, MPI_COMM_WORLD);
+        ax += t[0];
+        atx += t[1];
+        chk += a[0] + (M > 0 ? b[0] : 0.0);
     }
-    std::printf("{\"N\": %d, \"M\": %d, \"reps\": %d, \"threads\": %d, \"ax_ms\": %.3f, \"atx_ms\": %.3f, "
-                "\"check\": %.6g}\n",
-                N, M, reps, omp_get_max_threads(), ax / reps * 1e3, atx / reps * 1e3, chk);
+    if (rank == 0)
+        std::printf("{\"N\": %d, \"M\": %d, \"reps\": %d, \"np\": %d, \"threads\": %d, \"ax_ms\": %.3f, "
+                    "\"atx_ms\": %.3f, \"check\": %.6g}\n",
+                    N, Mt, reps, np, omp_get_max_threads(), ax / reps * 1e3, atx / reps * 1e3, chk);
     _mm_free(X);
     return 0;
 }

@@ -63,6 +63,26 @@ def test_cpu_reference_ops_leg():
     assert r["kind"] == "reference" and r["cores"] == 2 and r["ax_ms"] > 0 and r["atx_ms"] > 0
     want = 1.0 / ((15 * r["ax_ms"] + 13 * r["atx_ms"]) * 1e-3)
     assert abs(r["value"] - want) <= 1e-9 * want
+    # the reference's own decompositions of the 2 cores: 1 x 2 in-process, 2 x 1 under mpiexec (MPICH), the
+    # stated value the fastest of them (README.md:36-38, the per-marker OpenMP fork of src/data.cpp:356-361)
+    lays = {(lay["np"], lay["omp"]): lay for lay in r["layouts"]}
+    assert set(lays) == {(1, 2), (2, 1)}, r.get("layout_errors")
+    assert r["value"] >= max(lay["it_per_s"] for lay in r["layouts"]) * (1 - 1e-4)
+    assert (r["np"], r["omp"]) in lays and r["value_np1"] > 0
+
+
+def test_stated_cpu_baseline_is_the_faster_measurement():
+    sys.path.insert(0, ROOT)
+    import bench
+
+    port = {"value": 0.4, "unit": "VAMP iterations/s", "kind": "port", "cores": 16}
+    ref = {"value": 0.9, "unit": "VAMP iterations/s", "kind": "reference", "cores": 16, "np": 16, "omp": 1,
+           "sample": "s", "projected": True}
+    line = bench.stated_cpu_baseline({"cpu_baseline": dict(port), "cpu_reference_ops": dict(ref)})
+    assert line["cpu_baseline"]["kind"] == "reference" and line["cpu_baseline"]["value"] == 0.9
+    assert line["cpu_port"] == port
+    line = bench.stated_cpu_baseline({"cpu_baseline": dict(port), "cpu_reference_ops": dict(ref, value=0.1)})
+    assert line["cpu_baseline"] == port and "cpu_port" not in line
 
 
 def _lines(p):
