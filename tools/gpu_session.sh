@@ -23,6 +23,8 @@
 #                2-rank launcher on a 1-GPU box (one failure line, rc != 0)
 #   rccl         the 1-rank RCCL path against the direct one (rates, timing on/off, traces compared)
 #   ceiling      the HBM read ceiling of this box (tools/hbm_ceiling, 4 GB and 50 GB buffers)
+#   ablation     the C2 operator's components removed one at a time (tools/op_ablation.py, build_dbg/: TM_DBG=1)
+#   benchc2      the default C2 line, both CPU legs
 #   c4           the probit shard's line and its per-iteration kernel trace
 #   bases        rank 0's 1-GPU bases (tools/one_gpu_bases.py)
 #   final        smoke, the default C2 line (both CPU legs), its kernel stats
@@ -150,6 +152,10 @@ for s in "$@"; do
     ceiling)     # the HBM read ceiling (tools/hbm_ceiling: every byte of a 4 GB / 50 GB buffer read once)
         step ceiling_4 200 tools/hbm_ceiling 4 15
         step ceiling_50 300 tools/hbm_ceiling 50 5 ;;
+    ablation)    # the C2 operator's components, one at a time, against the same process's read stream (TM_DBG build)
+        step ablation 400 env VAMPOMI_LIB="$PWD/build_dbg/lib/libvampomi.so" python tools/op_ablation.py 10000 50000 40 3 ;;
+    benchc2)     # the default C2 line with both CPU legs
+        step bench_c2 400 python bench.py --steps 20 --warmup 5 ;;
     c4)          # the probit shard: its line, and a kernel trace of 10 iterations (A passes against the rest)
         step bench_c4 400 python bench.py --config c4 --steps 6 --warmup 2 --no-cpu-baseline
         step trace_c4 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_c4" -o run --output-format csv -- \

@@ -396,6 +396,10 @@ __device__ __forceinline__ void atax_team_body(const double* __restrict__ X, int
 #pragma unroll
                 for (int i = 0; i < RING; ++i) {
                     const int m = base + i;  // columns relative to mb (32-bit: scalar compares)
+                    if (dbg & 4096) {  // timing experiment: no hand-off work at all, only the step's barrier
+                        __syncthreads();
+                        continue;
+                    }
                     // the column polled now (finished P steps later), the column finished now
                     const int ci = m - L + P, cf = m - L;
                     const int cic = ci < 0 ? 0 : ci < n ? ci : n - 1;
@@ -614,7 +618,10 @@ __device__ __forceinline__ void atax_team_body(const double* __restrict__ X, int
             }
 #pragma unroll
             for (int k = 0; k < K; ++k) {
-                if constexpr (E == 2) {
+                if (TM_DBG && (dbg & 2048)) {  // timing experiment (TM_DBG builds): no LDS q reads
+                    q[k][0] = 0.5;
+                    q[k][E - 1] = 0.25;
+                } else if constexpr (E == 2) {
                     const v2d qq = *reinterpret_cast<const v2d*>(q_lds + k * QS + jq);
                     q[k][0] = qq.x;
                     q[k][E - 1] = qq.y;

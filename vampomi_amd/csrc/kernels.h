@@ -201,7 +201,8 @@ struct OpArgs {
     unsigned long long* ts;  // experiment builds (TM_TS=1) only: per workgroup {start, end, XCC id, HW id}
     int dbg;  // timing experiments only (VAMPOMI_OP_DBG; results are wrong when set, except bit 5):
               // bit 0 no poll waits, 1 no publishes, 2 no butterfly, 3 no A d accumulation,
-              // 5 write-through hand-off even when the team shares an XCD
+              // 5 write-through hand-off even when the team shares an XCD, 11 no LDS q reads,
+              // 12 no hand-off work (the hand-off wave only keeps the step barriers)
     OpFold fold;  // team kernels only (atax_team.hip)
 };
 std::string op_kernel_name(int K, const OpPlan& pl);
