@@ -73,6 +73,11 @@ def load() -> C.CDLL:
         lib.orc_ax.argtypes = [p, i64, i64, i64, p, p, p, p, ALLREDUCE_FN, p]
         lib.orc_atx.argtypes = [p, i64, i64, i64, p, p, p, p]
         lib.orc_set_atx_block.argtypes = [C.c_int]
+        lib.orc_set_assoc.argtypes = [C.c_int, C.c_int, C.c_int, C.c_uint64]
+        lib.orc_assoc_dot.restype = d
+        lib.orc_assoc_dot.argtypes = [p, p, i64, C.c_int]
+        lib.orc_dev_dp.restype = d
+        lib.orc_dev_dp.argtypes = [p, p, i64, C.c_int, C.c_int]
         lib.orc_g1.restype = d
         lib.orc_g1.argtypes = [d, d, p, p, C.c_int]
         lib.orc_g1d.restype = d
@@ -172,6 +177,17 @@ _gomp = None
 def set_atx_block(B: int) -> None:
     """Sensitivity mode: A^T.u sums samples in blocks of B rows (0 = off)."""
     load().orc_set_atx_block(int(B))
+
+
+ASSOC_DEFAULT, ASSOC_DEVICE, ASSOC_REFRUN = 0, 1, 2
+
+
+def set_assoc(mode: int = ASSOC_DEFAULT, a: int = 0, b: int = 0, seed: int = 0) -> None:
+    """Association mode of the scalar sums (vamp_oracle.c; single-rank runs):
+    ASSOC_DEVICE with a = team size T, b = workgroups of the engine's operator
+    plan; ASSOC_REFRUN with a = OpenMP threads of one reference rank and the
+    seed of its threads' arrival order; ASSOC_DEFAULT the restatement."""
+    load().orc_set_assoc(int(mode), int(a), int(b), int(seed) & (2**64 - 1))
 
 
 def g1(y: float, gam1: float, probs, vars_scaled) -> float:

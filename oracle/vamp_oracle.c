@@ -122,11 +122,194 @@ static double allreduce1(const orc_problem* pb, double v) {
     return v;
 }
 
+/* ------------------------------------------------------------------------- */
+/* Association modes (sensitivity measurement for the probit parity bar,      */
+/* tests/golden/make_c4_spread.py; ORC_ASSOC_DEFAULT otherwise).  The same    */
+/* arithmetic, the sums grouped differently:                                   */
+/*  - ORC_ASSOC_DEVICE (T, grid): as the MI355X engine groups them at its      */
+/*    team plan (vampomi_amd/csrc): a reduction over n elements on nblk blocks */
+/*    of 256 threads (thread t of block b takes e = 256 b + t, + 256 nblk, ... */
+/*    in order; a block adds its 4 waves' xor-butterfly sums in wave order;    */
+/*    the last block's thread t adds the partials of blocks t, t + 256, ...,   */
+/*    then the same butterfly and wave order: dots_part / block_put_sums /     */
+/*    red_final in kernels.hip) with nblk = red_blocks(n) for the dots, the    */
+/*    CG's cg_init / cg_update sums and the denoisers' sums, ceil(M/256) for   */
+/*    the EM round's (em_kernel); the CG's <d,p> as the one-pass operator      */
+/*    forms it (each workgroup over the columns its team member owns, then    */
+/*    lanes over workgroups: atax_team.hip, ticket_sum_blocks in kdev.h); the  */
+/*    CG's beta from the correctly rounded 1/rz (kdev.h cg_decide_into).       */
+/*  - ORC_ASSOC_REFRUN (threads, seed): as ONE rank of the reference sums with */
+/*    OMP_NUM_THREADS = threads: inner_prod's `omp parallel for reduction`     */
+/*    (src/utilities.cpp:138-158) gives each thread a contiguous static chunk, */
+/*    summed in order, and adds the threads' sums in arrival order (here a     */
+/*    seeded random order per call); sum_d and the EM sums are the reference's */
+/*    sequential loops (src/vamp_probit.cpp:120-124, src/vamp.cpp:576,590-593).*/
+/* Only single-rank runs use the non-default modes (the call counter of the    */
+/* arrival order is shared).                                                   */
+/* ------------------------------------------------------------------------- */
+static int g_assoc = ORC_ASSOC_DEFAULT;
+static int g_dev_T = 1, g_dev_grid = 256, g_ref_threads = 1;
+static uint64_t g_ref_seed = 0, g_ref_calls = 0;
+
+void orc_set_assoc(int mode, int a, int b, uint64_t seed) {
+    g_assoc = mode;
+    g_dev_T = mode == ORC_ASSOC_DEVICE && a > 0 ? a : 1;
+    g_dev_grid = mode == ORC_ASSOC_DEVICE && b > 0 ? b : 256;
+    g_ref_threads = mode == ORC_ASSOC_REFRUN && a > 0 ? a : 1;
+    g_ref_seed = seed;
+    g_ref_calls = 0;
+}
+
+/* the xor butterfly over 64 lanes (kdev.h wave_sum): every lane ends with the
+ * same value, lane 0's tree: (l, l + o) for o = 32, 16, ..., 1 */
+static double wave64(const double* v) {
+    double t[64];
+    memcpy(t, v, sizeof t);
+    for (int o = 32; o > 0; o >>= 1)
+        for (int l = 0; l < o; ++l) t[l] = t[l] + t[l + o];
+    return t[0];
+}
+
+/* 256 threads' values: each wave's butterfly, the 4 wave sums in order */
+static double block256(const double* th) {
+    return ((wave64(th) + wave64(th + 64)) + wave64(th + 128)) + wave64(th + 192);
+}
+
+static int dev_red_blocks(int64_t n) { /* kernels.hip red_blocks */
+    int64_t b = (n + 511) / 512;
+    if (b < 1) b = 1;
+    if (b > 1024) b = 1024;
+    return (int)b;
+}
+
+static int dev_cg_blocks(int64_t M) { /* kernels.hip cg_update: mblocks (2 elements per thread) */
+    int64_t b = (M + 511) / 512;
+    if (b < 1) b = 1;
+    if (b > 512) b = 512;
+    return (int)b;
+}
+
+/* sum over e < n of a[e] * b[e] (b null: a[e]) grouped as a device reduction on nblk blocks */
+static double dev_red(const double* a, const double* b, int64_t n, int nblk) {
+    const int64_t stride = (int64_t)nblk * 256;
+    double* part = (double*)malloc(sizeof(double) * (size_t)nblk);
+#pragma omp parallel for schedule(static)
+    for (int bk = 0; bk < nblk; ++bk) {
+        double th[256];
+        for (int t = 0; t < 256; ++t) {
+            double acc = 0.0;
+            for (int64_t e = (int64_t)bk * 256 + t; e < n; e += stride) acc += b ? a[e] * b[e] : a[e];
+            th[t] = acc;
+        }
+        part[bk] = block256(th);
+    }
+    double th[256];
+    for (int t = 0; t < 256; ++t) {
+        double acc = 0.0;
+        for (int bk = t; bk < nblk; bk += 256) acc += part[bk];
+        th[t] = acc;
+    }
+    free(part);
+    return block256(th);
+}
+
+/* <d, p> as the one-pass team operator forms it (grid workgroups, teams of T,
+ * teams of one XCD numbered together: atax_team.hip); each workgroup's sum
+ * over the columns its member owns, in column order, then lane l adds
+ * workgroups l, l + 64, ... and the butterfly */
+static double dev_dp(const double* d, const double* p, int64_t M, int T, int grid) {
+    const int nteams = grid / T;
+    double* part = (double*)calloc((size_t)grid, sizeof(double));
+#pragma omp parallel for schedule(static)
+    for (int bk = 0; bk < grid; ++bk) {
+        const int g = bk >> 3, member = g % T;
+        const int team = g / T + (nteams >> 3) * (bk & 7);
+        /* teams of T > 1: interleaved columns (configurations 2-5); T = 1: a
+         * contiguous range per workgroup (configurations 0-1) */
+        const int ilv = T > 1;
+        const int64_t mb = ilv ? team : (int64_t)team * M / nteams;
+        const int64_t n = ilv ? (team < M ? (M - team + nteams - 1) / nteams : 0)
+                              : (int64_t)(team + 1) * M / nteams - mb;
+        const int64_t cs = ilv ? nteams : 1;
+        double acc = 0.0;
+        for (int64_t m = 0; m < n; ++m)
+            if ((m & (T - 1)) == member) {
+                const int64_t col = mb + m * cs;
+                acc += d[col] * p[col];
+            }
+        part[bk] = acc;
+    }
+    double lanes[64];
+    for (int l = 0; l < 64; ++l) {
+        double acc = 0.0;
+        for (int bk = l; bk < grid; bk += 64) acc += part[bk];
+        lanes[l] = acc;
+    }
+    free(part);
+    return wave64(lanes);
+}
+
+/* inner_prod's local sum in the reference's OpenMP form (REFRUN) */
+static double refrun_inner(const double* a, const double* b, int64_t n) {
+    const int T = g_ref_threads;
+    double part[1024];
+    int order[1024];
+    const int nt = T < 1024 ? T : 1024;
+    const int64_t q = n / nt, r = n % nt;
+    int64_t lo = 0;
+    for (int t = 0; t < nt; ++t) {
+        const int64_t len = q + (t < r ? 1 : 0);
+        double acc = 0.0;
+        for (int64_t i = lo; i < lo + len; ++i) acc += a[i] * b[i];
+        part[t] = acc;
+        lo += len;
+        order[t] = t;
+    }
+    uint64_t h = orc_splitmix64(g_ref_seed ^ orc_splitmix64(++g_ref_calls));
+    for (int t = nt - 1; t > 0; --t) { /* Fisher-Yates: the arrival order of the threads' sums */
+        h = orc_splitmix64(h);
+        const int j = (int)(h % (uint64_t)(t + 1));
+        const int x = order[t];
+        order[t] = order[j];
+        order[j] = x;
+    }
+    double s = 0.0;
+    for (int t = 0; t < nt; ++t) s += part[order[t]];
+    return s;
+}
+
+static double seq_dot(const double* a, const double* b, int64_t n) {
+    double s = 0.0;
+    for (int64_t i = 0; i < n; ++i) s += a[i] * b[i];
+    return s;
+}
+
+/* the kind of sum a call site is (it picks the grouping in the non-default modes) */
+enum { SUM_INNER = 0, SUM_CG = 1, SUM_ACC_M = 2, SUM_EM = 3, SUM_ACC_N = 4 };
+
+static double assoc_sum(const double* a, const double* b, int64_t n, int kind) {
+    if (g_assoc == ORC_ASSOC_DEVICE) {
+        const int nblk = kind == SUM_CG ? dev_cg_blocks(n) : kind == SUM_EM ? (int)((n + 255) / 256) : dev_red_blocks(n);
+        return dev_red(a, b, n, nblk > 0 ? nblk : 1);
+    }
+    if (g_assoc == ORC_ASSOC_REFRUN) return kind == SUM_INNER || kind == SUM_CG ? refrun_inner(a, b, n) : seq_dot(a, b, n);
+    return orc_dot(a, b, n);
+}
+
+/* one sum of the current association mode (kind: 0 inner_prod, 1 the CG's
+ * sums, 2 sum over M (sum_d), 3 the EM round's, 4 sum over N; tests) */
+double orc_assoc_dot(const double* a, const double* b, int64_t n, int kind) { return assoc_sum(a, b, n, kind); }
+/* the CG's <d, p> as the device's operator forms it at plan (T, grid) (tests) */
+double orc_dev_dp(const double* d, const double* p, int64_t M, int T, int grid) { return dev_dp(d, p, M, T, grid); }
+
 /* inner_prod(u, v, sync) — src/utilities.cpp:138-158 */
+static double inner_prod_k(const orc_problem* pb, const double* a, const double* b, int64_t n, int sync, int kind) {
+    double s = assoc_sum(a, b, n, kind);
+    return sync ? allreduce1(pb, s) : s;
+}
 static double inner_prod(const orc_problem* pb, const double* a, const double* b, int64_t n,
                          int sync) {
-    double s = orc_dot(a, b, n);
-    return sync ? allreduce1(pb, s) : s;
+    return inner_prod_k(pb, a, b, n, sync, SUM_INNER);
 }
 
 /* ------------------------------------------------------------------------- */
@@ -482,26 +665,27 @@ static void precondCG(orc_vamp* s, const double* v, const double* mu_start, doub
     memcpy(p, z, sizeof(double) * (size_t)M);
     double prev_onsager = 0;
     int it_done = 0;
-    double norm_v = sqrt(inner_prod(pb, v, v, M, 1));
+    double norm_v = sqrt(inner_prod_k(pb, v, v, M, 1, SUM_CG));
     for (int i = 0; i < s->CG_max_iter; ++i) {
         it_done = i + 1;
         lmmse_mult(s, p, tau, d, tmpN);
-        double rz = inner_prod(pb, r, z, M, 1);
-        double dp = inner_prod(pb, d, p, M, 1);
+        double rz = inner_prod_k(pb, r, z, M, 1, SUM_CG);
+        double dp = g_assoc == ORC_ASSOC_DEVICE ? allreduce1(pb, dev_dp(d, p, M, g_dev_T, g_dev_grid))
+                                                : inner_prod_k(pb, d, p, M, 1, SUM_CG);
         double alpha = rz / dp;
         for (int64_t j = 0; j < M; ++j) mu[j] += alpha * p[j];
         if (denoiser == 0) {
-            double onsager = s->gam2 * inner_prod(pb, v, mu, M, 1);
+            double onsager = s->gam2 * inner_prod_k(pb, v, mu, M, 1, SUM_CG);
             double rel_err = onsager != 0 ? fabs((onsager - prev_onsager) / onsager) : 1;
             if (rel_err < 1e-8) break;
             prev_onsager = onsager;
         }
-        double beta = pow(rz, -1); /* :731 */
+        double beta = g_assoc == ORC_ASSOC_DEVICE ? 1.0 / rz : pow(rz, -1); /* :731 */
         for (int64_t j = 0; j < M; ++j) r[j] -= d[j] * alpha;
         for (int64_t j = 0; j < M; ++j) z[j] = r[j] / diag;
-        beta *= inner_prod(pb, r, z, M, 1);
+        beta *= inner_prod_k(pb, r, z, M, 1, SUM_CG);
         for (int64_t j = 0; j < M; ++j) p[j] = z[j] + beta * p[j];
-        double rel_err = sqrt(inner_prod(pb, r, r, M, 1)) / norm_v;
+        double rel_err = sqrt(inner_prod_k(pb, r, r, M, 1, SUM_CG)) / norm_v;
         if (s->verbosity >= 2 && pb->rank == 0)
             printf("[CG] it = %d: ||r_it|| / ||RHS|| = %g\n", i, rel_err);
         if (rel_err < s->CG_err_tol) break;
@@ -564,7 +748,7 @@ static void update_prior(orc_vamp* s) {
             /* blocked deterministic sum of pin */
             double* onesv = (double*)malloc(sizeof(double) * (size_t)(M > 0 ? M : 1));
             for (int64_t i = 0; i < M; ++i) onesv[i] = 1.0;
-            lam_local = orc_dot(pin, onesv, M);
+            lam_local = assoc_sum(pin, onesv, M, SUM_EM);
             free(onesv);
         }
         double lambda_total = allreduce1(pb, lam_local);
@@ -583,8 +767,8 @@ static void update_prior(orc_vamp* s) {
                 colb[i] = beta[i * Lm + j];
                 colg[i] = gammas[i * Lm + j];
             }
-            double res = orc_dot(colb, pin, M);
-            double res_gammas = orc_dot(colg, pin, M);
+            double res = assoc_sum(colb, pin, M, SUM_EM);
+            double res_gammas = assoc_sum(colg, pin, M, SUM_EM);
             double res_gammas_total = allreduce1(pb, res_gammas);
             double res_total = allreduce1(pb, res);
             if (s->learn_vars == 1) s->vars[j + 1] = res_gammas_total / res_total;
@@ -763,7 +947,7 @@ int orc_vamp_infere_linear(const orc_problem* pb, const orc_params* prm, orc_res
         {
             double* onesv = tmpM;
             for (int64_t i = 0; i < M; ++i) onesv[i] = 1.0;
-            double sum_d = orc_dot(x1_hat_d, onesv, M);
+            double sum_d = assoc_sum(x1_hat_d, onesv, M, SUM_ACC_M);
             alpha1 = allreduce1(pb, sum_d) / (double)Mt; /* :221-223 */
         }
         eta1 = s.gam1 / alpha1;
@@ -1057,7 +1241,7 @@ int orc_vamp_infere_probit(const orc_problem* pb, const orc_params* prm, orc_res
         {
             double* onesv = v;
             for (int64_t i = 0; i < M; ++i) onesv[i] = 1.0;
-            alpha1 = allreduce1(pb, orc_dot(tmpM, onesv, M)) / (double)Mt; /* :120-129 */
+            alpha1 = allreduce1(pb, assoc_sum(tmpM, onesv, M, SUM_ACC_M)) / (double)Mt; /* :120-129 */
         }
         eta1 = s.gam1 / alpha1;          /* :130 */
         if (it > 1) update_prior(&s);    /* :139 (after g1 / g1d) */
@@ -1091,7 +1275,7 @@ int orc_vamp_infere_probit(const orc_problem* pb, const orc_params* prm, orc_res
             for (int64_t i = 0; i < N; ++i) zacc[i] = orc_g1d_bin(p1[i], tau1, y[i]);
             double* onesv = p2;
             for (int64_t i = 0; i < N; ++i) onesv[i] = 1.0;
-            beta1 = orc_dot(zacc, onesv, N); /* local: y and p1 are replicated */
+            beta1 = assoc_sum(zacc, onesv, N, SUM_ACC_N); /* local: y and p1 are replicated */
         }
         if (beta1 >= N) beta1 = N - 1.0;
         beta1 /= N;

@@ -78,6 +78,16 @@ void orc_atx(const double* X, int64_t N, int64_t ld, int64_t M, const double* ma
 /* sensitivity mode: orc_atx sums samples in blocks of B rows (0 = sequential,
  * the reference's order); process-wide, test infrastructure only */
 void orc_set_atx_block(int B);
+/* Association modes (sensitivity measurement, vamp_oracle.c): the default
+ * restatement; the MI355X engine's grouping of every scalar reduction at a
+ * team plan (a = team size T, b = workgroups); one reference rank's OpenMP
+ * inner_prod with a = threads and a seeded arrival order of their sums. */
+#define ORC_ASSOC_DEFAULT 0
+#define ORC_ASSOC_DEVICE 1
+#define ORC_ASSOC_REFRUN 2
+void orc_set_assoc(int mode, int a, int b, uint64_t seed);
+double orc_assoc_dot(const double* a, const double* b, int64_t n, int kind);
+double orc_dev_dp(const double* d, const double* p, int64_t M, int T, int grid);
 
 /* ---- denoiser (src/vamp.cpp:440-492) ---- */
 double orc_g1(double y, double gam1, const double* probs, const double* vars, int L);

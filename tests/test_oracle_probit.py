@@ -112,3 +112,96 @@ def test_probit_learns_the_signal():
     m = g["metrics"]
     assert m[-1, 10] > 0.9 and m[-1, 11] > 0.7  # accuracy of x2, corr(x2, beta)
     assert np.isnan(m[0, 5])  # x1 = 0 at iteration 1: corr 0/0
+
+
+def _wave64(v):
+    t = list(v)
+    o = 32
+    while o:
+        for l in range(o):
+            t[l] = t[l] + t[l + o]
+        o >>= 1
+    return t[0]
+
+
+def _block256(th):
+    return ((_wave64(th[:64]) + _wave64(th[64:128])) + _wave64(th[128:192])) + _wave64(th[192:256])
+
+
+def _dev_red_py(a, b, nblk):
+    """kernels.hip's grouping of a reduction (dots_part, block_put_sums, red_final), in Python floats."""
+    n, stride = len(a), nblk * 256
+    part = []
+    for bk in range(nblk):
+        th = []
+        for t in range(256):
+            acc = 0.0
+            for e in range(bk * 256 + t, n, stride):
+                acc += float(a[e]) * float(b[e])
+            th.append(acc)
+        part.append(_block256(th))
+    th = []
+    for t in range(256):
+        acc = 0.0
+        for bk in range(t, nblk, 256):
+            acc += part[bk]
+        th.append(acc)
+    return _block256(th)
+
+
+def test_association_modes():
+    """The oracle's association modes (vamp_oracle.c, the probit bar's
+    measurement): the default is orc_dot; DEVICE groups a sum exactly as
+    kernels.hip's reductions do (checked against a Python restatement of
+    dots_part / block_put_sums / red_final, bit for bit) and <d,p> as the team
+    operator does; REFRUN with one thread is the reference's sequential loop
+    and with several a reordering of the same chunk sums."""
+    import ctypes as C
+
+    lib = O.load()
+    P = lambda x: x.ctypes.data_as(C.c_void_p)  # noqa: E731
+    rng = np.random.default_rng(11)
+    for n in (1, 300, 5000, 70001):
+        a, b = rng.normal(size=n), rng.normal(size=n)
+        O.set_assoc()
+        assert lib.orc_assoc_dot(P(a), P(b), n, 0) == lib.orc_dot(P(a), P(b), n)
+        O.set_assoc(O.ASSOC_DEVICE, 16, 256)
+        if n <= 5000:
+            nblk = max(1, min(1024, -(-n // 512)))
+            assert lib.orc_assoc_dot(P(a), P(b), n, 0) == _dev_red_py(a, b, nblk), n
+            assert lib.orc_assoc_dot(P(a), P(b), n, 3) == _dev_red_py(a, b, -(-n // 256)), n  # the EM round's grid
+        O.set_assoc(O.ASSOC_REFRUN, 1, 0, 5)
+        seq = 0.0
+        for i in range(n):
+            seq += float(a[i]) * float(b[i])
+        assert lib.orc_assoc_dot(P(a), P(b), n, 0) == seq
+        O.set_assoc(O.ASSOC_REFRUN, 8, 0, 5)
+        got = {lib.orc_assoc_dot(P(a), P(b), n, 0) for _ in range(16)}
+        assert all(abs(g - seq) <= 1e-12 * (np.sum(np.abs(a * b)) + 1e-300) for g in got)
+        if n >= 5000:
+            assert len(got) > 1  # the arrival order differs from call to call
+    O.set_assoc()
+    # <d, p> of the operator: member-owned columns per workgroup, lanes over workgroups, butterfly
+    M = 4099
+    d, p = rng.normal(size=M), rng.normal(size=M)
+    for T, grid in ((16, 256), (2, 256), (1, 256)):
+        nteams = grid // T
+        part = []
+        for bk in range(grid):
+            g, member = bk >> 3, (bk >> 3) % T
+            team = g // T + (nteams >> 3) * (bk & 7)
+            if T > 1:
+                cols = [team + m * nteams for m in range(max(0, -(-(M - team) // nteams))) if (m & (T - 1)) == member]
+            else:
+                cols = range(team * M // nteams, (team + 1) * M // nteams)
+            acc = 0.0
+            for c in cols:
+                acc += float(d[c]) * float(p[c])
+            part.append(acc)
+        lanes = []
+        for l in range(64):
+            acc = 0.0
+            for bk in range(l, grid, 64):
+                acc += part[bk]
+            lanes.append(acc)
+        assert lib.orc_dev_dp(P(d), P(p), M, T, grid) == _wave64(lanes), T
