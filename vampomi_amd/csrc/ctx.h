@@ -49,6 +49,11 @@ struct CollScope {
 struct VampRun;
 class IterWriter;
 struct LoopbackComm;  // engine.cpp: test-only in-process communicator
+struct ShmComm;       // shmcomm.cpp: test-only cross-process communicator (VAMPOMI_COMM=shm)
+std::shared_ptr<ShmComm> shm_join(const void* id, int P, int rank, std::string* err);
+std::string shm_allreduce(ShmComm& s, int rank, double* buf, size_t n, uint64_t seq, const char* site, int line,
+                          double limit_s);
+void shm_poison(ShmComm& s, const std::string& why);
 
 struct TimedLaunch {
     hipEvent_t a, b;
@@ -92,6 +97,7 @@ struct vampomi_ctx {
     ncclComm_t comm = nullptr;
     bool use_comm = false;  // nranks > 1 (or VAMPOMI_FORCE_RCCL): all-reduces through RCCL
     std::shared_ptr<LoopbackComm> loopback;  // VAMPOMI_COMM=loopback: ranks are threads of one process
+    std::shared_ptr<ShmComm> shm;            // VAMPOMI_COMM=shm: ranks are processes of one host
     uint64_t coll_seq = 0;  // collectives issued so far (divergence checks)
     bool aborted = false;   // comm_abort ran: no further collective
 

@@ -464,9 +464,26 @@ static vampomi_status rccl_check(vampomi_ctx* c, size_t n, const char* site, int
     return VAMPOMI_OK;
 }
 
+// the shm communicator (shmcomm.cpp): the buffer through the host, summed in
+// rank order in the shared segment, like the loopback one
+static vampomi_status shm_allreduce_dev(vampomi_ctx* c, double* buf, size_t n, const char* site, int line) {
+    std::vector<double> h(n);
+    HIPCHK(hipMemcpyAsync(h.data(), buf, n * 8, hipMemcpyDeviceToHost, c->st));
+    STCHK(sync_stream(c, c->st));
+    const std::string err = shm_allreduce(*c->shm, c->rank, h.data(), n, ++c->coll_seq, site, line, coll_limit_s(c));
+    if (!err.empty()) {
+        c->aborted = true;  // the segment is poisoned already: every rank fails at its next collective
+        return fail(VAMPOMI_ERR_STATE, err + " (rank " + std::to_string(c->rank) + ")");
+    }
+    HIPCHK(hipMemcpyAsync(buf, h.data(), n * 8, hipMemcpyHostToDevice, c->st));
+    STCHK(sync_stream(c, c->st));
+    return VAMPOMI_OK;
+}
+
 vampomi_status allreduce_dev(vampomi_ctx* c, double* buf, size_t n, const char* site, int line) {
     if (!c->use_comm || n == 0) return VAMPOMI_OK;
     if (c->loopback) return loopback_allreduce(c, buf, n, site, line);
+    if (c->shm) return shm_allreduce_dev(c, buf, n, site, line);
     ++c->coll_seq;
     static const bool check = std::getenv("VAMPOMI_COLL_CHECK") && std::atoi(std::getenv("VAMPOMI_COLL_CHECK"));
     if (check) STCHK(rccl_check(c, n, site, line));
@@ -501,6 +518,8 @@ void comm_abort(vampomi_ctx* c, const std::string& why) {
         std::lock_guard<std::mutex> g(c->loopback->mu);
         if (c->loopback->poison.empty()) c->loopback->poison = "rank " + std::to_string(c->rank) + " aborted: " + why;
         c->loopback->cv.notify_all();
+    } else if (c->shm) {
+        shm_poison(*c->shm, "rank " + std::to_string(c->rank) + " aborted: " + why);
     } else if (c->comm) {
         (void)ncclCommAbort(c->comm);
         c->comm = nullptr;
@@ -1273,6 +1292,11 @@ extern "C" vampomi_status vampomi_open(const vampomi_shard_desc* d, vampomi_ctx*
     if (c->use_comm && mode && std::strcmp(mode, "loopback") == 0) {
         if (!d->comm_id) return fail(VAMPOMI_ERR_ARG, "the loopback communicator needs a communicator id");
         c->loopback = loopback_join(d->comm_id, c->nranks);
+    } else if (c->use_comm && mode && std::strcmp(mode, "shm") == 0) {
+        if (!d->comm_id) return fail(VAMPOMI_ERR_ARG, "the shm communicator needs a communicator id");
+        std::string err;
+        c->shm = shm_join(d->comm_id, c->nranks, c->rank, &err);
+        if (!c->shm) return fail(VAMPOMI_ERR_STATE, err);
     } else if (c->use_comm) {
         ncclUniqueId id;
         if (d->comm_id)
