@@ -319,8 +319,8 @@ vampomi_status vampomi_reset_stats(vampomi_ctx* ctx);
  * -1 (operator: whole columns per workgroup while
  * K*N fits the LDS, else teams of workgroups; 0 forces the whole-column
  * kernel, T*10 + c (c < 10) or 1000 + T*100 + c the team kernel with team size T and configuration c,
- * vampomi_amd/csrc/atax_team.hip).  which = 4: the side stream of the
- * prefetched EM/denoiser, 0 off, 1 on (default: on with several ranks).
+ * vampomi_amd/csrc/atax_team.hip).  which = 4 (the side stream of rounds
+ * 2-5) was removed: VAMPOMI_ERR_ARG.
  * which = 5: the CG head start of the linear model (the Onsager solve's first
  * step in the pass that starts the x2 solve, pcg.cpp), 0 off, 1 on (default
  * on; VAMPOMI_HEADSTART=0 turns it off at vampomi_open).  which = 6: the

@@ -125,6 +125,59 @@ def oracle_with_spread(X, y, beta, Mt, ranks=(2, 3, 4), blocks=(), ref=None, per
     return ref, sp
 
 
+# The reference's own runs: one rank with OMP_NUM_THREADS = T sums each
+# inner_prod over T contiguous chunks and adds the threads' sums in arrival
+# order (src/utilities.cpp:138-158; ORC_ASSOC_REFRUN, vamp_oracle.c), and
+# `mpirun -np P` splits every sum over markers over the ranks (divide_work).
+# Every member of this ensemble is a run the reference itself performs.
+REF_THREADS = (4, 8, 16, 32, 64, 128)
+
+
+def reference_ensemble(X, y, beta, Mt, ref, threads=REF_THREADS, seeds=(1, 2, 3, 4), ranks=(2, 3), **kw):
+    """Per-variant spread (norm-relative change of x1 / r1 per iteration, and
+    element-wise of params, metrics, prior) of the reference's own runs around
+    the oracle's restatement run `ref`: one rank at T threads x arrival-order
+    seeds, and P ranks.  Returns {(kind, a, b): own} with kind 0 = (T, seed),
+    1 = (P ranks, 0)."""
+    out = {}
+    n = ref["iterations"]
+
+    def own_of(res):
+        own = {}
+        for key in ("x1", "r1"):
+            h = np.concatenate([r[f"{key}_hist"] for r in res], axis=1)
+            num = np.linalg.norm(h - ref[f"{key}_hist"], axis=1)
+            den = np.maximum(np.linalg.norm(ref[f"{key}_hist"], axis=1), 1e-300)
+            own[key] = num / den
+        for key in ("params", "metrics", "prior"):
+            if key in ref:
+                a, b = res[0][key], ref[key]
+                with np.errstate(invalid="ignore", divide="ignore"):
+                    own[key] = np.where(np.isnan(a) & np.isnan(b), 0.0, np.abs(a - b) / np.maximum(np.abs(b), 1e-300))
+        return own
+
+    kw = {k: v for k, v in kw.items() if k not in ("out_dir", "out_name")}
+    for T in threads:
+        for sd in seeds:
+            O.set_assoc(O.ASSOC_REFRUN, T, 0, sd)
+            try:
+                r = O.vamp_infere(X, y, Mt, true_signal=beta, **kw)
+            finally:
+                O.set_assoc()
+            assert r["iterations"] == n
+            out[(0, T, sd)] = own_of([r])
+    for P in ranks:
+        res = sharded_oracle(X, y, beta, Mt, P, **kw)
+        assert res[0]["iterations"] == n
+        out[(1, P, 0)] = own_of(res)
+    return out
+
+
+def ensemble_quantile(per_variant: dict, key: str, q: float = 0.9):
+    """The q-quantile over the ensemble's variants, per iteration (or element)."""
+    return np.quantile(np.stack([v[key] for v in per_variant.values()]), q, axis=0)
+
+
 # The probit parity bar's multiple of the oracle's own rank-count spread
 # (DESIGN.md §3): the GPU must stay within PROBIT_K x the amount by which the
 # reference's own result moves when its all-reduce order changes.  Set to

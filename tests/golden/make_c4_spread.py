@@ -1,28 +1,34 @@
-"""C4 shard sensitivity fixture: how far the reference's own probit result
-moves under a change of summation order, measured on the oracle at the whole
-per-GPU C4 shard (BASELINE configs[3]: N = 50,000 samples; 50,000 of its
-200,000 markers), 8 iterations (src/vamp_probit.cpp:19-488).
+"""C4 shard parity fixture (round 6): how far the reference's OWN runs move
+from one another on the whole per-GPU C4 probit shard (BASELINE configs[3]:
+N = 50,000 samples; 50,000 of its 200,000 markers), 8 iterations
+(src/vamp_probit.cpp:19-488), and where the device's own grouping of the sums
+lands, measured on the oracle.
 
 The problem: X = the index-keyed Gaussian design (seed 20250711, bit-identical
 on the device, `Data.generate`), y / beta = tests/_data.py phen_from_markers
 thresholded at 0.  Stored (tests/golden/oracle_c4_spread.npz):
 * the inputs the device cannot regenerate by itself: y (0/1) and beta;
-* the single-rank oracle run's per-iteration x1 / r1 norms, params and counts
-  (the GPU test re-runs the oracle on the GPU box's host and checks it is this
-  run, bit for bit);
-* per variant, per iteration, the norm-relative change of x1 / r1 (and
-  element-wise of params, metrics, prior rows) against the single-rank run:
-  ranks P = 2, 3 (what `mpirun -np` changes), P = 64, 128 virtual shards (the
-  sums over markers split as finely as the device's team slots split them),
-  and orc_atx's sample sums in blocks of 128 rows, alone and with 128 shards
-  (the device's A^T sums over lanes, waves and team members).
+* the restatement's run (ORC_ASSOC_DEFAULT): per-iteration x1 / r1 norms,
+  params and counts (the GPU test re-runs it on the GPU box's host and checks
+  it is this run);
+* the ensemble of the reference's own runs (tests/_data.py
+  reference_ensemble): one rank at OMP_NUM_THREADS = 4 ... 128, four arrival
+  orders of the threads' sums each (inner_prod's `omp parallel for
+  reduction`, src/utilities.cpp:138-158; sum_d and the EM sums sequential as
+  the reference writes them), and 2 and 3 ranks (`mpirun -np`).  Per variant,
+  per iteration: the norm-relative change of x1 / r1 (element-wise of params,
+  metrics, prior rows) against the restatement's run.  The GPU test's bar is
+  PROBIT_K_ENSEMBLE x the 90th percentile over these variants;
+* (tests/golden/oracle_c4_devorder.npz) the device-order run
+  (ORC_ASSOC_DEVICE at the C4 plan: teams of 16, 256 workgroups): its x1 / r1
+  at every iteration as float32 differences from the restatement's run
+  (exact to ~1e-16 relative after adding back), its counts and params.  The
+  GPU test checks the GPU lands on it.
 
-tests/test_gpu_probit.py::test_c4_full_shard_vs_oracle holds the device to
-PROBIT_K x the largest of these per iteration.  Run in the build container
-(20 GB for X; about 25 min on 8 cores):
+Run in the build container (20 GB for X; about 2 h on 8 cores for the
+ensemble, 10 min for the device-order part):
 
-    python tests/golden/make_c4_spread.py
-    python tests/golden/make_c4_spread.py --add 256 512 1024   # finer virtual shards
+    python tests/golden/make_c4_spread.py [ensemble] [device]
 """
 from __future__ import annotations
 
@@ -37,13 +43,12 @@ ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
-from _data import oracle_with_spread, phen_from_markers  # noqa: E402
+from _data import phen_from_markers, reference_ensemble  # noqa: E402
 from oracle import pyoracle as O  # noqa: E402
 
 N, MT, SEED, ITS = 50000, 50000, 20250711, 8
-RANKS = (2, 3, 64, 128)
-BLOCKS = ((1, 128), (128, 128))
 GEN_GAUSS = 0
+DEV_T, DEV_GRID = 16, 256  # the C4 shard's operator plan on a 256-CU MI355X (tests/test_op_plan.py)
 
 
 def c4_inputs(X):
@@ -52,38 +57,42 @@ def c4_inputs(X):
 
 
 def main():
-    """`make_c4_spread.py` makes the fixture; `make_c4_spread.py --add P ...`
-    adds P-rank variants to the committed one (the single-rank run is redone,
-    the stored variants kept)."""
-    add = [int(a) for a in sys.argv[sys.argv.index("--add") + 1:]] if "--add" in sys.argv else None
+    parts = [a for a in sys.argv[1:] if a in ("ensemble", "device")] or ["ensemble", "device"]
     t0 = time.time()
     X = O.generate_markers(SEED, GEN_GAUSS, N, 0, MT)
     y, beta = c4_inputs(X)
     kw = dict(model="bin_class", max_iter=ITS, stop_criteria_thr=0.0)
     ref = O.vamp_infere(X, y, MT, true_signal=beta, **kw)
-    print(f"single rank: {time.time() - t0:.0f} s", flush=True)
-    pv = {}
-    if add:
-        old = np.load(os.path.join(HERE, "oracle_c4_spread.npz"))
-        assert np.array_equal(old["ref_x1_norm"], np.linalg.norm(ref["x1_hist"], axis=1)), "not the stored run"
-        for i, v in enumerate(old["variants"]):
-            pv[tuple(int(a) for a in v)] = {key: old[f"spread_{key}"][i] for key in ("x1", "r1", "params", "metrics",
-                                                                                    "prior")}
-        oracle_with_spread(X, y, beta, MT, ranks=tuple(add), blocks=(), ref=ref, per_variant=pv, **kw)
-    else:
-        oracle_with_spread(X, y, beta, MT, ranks=RANKS, blocks=BLOCKS, ref=ref, per_variant=pv, **kw)
-    variants = sorted(pv)
-    out = dict(N=N, Mt=MT, seed=SEED, its=ITS, y=y.astype(np.uint8), beta=beta,
-               ref_x1_norm=np.linalg.norm(ref["x1_hist"], axis=1), ref_r1_norm=np.linalg.norm(ref["r1_hist"], axis=1),
-               ref_params=ref["params"], ref_cg=ref["cg_iters"], ref_ons=ref["ons_iters"], ref_L=ref["L"],
-               variants=np.array(variants, dtype=np.int64))
-    for key in ("x1", "r1", "params", "metrics", "prior"):
-        out[f"spread_{key}"] = np.stack([pv[v][key] for v in variants])
-    np.savez_compressed(os.path.join(HERE, "oracle_c4_spread.npz"), **out)
-    for v in variants:
-        print(v, "x1", np.array2string(pv[v]["x1"], precision=2), "r1", np.array2string(pv[v]["r1"], precision=2))
-    print(f"oracle_c4_spread.npz: {time.time() - t0:.0f} s; cg {ref['cg_iters'].tolist()} "
-          f"ons {ref['ons_iters'].tolist()}")
+    print(f"restatement: {time.time() - t0:.0f} s; cg {ref['cg_iters'].tolist()} ons {ref['ons_iters'].tolist()}",
+          flush=True)
+    base = dict(N=N, Mt=MT, seed=SEED, its=ITS, ref_x1_norm=np.linalg.norm(ref["x1_hist"], axis=1),
+                ref_r1_norm=np.linalg.norm(ref["r1_hist"], axis=1), ref_params=ref["params"], ref_cg=ref["cg_iters"],
+                ref_ons=ref["ons_iters"], ref_L=ref["L"])
+    if "device" in parts:
+        O.set_assoc(O.ASSOC_DEVICE, DEV_T, DEV_GRID)
+        try:
+            dv = O.vamp_infere(X, y, MT, true_signal=beta, **kw)
+        finally:
+            O.set_assoc()
+        assert np.array_equal(dv["cg_iters"], ref["cg_iters"]) and np.array_equal(dv["ons_iters"], ref["ons_iters"])
+        np.savez_compressed(os.path.join(HERE, "oracle_c4_devorder.npz"), **base, dev_T=DEV_T, dev_grid=DEV_GRID,
+                            dev_x1_diff=(dv["x1_hist"] - ref["x1_hist"]).astype(np.float32),
+                            dev_r1_diff=(dv["r1_hist"] - ref["r1_hist"]).astype(np.float32),
+                            dev_params=dv["params"], dev_L=dv["L"])
+        dgap = np.linalg.norm(dv["x1_hist"] - ref["x1_hist"], axis=1) / np.linalg.norm(ref["x1_hist"], axis=1)
+        print(f"device order: {time.time() - t0:.0f} s; vs restatement", np.array2string(dgap, precision=2),
+              flush=True)
+    if "ensemble" in parts:
+        pv = reference_ensemble(X, y, beta, MT, ref, **kw)
+        variants = sorted(pv)
+        out = dict(base, y=y.astype(np.uint8), beta=beta, variants=np.array(variants, dtype=np.int64))
+        for key in ("x1", "r1", "params", "metrics", "prior"):
+            out[f"spread_{key}"] = np.stack([pv[v][key] for v in variants])
+        np.savez_compressed(os.path.join(HERE, "oracle_c4_spread.npz"), **out)
+        for v in variants:
+            print(v, "x1", np.array2string(pv[v]["x1"], precision=2), flush=True)
+        print("x1 q90", np.array2string(np.quantile(out["spread_x1"], 0.9, axis=0), precision=2))
+    print(f"done: {time.time() - t0:.0f} s")
 
 
 if __name__ == "__main__":

@@ -57,8 +57,10 @@ def _launch(cmd, P, tmp, tag, extra_env=None):
     rdzv = os.path.join(tmp, f".{tag}.rdzv")
     procs, logs = [], []
     for r in range(P):
+        # VAMPOMI_RUN_ID: the job's id (as mpirun / torchrun / slurm give one): the rendezvous needs no
+        # 3 s settling of the id file; VAMPOMI_COMM_INIT_TIMEOUT_S bounds the join
         env = dict(os.environ, VAMPOMI_RANK=str(r), VAMPOMI_NRANKS=str(P), VAMPOMI_COMM="shm", VAMPOMI_RDZV=rdzv,
-                   VAMPOMI_COLL_TIMEOUT_S="60")
+                   VAMPOMI_COLL_TIMEOUT_S="60", VAMPOMI_COMM_INIT_TIMEOUT_S="60", VAMPOMI_RUN_ID=f"{tag}-{os.getpid()}")
         env.update(extra_env or {})
         log = os.path.join(tmp, f"{tag}_rank{r}.log")
         logs.append(log)
@@ -108,7 +110,7 @@ def _loopback(N, Mt, P, Xp, yp, tp, out, its, model):
     try:
         th = [threading.Thread(target=work, args=(r,), daemon=True) for r in range(P)]
         [t.start() for t in th]
-        [t.join(300) for t in th]
+        [t.join(120) for t in th]
         assert not any(t.is_alive() for t in th), "loopback ranks stuck"
         assert not errs, errs
     finally:
@@ -130,7 +132,7 @@ def test_cli_processes_match_loopback_ranks_bytewise(tmp_path, model, P):
     for d in (out_p, out_l, out_1):
         d.mkdir()
     procs, logs = _launch(_cli(Xp, yp, tp, N, Mt, out_p, its, model), P, str(tmp_path), "job")
-    rcs = _wait(procs, 240)
+    rcs = _wait(procs, 120)
     assert rcs == [0] * P, [open(lg).read()[-2000:] for lg in logs]
     assert not os.path.exists(tmp_path / ".job.rdzv")  # rank 0 removed the rendezvous file after the join
     _loopback(N, Mt, P, Xp, yp, tp, out_l, its, model)
@@ -140,7 +142,7 @@ def test_cli_processes_match_loopback_ranks_bytewise(tmp_path, model, P):
     for f in files:
         assert (out_p / f).read_bytes() == (out_l / f).read_bytes(), f
     # against the one-process CLI: the same counts (and, linear, x1_hat within the parity bar)
-    r = subprocess.run(_cli(Xp, yp, tp, N, Mt, out_1, its, model), capture_output=True, text=True, timeout=240)
+    r = subprocess.run(_cli(Xp, yp, tp, N, Mt, out_1, its, model), capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout[-2000:]
     one = [(int(a), int(b), int(c)) for a, b, c in
            re.findall(r"it (\d+): CG iterations (\d+), onsager CG iterations (\d+)", r.stdout)]
@@ -164,11 +166,11 @@ def test_cli_rank_killed_mid_run_ends_every_process(tmp_path):
     t0 = time.monotonic()
     while not _counts(logs[0]) or _counts(logs[0])[-1][0] < 3:
         assert procs[0].poll() is None and procs[1].poll() is None, [open(lg).read()[-2000:] for lg in logs]
-        assert time.monotonic() - t0 < 120, "the run did not get under way"
+        assert time.monotonic() - t0 < 90, "the run did not get under way"
         time.sleep(0.05)
     os.kill(procs[1].pid, signal.SIGKILL)
     t_kill = time.monotonic()
-    rc0 = procs[0].wait(90)
+    rc0 = procs[0].wait(70)
     rc1 = procs[1].wait(10)
     waited = time.monotonic() - t_kill
     assert rc1 == -signal.SIGKILL

@@ -290,47 +290,29 @@ def test_divergent_collectives_fail_on_every_rank(monkeypatch):
         assert "rank 0:" in str(e) and "rank 1:" in str(e)
 
 
-@pytest.mark.parametrize("P", [1, 2])
-@pytest.mark.parametrize("em", [dict(), dict(EM_max_iter=3, EM_err_thr=1e-9), dict(learn_prior_delay=4)])
-def test_side_stream_bitwise(monkeypatch, P, em):
-    """north_star's second HIP stream: the prefetched EM sums and denoiser of
-    iteration it+1 on the side stream beside iteration it's reductions give
-    bitwise the one-stream results (same fixed-order kernels), on one rank and
-    on two loopback ranks, with one EM round, several, and none (delay)."""
-    N, Mt = 1001, 2003
-    X, y, beta = make_problem(N, Mt)
-    out = {}
-    for side in (0, 1):
-        def fn(r, d, side=side):
-            d.set_variant(4, side)
-            return _vamp(d, X, y, beta, max_iter=12, stop_criteria_thr=0.0, **em)
-
-        if P == 1:
-            with va.Data(N, Mt) as d:
-                out[side] = [fn(0, d)]
-        else:
-            out[side] = run_ranks(monkeypatch, P, N, Mt, fn)
-    for a, b in zip(out[0], out[1]):
-        for k in ("iterations", "cg_iters", "ons_iters", "L"):
-            assert a[k] == b[k], k
-        for k in ("x1_hist", "r1_hist", "params", "metrics"):
-            np.testing.assert_array_equal(np.asarray(a[k]), np.asarray(b[k]), err_msg=k)
+def test_side_stream_removed():
+    """Rounds 2-5 ran the prefetched EM / denoiser on a second HIP stream
+    (set_variant(4)); it never shortened an iteration (0.5 % slower at one
+    rank, unused by the host-free multi-rank tail) and was removed in round 6
+    (DESIGN.md §6).  The hook now refuses, so no caller believes it is on."""
+    with va.Data(1001, 2003) as d:
+        with pytest.raises(va.VampomiError) as e:
+            d.set_variant(4, 1)
+        assert e.value.status == 1  # ERR_ARG
 
 
 @pytest.mark.parametrize("P", [1, 2])
-def test_team_operator_beside_side_stream_and_writer(monkeypatch, tmp_path, P):
+def test_team_operator_beside_the_writer(monkeypatch, tmp_path, P):
     """N = 12,000: the one-pass operator runs as teams of 4 workgroups that
-    must all be resident.  With the side stream on (EM / denoiser of the next
-    iteration) and the iteration writer's kernel + copy stream busy, every
-    team launch still completes (no hand-off timeout) and the results are
-    bitwise those of the plain one-stream run without files; the files hold
-    what the history holds."""
+    must all be resident.  With the iteration writer's kernel + copy stream
+    busy, every team launch still completes (no hand-off timeout) and the
+    results are bitwise those of the run without files; the files hold what
+    the history holds."""
     N, Mt, its = 12000, 3001, 8
     X, y, beta = make_problem(N, Mt, seed=4)
     out = {}
     for busy in (0, 1):
         def fn(r, d, busy=busy):
-            d.set_variant(4, busy)
             kw = dict(out_dir=str(tmp_path / f"b{busy}"), out_name="t") if busy else {}
             return _vamp(d, X, y, beta, max_iter=its, stop_criteria_thr=0.0, **kw)
 

@@ -50,7 +50,7 @@ struct VampRun;
 class IterWriter;
 struct LoopbackComm;  // engine.cpp: test-only in-process communicator
 struct ShmComm;       // shmcomm.cpp: test-only cross-process communicator (VAMPOMI_COMM=shm)
-std::shared_ptr<ShmComm> shm_join(const void* id, int P, int rank, std::string* err);
+std::shared_ptr<ShmComm> shm_join(const void* id, int P, int rank, double limit_s, std::string* err);
 std::string shm_allreduce(ShmComm& s, int rank, double* buf, size_t n, uint64_t seq, const char* site, int line,
                           double limit_s);
 void shm_poison(ShmComm& s, const std::string& why);
@@ -76,18 +76,7 @@ struct vampomi_ctx {
     int64_t N = 0, Mt = 0, M = 0, S = 0, Mm = 0, ld = 0;
     double alpha_scale = 1.0;
     double sqrtN = 1.0;
-    hipStream_t st = nullptr;
-    // side stream: the prefetched denoiser/EM of iteration it+1 runs on it
-    // beside iteration it's updateNoisePrec / err_measures / NMSE reductions
-    // on st (north_star's second HIP stream). Collectives stay on st. Its
-    // reductions have their own partials and ticket; st waits on ev_join
-    // before it reads their results (DotBatch::side, flush)
-    hipStream_t st2 = nullptr;
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-    double* red_part2 = nullptr;
-    unsigned* ticket2 = nullptr;
-    bool side_open = false;  // the side stream has work st has not joined (DotBatch fork .. flush)
-    bool side_on = false;  // default: several ranks; VAMPOMI_SIDE_STREAM=0/1 or vampomi_dev_set_variant(c, 4, 0/1)
+    hipStream_t st = nullptr;  // every launch and collective of the context (one stream: DESIGN.md §6)
     bool mr_tail = true;   // several ranks: the linear iteration's tail without host waits (vamp.cpp), as agreed
     double coll_limit_s = 0.0;  // > 0: the limit of the collective in progress (vampomi_barrier_timeout)
     bool mr_tail_req = true;  // this rank's VAMPOMI_MR_TAIL (0: off), agreed over the ranks by op_agree
@@ -119,7 +108,7 @@ struct vampomi_ctx {
     unsigned* ticket = nullptr; // arrival counter of the fused reductions (zero between launches)
     unsigned long long* h_flag = nullptr;  // mapped host word the stream stores sync sequence numbers into
     unsigned long long* d_flag = nullptr;
-    unsigned long long sync_seq = 0, side_seq = 0;
+    unsigned long long sync_seq = 0;
     vk::CgState* cgs = nullptr;     // device-side CG control (pcg.cpp), two states (the folded decisions alternate)
     vk::CgMirror* h_cgm = nullptr;  // its mapped host mirror, and the mirror's device address
     vk::CgMirror* d_cgm = nullptr;
@@ -170,8 +159,9 @@ struct vampomi_ctx {
 vampomi_status dev_alloc(double** p, size_t n);
 void dev_free(double*& p);
 vampomi_status host_sync(vampomi_ctx* c);
-// spins until the context's host flag reaches seq (stores from the stream)
-// (word 1: the side stream's sequence, stored by its one-rank reductions)
+// spins until word `word` of the context's host flag block reaches seq (stores
+// from the stream; word 0 the stream's sync sequence, kCgPackWord.. the CG's
+// packed decisions)
 vampomi_status wait_flag(vampomi_ctx* c, unsigned long long seq, int word = 0);
 // hipStreamSynchronize, except with an RCCL communicator: polls the stream and
 // the communicator, and aborts / fails on a broken job or after
@@ -251,8 +241,6 @@ class DotBatch {
     // reserves nq result slots for a fused reduction kernel: *ro says where the
     // kernel writes; the values reach out[0..nq) at flush()
     vampomi_status sink(int nq, bool sync, double* out, vk::RedOut* ro);
-    // the main stream continues after the side stream's work (no host wait)
-    vampomi_status join();
     vampomi_status flush();
     bool empty() const { return sinks_.empty(); }
     // one rank: the device address where the result that flush() will copy to
@@ -267,14 +255,7 @@ class DotBatch {
     // several ranks: the device address of the slot whose value flush() will
     // copy to out (final after reduce_now() for a synced result); else null
     double* dev_slot(const double* out) const;
-    // on = true: the following sinks/adds run on the context's side stream
-    // (ordered after everything queued on st so far); flush() joins it back.
-    // No effect (one stream) when the context's side stream is off
-    vampomi_status side(bool on);
-    // the side stream's work starts from st's state NOW (launches queued on st
-    // after this call may overlap it); side(true) forks here if not yet done
-    vampomi_status fork();
-    // the stream the next launch of this batch goes to
+    // the stream the batch's launches go to (the context's)
     hipStream_t stream() const;
 
    private:
@@ -289,9 +270,7 @@ class DotBatch {
     vampomi_ctx* c_;
     int nsync_ = 0, nlocal_ = 0;
     int nred_ = 0;  // synced slots [0, nred_) already all-reduced (reduce_now)
-    bool on_side_ = false, forked_ = false;
     unsigned long long last_seq_ = 0;  // one rank: flag value the last reduction kernel stores
-    unsigned long long side_seq_ = 0;  // ... and the last side-stream reduction (flag word 1)
     std::vector<Sink> sinks_;
 };
 

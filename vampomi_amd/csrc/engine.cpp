@@ -287,7 +287,7 @@ static constexpr double kQueryAfterS = 0.5, kQueryEveryS = 0.25;
 vampomi_status wait_flag(vampomi_ctx* c, unsigned long long seq, int word) {
     const auto t0 = std::chrono::steady_clock::now();
     double next_query = kQueryAfterS;
-    hipStream_t st = word == 1 ? c->st2 : c->st;  // word 1: the side stream's sequence
+    hipStream_t st = c->st;
     for (uint64_t spin = 1;; ++spin) {
         if (__atomic_load_n(c->h_flag + word, __ATOMIC_ACQUIRE) >= seq) return VAMPOMI_OK;
         if ((spin & 4095) == 0) {
@@ -547,21 +547,16 @@ vampomi_status DotBatch::sink(int nq, bool sync, double* out, vk::RedOut* ro) {
     int& used = sync ? nsync_ : nlocal_;
     const int base = sync ? SL_SYNC : SL_LOCAL, cap = sync ? SL_NSYNC : SL_NLOCAL;
     if (used + nq > cap) return fail(VAMPOMI_ERR_STATE, "DotBatch overflow");
-    ro->part = on_side_ ? c_->red_part2 : c_->red_part;
+    ro->part = c_->red_part;
     ro->out = (c_->use_comm ? c_->scal : c_->d_hscal) + base + used;
-    ro->ticket = on_side_ ? c_->ticket2 : c_->ticket;
+    ro->ticket = c_->ticket;
     ro->flag = nullptr;
     ro->seq = 0;
-    // results land in host memory: the kernel flags their arrival (word 0
-    // counts along st, word 1 along the side stream: each is monotone)
+    // results land in host memory: the kernel flags their arrival (a sequence
+    // number along the stream, monotone)
     if (!c_->use_comm && c_->h_flag) {
-        if (on_side_) {
-            ro->flag = c_->d_flag + 1;
-            ro->seq = side_seq_ = ++c_->side_seq;
-        } else {
-            ro->flag = c_->d_flag;
-            ro->seq = last_seq_ = ++c_->sync_seq;
-        }
+        ro->flag = c_->d_flag;
+        ro->seq = last_seq_ = ++c_->sync_seq;
     }
     sinks_.push_back(Sink{base + used, nq, out});
     used += nq;
@@ -654,19 +649,14 @@ vampomi_status DotBatch::build(const std::vector<Group>& groups, const vk::G1Cha
     if (chain && !a.g1.out) return fail(VAMPOMI_ERR_ARG, "DotBatch: the chained group is not in the launch");
     if (a.copy.n != (int)copies.size()) return fail(VAMPOMI_ERR_ARG, "DotBatch: a copied group is not in the launch");
     ro = vk::RedOut{};
-    ro.part = on_side_ ? c_->red_part2 : c_->red_part;
-    ro.ticket = on_side_ ? c_->ticket2 : c_->ticket;
+    ro.part = c_->red_part;
+    ro.ticket = c_->ticket;
     ro.out = base + SL_LOCAL + nlocal_;
     ro.out2 = base + SL_SYNC + nsync_;
     ro.split = nloc;
     if (!c_->use_comm && c_->h_flag) {  // one flag for the launch (see sink)
-        if (on_side_) {
-            ro.flag = c_->d_flag + 1;
-            ro.seq = side_seq_ = ++c_->side_seq;
-        } else {
-            ro.flag = c_->d_flag;
-            ro.seq = last_seq_ = ++c_->sync_seq;
-        }
+        ro.flag = c_->d_flag;
+        ro.seq = last_seq_ = ++c_->sync_seq;
     }
     nlocal_ += nloc;
     nsync_ += nsyn;
@@ -689,48 +679,14 @@ double* DotBatch::dev_slot(const double* out) const {
 
 vampomi_status DotBatch::reduce_now() {
     if (!c_->use_comm || nsync_ == nred_) return VAMPOMI_OK;
-    if (on_side_ || forked_) return fail(VAMPOMI_ERR_STATE, "DotBatch::reduce_now with the side stream open");
     STCHK(allreduce_dev(c_, c_->scal + SL_SYNC + nred_, (size_t)(nsync_ - nred_)));
     nred_ = nsync_;
     return VAMPOMI_OK;
 }
 
-hipStream_t DotBatch::stream() const { return on_side_ ? c_->st2 : c_->st; }
-
-vampomi_status DotBatch::fork() {
-    if (forked_ || !c_->side_on || !c_->st2) return VAMPOMI_OK;
-    HIPCHK(hipEventRecord(c_->ev_fork, c_->st));
-    HIPCHK(hipStreamWaitEvent(c_->st2, c_->ev_fork, 0));
-    forked_ = true;
-    c_->side_open = true;
-    return VAMPOMI_OK;
-}
-
-vampomi_status DotBatch::side(bool on) {
-    on_side_ = on && c_->side_on && c_->st2;
-    if (on_side_) STCHK(fork());  // the side stream starts after everything queued on st so far
-    return VAMPOMI_OK;
-}
-
-vampomi_status DotBatch::join() {
-    on_side_ = false;
-    if (forked_) {  // st continues after the side stream's work
-        HIPCHK(hipEventRecord(c_->ev_join, c_->st2));
-        HIPCHK(hipStreamWaitEvent(c_->st, c_->ev_join, 0));
-        forked_ = false;
-        c_->side_open = false;
-    }
-    return VAMPOMI_OK;
-}
+hipStream_t DotBatch::stream() const { return c_->st; }
 
 vampomi_status DotBatch::flush() {
-    const bool had_side = side_seq_ != 0;
-    STCHK(join());
-    if (side_seq_) {  // one rank: the host reads the side results when their own kernel flags them
-        c_->stats.host_syncs++;
-        STCHK(wait_flag(c_, side_seq_, 1));
-        side_seq_ = 0;
-    }
     if (sinks_.empty()) return VAMPOMI_OK;
     if (c_->use_comm) {  // slots in device memory: all-reduce the synced ones, then publish both ranges
         if (nsync_ > nred_) STCHK(allreduce_dev(c_, c_->scal + SL_SYNC + nred_, (size_t)(nsync_ - nred_)));
@@ -752,7 +708,7 @@ vampomi_status DotBatch::flush() {
     } else if (last_seq_) {
         c_->stats.host_syncs++;
         STCHK(wait_flag(c_, last_seq_));
-    } else if (!had_side) {
+    } else {
         STCHK(host_sync(c_));
     }
     for (const Sink& k : sinks_)
@@ -997,11 +953,6 @@ static void team_gate_leave(vampomi_ctx* c) {  // after the context's stream has
 // T: the launch's team size (its plan's)
 template <class Launch>
 static vampomi_status team_launch(vampomi_ctx* c, int T, Launch&& launch) {
-    if (c->side_open && c->st2) {  // never beside the context's own side-stream work (not reached: batches join first)
-        HIPCHK(hipEventRecord(c->ev_join, c->st2));
-        HIPCHK(hipStreamWaitEvent(c->st, c->ev_join, 0));
-        c->side_open = false;
-    }
     if (T <= 1 || !c->team_reg) {
         HIPCHK(launch());
         return VAMPOMI_OK;
@@ -1169,12 +1120,11 @@ extern "C" vampomi_status vampomi_comm_unique_id(void* out) {
 void release_ctx_resources(vampomi_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->st) (void)hipStreamSynchronize(c->st);
-    if (c->st2) (void)hipStreamSynchronize(c->st2);
     team_gate_leave(c);
     resolve_timing(c);
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
     c->ev_pool.clear();
-    for (double** p : {&c->X, &c->mave, &c->msig, &c->y, &c->ax_part, &c->red_part, &c->red_part2, &c->scal, &c->nbuf, &c->mbuf,
+    for (double** p : {&c->X, &c->mave, &c->msig, &c->y, &c->ax_part, &c->red_part, &c->scal, &c->nbuf, &c->mbuf,
                        &c->op_part, &c->op_nvec})
         dev_free(*p);
     if (c->op_xg) (void)hipFree(c->op_xg);
@@ -1189,8 +1139,6 @@ void release_ctx_resources(vampomi_ctx* c) {
     c->h_scal = nullptr;
     if (c->ticket) (void)hipFree(c->ticket);
     c->ticket = nullptr;
-    if (c->ticket2) (void)hipFree(c->ticket2);
-    c->ticket2 = nullptr;
     if (c->h_flag) (void)hipHostFree(c->h_flag);
     c->h_flag = nullptr;
     if (c->h_cgm) (void)hipHostFree(c->h_cgm);
@@ -1206,10 +1154,6 @@ void release_ctx_resources(vampomi_ctx* c) {
             (void)ncclCommAbort(c->comm);
     }
     c->comm = nullptr;
-    for (hipEvent_t* e : {&c->ev_fork, &c->ev_join})
-        if (*e) (void)hipEventDestroy(*e), *e = nullptr;
-    if (c->st2) (void)hipStreamDestroy(c->st2);
-    c->st2 = nullptr;
 
     if (c->st) (void)hipStreamDestroy(c->st);
     c->st = nullptr;
@@ -1249,12 +1193,8 @@ extern "C" vampomi_status vampomi_open(const vampomi_shard_desc* d, vampomi_ctx*
     STCHK(dev_alloc(&c->ax_part, (size_t)c->axp.nslots * vk::kMaxRhs * c->ld));
     c->red_cap = red_capacity(Mx);
     STCHK(dev_alloc(&c->red_part, c->red_cap));
-    STCHK(dev_alloc(&c->red_part2, c->red_cap));
-    HIPCHK(hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking));
     c->writer.reset(new IterWriter());  // the per-iteration output (writer.h): staging and thread now
     STCHK(c->writer->open(c.get()));
-    HIPCHK(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
-    HIPCHK(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
     STCHK(dev_alloc(&c->scal, SL_TOTAL));
     HIPCHK(hipHostMalloc((void**)&c->h_scal, SL_TOTAL * sizeof(double), hipHostMallocMapped | hipHostMallocCoherent));
     HIPCHK(hipHostGetDevicePointer((void**)&c->d_hscal, c->h_scal, 0));
@@ -1263,8 +1203,6 @@ extern "C" vampomi_status vampomi_open(const vampomi_shard_desc* d, vampomi_ctx*
     HIPCHK(hipHostGetDevicePointer((void**)&c->d_flag, c->h_flag, 0));
     HIPCHK(hipMalloc((void**)&c->ticket, 64 * sizeof(unsigned)));
     HIPCHK(hipMemsetAsync(c->ticket, 0, 64 * sizeof(unsigned), c->st));
-    HIPCHK(hipMalloc((void**)&c->ticket2, 64 * sizeof(unsigned)));
-    HIPCHK(hipMemsetAsync(c->ticket2, 0, 64 * sizeof(unsigned), c->st));
     STCHK(dev_alloc(&c->nbuf, (size_t)vk::kMaxRhs * c->ld));
     HIPCHK(hipMemsetAsync(c->nbuf, 0, (size_t)vk::kMaxRhs * c->ld * 8, c->st));
     STCHK(dev_alloc(&c->mbuf, (size_t)2 * vk::kMaxRhs * Mx));
@@ -1279,12 +1217,6 @@ extern "C" vampomi_status vampomi_open(const vampomi_shard_desc* d, vampomi_ctx*
     // be exercised on a single GPU
     const char* force = std::getenv("VAMPOMI_FORCE_RCCL");
     c->use_comm = c->nranks > 1 || (force && std::atoi(force) != 0);
-    // the side stream overlaps the EM/denoiser with the reductions and their
-    // all-reduces: on where collectives exist (several ranks); one rank runs
-    // one stream, 0.5 % faster at C2 (profiles/r02j_side_ab_c2.txt: the
-    // cross-queue events cost more than the 5-17 us kernels they overlap)
-    c->side_on = c->use_comm;
-    if (const char* sv = std::getenv("VAMPOMI_SIDE_STREAM")) c->side_on = std::atoi(sv) != 0;
     if (const char* mv = std::getenv("VAMPOMI_MR_TAIL")) c->mr_tail = c->mr_tail_req = std::atoi(mv) != 0;
     if (const char* fv = std::getenv("VAMPOMI_CG_FOLD")) c->cg_fold = std::atoi(fv) != 0;
     if (const char* hv = std::getenv("VAMPOMI_HEADSTART")) c->hs_on = c->hs_on_req = std::atoi(hv) != 0;
@@ -1295,7 +1227,7 @@ extern "C" vampomi_status vampomi_open(const vampomi_shard_desc* d, vampomi_ctx*
     } else if (c->use_comm && mode && std::strcmp(mode, "shm") == 0) {
         if (!d->comm_id) return fail(VAMPOMI_ERR_ARG, "the shm communicator needs a communicator id");
         std::string err;
-        c->shm = shm_join(d->comm_id, c->nranks, c->rank, &err);
+        c->shm = shm_join(d->comm_id, c->nranks, c->rank, comm_init_timeout_s(), &err);
         if (!c->shm) return fail(VAMPOMI_ERR_STATE, err);
     } else if (c->use_comm) {
         ncclUniqueId id;
@@ -1882,9 +1814,8 @@ extern "C" vampomi_status vampomi_dev_set_variant(vampomi_ctx* c, int which, int
             c->op_variant = variant;
             c->op_ready = false;
         }
-    } else if (which == 4) {  // side stream for the prefetched denoiser/EM: 0 off, 1 on
-        if (variant != 0 && variant != 1) return fail(VAMPOMI_ERR_ARG, "side stream: 0 or 1");
-        c->side_on = variant == 1;
+    } else if (which == 4) {  // (the side stream of rounds 2-5: removed in round 6)
+        return fail(VAMPOMI_ERR_ARG, "no side stream: every launch runs on the context's stream (DESIGN.md §6)");
     } else if (which == 5) {  // the CG head start (pcg.cpp): 0 off, 1 on
         if (variant != 0 && variant != 1) return fail(VAMPOMI_ERR_ARG, "head start: 0 or 1");
         c->hs_on_req = variant == 1;  // several ranks: applied and agreed at the next vampomi_vamp_begin

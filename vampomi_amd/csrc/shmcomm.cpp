@@ -48,7 +48,8 @@ struct ShmHdr {
     std::atomic<uint64_t> gen;   // completed collectives
     std::atomic<int> arrived;    // ranks in the current one
     std::atomic<int> poisoned;   // non-zero: the job failed; why[] says why
-    std::atomic<int> joined;     // ranks that mapped the segment
+    std::atomic<int> joined;     // ranks that hold a mapping of the segment
+    std::atomic<int> opened;     // ranks that ever mapped it (monotone: the join barrier)
     std::atomic<int> why_lock;
     int P;
     uint64_t cap;  // doubles per rank slot
@@ -115,7 +116,7 @@ std::string shm_why(const ShmComm& s) {
     return std::string(s.h->why, strnlen(s.h->why, sizeof s.h->why));
 }
 
-std::shared_ptr<ShmComm> shm_join(const void* id, int P, int rank, std::string* err) {
+std::shared_ptr<ShmComm> shm_join(const void* id, int P, int rank, double limit_s, std::string* err) {
     if (P < 1 || P > kShmMaxRanks || rank < 0 || rank >= P) {
         *err = "shm communicator: 1..64 ranks";
         return nullptr;
@@ -156,8 +157,34 @@ std::shared_ptr<ShmComm> shm_join(const void* id, int P, int rank, std::string* 
     h->P = P;
     h->cap = cap;
     h->pid[rank] = (int)::getpid();
+    h->joined.fetch_add(1);
     // the last rank to map the segment removes its name (every rank holds a mapping)
-    if (h->joined.fetch_add(1) + 1 == P) ::shm_unlink(s->name.c_str());
+    if (h->opened.fetch_add(1) + 1 == P) ::shm_unlink(s->name.c_str());
+    // Joining is collective, like RCCL's communicator init: every rank returns
+    // once all P have joined (main_meth.exe's rank 0 removes the id's
+    // rendezvous file after its open returns, so every rank must have read it
+    // by then), or fails after limit_s / when a joined peer process is gone.
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint64_t spin = 1; h->opened.load(std::memory_order_acquire) < P; ++spin) {
+        if (h->poisoned.load(std::memory_order_acquire)) {
+            *err = "shm communicator: " + std::string(h->why, strnlen(h->why, sizeof h->why));
+            return nullptr;
+        }
+        for (int r = 0; r < P; ++r)
+            if (r != rank && pid_gone(h->pid[r])) {
+                *err = "shm communicator: rank " + std::to_string(r) + " exited before every rank joined";
+                shm_poison(*s, *err);
+                return nullptr;
+            }
+        if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit_s) {
+            *err = "shm communicator: not every rank joined within " + std::to_string((int)limit_s) +
+                   " s (VAMPOMI_COMM_INIT_TIMEOUT_S)";
+            shm_poison(*s, *err);
+            ::shm_unlink(s->name.c_str());
+            return nullptr;
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(spin < 1000 ? 50 : 2000));
+    }
     return s;
 }
 

@@ -65,8 +65,8 @@ vampomi_ctx::~vampomi_ctx() {
 }
 
 // updatePrior (src/vamp.cpp:531-643) on mixture m, from r1 and gam1, split in
-// two so that a caller can queue the first EM round's sums early (on the side
-// stream) and resolve them with other reductions: em_begin queues round 0
+// two so that a caller can queue the first EM round's sums early, with other
+// reductions, and resolve them together: em_begin queues round 0
 // into b; after b.flush(), em_finish does its host part, the further rounds
 // (each with its own batch) and the merge.  update_prior runs both.
 vampomi_status em_begin(vampomi_ctx* c, const EmParams& P, const Mixture& m, double gam1, const double* r1,
@@ -636,8 +636,8 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
     STCHK(check_device_values(c, R, it));  // (the solves' flags came after the previous iteration's launches)
     if (res && res->cg_iters) res->cg_iters[it - 1] = sx.iters;
     if (res && res->ons_iters) res->ons_iters[it - 1] = so.iters;
-    // r1 (:348-350): its own launch, or (the side stream's EM round below)
-    // formed by the first EM round's kernel
+    // r1 (:348-350): its own launch, or (the EM round below) formed by the
+    // first EM round's kernel
     const bool next = R.fuse && it < R.prm.max_iter;
     const bool em_next = next && it + 1 > R.prm.learn_prior_delay;
     const bool r1_in_em = next && arec && em_next && R.prm.EM_max_iter >= 1;
@@ -661,7 +661,6 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
         R.gam1 = R.prm.rho * R.gam1 + (1 - R.prm.rho) * gam1_prev;  // :346
     };
     // ---- prefetch: denoising of iteration it+1 (discarded if the stop fires) ----
-    // (batch_rhs >= 3: on the side stream, beside the reductions below)
     DotBatch fin(c);
     double* dsc = c->scal + SL_CHAIN;
     // updateNoisePrec's two sums (:508-521) and the NMSE sums (:409-413); with
@@ -748,10 +747,8 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
     }
     EmState em;
     if (next) R.mix_next = R.mix;
-    if (next && arec) {  // the side stream starts from r1 and x1; its EM sums are queued before these reductions
-        if (!mr) STCHK(fin.fork());  // (mr: one stream, the all-reduces between the launches)
+    if (next && arec) {  // iteration it+1's EM sums, queued before these reductions
         if (em_next) {
-            if (!mr) STCHK(fin.side(true));
             vk::EmUpd eu;
             eu.Mt = Mt;
             eu.learn_vars = R.prm.learn_vars;
@@ -783,7 +780,6 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
                     HIPCHK(vk::tail_post(t, c->st));
                 }
             }
-            if (!mr) STCHK(fin.side(false));
         }
     }
     if (next && !arec) {  // the pass below carries the next z1 = A x1_hat: denoise first
@@ -825,26 +821,20 @@ extern "C" vampomi_status vampomi_vamp_step(vampomi_ctx* c, int* stopped) {
     else if (!shared)
         STCHK(err_queue(c, R, R.x2, ax2, fin, R.e2m, R.e2n, R.e2s));
     R.passes_ref += 1;
-    // Second stream (batch_rhs >= 3, north_star): iteration it+1's EM sums run
-    // on the side stream beside these reductions and share their all-reduce
-    // and host wait; then its denoiser (g1, g1d, sum of g1d) runs there beside
-    // the NMSE sums, again one all-reduce and one wait. Every reduction is the
-    // same fixed-order kernel as on one stream, so the values are bitwise the
-    // same (tests/test_gpu_sharded.py::test_side_stream_bitwise)
+    // Iteration it+1's EM sums share these reductions' all-reduce and host
+    // wait; then its denoiser (g1, g1d, sum of g1d) shares the NMSE sums'
+    // (several EM rounds, or VAMPOMI_MR_TAIL=0 on several ranks: the host's
+    // mixture update between them)
     if (next && arec && em_next && !devem) {
         STCHK(fin.flush());
         if (chain) host_gam1();  // (the device formed the same values for the EM round)
         STCHK(em_finish(c, em_params(R), R.mix_next, R.gam1, R.r1, em));
     }
-    if (next && arec && !devem) {
-        STCHK(fin.side(true));  // forks again after an EM flush
+    if (next && arec && !devem)
         STCHK(denoise_into(c, R.mix_next, R.gam1, R.r1, R.x1n, R.x1, true, R.prm.rho, R.x1d, fin, &R.sum_d));
-        STCHK(fin.side(false));
-    }
     if (!shared) STCHK(fin.add_many(M, {gnm}));  // NMSE (:409-413)
     // iteration it+1's prelude and solves' start, queued now (set up above)
     if (ahead) {
-        STCHK(fin.join());  // (x1n, r1 and the scalars may come from the side stream)
         STCHK(pcg_run(c, {&A.so, &A.sx}, 0.0, 0.0, R.prm.CG_max_iter, R.prm.CG_err_tol, R.nsc, nullptr, nullptr,
                       R.x1n, R.z1buf, true, nullptr, &A.hs, &A.pr, PreMode::ahead));
         R.pre_ahead = it + 1;
