@@ -167,6 +167,14 @@ def test_c2_bench_window_vs_oracle_fixture(c2_problem):
         assert np.all(np.abs(h @ P.T - z[f"{key}_proj"]) <= bound), key
         for q, k in enumerate(z["keep_its"]):
             assert relerr(h[k - 1], z[key][q]) <= 1e-10, (key, k)
+        if f"{key}_blocks" in z:  # (round 6 fixture)
+            got, want = block_checks(h, P), z[f"{key}_blocks"]
+            nb = want.shape[1]
+            # the whole vector's 1e-10 bar spent on one block: its norm moves by at most ||delta||, a
+            # projection on a +-1 probe by at most sqrt(block length) * ||delta||
+            tol = 1e-10 * nrm[:, None, None] * np.array([1.0, np.sqrt(Mt / nb + 1), np.sqrt(Mt / nb + 1)])[None, None, :]
+            bad = np.abs(got - want) > tol
+            assert not np.any(bad), (key, np.argwhere(bad)[:5])
 
 
 def test_cli_on_reference_written_files(tmp_path):
@@ -256,12 +264,16 @@ def test_c3_full_shard_window_vs_oracle_fixture():
     generator, bit-identical here, y / beta stored).  Every iteration: CG /
     Onsager / mixture counts exact, params within 1e-9, the norms and four
     +-1 projections of x1_hat / r1 within the 1e-10 norm bar (a projection
-    moves by at most sqrt(M) * ||delta||); the whole x1_hat / r1 at
-    iterations 3, 7 and 12 within 1e-10 (src/vamp.cpp:110-438)."""
+    moves by at most sqrt(M) * ||delta||), and per block of 256 contiguous
+    markers its norm and two +-1 projections within the same bar on the
+    block (a localized error moves its block's checks to first order);
+    the whole x1_hat / r1 at iterations 3, 7 and 12 within 1e-10
+    (src/vamp.cpp:110-438)."""
     import sys
 
     sys.path.insert(0, G)
     from make_c2_window import probes
+    from make_c3_window import block_checks
 
     z = np.load(os.path.join(G, "oracle_c3_window.npz"))
     N, Mt, its = int(z["N"]), int(z["Mt"]), int(z["its"])
