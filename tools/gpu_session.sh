@@ -154,6 +154,8 @@ for s in "$@"; do
         step ceiling_50 300 tools/hbm_ceiling 50 5 ;;
     ablation)    # the C2 operator's components, one at a time, against the same process's read stream (TM_DBG build)
         step ablation 400 env VAMPOMI_LIB="$PWD/build_dbg/lib/libvampomi.so" python tools/op_ablation.py 10000 50000 40 3 ;;
+    ablibs)      # the C2 operator with a component removed at compile time (TM_ABL builds), against production
+        step ablibs 600 bash tools/op_ablation_libs.sh 3 ;;
     benchc2)     # the default C2 line with both CPU legs
         step bench_c2 400 python bench.py --steps 20 --warmup 5 ;;
     c4)          # the probit shard: its line, and a kernel trace of 10 iterations (A passes against the rest)

@@ -39,6 +39,16 @@ lib = va.load()
 d = va.Data(N, Mt)
 d.generate(1, va.GEN_GAUSS)
 name = d.kernel_name(3, K)
+if os.environ.get("OP_ABL_ONE"):
+    # one library (a TM_ABL build has its ablation baked in; the production library none): the operator's
+    # launch time and the same process's read stream, as one JSON line (tools/op_ablation_libs.sh)
+    ms = C.c_double()
+    _lib.check(lib.vampomi_dev_time_pass(d.ctx, 3, K, 3, C.byref(ms)))
+    _lib.check(lib.vampomi_dev_time_pass(d.ctx, 3, K, reps, C.byref(ms)))
+    c = d.read_ceiling(9)
+    print(json.dumps({"lib": os.environ.get("VAMPOMI_LIB", "production"), "kernel": name, "op_us": round(ms.value * 1e3, 1),
+                      "stream_us": round(c["us_med"], 1)}), flush=True)
+    sys.exit(0)
 times = {s: [] for s, _ in SETTINGS}
 ceil = []
 for r in range(rounds):

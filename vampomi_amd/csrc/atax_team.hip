@@ -61,6 +61,10 @@ typedef unsigned int v2u __attribute__((ext_vector_type(2)));
 #ifndef TM_DBG
 #define TM_DBG 0  // 1: honour OpArgs.dbg (timing experiments); 0: its branches compile out
 #endif
+#ifndef TM_ABL
+#define TM_ABL 0  // ablation builds (tools/op_ablation.py): these VAMPOMI_OP_DBG bits baked in as constants, so the
+                  // rest of the schedule is the production kernel's (a TM_DBG build's run-time branches are not)
+#endif
 static constexpr int kTmThreads = 512;        // 8 waves, 2 per SIMD: <= 256 VGPRs per lane
 static constexpr int kTmLdsHead = 4;          // dynamic LDS words before q: the folded decision (team_plan's +4)
 static constexpr int kTmMaxT = 32;            // members per team (one XCD under round-robin dealing)
@@ -275,7 +279,7 @@ __device__ __forceinline__ void atax_team_body(const double* __restrict__ X, int
     // build (the branches cost the hand-off wave's chain 2 % at the C3 shard);
     // T = 1 keeps them: at 252-256 VGPRs its schedule without them waits more
     // (C2 K = 2: 613 against 591 us, profiles/r02f_op_experiments.txt)
-    const int dbg = (TM_DBG || !COMM) ? a.dbg : 0;
+    const int dbg = TM_ABL ? TM_ABL : (TM_DBG || !COMM) ? a.dbg : 0;
     constexpr int CW = COMM ? 7 : 8;  // streaming waves
     constexpr int RS = tm_rows_per_step(COMM, E);
     static_assert(E == 1 || E == 2, "doubles per lane per load");
@@ -618,7 +622,7 @@ __device__ __forceinline__ void atax_team_body(const double* __restrict__ X, int
             }
 #pragma unroll
             for (int k = 0; k < K; ++k) {
-                if (TM_DBG && (dbg & 2048)) {  // timing experiment (TM_DBG builds): no LDS q reads
+                if ((TM_DBG || TM_ABL) && (dbg & 2048)) {  // timing experiment: no LDS q reads
                     q[k][0] = 0.5;
                     q[k][E - 1] = 0.25;
                 } else if constexpr (E == 2) {
