@@ -347,6 +347,12 @@ def test_probit_parity_team_operator():
     _assert_probit_parity(s, ref, spread)
 
 
+# The C4 bar's multiple of the reference's own run-to-run spread (VERDICT r05
+# item 1: k <= 2 x the ensemble's 90th percentile, every member of the
+# ensemble a run the reference performs itself)
+PROBIT_K_ENSEMBLE = 2.0
+
+
 def test_c4_full_shard_vs_oracle():
     """The WHOLE per-GPU C4 probit shard (N = 50,000 x 50,000 Gaussian
     markers, 20 GB; four of them are configs[3]) on the production schedule,
@@ -354,16 +360,23 @@ def test_c4_full_shard_vs_oracle():
     run on this host (the index-keyed generator is bit-identical on both
     sides; y / beta from tests/golden/oracle_c4_spread.npz)
     (src/vamp_probit.cpp:19-488).  Counts exact (iterations, CG, Onsager,
-    mixture sizes, confusion counts); iteration 1 within 1e-10.  From
-    iteration 2 on, r1 = (x2 - alpha2 r2) / (1 - alpha2) (:337-338) cancels to
-    1 - alpha2, so the reference's own result is only defined to its
-    sensitivity to the summation order, MEASURED on the oracle at this shard
-    (make_c4_spread.py: 2, 3, 64 and 128 ranks / virtual shards -- the sums
-    over markers split as the device's team slots split them -- and the
-    sample sums of A^T.u in blocks of 128 rows): the bar is PROBIT_K x the
-    largest of those spreads per iteration, and the gap / spread ratios are
-    recorded (VAMPOMI_PROBIT_RATIOS)."""
-    z = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "oracle_c4_spread.npz"))
+    mixture sizes, confusion counts); iteration 1 within 1e-10.
+
+    From iteration 2 on, r1 = (x2 - alpha2 r2) / (1 - alpha2) (:337-338)
+    cancels to 1 - alpha2 ~ 4e-8, so the reference's result is defined only to
+    its own sensitivity to the order of its sums.  Two measurements, both on
+    the oracle at this shard (tests/golden/make_c4_spread.py):
+    * the device's own grouping of every scalar sum (ORC_ASSOC_DEVICE at the
+      C4 plan, oracle_c4_devorder.npz): the GPU lands on it -- within 0.2 x
+      its gap to the restatement at iterations 2-8, within 1e-10 (north_star's
+      bar) from iteration 3;
+    * the reference's own runs (OMP_NUM_THREADS 4-128 x four arrival orders of
+      inner_prod's thread sums, and 2 and 3 ranks): the GPU's gap to the
+      restatement is within PROBIT_K_ENSEMBLE x their 90th percentile.
+    The ratios are recorded (VAMPOMI_PROBIT_RATIOS; profiles/r06_c4_*)."""
+    G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    z = np.load(os.path.join(G, "oracle_c4_spread.npz"))
+    zd = np.load(os.path.join(G, "oracle_c4_devorder.npz"))
     N, Mt, its, seed = int(z["N"]), int(z["Mt"]), int(z["its"]), int(z["seed"])
     y, beta = z["y"].astype(np.float64), z["beta"]
     with va.Data(N, Mt) as d:
@@ -375,20 +388,37 @@ def test_c4_full_shard_vs_oracle():
         assert d.stats().op.launches > 0, "the one-pass team operator did not run"
         n = s["iterations"]
         s["x1_hist"], s["r1_hist"], s["x1_final"] = v.x1_hist[:n, :d.M].copy(), v.r1_hist[:n, :d.M].copy(), x1
+    assert _op_plan(N, Mt) == (int(zd["dev_T"]), int(zd["dev_grid"])), "the fixture's device order is not this plan's"
     X = O.generate_markers(seed, va.GEN_GAUSS, N, 0, Mt)
     ref = O.vamp_infere(X, y, Mt, true_signal=beta, model="bin_class", max_iter=its, stop_criteria_thr=0.0)
     del X
-    # the fixture's spreads were measured around this very run
+    # the fixtures were measured around this very run
     assert np.allclose(np.linalg.norm(ref["x1_hist"], axis=1), z["ref_x1_norm"], rtol=1e-13, atol=0)
     assert np.array_equal(ref["cg_iters"], z["ref_cg"]) and np.array_equal(ref["ons_iters"], z["ref_ons"])
-    spread = {key: np.max(z[f"spread_{key}"], axis=0) for key in ("x1", "r1", "params", "metrics", "prior")}
+    assert np.array_equal(z["ref_x1_norm"], zd["ref_x1_norm"])
     for key in ("iterations", "cg_iters", "ons_iters", "L"):
         want = ref[key] if key == "iterations" else ref[key].tolist()
         assert s[key] == want, key
     test = "tests/test_gpu_probit.py::test_c4_full_shard_vs_oracle"
     gap1 = {key: relerr(s[f"{key}_hist"][0], ref[f"{key}_hist"][0]) for key in ("x1", "r1")}
     assert max(gap1.values()) <= 1e-10, gap1
-    _assert_probit_parity(s, ref, spread, test=test)
+    # the device's grouping of the sums: the GPU lands on it
+    for key in ("x1", "r1"):
+        dev = ref[f"{key}_hist"] + zd[f"dev_{key}_diff"].astype(np.float64)
+        g_seq = np.array([relerr(s[f"{key}_hist"][i], ref[f"{key}_hist"][i]) for i in range(its)])
+        g_dev = np.array([relerr(s[f"{key}_hist"][i], dev[i]) for i in range(its)])
+        f = os.environ.get("VAMPOMI_PROBIT_RATIOS")
+        if f:
+            import json
+
+            with open(f, "a") as fh:
+                fh.write(json.dumps({"test": test + "[device order]", "key": key, "gap_seq": g_seq.tolist(),
+                                     "gap_dev": g_dev.tolist()}) + "\n")
+        assert np.all(g_dev[1:] <= 0.2 * g_seq[1:]), (key, g_dev / np.maximum(g_seq, 1e-300))
+        assert np.all(g_dev[2:] <= 1e-10), (key, g_dev)
+    # the reference's own spread: its runs' 90th percentile
+    spread = {key: np.quantile(z[f"spread_{key}"], 0.9, axis=0) for key in ("x1", "r1", "params", "metrics", "prior")}
+    _assert_probit_parity(s, ref, spread, k=PROBIT_K_ENSEMBLE, test=test)
 
 
 def _op_plan(N, M, cus=256):
