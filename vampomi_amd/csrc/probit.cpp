@@ -98,7 +98,7 @@ vampomi_status probit_step(vampomi_ctx* c, VampRun& R) {
     }
     R.passes_ref += 1;
     R.eta1 = R.gam1 / alpha1_raw;                                        // :130
-    if (it > 1) STCHK(update_prior(c, R, R.mix, R.gam1, R.r1));         // :139, after g1/g1d
+    if (it > 1 && R.em_head != it) STCHK(update_prior(c, R, R.mix, R.gam1, R.r1));  // :139, after g1/g1d
     if (res && res->L_hist) res->L_hist[it - 1] = R.mix.L;
     R.alpha1 = it > 1 ? rho * alpha1_raw + (1 - rho) * alpha1_prev : alpha1_raw;  // :160-165
     STCHK(write_bins(c, R));                                             // :168-186
@@ -107,14 +107,23 @@ vampomi_status probit_step(vampomi_ctx* c, VampRun& R) {
 
     // ---------------- denoising z (:202-253) + accuracy of x1 (:189, :271-282) ----------------
     double bsum = 0, cnt1[4] = {}, xc1[3] = {};
-    {
-        DotBatch b(c);
+    // (queued by iteration it-1 with its last batch, z_head: the same launches on the same inputs)
+    auto queue_z = [&](DotBatch& b, const double* x1v, const double* zx, double* bs, double* cnt, double* xc) {
         vk::RedOut ro{};
-        STCHK(b.sink(1, false, &bsum, &ro));  // y, p1 replicated: local sum
+        STCHK(b.sink(1, false, bs, &ro));  // y, p1 replicated: local sum
         HIPCHK(vk::probit_denoise(N, R.p1, c->y, R.tau1, R.z1h, ro, c->st));
-        STCHK(b.sink(4, false, cnt1, &ro));
-        HIPCHK(vk::probit_confusion(N, 1, zx1, ld, c->y, ro, c->st));
-        STCHK(b.add({T(R.x1, R.ts), T(R.x1, R.x1), T(R.ts, R.ts)}, M, true, xc1));
+        STCHK(b.sink(4, false, cnt, &ro));
+        HIPCHK(vk::probit_confusion(N, 1, zx, ld, c->y, ro, c->st));
+        STCHK(b.add({T(x1v, R.ts), T(x1v, x1v), T(R.ts, R.ts)}, M, true, xc));
+        return VAMPOMI_OK;
+    };
+    if (R.z_head == it) {
+        bsum = R.zh_bsum;
+        std::memcpy(cnt1, R.zh_cnt, sizeof cnt1);
+        std::memcpy(xc1, R.zh_xc, sizeof xc1);
+    } else {
+        DotBatch b(c);
+        STCHK(queue_z(b, R.x1, zx1, &bsum, cnt1, xc1));
         STCHK(b.flush());
     }
     R.beta1 = bsum;
@@ -235,6 +244,16 @@ vampomi_status probit_step(vampomi_ctx* c, VampRun& R) {
         HIPCHK(vk::probit_confusion(N, 1, R.nb3 + ld, ld, c->y, ro, c->st));  // :403-408
     }
     STCHK(fin.add({T(R.x1p, R.x1, vk::DIFF2), T(R.x1p, R.x1p)}, M, true, R.nm));  // NMSE (:444-448)
+    // iteration it+1's head, queued with this iteration's last reductions so
+    // that it needs no host waits of its own (discarded if the stop fires):
+    // its updatePrior (:139) reads r1 and gam1 of this iteration and runs
+    // after its g1 / g1d (the prefetched denoising above used this mixture);
+    // its z-side denoising (:202-253) reads p1 and tau1 formed just above, and
+    // its accuracy counts A.(x1n/sqrtN), which the pass above carried
+    EmState em_h;
+    const bool em_h_on = next && R.prm.EM_max_iter >= 1;
+    if (em_h_on) STCHK(em_begin(c, em_params(R), R.mix, R.gam1, R.r1, fin, em_h));
+    if (next) STCHK(queue_z(fin, R.x1n, R.nb3 + 2 * ld, &R.zh_bsum, R.zh_cnt, R.zh_xc));
     STCHK(fin.flush());
     R.params[4] = R.alpha2;
     R.params[5] = R.beta2;
@@ -266,6 +285,13 @@ vampomi_status probit_step(vampomi_ctx* c, VampRun& R) {
     if ((it > 1 && NMSE < R.prm.stop_criteria_thr) || it >= R.prm.max_iter) R.stopped = true;
     STCHK(end_iteration_io(c, R));  // write_bins' and the rows' failures, on every rank at once
     R.have_next = next && !R.stopped;
+    if (R.have_next) {  // (after this iteration's prior row: the update is iteration it+1's)
+        if (em_h_on) {
+            STCHK(em_finish(c, em_params(R), R.mix, R.gam1, R.r1, em_h));
+            R.em_head = it + 1;
+        }
+        R.z_head = it + 1;
+    }
     if (R.have_next) R.alpha1_next = R.sum_d / (double)Mt;
     if (res) {
         res->iterations_run = it;

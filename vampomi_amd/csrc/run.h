@@ -29,6 +29,11 @@ struct VampRun {
     int z1n_slot = 2;    // nb3 slot of the prefetched z1
     int bern_it = 0;     // probit: the iteration whose probe bern holds (drawn one iteration early)
     int abern_it = 0;    // probit: the iteration whose A.bern is in nb3 slot 3
+    // probit: iteration it+1's head, resolved at iteration it's last flush
+    // (probit.cpp): its updatePrior applied (em_head == it+1), and its z-side
+    // denoising sums and accuracy counts (z_head == it+1)
+    int em_head = 0, z_head = 0;
+    double zh_bsum = 0, zh_cnt[4] = {}, zh_xc[3] = {};
     int hs_it = 0;       // linear: the iteration whose A.bern is in abern (the CG head start)
     std::string out_dir, out_name, p_params, p_metrics, p_prior;
     int it = 0;
