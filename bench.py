@@ -459,7 +459,13 @@ def ref_ops_time(w: dict, seed: int, threads: int) -> dict:
         return {"skipped": "oracle/_ref/ref_data not built (needs /root/reference in the build container)"}
     N, Mt = w["N"], w["Mt"]
     layouts, errors = [], []
+    t0 = time.perf_counter()
+    budget = float(os.environ.get("VAMPOMI_REF_LEG_BUDGET_S", "240"))  # the whole leg (a few s per layout at C2)
     for P, omp in ref_layouts(threads):
+        left = budget - (time.perf_counter() - t0)
+        if left < 10:
+            errors.append(f"np={P}: skipped, the leg's {budget:.0f} s budget is spent")
+            continue
         Ms = min(Mt, P * (INT_MAX // N))
         env = dict(os.environ, OMP_NUM_THREADS=str(omp))
         cmd = [exe, "time", str(N), str(Ms), "2", str(seed)]
@@ -469,7 +475,7 @@ def ref_ops_time(w: dict, seed: int, threads: int) -> dict:
                 continue
             cmd = [MPIEXEC, "-np", str(P)] + cmd
         try:
-            out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+            out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=min(150.0, left))
         except subprocess.TimeoutExpired:
             errors.append(f"np={P}: timed out")
             continue
