@@ -414,8 +414,9 @@ def test_c4_full_shard_vs_oracle():
             with open(f, "a") as fh:
                 fh.write(json.dumps({"test": test + "[device order]", "key": key, "gap_seq": g_seq.tolist(),
                                      "gap_dev": g_dev.tolist()}) + "\n")
+        # (measured, round 6: 4e-5 - 1e-4 of the gap, <= 4.1e-13 at iteration 2)
         assert np.all(g_dev[1:] <= 0.2 * g_seq[1:]), (key, g_dev / np.maximum(g_seq, 1e-300))
-        assert np.all(g_dev[2:] <= 1e-10), (key, g_dev)
+        assert np.all(g_dev[1:] <= 1e-10), (key, g_dev)  # north_star's bar, against the device's order
     # the reference's own spread: its runs' 90th percentile
     spread = {key: np.quantile(z[f"spread_{key}"], 0.9, axis=0) for key in ("x1", "r1", "params", "metrics", "prior")}
     _assert_probit_parity(s, ref, spread, k=PROBIT_K_ENSEMBLE, test=test)
