@@ -484,6 +484,9 @@ def ref_ops_time(w: dict, seed: int, threads: int) -> dict:
             errors.append(f"np={P}: exit {out.returncode}: {out.stderr[-200:]}")
             continue
         r = json.loads(lines[-1])
+        # progress on stderr (a long CPU leg is not a hung run)
+        print(f"[cpu reference leg] np={P} x omp={r['threads']}: Ax {r['ax_ms']:.1f} ms, ATx {r['atx_ms']:.1f} ms "
+              f"on {N} x {Ms}", file=sys.stderr, flush=True)
         scale = Mt / Ms
         lay = {"np": P, "omp": r["threads"], "ax_ms": round(r["ax_ms"] * scale, 3),
                "atx_ms": round(r["atx_ms"] * scale, 3), "Ms": Ms}
