@@ -164,7 +164,12 @@ def load() -> C.CDLL:
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"{LIB_PATH} not built: run `python -m vampomi_amd.build`")
         lib = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+        # another build named by VAMPOMI_LIB (an earlier round's, for an A/B)
+        # may lack entry points added since; the product library may not
+        other = bool(os.environ.get("VAMPOMI_LIB"))
         for name, (res, args) in SIGNATURES.items():
+            if other and not hasattr(lib, name):
+                continue
             f = getattr(lib, name)
             f.restype = res
             f.argtypes = args
