@@ -163,7 +163,9 @@ for s in "$@"; do
         step trace_c4 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_c4" -o run --output-format csv -- \
             python bench.py --config c4 --steps 10 --warmup 2 --no-cpu-baseline --no-timing
         python tools/trace_cmp.py "$(find "$OUT/prof_c4" -name 'run_kernel_trace.csv' | head -1)" --skip 2 \
-            --mark probit_denoise_kernel | tee "$OUT/trace_c4.txt" ;;
+            --mark probit_denoise_kernel | tee "$OUT/trace_c4.txt"
+        python tools/trace_gaps.py "$(find "$OUT/prof_c4" -name 'run_kernel_trace.csv' | head -1)" 0.3 \
+            > "$OUT/gaps_c4.txt" ;;
     bases)
         step bases 200 python tools/one_gpu_bases.py ;;
     final)
