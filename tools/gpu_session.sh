@@ -13,7 +13,8 @@
 #                $OLD (default build_ab/, make -C vampomi_amd/csrc OBJDIR=../../build_ab/obj LIBDIR=../../build_ab/lib BINDIR=../../build_ab/bin at the base commit), compared bit for bit
 #   ab           C2 lines alternating this build and $OLD, $ROUNDS rounds
 #   envab        C2 lines alternating the settings in $ENVAB ("A=1;A=2;...")
-#   envtrace     a kernel trace of the C2 line per setting in $ENVAB, per-iteration kernel times side by side
+#   envtrace     a kernel trace of the C2 line ($ENVCFG: another config, $ENVSTEPS steps) per setting in $ENVAB,
+#                per-iteration kernel times side by side
 #   trace        rocprofv3 kernel trace of the C2 line + the gap analysis
 #   trace_old    the same for $OLD
 #   hiptrace     rocprofv3 HIP API + kernel trace of a short C2 line
@@ -100,7 +101,7 @@ for s in "$@"; do
         for e in "${settings[@]}"; do
             i=$((i + 1))
             step envtrace$i 300 env $e rocprofv3 --kernel-trace --stats -d "$OUT/prof_env$i" -o run --output-format csv \
-                -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-timing
+                -- python bench.py --config "${ENVCFG:-c2}" --steps "${ENVSTEPS:-20}" --warmup 5 --no-cpu-baseline --no-timing
             traces+=("$(find "$OUT/prof_env$i" -name 'run_kernel_trace.csv' | head -1)")
         done
         python tools/trace_cmp.py "${traces[@]}" | tee "$OUT/envtrace_cmp.txt" ;;

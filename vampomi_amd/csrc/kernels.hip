@@ -2231,6 +2231,7 @@ __global__ __launch_bounds__(kBlock) void cg_update_kernel(int64_t M, CgVecs c, 
     }
 }
 
+constexpr int kCguBlocks = 512;
 hipError_t cg_update(int K, int64_t M, const CgVecs& c, double diag, CgState* cs, const double* dp_dev,
                      const double* pp_dev, int fuse, const RedOut& ro, const CgDecide& dc, hipStream_t st) {
     // VAMPOMI_CG_EPT: M elements per thread (tuning experiments; default 2, red_blocks)
@@ -2239,8 +2240,16 @@ hipError_t cg_update(int K, int64_t M, const CgVecs& c, double diag, CgState* cs
     int nb = 0;
     if (c.adpart) {
         if (K > kOpMaxK || c.adslots < 1 || !c.Q[0]) return hipErrorInvalidValue;
-        nb = (int)std::min<int64_t>(K * cdiv(c.nA, 128), kRedBlocks - mb);
-        nb = std::max(nb, 1);
+        // at most kCguBlocks workgroups in all (two per CU): every one takes the
+        // step's ticket, and beyond that their arrivals cost more than the tiles
+        // they share (C4 shard, 782 slot-sum workgroups: 164.8 -> 127.4 us of
+        // cg_update per iteration at 400, 142.0 at 158; C2's 158 is best at C2,
+        // profiles/r06n_cgu_blocks.txt).  Each workgroup takes tiles nb apart,
+        // the same tiles summed the same way: bitwise the same for any nb.
+        // VAMPOMI_CGU_NB: the count itself (tuning experiments)
+        static const int nbset = std::getenv("VAMPOMI_CGU_NB") ? std::atoi(std::getenv("VAMPOMI_CGU_NB")) : 0;
+        nb = (int)std::min<int64_t>(K * cdiv(c.nA, 128), nbset > 0 ? nbset : std::max(kCguBlocks - mb, 1));
+        nb = std::max(std::min(nb, kRedBlocks - mb), 1);
     }
     // the 32-load slot rounds only where a wave sums >= 32 slots (C2's team of
     // 2); else rounds of <= 8 loads and the registers of more workgroups per CU
