@@ -88,6 +88,18 @@ __device__ bool red_ticket(const RedOut& ro, int nblocks) {
     return is_last;
 }
 
+// red_ticket for a block that published nothing: no wait for its own stores
+// (block-uniform; the barrier: every wave of the block is past its start)
+__device__ bool red_ticket_nowait(const RedOut& ro, int nblocks) {
+    __shared__ int is_last;
+    __syncthreads();
+    if (threadIdx.x == 0)
+        is_last = __hip_atomic_fetch_add(ro.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                  (unsigned)nblocks - 1;
+    __syncthreads();
+    return is_last;
+}
+
 // the last block's sums of the nblk blocks' partials at ro.part, into ro.out
 // (and keep); finish: then re-arm the ticket and store the host flag
 __device__ void red_final(const RedOut& ro, int nq, int nblk, double* keep, bool finish) {
@@ -2045,11 +2057,29 @@ __global__ void cg_decide_kernel(CgState* cs, const double* __restrict__ red, in
 // K systems, not kMaxRhs (at K = 2: a quarter of the live registers, no
 // spills, and only the K systems' vector pointers loaded from the arguments);
 // every per-element operation and every sum is the same, in the same order.
+// CGU_ABL (experiment builds only, results wrong; tools/cgu_ablation.sh):
+// 1 = no slot sums / N-side updates, 2 = no M-side loads / stores, 4 = no
+// decision, 8 = no last-block sums (nor decision), 16 = no partials and no
+// ticket, 32 = a constant state instead of *cs and <d,p>
+#ifndef CGU_ABL
+#define CGU_ABL 0
+#endif
 template <int K, int W>
 __global__ __launch_bounds__(kBlock) void cg_update_kernel(int64_t M, CgVecs c, double diag,
                                                            CgState* cs, const double* __restrict__ dp_dev,
                                                            const double* __restrict__ pp_dev, int fuse, RedOut ro,
                                                            CgDecide dc, int mblocks) {
+#if CGU_ABL & 32
+    CgState st{};
+    st.K = K;
+    st.any = 1;
+    for (int k = 0; k < K; ++k) {
+        st.active[k] = 1;
+        st.rz[k] = st.vv[k] = 1.0;
+    }
+    double dpv[K], ppv[K];
+    for (int k = 0; k < K; ++k) dpv[k] = 1.0, ppv[k] = 0.0;
+#else
     const CgState st = *cs;
     double dpv[K], ppv[K];
 #pragma unroll
@@ -2057,8 +2087,8 @@ __global__ __launch_bounds__(kBlock) void cg_update_kernel(int64_t M, CgVecs c, 
         dpv[k] = dp_dev[k];
         ppv[k] = pp_dev ? pp_dev[k] : 0.0;
     }
+#endif
     if (!st.any) return;
-    __shared__ double lds[4];
     __shared__ double fin[3 * kMaxRhs];  // the step's final sums, for the deciding thread
     // blocks [0, mblocks) stream the M-vectors; with c.adpart the blocks past
     // them sum the operator's A d partials and update the N-vectors
@@ -2089,7 +2119,8 @@ __global__ __launch_bounds__(kBlock) void cg_update_kernel(int64_t M, CgVecs c, 
     // (W < 32, the large-N plans: one element per round, fewer registers and
     // more workgroups per CU; the same sums in the same order)
     constexpr int H = W >= 32 || K >= 3 ? 2 : 1;  // (K >= 3 keeps two: one would spill to scratch)
-    for (int64_t i0 = (int64_t)blockIdx.x * kBlock + threadIdx.x; mpart && i0 < M; i0 += H * mstride) {
+    for (int64_t i0 = (int64_t)blockIdx.x * kBlock + threadIdx.x; mpart && !(CGU_ABL & 2) && i0 < M;
+         i0 += H * mstride) {
         double pv[H][K], zv[H][K], muv[H][K], rv[H][K], dv[H][K], vv[H][K], wv[H][K], sv[H][K];
         const bool two = H == 2 && i0 + mstride < M;
 #pragma unroll
@@ -2144,7 +2175,7 @@ __global__ __launch_bounds__(kBlock) void cg_update_kernel(int64_t M, CgVecs c, 
         const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, ns = c.adslots;
         const int nb = (int)gridDim.x - mblocks;
         const int64_t tpk = (c.nA + 127) / 128;  // tiles per system
-        for (int64_t tile = (int)blockIdx.x - mblocks; !mpart && tile < K * tpk; tile += nb) {
+        for (int64_t tile = (int)blockIdx.x - mblocks; !(CGU_ABL & 1) && !mpart && tile < K * tpk; tile += nb) {
             const int k = (int)(tile / tpk);
             const int64_t i = (tile - k * tpk) * 128 + 2 * lane;  // < adld (a multiple of 16)
             const bool ok = i < c.nA;
@@ -2220,10 +2251,26 @@ __global__ __launch_bounds__(kBlock) void cg_update_kernel(int64_t M, CgVecs c, 
         for (int k = 0; k < K; ++k)
             if (on[k] && c.AW[k]) c.AW[k][i] = aw[k] + alpha[k] * as[k];
     }
-    block_put_sums<3 * K>(acc, 3 * K, ro, (int64_t)blockIdx.x * 3 * K);
+    // The M-side blocks publish their sums.  The slot-sum blocks' sums are
+    // zero: they publish none, and the last block adds the first mblocks
+    // blocks' partials (the same partials in the same order, without the
+    // zeros: the same bits).  Every block still takes the ticket, so that the
+    // decision below, which rewrites *cs, follows every block's read of the
+    // state; a slot-sum block takes it without waiting for its vector stores
+    // (the decision reads none of them; the next launch sees them after the
+    // kernel boundary).
+    bool last = false;
+    if (CGU_ABL & 16) {
+    } else if (mpart) {
+        block_put_sums<3 * K>(acc, 3 * K, ro, (int64_t)blockIdx.x * 3 * K);
+        last = red_ticket(ro, (int)gridDim.x);
+    } else {
+        last = red_ticket_nowait(ro, (int)gridDim.x);
+    }
+    if (last && !(CGU_ABL & 8)) red_final(ro, 3 * K, mblocks, fin, true);
     // one rank: the last block decides the step itself (its sums are final),
     // from the state read at the start (only this decision writes it)
-    if (red_finish(ro, 3 * K, lds, fin) && dc.on && threadIdx.x == 0) {
+    if (last && dc.on && threadIdx.x == 0 && !(CGU_ABL & 12)) {
         double r[3 * kMaxRhs];
 #pragma unroll
         for (int q = 0; q < 3 * kMaxRhs; ++q) r[q] = q < 3 * K ? fin[q] : 0.0;
