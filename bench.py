@@ -71,7 +71,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 PMC_FILES = [os.path.join(ROOT, "profiles", f)
-             for f in ("r05zz_pmc_traffic_{}.json", "r05z_pmc_traffic_{}.json", "r05_pmc_traffic_{}.json", "r04_pmc_traffic_{}.json", "r03z_pmc_traffic_{}.json", "r03y_pmc_traffic_{}.json", "r03l_pmc_traffic_{}.json",
+             for f in ("r06zz_pmc_traffic_{}.json", "r06z_pmc_traffic_{}.json", "r05zz_pmc_traffic_{}.json", "r05z_pmc_traffic_{}.json", "r05_pmc_traffic_{}.json", "r04_pmc_traffic_{}.json", "r03z_pmc_traffic_{}.json", "r03y_pmc_traffic_{}.json", "r03l_pmc_traffic_{}.json",
                        "r03g_pmc_traffic_{}.json",
                        "r03f_pmc_traffic_{}.json", "r03e_pmc_traffic_{}.json", "r02j_pmc_traffic_{}.json",
                        "r02i_pmc_traffic_{}.json", "r02h_pmc_traffic_{}.json", "r02_pmc_traffic_{}.json",
